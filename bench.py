@@ -1,0 +1,159 @@
+#!/usr/bin/env python3
+"""Benchmark: positions solved per second on the synthetic sum-of-Four-To-One
+state space (BASELINE.json config 4).
+
+A "step" is one complete strong solve from the root: table reset, forward
+expansion of every level, retrograde pass of every level, root word back on
+the host.  N=1 workload: heaps 31^6 = 2^30 = 1,073,741,824 positions,
+187 levels, 12,280,922,112 edges.  For N>1 (one process per GPU, launched by
+torch.distributed.run) every rank solves... see DESIGN.md §Multi-GPU.
+
+Prints ONE JSON line (rank 0).  Fields beyond the driver contract:
+  roofline      dominant kernel's algorithmic bytes (SURVEY §8d model) per
+                launch / its HIP-event-timed average duration, vs 8 TB/s
+  cpu_baseline  the oracle (oracle/, one core) on a bounded sample of the
+                same game family, timed on this host
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
+
+
+def heaps_for(world):
+    """Weak scaling: 2^30 positions per GPU.  N=1: 31^6."""
+    base = [31] * 6
+    k = {1: 0, 2: 1, 4: 2, 8: 3}.get(world)
+    if k is None:
+        raise SystemExit("--gpus must be 1, 2, 4 or 8")
+    return [63] * k + base[k:]
+
+
+def algorithmic_bytes(positions, edges):
+    """forward 24 B/position + 8 B/edge; backward 12 B/position
+    + 12 B/edge (8-B keys, 4-B value words)."""
+    fwd = 24 * positions + 8 * edges
+    bwd = 12 * positions + 12 * edges
+    return fwd, bwd
+
+
+def cpu_baseline(sample_heaps="31:31:31:31:15"):
+    """Oracle (one core, scalar C port) on a bounded sample: the same game
+    family at 2^24 positions (about 10-15 s)."""
+    from oracle.oracle import Game
+    g = Game("sum_four_to_one", "heaps=" + sample_heaps)
+    t0 = time.perf_counter()
+    sol = g.solve(1 << 25)
+    dt = time.perf_counter() - t0
+    return {"value": sol.count / dt, "unit": "positions/s", "cores": 1,
+            "kind": "port",
+            "sample": "oracle/ scalar C retrograde, sum_four_to_one heaps=%s "
+                      "(%d positions, %d edges, root %s), %.2f s"
+                      % (sample_heaps, sol.count, sol.edges, sol.root_line, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--heaps", default=None,
+                    help="override the synthetic heaps, e.g. 31:31:31:31")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("WORLD_SIZE=%d but --gpus %d" % (world, args.gpus))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from gamesmanmpi_amd.games import GameSpec
+    from gamesmanmpi_amd.solver import Solver
+
+    heaps = args.heaps.split(":") if args.heaps else heaps_for(1)
+    params = "heaps=" + ":".join(str(h) for h in heaps)
+    spec = GameSpec("sum_four_to_one", params)
+    solver = Solver(spec, device="cuda:%d" % local, kernel_timing=False)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        solver.solve()
+    barrier()
+    t0 = time.perf_counter()
+    results = []
+    for _ in range(args.steps):
+        results.append(solver.solve())
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    r = results[-1]
+    positions_total = r.positions * world
+
+    # roofline of the dominant kernel: one extra timed solve with HIP events
+    # around every launch (on the stream the kernels run on)
+    tsolver = Solver(spec, device="cuda:%d" % local, kernel_timing=True)
+    tr = tsolver.solve()
+    del tsolver
+    fwd_b, bwd_b = algorithmic_bytes(tr.positions, tr.edges)
+    if tr.ms_resolve_kernels >= tr.ms_expand_kernels:
+        kname, kb, kms, kn = ("k_resolve", bwd_b, tr.ms_resolve_kernels,
+                              tr.n_resolve_launches)
+    else:
+        kname, kb, kms, kn = ("k_expand", fwd_b, tr.ms_expand_kernels,
+                              tr.n_expand_launches)
+    achieved = (kb / kn) / (kms / kn / 1e3) / 1e9  # GB/s
+    line = {
+        "metric": "positions solved/sec (node)",
+        "value": positions_total * args.steps / elapsed,
+        "unit": "positions/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64 keys / u32 words (integer)",
+        "data": "synthetic: sum of Four-To-One heaps, fully determined state space",
+        "config": {"workload": "sum_four_to_one heaps=%s" % ":".join(map(str, heaps)),
+                   "positions_per_gpu": r.positions, "edges_per_gpu": r.edges,
+                   "levels": r.levels, "root": r.root_line,
+                   "parallelism": "md5 shards x%d" % world if world > 1 else "1 GPU"},
+        "roofline": {"bound": "hbm", "kernel": kname,
+                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "launches": kn, "ms_kernel_total": kms,
+                     "algorithmic_bytes_total": kb},
+        "phase_ms": {"forward": r.ms_forward, "backward": r.ms_backward,
+                     "solve_wall": r.ms_total},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline()
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

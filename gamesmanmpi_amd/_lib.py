@@ -1,0 +1,139 @@
+"""ctypes binding of the C-ABI in include/gamesman.h (libgamesman_hip.so).
+
+torch is imported before the library is loaded so both share one HIP runtime
+(torch/lib/libamdhip64.so.7 has the same soname the library links against);
+device buffers allocated by torch are then valid addresses for the kernels.
+There is no CPU fallback: if the library is missing this module raises.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIBPATH = os.path.join(HERE, "libgamesman_hip.so")
+
+GM_EINVAL, GM_EHIP, GM_EFULL, GM_ECORRUPT, GM_ENOGPU = -1, -2, -3, -4, -5
+GM_F_KERNEL_TIMING = 1
+GM_MAXCHILD = 32
+GM_NO_WORD = 0xFFFFFFFF
+
+
+class GmError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("%s (code %d)" % (msg, code))
+        self.code = code
+
+
+class TableFull(GmError):
+    pass
+
+
+class gm_plan_t(ctypes.Structure):
+    _fields_ = [("table_slots", ctypes.c_uint64),
+                ("level_capacity", ctypes.c_uint64),
+                ("scratch_bytes", ctypes.c_uint64),
+                ("max_levels", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
+
+
+class gm_buffers(ctypes.Structure):
+    _fields_ = [("table", ctypes.c_void_p),
+                ("table_slots", ctypes.c_uint64),
+                ("levels", ctypes.c_void_p),
+                ("level_capacity", ctypes.c_uint64),
+                ("scratch", ctypes.c_void_p),
+                ("scratch_bytes", ctypes.c_uint64),
+                ("stream", ctypes.c_void_p),
+                ("flags", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
+
+
+class gm_result(ctypes.Structure):
+    _fields_ = [("root_word", ctypes.c_uint32),
+                ("root_value", ctypes.c_int32),
+                ("root_remoteness", ctypes.c_uint64),
+                ("positions", ctypes.c_uint64),
+                ("edges", ctypes.c_uint64),
+                ("primitives", ctypes.c_uint64),
+                ("levels", ctypes.c_uint32),
+                ("max_level_width", ctypes.c_uint32),
+                ("ms_total", ctypes.c_double),
+                ("ms_forward", ctypes.c_double),
+                ("ms_backward", ctypes.c_double),
+                ("ms_expand_kernels", ctypes.c_double),
+                ("ms_resolve_kernels", ctypes.c_double),
+                ("n_expand_launches", ctypes.c_uint64),
+                ("n_resolve_launches", ctypes.c_uint64)]
+
+
+# every symbol include/gamesman.h declares (tests check the exports)
+EXPORTS = (
+    "gm_game_lookup", "gm_game_info", "gm_root", "gm_encode", "gm_decode",
+    "gm_encode_batch", "gm_decode_batch", "gm_str_utf8", "gm_host_expand", "gm_plan", "gm_solver_create",
+    "gm_solver_solve", "gm_solver_query", "gm_solver_positions",
+    "gm_solver_destroy", "gm_solve", "gm_owner", "gm_owner_host",
+    "gm_last_error", "gm_version",
+)
+
+_lib = None
+
+
+def load():
+    """Load libgamesman_hip.so (after torch) and declare signatures."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    import torch  # noqa: F401  -- share torch's HIP runtime (see docstring)
+    if not os.path.exists(LIBPATH):
+        raise ImportError(
+            "libgamesman_hip.so not built: run `python -c 'import "
+            "__graft_entry__ as g; g.build()'` (or `make -C gamesmanmpi_amd`)")
+    L = ctypes.CDLL(LIBPATH)
+    c = ctypes
+    P = c.POINTER
+    sig = {
+        "gm_game_lookup": [c.c_char_p, c.c_char_p, P(c.c_int)],
+        "gm_game_info": [c.c_int, P(c.c_uint64), P(c.c_uint32), P(c.c_uint32)],
+        "gm_root": [c.c_int, P(c.c_uint64)],
+        "gm_encode": [c.c_int, c.c_char_p, c.c_size_t, P(c.c_uint64)],
+        "gm_decode": [c.c_int, c.c_uint64, c.c_void_p, c.c_size_t,
+                      P(c.c_size_t)],
+        "gm_encode_batch": [c.c_int, c.c_void_p, c.c_size_t, c.c_void_p,
+                            c.c_size_t, c.c_void_p],
+        "gm_decode_batch": [c.c_int, c.c_void_p, c.c_size_t, c.c_void_p,
+                            c.c_size_t, c.c_void_p],
+        "gm_str_utf8": [c.c_int, c.c_uint64, c.c_void_p, c.c_size_t,
+                        P(c.c_size_t)],
+        "gm_host_expand": [c.c_int, c.c_void_p, c.c_size_t, c.c_void_p,
+                           c.c_void_p, c.c_void_p],
+        "gm_plan": [c.c_int, c.c_uint64, P(gm_plan_t)],
+        "gm_solver_create": [c.c_int, P(gm_buffers), P(c.c_void_p)],
+        "gm_solver_solve": [c.c_void_p, P(gm_result)],
+        "gm_solver_query": [c.c_void_p, c.c_void_p, c.c_uint64, c.c_void_p],
+        "gm_solver_positions": [c.c_void_p, c.c_void_p, c.c_uint64,
+                                P(c.c_uint64)],
+        "gm_solve": [c.c_int, c.c_uint64, c.c_int, P(gm_buffers),
+                     P(gm_result)],
+        "gm_owner": [c.c_int, c.c_void_p, c.c_uint64, c.c_int, c.c_void_p,
+                     c.c_void_p],
+        "gm_owner_host": [c.c_int, c.c_void_p, c.c_size_t, c.c_int,
+                          c.c_void_p],
+    }
+    for name, args in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = c.c_int
+    L.gm_solver_destroy.argtypes = [c.c_void_p]
+    L.gm_solver_destroy.restype = None
+    L.gm_last_error.restype = c.c_char_p
+    L.gm_version.restype = c.c_char_p
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc == 0:
+        return
+    msg = load().gm_last_error().decode(errors="replace")
+    if rc == GM_EFULL:
+        raise TableFull(rc, msg)
+    raise GmError(rc, msg)

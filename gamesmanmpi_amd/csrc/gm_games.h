@@ -1,0 +1,322 @@
+// gm_games.h -- device-side game descriptors for the MI355X solver.
+//
+// Each reference game module (test_games/*.py) is paired with a descriptor
+// over a packed 64-bit state ("key").  A descriptor provides, for one key:
+//   prim(key)                      -> WIN/LOSS/TIE/DRAW or UNDECIDED
+//                                     (the module's primitive())
+//   children(key, emit)            -> calls emit(child, step) for each child
+//                                     in gen_moves() order, each do_move()'d,
+//                                     with the child's level step (1 or 2)
+//                                     for the tier pipeline
+// These are __host__ __device__ so the same code serves the GPU kernels and
+// gm_host_expand (the C-ABI's host-side parity probe).  Canonical-bytes
+// <-> key conversion lives in gm_codec.cpp.
+//
+// Value codes follow src/utils.py:3 (WIN=0, LOSS=1, TIE=2, DRAW=3,
+// UNDECIDED=4).  A resolved position is stored as one 32-bit word:
+//   bits [0,2) value, bits [2,32) remoteness  (remoteness needs >= 30 bits:
+//   the Four-To-One 2^30 chain reaches 715,827,883; SURVEY.md §7 "Hard
+//   parts").
+#pragma once
+#include <stdint.h>
+
+#ifndef __HIP_DEVICE_COMPILE__
+#include <string.h>
+#endif
+
+#if defined(__HIPCC__)
+#define GM_HD __host__ __device__ __forceinline__
+#else
+#define GM_HD inline
+#endif
+
+namespace gm {
+
+enum : int { WIN = 0, LOSS = 1, TIE = 2, DRAW = 3, UNDECIDED = 4 };
+
+enum GameKind : int {
+  K_SUM = 1,     // four_to_one.py (1 heap) and sum_four_to_one.py (K heaps)
+  K_TTT = 2,     // tic_tac_toe_np.py and mttt.py (same graph)
+  K_TOOT = 3,    // toot_and_otto_bitstring.py
+  K_OTHELLO = 4  // othello_bit_new.py (square boards)
+};
+
+constexpr int MAXCHILD = 32;
+constexpr uint64_t EMPTY_KEY = ~0ull;
+constexpr uint32_t NO_WORD = 0xFFFFFFFFu;
+
+GM_HD uint32_t make_word(int value, uint32_t rem) { return (uint32_t)value | (rem << 2); }
+
+// ---------------------------------------------------------------------------
+// Descriptor parameter block (passed to kernels by value).
+// ---------------------------------------------------------------------------
+struct Desc {
+  int kind;
+  int variant;     // K_TTT: 0 = tic_tac_toe_np, 1 = mttt; K_SUM: 0 = sum, 1 = four_to_one
+  int L, H, A;     // board games
+  int nbits;       // bitstring length (toot/othello canonical form)
+  // K_SUM
+  int nheaps;
+  int pow2;        // every base is a power of two -> shift/mask digits
+  uint32_t heap[16];
+  uint32_t base[16];
+  uint32_t shift[16];
+  uint64_t stride[16];
+  uint32_t root_sum;
+  // K_TOOT word-start masks (directions (1,0),(0,1),(1,1),(1,-1))
+  uint64_t tmask[4];
+  int tstep[4];
+  uint64_t full;   // all-cells mask
+  uint64_t root;   // root key
+  int max_levels;  // levels the pipeline must provision (root level = 0)
+};
+
+GM_HD int popc64(uint64_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __popcll(v);
+#else
+  return __builtin_popcountll(v);
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// Sum of Four-To-One heaps (four_to_one.py:7-22 per heap;
+// gamesmanmpi_amd/games/sum_four_to_one.py).  key = mixed-radix rank, heap 0
+// least significant.  Level = root_sum - digit sum; a -1 move steps one
+// level, a -2 move two.
+// ---------------------------------------------------------------------------
+GM_HD uint32_t sum_digit(const Desc& d, uint64_t r, int i) {
+  if (d.pow2) return (uint32_t)((r >> d.shift[i]) & (d.base[i] - 1));
+  return (uint32_t)((r / d.stride[i]) % d.base[i]);
+}
+GM_HD int sum_prim(const Desc&, uint64_t r) { return r == 0 ? LOSS : UNDECIDED; }
+template <class F>
+GM_HD int sum_children(const Desc& d, uint64_t r, F&& emit) {
+  int n = 0;
+  if (d.pow2) {
+    for (int i = 0; i < d.nheaps; i++) {
+      uint32_t h = (uint32_t)((r >> d.shift[i]) & (d.base[i] - 1));
+      if (h >= 1) { emit(r - d.stride[i], 1); n++; }
+      if (h >= 2) { emit(r - 2 * d.stride[i], 2); n++; }
+    }
+  } else {
+    uint64_t rest = r;
+    for (int i = 0; i < d.nheaps; i++) {
+      uint64_t q = rest / d.base[i];
+      uint32_t h = (uint32_t)(rest - q * d.base[i]);
+      rest = q;
+      if (h >= 1) { emit(r - d.stride[i], 1); n++; }
+      if (h >= 2) { emit(r - 2 * d.stride[i], 2); n++; }
+    }
+  }
+  return n;
+}
+GM_HD int sum_level(const Desc& d, uint64_t r) {
+  uint32_t s = 0;
+  for (int i = 0; i < d.nheaps; i++) s += sum_digit(d, r, i);
+  return (int)(d.root_sum - s);
+}
+
+// ---------------------------------------------------------------------------
+// Tic-tac-toe (tic_tac_toe_np.py:7-61 / mttt.py:11-127).  key: 2 bits per
+// cell in reading order (np cell [x][y] -> 3x+y; mttt char i -> i);
+// 1 = first mover (np 1 / mttt 'X'), 2 = second (np 2 / mttt 'O').
+// ---------------------------------------------------------------------------
+GM_HD uint32_t ttt_plane(uint64_t k, uint32_t who) {
+  uint32_t m = 0;
+  for (int c = 0; c < 9; c++) m |= (uint32_t)(((k >> (2 * c)) & 3) == who) << c;
+  return m;
+}
+GM_HD bool ttt_line(uint32_t m) {
+  // rows, columns, diagonals of the 3x3 reading-order grid: every line the
+  // reference's 4-direction scan can find (tic_tac_toe_np.py:50-56)
+  const uint32_t L8[8] = {0007, 0070, 0700, 0111, 0222, 0444, 0421, 0124};
+  for (int i = 0; i < 8; i++)
+    if ((m & L8[i]) == L8[i]) return true;
+  return false;
+}
+GM_HD int ttt_prim(const Desc&, uint64_t k) {
+  uint32_t a = ttt_plane(k, 1), b = ttt_plane(k, 2);
+  if (ttt_line(a) || ttt_line(b)) return LOSS;  // checked before fullness
+  return ((a | b) == 0777) ? TIE : UNDECIDED;
+}
+template <class F>
+GM_HD int ttt_children(const Desc&, uint64_t k, F&& emit) {
+  uint32_t a = ttt_plane(k, 1), b = ttt_plane(k, 2);
+  uint64_t who = popc64(a) > popc64(b) ? 2 : 1;  // tic_tac_toe_np.py:13-25
+  int n = 0;
+  for (int c = 0; c < 9; c++)
+    if (!(((a | b) >> c) & 1)) { emit(k | (who << (2 * c)), 1); n++; }
+  return n;
+}
+GM_HD int ttt_level(const Desc&, uint64_t k) {
+  return popc64(ttt_plane(k, 1) | ttt_plane(k, 2));
+}
+
+// ---------------------------------------------------------------------------
+// Toot-and-Otto (toot_and_otto_bitstring.py).  key bits:
+//   [0,A) T plane, [A,2A) O plane (cell index L*y+x as in board_get :179-185)
+//   [2A, 2A+12) hands, 3 bits each: P1-T, P1-O, P2-T, P2-O (0..6)
+//   2A+12: the live turn bit (board[-1], :218-222), 1 = player 1 to move
+// Level = pieces on the board.
+// ---------------------------------------------------------------------------
+GM_HD uint64_t shr_s(uint64_t v, int s) { return s >= 0 ? (v >> s) : (v << (-s)); }
+GM_HD int toot_count(const Desc& d, uint64_t first, uint64_t mid) {
+  // word = first, mid, mid, first along each direction (TOOT: T,O,O,T)
+  int n = 0;
+  for (int i = 0; i < 4; i++) {
+    int s = d.tstep[i];
+    n += popc64(d.tmask[i] & first & shr_s(mid, s) & shr_s(mid, 2 * s) & shr_s(first, 3 * s));
+  }
+  return n;
+}
+GM_HD int toot_prim(const Desc& d, uint64_t k) {
+  uint64_t t = k & d.full, o = (k >> d.A) & d.full;
+  int toot = toot_count(d, t, o), otto = toot_count(d, o, t);
+  bool p1 = (k >> (2 * d.A + 12)) & 1;
+  if (toot == otto) return ((t | o) == d.full) ? TIE : UNDECIDED;  // :80-81
+  return ((toot > otto) != p1) ? LOSS : WIN;                         // :82-85
+}
+template <class F>
+GM_HD int toot_children(const Desc& d, uint64_t k, F&& emit) {
+  const int A = d.A, L = d.L, H = d.H;
+  uint64_t t = k & d.full, o = (k >> A) & d.full, occ = t | o;
+  int p1 = (int)((k >> (2 * A + 12)) & 1);
+  int hb = 2 * A + (p1 ? 0 : 6);  // player 1 hands at 2A, player 2 at 2A+6
+  uint32_t nT = (uint32_t)((k >> hb) & 7), nO = (uint32_t)((k >> (hb + 3)) & 7);
+  uint64_t turn = 1ull << (2 * A + 12);
+  int n = 0;
+  for (int x = 0; x < L; x++) {
+    if ((occ >> (L * (H - 1) + x)) & 1) continue;  // column full (:95)
+    int y = 0;
+    while ((occ >> (L * y + x)) & 1) y++;          // lowest blank (:112-115)
+    uint64_t cell = 1ull << (L * y + x);
+    if (nT > 0) { emit((k - (1ull << hb)) ^ turn ^ cell, 1); n++; }
+    if (nO > 0) { emit((k - (1ull << (hb + 3))) ^ turn ^ (cell << A), 1); n++; }
+  }
+  return n;
+}
+GM_HD int toot_level(const Desc& d, uint64_t k) {
+  return popc64((k | (k >> d.A)) & d.full);
+}
+
+// ---------------------------------------------------------------------------
+// Othello (othello_bit_new.py), square boards.  key bits:
+//   [0,A) WHITE plane, [A,2A) BLACK plane (board_get :251-257)
+//   2A: 1 = BLACK to move (turn_count == 1), 0 = WHITE (turn_count == 2)
+//   [2A+1, 2A+3): pass_count (0..2)
+// Level = pieces - 4 + pass_count (every edge steps one level, passes
+// included; a pass never switches the turn, :122-124).
+// ---------------------------------------------------------------------------
+GM_HD int oth_prim(const Desc& d, uint64_t k) {
+  const int A = d.A;
+  uint64_t w = k & d.full, b = (k >> A) & d.full;
+  uint32_t passes = (uint32_t)((k >> (2 * A + 1)) & 3);
+  if ((w | b) == d.full || passes >= 2) {  // :82-83
+    int wc = popc64(w), bc = popc64(b);
+    if (bc == wc) return TIE;
+    bool black_to_move = (k >> (2 * A)) & 1;
+    return ((bc > wc) != black_to_move) ? LOSS : WIN;  // :71-73
+  }
+  return UNDECIDED;
+}
+// pieces flipped by `me` playing cell (x,y); 0 if the move is not legal
+GM_HD uint64_t oth_flips(const Desc& d, uint64_t me, uint64_t opp, int x, int y) {
+  const int L = d.L, H = d.H;
+  uint64_t flips = 0;
+  for (int dx = -1; dx <= 1; dx++)
+    for (int dy = -1; dy <= 1; dy++) {
+      if (dx == 0 && dy == 0) continue;
+      uint64_t run = 0;
+      int cx = x + dx, cy = y + dy;
+      while (cx >= 0 && cx < L && cy >= 0 && cy < H) {
+        uint64_t bit = 1ull << (L * cy + cx);
+        if (opp & bit) { run |= bit; cx += dx; cy += dy; continue; }
+        if ((me & bit) && run) flips |= run;
+        break;
+      }
+    }
+  return flips;
+}
+template <class F>
+GM_HD int oth_children(const Desc& d, uint64_t k, F&& emit) {
+  const int A = d.A, L = d.L, H = d.H;
+  uint64_t w = k & d.full, b = (k >> A) & d.full;
+  bool black = (k >> (2 * A)) & 1;
+  uint64_t me = black ? b : w, opp = black ? w : b;
+  int n = 0;
+  for (int x = 0; x < L; x++)       // gen_moves: x outer, y inner (:163-166)
+    for (int y = 0; y < H; y++) {
+      uint64_t cell = 1ull << (L * y + x);
+      if ((w | b) & cell) continue;
+      uint64_t f = oth_flips(d, me, opp, x, y);
+      if (!f) continue;
+      uint64_t nme = me | cell | f, nopp = opp & ~f;
+      uint64_t nw = black ? nopp : nme, nb = black ? nme : nopp;
+      // reset_pass, place + flip, incr_turn (:125-129)
+      emit(nw | (nb << A) | ((uint64_t)(!black) << (2 * A)), 1);
+      n++;
+    }
+  if (n == 0) {  // [None]: incr_pass only (:122-124)
+    emit(k + (1ull << (2 * A + 1)), 1);
+    n = 1;
+  }
+  return n;
+}
+GM_HD int oth_level(const Desc& d, uint64_t k) {
+  return popc64((k | (k >> d.A)) & d.full) - 4 + (int)((k >> (2 * d.A + 1)) & 3);
+}
+
+// ---------------------------------------------------------------------------
+// Static dispatch.  children(d, key, emit) calls emit(child, level_step) in
+// gen_moves() order and returns the child count.
+// ---------------------------------------------------------------------------
+template <int KIND> struct Game;
+template <> struct Game<K_SUM> {
+  static GM_HD int prim(const Desc& d, uint64_t k) { return sum_prim(d, k); }
+  template <class F> static GM_HD int children(const Desc& d, uint64_t k, F&& f) { return sum_children(d, k, f); }
+  static GM_HD int level(const Desc& d, uint64_t k) { return sum_level(d, k); }
+};
+template <> struct Game<K_TTT> {
+  static GM_HD int prim(const Desc& d, uint64_t k) { return ttt_prim(d, k); }
+  template <class F> static GM_HD int children(const Desc& d, uint64_t k, F&& f) { return ttt_children(d, k, f); }
+  static GM_HD int level(const Desc& d, uint64_t k) { return ttt_level(d, k); }
+};
+template <> struct Game<K_TOOT> {
+  static GM_HD int prim(const Desc& d, uint64_t k) { return toot_prim(d, k); }
+  template <class F> static GM_HD int children(const Desc& d, uint64_t k, F&& f) { return toot_children(d, k, f); }
+  static GM_HD int level(const Desc& d, uint64_t k) { return toot_level(d, k); }
+};
+template <> struct Game<K_OTHELLO> {
+  static GM_HD int prim(const Desc& d, uint64_t k) { return oth_prim(d, k); }
+  template <class F> static GM_HD int children(const Desc& d, uint64_t k, F&& f) { return oth_children(d, k, f); }
+  static GM_HD int level(const Desc& d, uint64_t k) { return oth_level(d, k); }
+};
+
+GM_HD int any_prim(const Desc& d, uint64_t k) {
+  switch (d.kind) {
+    case K_SUM: return sum_prim(d, k);
+    case K_TTT: return ttt_prim(d, k);
+    case K_TOOT: return toot_prim(d, k);
+    default: return oth_prim(d, k);
+  }
+}
+template <class F>
+GM_HD int any_children(const Desc& d, uint64_t k, F&& f) {
+  switch (d.kind) {
+    case K_SUM: return sum_children(d, k, f);
+    case K_TTT: return ttt_children(d, k, f);
+    case K_TOOT: return toot_children(d, k, f);
+    default: return oth_children(d, k, f);
+  }
+}
+GM_HD int any_level(const Desc& d, uint64_t k) {
+  switch (d.kind) {
+    case K_SUM: return sum_level(d, k);
+    case K_TTT: return ttt_level(d, k);
+    case K_TOOT: return toot_level(d, k);
+    default: return oth_level(d, k);
+  }
+}
+
+}  // namespace gm

@@ -1,0 +1,891 @@
+// gm_solver.hip -- tier-synchronous retrograde solver for gfx950 (MI355X)
+// behind the C-ABI of include/gamesman.h.
+//
+// Replaces the reference's asynchronous per-state job machinery
+// (src/process.py:37-267, src/job.py) with a level-synchronous pipeline:
+//
+//   forward, level L = 0..T-1   K1+K2  k_expand<G>: every position of level L
+//                                      is tested with primitive(); the
+//                                      non-primitive ones generate their
+//                                      children (gen_moves+do_move fused),
+//                                      which are inserted into the HBM hash
+//                                      table by 64-bit CAS; a child inserted
+//                                      for the first time is appended
+//                                      (wave-aggregated atomics) to the
+//                                      position store of level L+1 or L+2.
+//   backward, level L = T-1..0  K3     k_resolve<G>: each position of level L
+//                                      re-generates its children, probes
+//                                      their 32-bit words and reduces them
+//                                      with the reference-canonical rule of
+//                                      _res_red/_remote_red (SURVEY §8a
+//                                      A8/A9), then stores its own word.
+//
+// HBM layout (caller-allocated, gamesman.h):
+//   table  : gm_slot[2^k] {u64 key, u32 word, u32 spare}, open addressing,
+//            linear probing, EMPTY key = ~0.  Replaces the resolved/remote
+//            CacheDicts (src/cache_dict.py) -- one 16-B line per probe
+//            serves both key compare and word.
+//   levels : u64 keys of every reachable position grouped by level.  +1
+//            children grow a stack from the front, +2 children a stack from
+//            the back, so each level is at most two contiguous segments.
+//   scratch: DevState (cursors, counters, error bits, per-level segments).
+// No host synchronisation inside the level loops: segment bounds travel
+// through device memory (k_finalize), so a whole solve is enqueued at once.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/gamesman.h"
+#include "gm_codec.h"
+#include "gm_games.h"
+#include "gm_md5.h"
+
+using namespace gm;
+typedef unsigned long long u64;
+
+// ---------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------
+static thread_local std::string g_err;
+static int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+#define HIPCHK(x)                                                                   \
+  do {                                                                              \
+    hipError_t e_ = (x);                                                            \
+    if (e_ != hipSuccess) return fail(GM_EHIP, "%s: %s", #x, hipGetErrorString(e_)); \
+  } while (0)
+
+enum : uint32_t {
+  ERR_TABLE_FULL = 1u,
+  ERR_LEVELS_FULL = 2u,
+  ERR_BAD_STEP = 4u,
+  ERR_CHILD_MISSING = 8u,
+  ERR_CHILD_UNRESOLVED = 16u,
+  ERR_NO_MOVES = 32u,
+  ERR_SELF_MISSING = 64u,
+};
+
+// ---------------------------------------------------------------------------
+// game registry
+// ---------------------------------------------------------------------------
+static std::mutex g_mu;
+static std::vector<Desc> g_games;
+
+static int kv(const char* params, const char* key, int dflt) {
+  if (!params) return dflt;
+  size_t kl = strlen(key);
+  for (const char* p = params; (p = strstr(p, key)); p += kl) {
+    if ((p == params || p[-1] == ',') && p[kl] == '=') return atoi(p + kl + 1);
+  }
+  return dflt;
+}
+
+static int build_desc(const char* name, const char* params, Desc* out) {
+  Desc d;
+  memset(&d, 0, sizeof d);
+  if (!strcmp(name, "four_to_one") || !strcmp(name, "sum_four_to_one")) {
+    d.kind = K_SUM;
+    if (name[0] == 'f') {
+      d.variant = 1;
+      int start = kv(params, "start", 4);  // four_to_one.py:7-8
+      if (start < 0) return fail(GM_EINVAL, "four_to_one start must be >= 0");
+      d.nheaps = 1;
+      d.heap[0] = (uint32_t)start;
+    } else {
+      const char* p = params ? strstr(params, "heaps=") : nullptr;
+      if (!p) return fail(GM_EINVAL, "sum_four_to_one needs heaps=h0:h1:...");
+      p += 6;
+      while (*p && *p != ',') {
+        if (d.nheaps >= 16) return fail(GM_EINVAL, "at most 16 heaps");
+        long h = strtol(p, nullptr, 10);
+        if (h < 0 || h > (1L << 30)) return fail(GM_EINVAL, "bad heap %ld", h);
+        d.heap[d.nheaps++] = (uint32_t)h;
+        while (*p && *p != ':' && *p != ',') p++;
+        if (*p == ':') p++;
+      }
+      if (d.nheaps == 0) return fail(GM_EINVAL, "no heaps");
+    }
+    unsigned __int128 stride = 1;
+    d.pow2 = 1;
+    d.root = 0;
+    d.root_sum = 0;
+    for (int i = 0; i < d.nheaps; i++) {
+      d.base[i] = d.heap[i] + 1;
+      d.stride[i] = (uint64_t)stride;
+      if (d.base[i] & (d.base[i] - 1)) d.pow2 = 0;
+      int sh = 0;
+      while ((1ull << sh) < (uint64_t)stride) sh++;
+      d.shift[i] = (uint32_t)sh;
+      d.root += (uint64_t)d.heap[i] * d.stride[i];
+      d.root_sum += d.heap[i];
+      stride *= d.base[i];
+      if (stride > ((unsigned __int128)1 << 62)) return fail(GM_EINVAL, "state space exceeds 2^62");
+    }
+    if (d.root_sum >= (1u << 30)) return fail(GM_EINVAL, "remoteness would exceed 30 bits");
+    d.max_levels = (int)d.root_sum + 1;
+  } else if (!strcmp(name, "tic_tac_toe_np") || !strcmp(name, "mttt")) {
+    d.kind = K_TTT;
+    d.variant = name[0] == 'm';
+    d.root = 0;
+    d.max_levels = 10;
+  } else if (!strcmp(name, "toot_and_otto_bitstring")) {
+    d.kind = K_TOOT;
+    d.L = kv(params, "length", 6);  // toot_and_otto_bitstring.py:8
+    d.H = kv(params, "height", 4);
+    d.A = d.L * d.H;
+    if (d.L < 1 || d.H < 1 || 2 * d.A + 13 > 64)
+      return fail(GM_EINVAL, "toot board %dx%d does not fit a 64-bit key (area <= 25)", d.L, d.H);
+    d.nbits = (2 * d.A + 17 + 7) / 8 * 8;
+    d.full = (1ull << d.A) - 1;
+    // word starts per direction: (1,0) (0,1) (1,1) (1,-1); steps in cell index
+    const int dxs[4] = {1, 0, 1, 1}, dys[4] = {0, 1, 1, -1};
+    for (int i = 0; i < 4; i++) {
+      uint64_t m = 0;
+      for (int x = 0; x < d.L; x++)
+        for (int y = 0; y < d.H; y++) {
+          int ex = x + 3 * dxs[i], ey = y + 3 * dys[i];
+          if (ex >= 0 && ex < d.L && ey >= 0 && ey < d.H) m |= 1ull << (d.L * y + x);
+        }
+      d.tmask[i] = m;
+      d.tstep[i] = dxs[i] + d.L * dys[i];
+    }
+    // initial_position (:36-44): hands 6,6,6,6; turn bit 0 (player 2 first)
+    d.root = 0;
+    for (int j = 0; j < 4; j++) d.root |= 6ull << (2 * d.A + 3 * j);
+    d.max_levels = d.A + 1;
+  } else if (!strcmp(name, "othello_bit_new")) {
+    d.kind = K_OTHELLO;
+    d.L = kv(params, "length", 8);  // othello_bit_new.py:8
+    d.H = kv(params, "height", 8);
+    d.A = d.L * d.H;
+    if (d.L != d.H)
+      return fail(GM_EINVAL, "othello descriptor supports square boards only (reference flip bounds "
+                             "are transposed for non-square boards, othello_bit_new.py:101,110)");
+    if (d.L < 2 || 2 * d.A + 3 > 64)
+      return fail(GM_EINVAL, "othello board %dx%d does not fit a 64-bit key (area <= 30)", d.L, d.H);
+    d.nbits = (2 * d.A + 16 + 7) / 8 * 8;
+    d.full = (1ull << d.A) - 1;
+    // initial_position (:37-48) with the module's float coordinates
+    // (length / 2 - 1): board index int(length*y + x)
+    auto put = [&](double x, double y, int white) {
+      int idx = (int)(d.L * y + x);
+      d.root |= 1ull << (white ? idx : d.A + idx);
+    };
+    double hx = d.L / 2.0, hy = d.H / 2.0;
+    d.root = 0;
+    put(hx - 1, hy - 1, 1);
+    put(hx - 1, hy, 0);
+    put(hx, hy - 1, 0);
+    put(hx, hy, 1);
+    // two incr_turn calls from 0 -> turn_count 2 (WHITE): bit 2A = 0
+    d.max_levels = d.A + 3;
+  } else {
+    return fail(GM_EINVAL, "no device descriptor for game '%s'", name);
+  }
+  *out = d;
+  return 0;
+}
+
+static const Desc* get_game(int id) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (id < 0 || id >= (int)g_games.size()) return nullptr;
+  return &g_games[id];
+}
+
+// ---------------------------------------------------------------------------
+// device helpers
+// ---------------------------------------------------------------------------
+struct LevelSeg {
+  u64 fb, fe;      // front segment [fb, fe) of the level store
+  u64 c2lo, c2hi;  // back segment: back-stack counts [c2lo, c2hi)
+};
+struct DevState {
+  u64 cursor_front;
+  u64 cursor_back;
+  u64 edges;
+  u64 prims;
+  u64 max_width;
+  uint32_t err;
+  uint32_t root_word;
+  LevelSeg seg[1];  // [max_levels + 2]
+};
+static size_t devstate_bytes(int max_levels) {
+  return sizeof(DevState) + sizeof(LevelSeg) * (size_t)(max_levels + 2);
+}
+
+__device__ __forceinline__ u64 mix64(u64 x) {  // splitmix64 finaliser
+  x ^= x >> 31;
+  x *= 0x7fb5d329728ea185ull;
+  x ^= x >> 27;
+  x *= 0x81dadef4bc2dd44dull;
+  x ^= x >> 33;
+  return x;
+}
+
+__device__ __forceinline__ u64 lanemask_lt() {
+  return (1ull << __lane_id()) - 1ull;
+}
+
+// Wave-aggregated append: one atomic per wave per call site.
+__device__ __forceinline__ u64 wave_reserve(u64* cursor, bool pred) {
+  u64 mask = __ballot(pred);
+  if (mask == 0) return 0;
+  int leader = __ffsll((long long)mask) - 1;
+  u64 base = 0;
+  if ((int)__lane_id() == leader) base = atomicAdd(cursor, (u64)__popcll(mask));
+  base = __shfl(base, leader);
+  return base + (u64)__popcll(mask & lanemask_lt());
+}
+
+// insert key; true iff this call created the slot
+__device__ __forceinline__ bool table_insert(gm_slot* tab, u64 mask, u64 key, uint32_t* err) {
+  u64 h = mix64(key) & mask;
+  for (u64 probe = 0; probe <= mask; probe++) {
+    u64 k = __hip_atomic_load(&tab[h].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (k == key) return false;
+    if (k == EMPTY_KEY) {
+      u64 old = atomicCAS((u64*)&tab[h].key, (u64)EMPTY_KEY, key);
+      if (old == EMPTY_KEY) return true;
+      if (old == key) return false;
+    }
+    h = (h + 1) & mask;
+  }
+  atomicOr(err, ERR_TABLE_FULL);
+  return false;
+}
+
+// slot index of key, or ~0 if absent
+__device__ __forceinline__ u64 table_find(const gm_slot* tab, u64 mask, u64 key) {
+  u64 h = mix64(key) & mask;
+  for (u64 probe = 0; probe <= mask; probe++) {
+    u64 k = tab[h].key;
+    if (k == key) return h;
+    if (k == EMPTY_KEY) return ~0ull;
+    h = (h + 1) & mask;
+  }
+  return ~0ull;
+}
+
+__device__ __forceinline__ u64 level_key(const u64* lv, u64 lcap, const LevelSeg& s, u64 i) {
+  u64 nf = s.fe - s.fb;
+  return i < nf ? lv[s.fb + i] : lv[lcap - 1 - (s.c2lo + (i - nf))];
+}
+
+// block-wide sum then one atomic per block
+__device__ __forceinline__ void block_add(u64* dst, u64 v) {
+  __shared__ u64 red[16];
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  int w = threadIdx.x >> 6;
+  if (__lane_id() == 0) red[w] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u64 s = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); i++) s += red[i];
+    if (s) atomicAdd(dst, s);
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// kernels
+// ---------------------------------------------------------------------------
+__global__ void k_seed(gm_slot* tab, u64 mask, u64* lv, DevState* st, u64 root) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    table_insert(tab, mask, root, &st->err);
+    lv[0] = root;
+    st->cursor_front = 1;
+    st->cursor_back = 0;
+    st->seg[0].fb = 0;
+    st->seg[0].fe = 1;
+    st->seg[0].c2lo = 0;
+    st->seg[0].c2hi = 0;
+    st->seg[1].c2lo = 0;
+    st->seg[1].c2hi = 0;
+  }
+}
+
+// K1+K2: expand level L, insert children, append new ones to L+1 / L+2.
+// The per-thread atomicAdd on a wave-uniform cursor is combined into one
+// atomic per wave by the AMDGPU atomic optimizer (Guideline 12).
+template <int KIND>
+__global__ __launch_bounds__(256) void k_expand(Desc d, gm_slot* tab, u64 mask, u64* lv, u64 lcap,
+                                                DevState* st, int L) {
+  const LevelSeg s = st->seg[L];
+  const u64 n = (s.fe - s.fb) + (s.c2hi - s.c2lo);
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  uint32_t err = 0;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    u64 key = level_key(lv, lcap, s, i);
+    if (Game<KIND>::prim(d, key) != UNDECIDED) continue;  // lookup(): primitive, no children
+    Game<KIND>::children(d, key, [&](u64 child, int step) {
+      if (!table_insert(tab, mask, child, &st->err)) return;
+      if (step == 1) {
+        u64 f = atomicAdd(&st->cursor_front, 1ull);
+        if (f < lcap) lv[f] = child;
+      } else if (step == 2) {
+        u64 b = atomicAdd(&st->cursor_back, 1ull);
+        if (b < lcap) lv[lcap - 1 - b] = child;
+      } else {
+        err |= ERR_BAD_STEP;
+      }
+    });
+  }
+  if (err) atomicOr(&st->err, err);
+}
+
+// level bookkeeping after expanding level L (one thread)
+__global__ void k_finalize(DevState* st, int L, u64 lcap) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    LevelSeg& nx = st->seg[L + 1];
+    nx.fb = st->seg[L].fe;
+    nx.fe = st->cursor_front;
+    LevelSeg& nn = st->seg[L + 2];
+    nn.c2lo = nx.c2hi;
+    nn.c2hi = st->cursor_back;
+    if (st->cursor_front + st->cursor_back > lcap) st->err |= ERR_LEVELS_FULL;
+    u64 w = (nx.fe - nx.fb) + (nx.c2hi - nx.c2lo);
+    if (w > st->max_width) st->max_width = w;
+  }
+}
+
+// K3: resolve level L from its children's words
+template <int KIND>
+__global__ __launch_bounds__(256) void k_resolve(Desc d, gm_slot* tab, u64 mask, const u64* lv, u64 lcap,
+                                                 DevState* st, int L) {
+  const LevelSeg s = st->seg[L];
+  const u64 n = (s.fe - s.fb) + (s.c2hi - s.c2lo);
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  u64 edges = 0, prims = 0;
+  uint32_t err = 0;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    u64 key = level_key(lv, lcap, s, i);
+    int p = Game<KIND>::prim(d, key);
+    uint32_t word;
+    if (p != UNDECIDED) {
+      word = make_word(p, 0);  // process.py:120-123: primitive, remoteness 0
+      prims++;
+    } else {
+      bool any_loss = false, any_tie = false, any_draw = false;
+      uint32_t min_loss = 0xFFFFFFFFu, max_all = 0;
+      int nch = Game<KIND>::children(d, key, [&](u64 c, int) {
+        u64 h = table_find(tab, mask, c);
+        if (h == ~0ull) { err |= ERR_CHILD_MISSING; return; }
+        uint32_t w = tab[h].word;
+        if (w == NO_WORD) { err |= ERR_CHILD_UNRESOLVED; return; }
+        uint32_t v = w & 3u, r = w >> 2;
+        if (v == LOSS) { any_loss = true; min_loss = min(min_loss, r); }
+        any_tie |= (v == TIE);
+        any_draw |= (v == DRAW);
+        max_all = max(max_all, r);
+      });
+      if (nch == 0) err |= ERR_NO_MOVES;
+      edges += (u64)nch;
+      // reference-canonical _res_red / _remote_red
+      if (any_loss) word = make_word(WIN, min_loss + 1);
+      else word = make_word(any_tie ? TIE : any_draw ? DRAW : LOSS, max_all + 1);
+    }
+    u64 h = table_find(tab, mask, key);
+    if (h == ~0ull) err |= ERR_SELF_MISSING;
+    else tab[h].word = word;
+  }
+  if (err) atomicOr(&st->err, err);
+  block_add(&st->edges, edges);
+  block_add(&st->prims, prims);
+}
+
+__global__ void k_query(const gm_slot* tab, u64 mask, const u64* keys, u64 n, uint32_t* words) {
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+    u64 h = table_find(tab, mask, keys[i]);
+    words[i] = h == ~0ull ? NO_WORD : tab[h].word;
+  }
+}
+
+__global__ void k_root_word(const gm_slot* tab, u64 mask, u64 root, DevState* st) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    u64 h = table_find(tab, mask, root);
+    st->root_word = h == ~0ull ? NO_WORD : tab[h].word;
+  }
+}
+
+__global__ void k_gather_positions(const u64* lv, u64 lcap, const DevState* st, u64* out) {
+  u64 nf = st->cursor_front, nb = st->cursor_back;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < nf + nb; i += (u64)gridDim.x * blockDim.x)
+    out[i] = i < nf ? lv[i] : lv[lcap - 1 - (i - nf)];
+}
+
+__global__ void k_owner(Desc d, const u64* keys, u64 n, uint32_t P, uint32_t* owners) {
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+    uint8_t s[56], dig[16];
+    int len = str_utf8_from_key(d, keys[i], s);
+    md5_block(s, len, dig);
+    owners[i] = md5_mod(dig, P);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// solver object
+// ---------------------------------------------------------------------------
+struct gm_solver {
+  Desc d;
+  gm_slot* tab;
+  u64 mask;
+  u64* lv;
+  u64 lcap;
+  DevState* st;
+  hipStream_t stream;
+  bool own_stream;
+  uint32_t flags;
+  int grid;
+};
+
+static const int kBlock = 256;
+
+static int launch_grid() {
+  static int g = 0;
+  if (!g) {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) {
+      hipDeviceProp_t p;
+      if (hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0) cus = p.multiProcessorCount;
+    }
+    g = cus * 8;  // Guideline 11: 8 blocks/CU, grid-stride the rest
+  }
+  return g;
+}
+
+template <int KIND>
+static void enqueue_level_expand(gm_solver* s, int L) {
+  hipLaunchKernelGGL(k_expand<KIND>, dim3(s->grid), dim3(kBlock), 0, s->stream, s->d, s->tab, s->mask, s->lv,
+                     s->lcap, s->st, L);
+}
+template <int KIND>
+static void enqueue_level_resolve(gm_solver* s, int L) {
+  hipLaunchKernelGGL(k_resolve<KIND>, dim3(s->grid), dim3(kBlock), 0, s->stream, s->d, s->tab, s->mask, s->lv,
+                     s->lcap, s->st, L);
+}
+static void do_expand(gm_solver* s, int L) {
+  switch (s->d.kind) {
+    case K_SUM: enqueue_level_expand<K_SUM>(s, L); break;
+    case K_TTT: enqueue_level_expand<K_TTT>(s, L); break;
+    case K_TOOT: enqueue_level_expand<K_TOOT>(s, L); break;
+    default: enqueue_level_expand<K_OTHELLO>(s, L); break;
+  }
+}
+static void do_resolve(gm_solver* s, int L) {
+  switch (s->d.kind) {
+    case K_SUM: enqueue_level_resolve<K_SUM>(s, L); break;
+    case K_TTT: enqueue_level_resolve<K_TTT>(s, L); break;
+    case K_TOOT: enqueue_level_resolve<K_TOOT>(s, L); break;
+    default: enqueue_level_resolve<K_OTHELLO>(s, L); break;
+  }
+}
+
+static std::string err_text(uint32_t e) {
+  std::string s;
+  if (e & ERR_TABLE_FULL) s += " table-full";
+  if (e & ERR_LEVELS_FULL) s += " level-store-full";
+  if (e & ERR_BAD_STEP) s += " bad-level-step";
+  if (e & ERR_CHILD_MISSING) s += " child-missing";
+  if (e & ERR_CHILD_UNRESOLVED) s += " child-unresolved";
+  if (e & ERR_NO_MOVES) s += " non-primitive-without-moves";
+  if (e & ERR_SELF_MISSING) s += " self-missing";
+  return s;
+}
+
+// ---------------------------------------------------------------------------
+// C-ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+const char* gm_last_error(void) { return g_err.c_str(); }
+const char* gm_version(void) { return "gamesmanmpi_amd 0.1 (gfx950)"; }
+
+int gm_game_lookup(const char* name, const char* params, int* game_id) {
+  if (!name || !game_id) return fail(GM_EINVAL, "null argument");
+  Desc d;
+  int rc = build_desc(name, params ? params : "", &d);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (size_t i = 0; i < g_games.size(); i++)
+    if (!memcmp(&g_games[i], &d, sizeof d)) { *game_id = (int)i; return 0; }
+  g_games.push_back(d);
+  *game_id = (int)g_games.size() - 1;
+  return 0;
+}
+
+int gm_game_info(int game, uint64_t* positions_bound, uint32_t* max_levels, uint32_t* key_bits) {
+  const Desc* d = get_game(game);
+  if (!d) return fail(GM_EINVAL, "bad game id %d", game);
+  uint64_t bound = 0;
+  uint32_t bits = 0;
+  switch (d->kind) {
+    case K_SUM: {
+      unsigned __int128 p = 1;
+      for (int i = 0; i < d->nheaps; i++) p *= d->base[i];
+      bound = (uint64_t)p;
+      bits = 64 - __builtin_clzll(bound | 1);
+      break;
+    }
+    case K_TTT: bound = 5478; bits = 18; break;
+    case K_TOOT: {
+      // reachable counts measured by the survey (Appendix B) where known
+      if (d->L == 3 && d->H == 3) bound = 11097;
+      else if (d->L == 4 && d->H == 3) bound = 200127;
+      else if (d->L == 3 && d->H == 4) bound = 126559;
+      else if (d->L == 4 && d->H == 4) bound = 3468773;
+      else if (d->L == 5 && d->H == 4) bound = 70184763;
+      else if (d->L == 6 && d->H == 4) bound = 1187212827ull;
+      else bound = 0;  // unknown: caller must pass an estimate to gm_plan
+      bits = 2 * d->A + 13;
+      break;
+    }
+    default:
+      if (d->L == 4) bound = 54089;
+      else bound = 0;
+      bits = 2 * d->A + 3;
+  }
+  if (positions_bound) *positions_bound = bound;
+  if (max_levels) *max_levels = (uint32_t)d->max_levels;
+  if (key_bits) *key_bits = bits;
+  return 0;
+}
+
+int gm_root(int game, uint64_t* key) {
+  const Desc* d = get_game(game);
+  if (!d || !key) return fail(GM_EINVAL, "bad game id %d", game);
+  *key = d->root;
+  return 0;
+}
+
+int gm_encode(int game, const uint8_t* canon, size_t n, uint64_t* key) {
+  const Desc* d = get_game(game);
+  if (!d || !canon || !key) return fail(GM_EINVAL, "bad argument");
+  if (d->kind == K_TOOT || d->kind == K_OTHELLO) {
+    if (key_from_bits(*d, canon, (int)n, key)) return fail(GM_EINVAL, "bytes are not a %s position", d->kind == K_TOOT ? "toot" : "othello");
+    return 0;
+  }
+  if (d->kind == K_TTT) {
+    if (n != 9) return fail(GM_EINVAL, "tic-tac-toe positions are 9 bytes");
+    uint64_t k = 0;
+    for (int c = 0; c < 9; c++) {
+      uint32_t v;
+      if (d->variant == 1) {
+        if (canon[c] == '_') v = 0;
+        else if (canon[c] == 'X') v = 1;
+        else if (canon[c] == 'O') v = 2;
+        else return fail(GM_EINVAL, "mttt cell must be _ X or O");
+      } else {
+        if (canon[c] > 2) return fail(GM_EINVAL, "tic_tac_toe_np cell must be 0, 1 or 2");
+        v = canon[c];
+      }
+      k |= (uint64_t)v << (2 * c);
+    }
+    *key = k;
+    return 0;
+  }
+  if (n == 0 || n > 20) return fail(GM_EINVAL, "bad integer position");
+  unsigned __int128 v = 0;
+  for (size_t i = 0; i < n; i++) {
+    if (canon[i] < '0' || canon[i] > '9') return fail(GM_EINVAL, "integer positions are non-negative decimals");
+    v = v * 10 + (canon[i] - '0');
+  }
+  unsigned __int128 space = 1;
+  for (int i = 0; i < d->nheaps; i++) space *= d->base[i];
+  if (v >= space) return fail(GM_EINVAL, "position outside the game's state space");
+  *key = (uint64_t)v;
+  return 0;
+}
+
+int gm_decode(int game, uint64_t key, uint8_t* canon, size_t cap, size_t* n) {
+  const Desc* d = get_game(game);
+  if (!d || !canon || !n) return fail(GM_EINVAL, "bad argument");
+  uint8_t tmp[64];
+  int m = canon_from_key(*d, key, tmp);
+  if ((size_t)m > cap) return fail(GM_EINVAL, "buffer too small");
+  memcpy(canon, tmp, (size_t)m);
+  *n = (size_t)m;
+  return 0;
+}
+
+int gm_encode_batch(int game, const uint8_t* canon, size_t stride, const uint8_t* lens, size_t n,
+                    uint64_t* keys) {
+  for (size_t i = 0; i < n; i++) {
+    int rc = gm_encode(game, canon + i * stride, lens[i], &keys[i]);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+int gm_decode_batch(int game, const uint64_t* keys, size_t n, uint8_t* canon, size_t stride, uint8_t* lens) {
+  const Desc* d = get_game(game);
+  if (!d || (n && (!keys || !canon || !lens))) return fail(GM_EINVAL, "bad argument");
+  for (size_t i = 0; i < n; i++) {
+    uint8_t tmp[64];
+    int m = canon_from_key(*d, keys[i], tmp);
+    if ((size_t)m > stride) return fail(GM_EINVAL, "stride too small");
+    memset(canon + i * stride, 0, stride);
+    memcpy(canon + i * stride, tmp, (size_t)m);
+    lens[i] = (uint8_t)m;
+  }
+  return 0;
+}
+
+int gm_str_utf8(int game, uint64_t key, uint8_t* out, size_t cap, size_t* n) {
+  const Desc* d = get_game(game);
+  if (!d || !out || !n) return fail(GM_EINVAL, "bad argument");
+  uint8_t tmp[64];
+  int m = str_utf8_from_key(*d, key, tmp);
+  if ((size_t)m > cap) return fail(GM_EINVAL, "buffer too small");
+  memcpy(out, tmp, (size_t)m);
+  *n = (size_t)m;
+  return 0;
+}
+
+int gm_host_expand(int game, const uint64_t* keys, size_t n, uint64_t* children, uint8_t* nchild, uint8_t* prim) {
+  const Desc* d = get_game(game);
+  if (!d || (n && (!keys || !children || !nchild || !prim))) return fail(GM_EINVAL, "bad argument");
+  for (size_t i = 0; i < n; i++) {
+    prim[i] = (uint8_t)any_prim(*d, keys[i]);
+    int c = 0;
+    if (prim[i] == UNDECIDED)
+      any_children(*d, keys[i], [&](uint64_t ck, int) {
+        if (c < GM_MAXCHILD) children[i * GM_MAXCHILD + c] = ck;
+        c++;
+      });
+    if (c > GM_MAXCHILD) return fail(GM_ECORRUPT, "more than %d children", GM_MAXCHILD);
+    nchild[i] = (uint8_t)c;
+  }
+  return 0;
+}
+
+int gm_owner_host(int game, const uint64_t* keys, size_t n, int world_size, uint32_t* owners) {
+  const Desc* d = get_game(game);
+  if (!d || world_size < 1 || (n && (!keys || !owners))) return fail(GM_EINVAL, "bad argument");
+  for (size_t i = 0; i < n; i++) {
+    uint8_t s[64], dig[16];
+    int len = str_utf8_from_key(*d, keys[i], s);
+    md5_block(s, len, dig);
+    owners[i] = md5_mod(dig, (uint32_t)world_size);
+  }
+  return 0;
+}
+
+int gm_plan(int game, uint64_t positions, gm_plan_t* out) {
+  const Desc* d = get_game(game);
+  if (!d || !out) return fail(GM_EINVAL, "bad argument");
+  if (positions == 0) {
+    gm_game_info(game, &positions, nullptr, nullptr);
+    if (positions == 0) return fail(GM_EINVAL, "no known position bound for this board; pass an estimate");
+  }
+  uint64_t slots = 1024;
+  while (slots < 2 * positions) slots <<= 1;  // load factor <= 0.5
+  out->table_slots = slots;
+  out->level_capacity = positions + 64;
+  out->scratch_bytes = (devstate_bytes(d->max_levels) + 255) / 256 * 256;
+  out->max_levels = (uint32_t)d->max_levels;
+  out->reserved = 0;
+  return 0;
+}
+
+int gm_solver_create(int game, const gm_buffers* buf, gm_solver** out) {
+  const Desc* d = get_game(game);
+  if (!d || !buf || !out) return fail(GM_EINVAL, "bad argument");
+  if (!buf->table || !buf->levels || !buf->scratch) return fail(GM_EINVAL, "null device buffer");
+  if (buf->table_slots < 2 || (buf->table_slots & (buf->table_slots - 1)))
+    return fail(GM_EINVAL, "table_slots must be a power of two");
+  if (buf->scratch_bytes < devstate_bytes(d->max_levels)) return fail(GM_EINVAL, "scratch too small");
+  if (buf->level_capacity < 1) return fail(GM_EINVAL, "level capacity too small");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(GM_ENOGPU, "no HIP device");
+  gm_solver* s = new gm_solver();
+  s->d = *d;
+  s->tab = (gm_slot*)buf->table;
+  s->mask = buf->table_slots - 1;
+  s->lv = (u64*)buf->levels;
+  s->lcap = buf->level_capacity;
+  s->st = (DevState*)buf->scratch;
+  s->flags = buf->flags;
+  s->grid = launch_grid();
+  if (buf->stream) {
+    s->stream = (hipStream_t)buf->stream;
+    s->own_stream = false;
+  } else {
+    hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      delete s;
+      return fail(GM_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
+    }
+    s->own_stream = true;
+  }
+  *out = s;
+  return 0;
+}
+
+void gm_solver_destroy(gm_solver* s) {
+  if (!s) return;
+  if (s->own_stream) (void)hipStreamDestroy(s->stream);
+  delete s;
+}
+
+int gm_solver_solve(gm_solver* s, gm_result* out) {
+  if (!s || !out) return fail(GM_EINVAL, "bad argument");
+  memset(out, 0, sizeof *out);
+  const int T = s->d.max_levels;
+  const bool timing = s->flags & GM_F_KERNEL_TIMING;
+  std::vector<hipEvent_t> ev;
+  auto new_event = [&](hipEvent_t* e) -> int {
+    HIPCHK(hipEventCreate(e));
+    ev.push_back(*e);
+    return 0;
+  };
+  hipEvent_t e0, e1, e2;
+  if (new_event(&e0) || new_event(&e1) || new_event(&e2)) return GM_EHIP;
+  std::vector<hipEvent_t> kx, kr;  // per-launch start/stop pairs
+  if (timing) {
+    kx.resize(2 * (size_t)T);
+    kr.resize(2 * (size_t)T);
+    for (auto& e : kx)
+      if (new_event(&e)) return GM_EHIP;
+    for (auto& e : kr)
+      if (new_event(&e)) return GM_EHIP;
+  }
+  auto t0 = std::chrono::steady_clock::now();
+  HIPCHK(hipEventRecord(e0, s->stream));
+  // fresh table: keys EMPTY, words NO_WORD
+  HIPCHK(hipMemsetAsync(s->tab, 0xFF, (s->mask + 1) * sizeof(gm_slot), s->stream));
+  HIPCHK(hipMemsetAsync(s->st, 0, devstate_bytes(T), s->stream));
+  hipLaunchKernelGGL(k_seed, dim3(1), dim3(64), 0, s->stream, s->tab, s->mask, s->lv, s->st, s->d.root);
+  for (int L = 0; L + 1 < T; L++) {
+    if (timing) HIPCHK(hipEventRecord(kx[2 * L], s->stream));
+    do_expand(s, L);
+    if (timing) HIPCHK(hipEventRecord(kx[2 * L + 1], s->stream));
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s->stream, s->st, L, s->lcap);
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(e1, s->stream));
+  for (int L = T - 1; L >= 0; L--) {
+    if (timing) HIPCHK(hipEventRecord(kr[2 * L], s->stream));
+    do_resolve(s, L);
+    if (timing) HIPCHK(hipEventRecord(kr[2 * L + 1], s->stream));
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(e2, s->stream));
+  hipLaunchKernelGGL(k_root_word, dim3(1), dim3(64), 0, s->stream, s->tab, s->mask, s->d.root, s->st);
+  HIPCHK(hipGetLastError());
+  std::vector<unsigned char> host(devstate_bytes(T));
+  HIPCHK(hipMemcpyAsync(host.data(), s->st, host.size(), hipMemcpyDeviceToHost, s->stream));
+  HIPCHK(hipStreamSynchronize(s->stream));
+  auto t1 = std::chrono::steady_clock::now();
+  const DevState* hs = (const DevState*)host.data();
+  const uint32_t word = hs->root_word;
+  float f = 0, b = 0;
+  HIPCHK(hipEventElapsedTime(&f, e0, e1));
+  HIPCHK(hipEventElapsedTime(&b, e1, e2));
+  out->ms_forward = f;
+  out->ms_backward = b;
+  out->ms_total = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  if (timing) {
+    double sx = 0, sr = 0;
+    for (int L = 0; L + 1 < T; L++) {
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, kx[2 * L], kx[2 * L + 1]));
+      sx += ms;
+    }
+    for (int L = 0; L < T; L++) {
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, kr[2 * L], kr[2 * L + 1]));
+      sr += ms;
+    }
+    out->ms_expand_kernels = sx;
+    out->ms_resolve_kernels = sr;
+    out->n_expand_launches = (uint64_t)(T - 1);
+    out->n_resolve_launches = (uint64_t)T;
+  }
+  for (auto e : ev) (void)hipEventDestroy(e);
+  out->positions = hs->cursor_front + hs->cursor_back;
+  out->edges = hs->edges;
+  out->primitives = hs->prims;
+  out->max_level_width = (uint32_t)std::max<u64>(hs->max_width, 1);
+  uint32_t lv = 0;
+  for (int L = 0; L < T; L++) {
+    const LevelSeg& g = hs->seg[L];
+    if ((g.fe - g.fb) + (g.c2hi - g.c2lo) > 0) lv++;
+  }
+  out->levels = lv;
+  out->root_word = word;
+  if (hs->err) {
+    bool full = hs->err & (ERR_TABLE_FULL | ERR_LEVELS_FULL);
+    return fail(full ? GM_EFULL : GM_ECORRUPT, "solve failed:%s", err_text(hs->err).c_str());
+  }
+  if (word == NO_WORD) return fail(GM_ECORRUPT, "root unresolved");
+  out->root_value = (int32_t)(word & 3u);
+  out->root_remoteness = word >> 2;
+  return 0;
+}
+
+int gm_solver_query(gm_solver* s, const uint64_t* keys_dev, uint64_t n, uint32_t* words_dev) {
+  if (!s || (n && (!keys_dev || !words_dev))) return fail(GM_EINVAL, "bad argument");
+  if (!n) return 0;
+  int grid = (int)std::min<u64>((n + kBlock - 1) / kBlock, (u64)s->grid);
+  hipLaunchKernelGGL(k_query, dim3(grid), dim3(kBlock), 0, s->stream, s->tab, s->mask, (const u64*)keys_dev, n,
+                     words_dev);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s->stream));
+  return 0;
+}
+
+int gm_solver_positions(gm_solver* s, uint64_t* keys_dev, uint64_t cap, uint64_t* n) {
+  if (!s || !n) return fail(GM_EINVAL, "bad argument");
+  u64 cur[2];
+  HIPCHK(hipStreamSynchronize(s->stream));
+  HIPCHK(hipMemcpy(cur, s->st, sizeof cur, hipMemcpyDeviceToHost));
+  *n = cur[0] + cur[1];
+  if (*n > cap || !keys_dev) return cap < *n ? fail(GM_EFULL, "need %llu slots", (unsigned long long)*n) : 0;
+  hipLaunchKernelGGL(k_gather_positions, dim3(s->grid), dim3(kBlock), 0, s->stream, s->lv, s->lcap, s->st,
+                     (u64*)keys_dev);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s->stream));
+  return 0;
+}
+
+int gm_solve(int game, uint64_t root, int ngpus, const gm_buffers* buf, gm_result* out) {
+  const Desc* d = get_game(game);
+  if (!d) return fail(GM_EINVAL, "bad game id %d", game);
+  if (ngpus != 1) return fail(GM_EINVAL, "gm_solve drives one GPU; run one process per GPU for sharded solves");
+  if (root != d->root) return fail(GM_EINVAL, "root must be the game's initial position");
+  gm_solver* s = nullptr;
+  int rc = gm_solver_create(game, buf, &s);
+  if (rc) return rc;
+  rc = gm_solver_solve(s, out);
+  gm_solver_destroy(s);
+  return rc;
+}
+
+int gm_owner(int game, const uint64_t* keys_dev, uint64_t n, int world_size, uint32_t* owners_dev, void* stream) {
+  const Desc* d = get_game(game);
+  if (!d || world_size < 1 || (n && (!keys_dev || !owners_dev))) return fail(GM_EINVAL, "bad argument");
+  if (!n) return 0;
+  int grid = (int)std::min<u64>((n + kBlock - 1) / kBlock, (u64)launch_grid());
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_owner, dim3(grid), dim3(kBlock), 0, st, *d, (const u64*)keys_dev, n, (uint32_t)world_size,
+                     owners_dev);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(st));
+  return 0;
+}
+
+}  // extern "C"

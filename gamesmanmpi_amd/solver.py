@@ -1,0 +1,174 @@
+"""Single-GPU solve driver: allocates HBM buffers with PyTorch-ROCm, hands
+their addresses to libgamesman_hip.so and reads results back.
+
+Stands in for one rank of the reference's Process (src/process.py:10-267):
+``Solver.solve()`` is Process.run until the root is resolved, and
+``Solver.query()`` reads the table that replaces the resolved/remote
+CacheDicts (src/cache_dict.py).  No CPU fallback exists: without a gfx950
+device the library returns GM_ENOGPU and this raises.
+"""
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from .games import GameSpec
+
+NAMES = ("WIN", "LOSS", "TIE", "DRAW")
+
+
+@dataclass
+class SolveResult:
+    root_value: int
+    root_remoteness: int
+    positions: int
+    edges: int
+    primitives: int
+    levels: int
+    max_level_width: int
+    ms_total: float
+    ms_forward: float
+    ms_backward: float
+    ms_expand_kernels: float = 0.0
+    ms_resolve_kernels: float = 0.0
+    n_expand_launches: int = 0
+    n_resolve_launches: int = 0
+    extra: dict = field(default_factory=dict)
+
+    @property
+    def root_line(self):
+        """Exactly what src/process.py:47-52 prints."""
+        return "%s in %d moves" % (NAMES[self.root_value],
+                                   self.root_remoteness)
+
+
+class Solver:
+    """Owns the device buffers of one game's solve on one GPU."""
+
+    def __init__(self, spec, positions=0, device=None, kernel_timing=False):
+        import torch
+        if not torch.cuda.is_available():
+            raise RuntimeError("gamesmanmpi_amd needs a ROCm GPU (gfx950); "
+                               "no device is visible")
+        self.torch = torch
+        self.spec = spec if isinstance(spec, GameSpec) else GameSpec(*spec)
+        self.device = torch.device(device if device is not None else "cuda")
+        self.kernel_timing = kernel_timing
+        self.positions_hint = int(positions or self.spec.positions_bound)
+        self._h = None
+        self._bufs = None
+        self._alloc(self.positions_hint)
+
+    def _alloc(self, positions):
+        torch = self.torch
+        L = _lib.load()
+        self._free()
+        plan = _lib.gm_plan_t()
+        _lib.check(L.gm_plan(self.spec.id, int(positions), ctypes.byref(plan)))
+        with torch.cuda.device(self.device):
+            table = torch.empty(plan.table_slots * 16, dtype=torch.uint8,
+                                device=self.device)
+            levels = torch.empty(plan.level_capacity, dtype=torch.int64,
+                                 device=self.device)
+            scratch = torch.empty(plan.scratch_bytes, dtype=torch.uint8,
+                                  device=self.device)
+            stream = torch.cuda.current_stream(self.device)
+        self._tensors = (table, levels, scratch)
+        b = _lib.gm_buffers()
+        b.table = table.data_ptr()
+        b.table_slots = plan.table_slots
+        b.levels = levels.data_ptr()
+        b.level_capacity = plan.level_capacity
+        b.scratch = scratch.data_ptr()
+        b.scratch_bytes = plan.scratch_bytes
+        b.stream = stream.cuda_stream
+        b.flags = _lib.GM_F_KERNEL_TIMING if self.kernel_timing else 0
+        self._bufs = b
+        self.plan = plan
+        h = ctypes.c_void_p()
+        _lib.check(L.gm_solver_create(self.spec.id, ctypes.byref(b),
+                                      ctypes.byref(h)))
+        self._h = h
+
+    def _free(self):
+        if self._h is not None:
+            _lib.load().gm_solver_destroy(self._h)
+            self._h = None
+        self._tensors = None
+
+    def __del__(self):
+        try:
+            self._free()
+        except Exception:  # noqa: BLE001 -- interpreter teardown
+            pass
+
+    def solve(self, max_retries=4):
+        """Full solve from the root; grows the buffers on GM_EFULL."""
+        L = _lib.load()
+        r = _lib.gm_result()
+        for attempt in range(max_retries + 1):
+            try:
+                with self.torch.cuda.device(self.device):
+                    _lib.check(L.gm_solver_solve(self._h, ctypes.byref(r)))
+                break
+            except _lib.TableFull:
+                if attempt == max_retries:
+                    raise
+                self.positions_hint *= 2
+                self._alloc(self.positions_hint)
+        return SolveResult(
+            root_value=r.root_value, root_remoteness=r.root_remoteness,
+            positions=r.positions, edges=r.edges, primitives=r.primitives,
+            levels=r.levels, max_level_width=r.max_level_width,
+            ms_total=r.ms_total, ms_forward=r.ms_forward,
+            ms_backward=r.ms_backward,
+            ms_expand_kernels=r.ms_expand_kernels,
+            ms_resolve_kernels=r.ms_resolve_kernels,
+            n_expand_launches=r.n_expand_launches,
+            n_resolve_launches=r.n_resolve_launches)
+
+    # -- reading the table -------------------------------------------------
+    def query(self, keys):
+        """Words (value | remoteness << 2; GM_NO_WORD if unreachable) of
+        `keys` (numpy uint64 array)."""
+        torch = self.torch
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        if len(keys) == 0:
+            return np.zeros(0, np.uint32)
+        kd = torch.from_numpy(keys.view(np.int64)).to(self.device)
+        wd = torch.empty(len(keys), dtype=torch.int32, device=self.device)
+        with torch.cuda.device(self.device):
+            _lib.check(_lib.load().gm_solver_query(
+                self._h, kd.data_ptr(), len(keys), wd.data_ptr()))
+        return wd.cpu().numpy().view(np.uint32)
+
+    def positions(self):
+        """Every reachable key (numpy uint64, level order)."""
+        torch = self.torch
+        n = ctypes.c_uint64()
+        L = _lib.load()
+        rc = L.gm_solver_positions(self._h, None, 0, ctypes.byref(n))
+        if rc not in (0, _lib.GM_EFULL):
+            _lib.check(rc)
+        out = torch.empty(max(1, n.value), dtype=torch.int64,
+                          device=self.device)
+        with torch.cuda.device(self.device):
+            _lib.check(L.gm_solver_positions(self._h, out.data_ptr(),
+                                             n.value, ctypes.byref(n)))
+        return out[:n.value].cpu().numpy().view(np.uint64)
+
+    def dump(self):
+        """(keys u64, value u8, remoteness u32) for every reachable
+        position."""
+        keys = self.positions()
+        w = self.query(keys)
+        if (w == _lib.GM_NO_WORD).any():
+            raise RuntimeError("unresolved positions in the table")
+        return keys, (w & 3).astype(np.uint8), (w >> 2).astype(np.uint32)
+
+
+def solve(name, params="", positions=0, device=None):
+    """Convenience: solve game `name` (reference file stem) on one GPU."""
+    s = Solver(GameSpec(name, params), positions=positions, device=device)
+    return s.solve(), s

@@ -386,11 +386,16 @@ static int ot_children(const game *g, const blob *s, blob *out) { /* gen_moves :
 }
 static void ot_root(const game *g, blob *s) { /* initial_position :36-55 */
   memset(s, 0, sizeof *s);
-  int L = g->length, H = g->height;
-  ot_set(g, s->b, L / 2 - 1, H / 2 - 1, WHITE);
-  ot_set(g, s->b, L / 2 - 1, H / 2, BLACK);
-  ot_set(g, s->b, L / 2, H / 2 - 1, BLACK);
-  ot_set(g, s->b, L / 2, H / 2, WHITE);
+  /* the module passes float coordinates (length / 2 - 1) and board_set
+   * indexes int(length * y + x) (:42-45, :260-262) */
+  double hx = g->length / 2.0, hy = g->height / 2.0;
+  const double px[4] = {hx - 1, hx - 1, hx, hx}, py[4] = {hy - 1, hy, hy - 1, hy};
+  const int col[4] = {WHITE, BLACK, BLACK, WHITE};
+  for (int i = 0; i < 4; i++) {
+    int idx = (int)(g->length * py[i] + px[i]);
+    bset(s->b, idx, col[i] == WHITE);
+    bset(s->b, g->area + idx, col[i] == BLACK);
+  }
   ot_incr_turn(g, s->b);
   ot_incr_turn(g, s->b);
 }

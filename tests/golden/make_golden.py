@@ -405,8 +405,15 @@ def main():
             md5_samples.append((name, seen[k]))
 
     if md5_samples:
-        with open(os.path.join(outdir, "md5_owner.json"), "w") as f:
-            json.dump(md5_owner_vectors(md5_samples), f, indent=0)
+        md5_path = os.path.join(outdir, "md5_owner.json")
+        rows = []
+        if os.path.exists(md5_path):  # keep other games' rows (merge)
+            with open(md5_path) as f:
+                done = {g for g, _ in md5_samples}
+                rows = [r for r in json.load(f) if r["game"] not in done]
+        rows += md5_owner_vectors(md5_samples)
+        with open(md5_path, "w") as f:
+            json.dump(rows, f, indent=0)
     with open(summary_path, "w") as f:
         json.dump(summary, f, indent=1, sort_keys=True)
 

@@ -1,0 +1,127 @@
+"""C-ABI checks that need no GPU: the library loads, exports every symbol the
+header declares, and its HOST-side entry points (codec, the product's own
+descriptors run on the host, md5 owners) agree with the reference's golden
+vectors.  No kernel is launched here."""
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import CASES, GOLDEN, ROOT, load_table
+
+
+def header_symbols():
+    with open(os.path.join(ROOT, "include", "gamesman.h")) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w ]+?\*?\s*\b(gm_\w+)\s*\(",
+                                 text, re.M)))
+
+
+def test_header_and_exports_agree():
+    from gamesmanmpi_amd import _lib
+    syms = header_symbols()
+    assert len(syms) >= 18
+    assert sorted(_lib.EXPORTS) == syms
+    lib = _lib.load()
+    for s in syms:
+        assert getattr(lib, s) is not None
+
+
+def test_unknown_game_is_an_error():
+    from gamesmanmpi_amd import _lib
+    from gamesmanmpi_amd.games import GameSpec
+    with pytest.raises(_lib.GmError):
+        GameSpec("chess")
+    with pytest.raises(_lib.GmError):
+        GameSpec("othello_bit_new", "length=4,height=3")  # non-square refused
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_codec_roundtrip_on_golden_tables(name):
+    from gamesmanmpi_amd.games import GameSpec
+    t = load_table(name)
+    if t is None:
+        pytest.skip("sha-only fixture")
+    spec = GameSpec(*CASES[name])
+    keys = spec.encode_batch(t["canon"], t["clen"])
+    assert len(np.unique(keys)) == len(keys)
+    c, cl = spec.decode_batch(keys, stride=t["canon"].shape[1])
+    np.testing.assert_array_equal(c, t["canon"])
+    np.testing.assert_array_equal(cl, t["clen"])
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_product_descriptor_vs_reference_movegen(name):
+    """The product's descriptors (run on the host) reproduce the reference
+    modules' primitive() and ordered gen_moves/do_move children."""
+    from gamesmanmpi_amd.games import GameSpec
+    path = os.path.join(GOLDEN, "movegen", name + ".json")
+    if not os.path.exists(path):
+        pytest.skip("no vectors")
+    spec = GameSpec(*CASES[name])
+    with open(path) as f:
+        rows = json.load(f)
+    keys = np.array([spec.encode(bytes.fromhex(r["pos"])) for r in rows],
+                    np.uint64)
+    pr, nc, ch = spec.host_expand(keys)
+    for i, row in enumerate(rows):
+        assert pr[i] == row["primitive"], row["pos"]
+        got = [spec.decode(k).hex() for k in ch[i, :nc[i]]]
+        assert got == row["children"], row["pos"]
+        assert spec.str_utf8(keys[i]).hex() == row["str_utf8"], row["pos"]
+
+
+def test_root_keys_match_reference_initial_positions(golden_summary):
+    from gamesmanmpi_amd.games import GameSpec
+    for name, (stem, params) in CASES.items():
+        spec = GameSpec(stem, params)
+        root = bytes.fromhex(golden_summary[name]["root_canon_hex"])
+        assert spec.decode(spec.root_key) == root, name
+
+
+def test_md5_owner_vectors():
+    """GameState.get_hash (src/game_state.py:22-30) owners for P=1..8, as
+    computed by the reference itself."""
+    from gamesmanmpi_amd.games import GameSpec
+    with open(os.path.join(GOLDEN, "md5_owner.json")) as f:
+        rows = json.load(f)
+    specs = {n: GameSpec(*CASES[n]) for n in CASES}
+    n = 0
+    for row in rows:
+        spec = specs[row["game"]]
+        key = spec.encode(bytes.fromhex(row["canon"]))
+        assert spec.str_utf8(key).hex() == row["str_utf8"]
+        for P, owner in row["owners"].items():
+            assert spec.owners_host(np.array([key], np.uint64),
+                                    int(P))[0] == owner, (row, P)
+        n += 1
+    assert n > 100
+
+
+def test_survey_md5_golden_values():
+    """SURVEY Appendix A.5 spot values."""
+    from gamesmanmpi_amd.games import GameSpec
+    s = GameSpec("four_to_one", "start=4")
+    k = np.array([4], np.uint64)
+    assert [s.owners_host(k, P)[0] for P in (1, 2, 4, 5, 8)] == [0, 0, 0, 0, 4]
+    o = GameSpec("othello_bit_new", "length=4,height=4")
+    k = np.array([o.root_key], np.uint64)
+    assert [o.owners_host(k, P)[0] for P in (2, 4, 5, 8)] == [0, 2, 1, 6]
+    t = GameSpec("toot_and_otto_bitstring", "length=6,height=4")
+    k = np.array([t.root_key], np.uint64)
+    assert t.str_utf8(t.root_key).hex() == "0000000000006666c280"
+    assert [t.owners_host(k, P)[0] for P in (2, 4, 5, 8)] == [1, 1, 0, 5]
+
+
+def test_plan_sizes():
+    import ctypes
+    from gamesmanmpi_amd import _lib
+    from gamesmanmpi_amd.games import GameSpec
+    s = GameSpec("sum_four_to_one", "heaps=31:31:31:31:31:31")
+    assert s.positions_bound == 1 << 30
+    assert s.max_levels == 187
+    p = _lib.gm_plan_t()
+    _lib.check(_lib.load().gm_plan(s.id, 0, ctypes.byref(p)))
+    assert p.table_slots == 1 << 31 and p.level_capacity >= 1 << 30
