@@ -35,12 +35,21 @@ def heaps_for(world):
     return [63] * k + base[k:]
 
 
-def algorithmic_bytes(positions, edges):
-    """forward 24 B/position + 8 B/edge; backward 12 B/position
-    + 12 B/edge (8-B keys, 4-B value words)."""
-    fwd = 24 * positions + 8 * edges
-    bwd = 12 * positions + 12 * edges
-    return fwd, bwd
+def algorithmic_bytes(positions, edges, layout):
+    """Bytes a kernel family must move, per DESIGN.md §Roofline.
+    hashed (SURVEY §8d keyed model): forward 24 B/position + 8 B/edge,
+      backward 12 B/position + 12 B/edge (8-B keys, 4-B value words).
+    dense (level-major perfect hash, key implicit in the slot): forward
+      8 B/position (own word read + first-reach mark) + 4 B/edge (child word
+      probe); backward 8 B/position (own word read + write) + 4 B/edge."""
+    if layout == "dense":
+        return 8 * positions + 4 * edges, 8 * positions + 4 * edges
+    return 24 * positions + 8 * edges, 12 * positions + 12 * edges
+
+
+def model_8d_bytes(positions, edges):
+    """SURVEY §8d per-position figure 36 + 20*b (whole solve)."""
+    return 36 * positions + 20 * edges
 
 
 def cpu_baseline(sample_heaps="31:31:31:31:15"):
@@ -66,6 +75,7 @@ def main():
     ap.add_argument("--heaps", default=None,
                     help="override the synthetic heaps, e.g. 31:31:31:31")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--layout", default="auto", choices=["auto", "dense", "hashed"])
     args = ap.parse_args()
 
     import torch
@@ -86,7 +96,8 @@ def main():
     heaps = args.heaps.split(":") if args.heaps else heaps_for(1)
     params = "heaps=" + ":".join(str(h) for h in heaps)
     spec = GameSpec("sum_four_to_one", params)
-    solver = Solver(spec, device="cuda:%d" % local, kernel_timing=False)
+    solver = Solver(spec, device="cuda:%d" % local, kernel_timing=False,
+                    layout=args.layout)
 
     def barrier():
         torch.cuda.synchronize()
@@ -111,15 +122,20 @@ def main():
 
     # roofline of the dominant kernel: one extra timed solve with HIP events
     # around every launch (on the stream the kernels run on)
-    tsolver = Solver(spec, device="cuda:%d" % local, kernel_timing=True)
+    layout = r.extra["layout"]
+    del solver
+    tsolver = Solver(spec, device="cuda:%d" % local, kernel_timing=True,
+                     layout=args.layout)
     tr = tsolver.solve()
     del tsolver
-    fwd_b, bwd_b = algorithmic_bytes(tr.positions, tr.edges)
+    fwd_b, bwd_b = algorithmic_bytes(tr.positions, tr.edges, layout)
     if tr.ms_resolve_kernels >= tr.ms_expand_kernels:
-        kname, kb, kms, kn = ("k_resolve", bwd_b, tr.ms_resolve_kernels,
+        kname, kb, kms, kn = ("k_dense_resolve" if layout == "dense"
+                              else "k_resolve", bwd_b, tr.ms_resolve_kernels,
                               tr.n_resolve_launches)
     else:
-        kname, kb, kms, kn = ("k_expand", fwd_b, tr.ms_expand_kernels,
+        kname, kb, kms, kn = ("k_dense_forward" if layout == "dense"
+                              else "k_expand", fwd_b, tr.ms_expand_kernels,
                               tr.n_expand_launches)
     achieved = (kb / kn) / (kms / kn / 1e3) / 1e9  # GB/s
     line = {
@@ -138,6 +154,7 @@ def main():
         "config": {"workload": "sum_four_to_one heaps=%s" % ":".join(map(str, heaps)),
                    "positions_per_gpu": r.positions, "edges_per_gpu": r.edges,
                    "levels": r.levels, "root": r.root_line,
+                   "layout": layout,
                    "parallelism": "md5 shards x%d" % world if world > 1 else "1 GPU"},
         "roofline": {"bound": "hbm", "kernel": kname,
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -145,7 +162,14 @@ def main():
                      "launches": kn, "ms_kernel_total": kms,
                      "algorithmic_bytes_total": kb},
         "phase_ms": {"forward": r.ms_forward, "backward": r.ms_backward,
-                     "solve_wall": r.ms_total},
+                     "solve_wall": r.ms_total,
+                     "expand_kernels": tr.ms_expand_kernels,
+                     "resolve_kernels": tr.ms_resolve_kernels},
+        "model_8d": {"bytes_per_position": model_8d_bytes(r.positions, r.edges) / r.positions,
+                     "equiv_GBps": model_8d_bytes(r.positions, r.edges) * world
+                     * args.steps / elapsed / 1e9,
+                     "frac_of_peak": model_8d_bytes(r.positions, r.edges) * world
+                     * args.steps / elapsed / 1e9 / HBM_PEAK_GBS},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline()

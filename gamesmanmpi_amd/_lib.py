@@ -13,6 +13,8 @@ LIBPATH = os.path.join(HERE, "libgamesman_hip.so")
 
 GM_EINVAL, GM_EHIP, GM_EFULL, GM_ECORRUPT, GM_ENOGPU = -1, -2, -3, -4, -5
 GM_F_KERNEL_TIMING = 1
+GM_F_FORCE_HASHED = 2
+GM_MODE_HASHED, GM_MODE_DENSE = 0, 1
 GM_MAXCHILD = 32
 GM_NO_WORD = 0xFFFFFFFF
 
@@ -28,11 +30,12 @@ class TableFull(GmError):
 
 
 class gm_plan_t(ctypes.Structure):
-    _fields_ = [("table_slots", ctypes.c_uint64),
+    _fields_ = [("table_bytes", ctypes.c_uint64),
+                ("table_slots", ctypes.c_uint64),
                 ("level_capacity", ctypes.c_uint64),
                 ("scratch_bytes", ctypes.c_uint64),
                 ("max_levels", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint32)]
+                ("mode", ctypes.c_uint32)]
 
 
 class gm_buffers(ctypes.Structure):
@@ -44,7 +47,7 @@ class gm_buffers(ctypes.Structure):
                 ("scratch_bytes", ctypes.c_uint64),
                 ("stream", ctypes.c_void_p),
                 ("flags", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint32)]
+                ("mode", ctypes.c_uint32)]
 
 
 class gm_result(ctypes.Structure):
@@ -105,7 +108,8 @@ def load():
                         P(c.c_size_t)],
         "gm_host_expand": [c.c_int, c.c_void_p, c.c_size_t, c.c_void_p,
                            c.c_void_p, c.c_void_p],
-        "gm_plan": [c.c_int, c.c_uint64, P(gm_plan_t)],
+        "gm_plan": [c.c_int, c.c_uint64, c.c_uint32, c.c_uint64,
+                    P(gm_plan_t)],
         "gm_solver_create": [c.c_int, P(gm_buffers), P(c.c_void_p)],
         "gm_solver_solve": [c.c_void_p, P(gm_result)],
         "gm_solver_query": [c.c_void_p, c.c_void_p, c.c_uint64, c.c_void_p],

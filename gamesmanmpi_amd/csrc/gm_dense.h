@@ -1,0 +1,296 @@
+// gm_dense.h -- dense (perfect-hash) tier pipeline for rank-indexable games.
+// Included by gm_solver.hip after the shared device helpers.
+//
+// For descriptors whose positions have a computable rank (K_SUM:
+// four_to_one and the sum of Four-To-One heaps) the open-addressing table
+// degenerates to a perfect hash, laid out LEVEL-MAJOR so that every child
+// access of a wave is one contiguous stream:
+//
+//   slot(key) = level(key) * W + prefix(key)
+//     prefix = rank / base[0]        (heap digits 1..K-1)
+//     level  = root_sum - digit sum  (so heap 0 = (root_sum - level) - digitsum(prefix))
+//
+// A position at (L, p) has its children at (L+1, p) / (L+2, p) (heap 0 -1/-2)
+// and (L+d, p - d*pstride[i]) (heap i>=1, -d): for 64 consecutive prefixes
+// of one wave each child kind is 64 consecutive words.  Slots whose heap-0
+// digit would fall outside [0, heap0] are holes: never read or written.
+// Per slot: one reach bit (bitmap, written by the forward pass) and one
+// 32-bit word value | remoteness << 2 (src/utils.py:3 value codes), written
+// by the backward pass for reached slots only.  The key is implicit in the
+// slot, so the traffic is ~0.2 B per position forward and 8 B per position
+// + 4 B per edge backward instead of the 36 + 20 B of
+// the keyed table.  ABSENT (0xFFFFFFFD) is a register-only "no such child"
+// marker; W_REACHED/W_UNREACHED never appear in resolved words.
+
+constexpr uint32_t W_UNREACHED = 0xFFFFFFFFu;
+constexpr uint32_t W_REACHED = 0xFFFFFFFEu;
+
+// digit i (i >= 1) of a prefix
+__device__ __forceinline__ uint32_t pdigit(const Desc& d, u64 p, int i) {
+  if (d.pow2) return (uint32_t)((p >> d.pshift[i]) & (d.base[i] - 1));
+  return (uint32_t)((p / d.pstride[i]) % d.base[i]);
+}
+
+// prefix digits into registers.  MAXH is the compile-time heap count (exact
+// for 1..8 heaps; 16 = generic bound with runtime checks) so every loop over
+// heaps unrolls and all child/parent loads issue before the first wait
+template <int MAXH>
+__device__ __forceinline__ uint32_t prefix_digits(const Desc& d, u64 p, uint32_t (&h)[MAXH]) {
+  uint32_t s = 0;
+#pragma unroll
+  for (int i = 1; i < MAXH; i++) {
+    h[i] = ((MAXH <= 8) || i < d.nheaps) ? pdigit(d, p, i) : 0u;
+    s += h[i];
+  }
+  return s;
+}
+
+// Digits of the 64 prefixes a wave covers.  For power-of-two bases and a
+// 64-aligned wave base, digit_i(p_base | lane) = digit_i(p_base) +
+// digit_i(lane): the first term is wave-uniform (computed on the scalar
+// unit), the second a per-lane constant computed once per kernel.  For
+// other bases every lane decomposes its own prefix.
+template <int MAXH, bool POW2>
+struct WaveDigits {
+  uint32_t hl[MAXH];  // POW2: digits of the lane offset
+  uint32_t sl;
+  __device__ __forceinline__ void init(const Desc& d) {
+    const uint32_t lane = __lane_id();
+    sl = 0;
+#pragma unroll
+    for (int i = 1; i < MAXH; i++) {
+      hl[i] = (POW2 && ((MAXH <= 8) || i < d.nheaps)) ? ((lane >> d.pshift[i]) & (d.base[i] - 1)) : 0u;
+      sl += hl[i];
+    }
+  }
+  // digits of p = wave_base + lane into h, returns the digit sum
+  __device__ __forceinline__ uint32_t digits(const Desc& d, u64 wave_base, u64 p, uint32_t (&h)[MAXH]) const {
+    if (!POW2) return prefix_digits<MAXH>(d, p, h);
+    const u64 wb = __builtin_amdgcn_readfirstlane((uint32_t)wave_base) |
+                   ((u64)__builtin_amdgcn_readfirstlane((uint32_t)(wave_base >> 32)) << 32);
+    uint32_t s = sl;
+#pragma unroll
+    for (int i = 1; i < MAXH; i++) {
+      uint32_t hb = ((MAXH <= 8) || i < d.nheaps) ? (uint32_t)((wb >> d.pshift[i]) & (d.base[i] - 1)) : 0u;
+      h[i] = hb + hl[i];
+      s += hb;
+    }
+    return s;
+  }
+};
+
+__device__ __forceinline__ uint32_t prefix_digit_sum(const Desc& d, u64 p) {
+  uint32_t s = 0;
+  for (int i = 1; i < d.nheaps; i++) s += pdigit(d, p, i);
+  return s;
+}
+
+__device__ __forceinline__ void slot_split(const Desc& d, u64 slot, u64* L, u64* p) {
+  if (d.wshift >= 0) {
+    *L = slot >> d.wshift;
+    *p = slot & (d.W - 1);
+  } else {
+    *L = slot / d.W;
+    *p = slot - *L * d.W;
+  }
+}
+
+// heap-0 digit of (L, p), or -1 for a hole
+__device__ __forceinline__ int64_t dense_h0(const Desc& d, u64 L, u64 p) {
+  int64_t h0 = (int64_t)d.root_sum - (int64_t)L - (int64_t)prefix_digit_sum(d, p);
+  return (h0 >= 0 && h0 <= (int64_t)d.heap[0]) ? h0 : -1;
+}
+
+__device__ __forceinline__ bool dense_slot_of(const Desc& d, u64 key, u64* slot) {
+  u64 rest = key, p = key / d.base[0];
+  uint32_t s = 0;
+  for (int i = 0; i < d.nheaps; i++) {
+    u64 q = rest / d.base[i];
+    s += (uint32_t)(rest - q * d.base[i]);
+    rest = q;
+  }
+  if (rest != 0 || s > d.root_sum) return false;  // outside the state space
+  *slot = (u64)(d.root_sum - s) * d.W + p;
+  return true;
+}
+
+// Reach marks live in a bitmap beside the words: level L's bit for prefix p
+// is bit (L * Wb + p), Wb = W rounded up to 64, so every 64-prefix group of
+// one level owns one 64-bit word (written whole by one lane after a ballot).
+__device__ __forceinline__ bool reach_bit(const u64* bits, u64 pos) {
+  return (bits[pos >> 6] >> (pos & 63)) & 1ull;
+}
+
+// Forward, PULL form, target level L: each non-hole slot of level L ORs the
+// reach bits of its parents -- the positions one move away, i.e. one heap +1
+// (level L-1) or +2 (level L-2), the undo-moves of four_to_one.py:10-17 --
+// and the wave writes its 64 bits at once.  Every bitmap word of a level is
+// written by exactly one lane: no initialisation, no races.
+// Grid-stride rounds each wave keeps in flight.  Measured on MI355X
+// (2^30-position solve): 1/1 -> 92 ms, pull 4 / resolve 2 -> 111 ms (the
+// extra registers cost occupancy: resolve 104 VGPRs, 4 waves/SIMD), so the
+// loads of one round per wave are what the memory system sees.
+constexpr int PULL_UNROLL = 1;
+constexpr int RESOLVE_UNROLL = 1;
+
+template <int MAXH, bool POW2>
+__global__ __launch_bounds__(256) void k_dense_pull(Desc d, u64* bits, u64 Wb, u64 L, u64 root_p) {
+  const u64 W = d.W;
+  const uint32_t S = d.root_sum - (uint32_t)L;
+  const u64 b0 = L * Wb, b1 = (L - 1) * Wb, b2 = (L - 2) * Wb;  // b1/b2 used only when L >= 1/2
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  const u64 n = (W + 63) & ~63ull;  // whole waves: every lane reaches the ballot
+  WaveDigits<MAXH, POW2> wd;
+  wd.init(d);
+  for (u64 p0 = (u64)blockIdx.x * blockDim.x + threadIdx.x; p0 < n; p0 += PULL_UNROLL * stride) {
+    bool par[PULL_UNROLL][2 * MAXH];
+    bool root_here[PULL_UNROLL];
+#pragma unroll
+    for (int u = 0; u < PULL_UNROLL; u++) {
+      const u64 p = p0 + u * stride;
+      root_here[u] = false;
+#pragma unroll
+      for (int j = 0; j < 2 * MAXH; j++) par[u][j] = false;
+      if (p >= W) continue;
+      uint32_t h[MAXH];
+      uint32_t s = wd.digits(d, p & ~63ull, p, h);
+      if (s > S || S - s > d.heap[0]) continue;  // hole
+      if (L == 0) {
+        root_here[u] = p == root_p;  // level 0 holds only the root
+        continue;
+      }
+      const uint32_t h0 = S - s;
+      par[u][0] = h0 + 1 <= d.heap[0] && reach_bit(bits, b1 + p);
+      par[u][1] = L >= 2 && h0 + 2 <= d.heap[0] && reach_bit(bits, b2 + p);
+#pragma unroll
+      for (int i = 1; i < MAXH; i++) {
+        const bool live = (MAXH <= 8) || i < d.nheaps;  // exact heap count when MAXH <= 8
+        par[u][2 * i] = live && h[i] + 1 <= d.heap[i] && reach_bit(bits, b1 + p + d.pstride[i]);
+        par[u][2 * i + 1] = live && L >= 2 && h[i] + 2 <= d.heap[i] && reach_bit(bits, b2 + p + 2 * d.pstride[i]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < PULL_UNROLL; u++) {
+      const u64 p = p0 + u * stride;
+      if (p >= n) break;  // wave-uniform: n and stride are multiples of 64
+      bool reached = root_here[u];
+#pragma unroll
+      for (int j = 0; j < 2 * MAXH; j++) reached |= par[u][j];
+      u64 m = __ballot(reached);
+      if (__lane_id() == 0) bits[(b0 + (p & ~63ull)) >> 6] = m;
+    }
+  }
+}
+
+// backward, level L: resolve every reached position from its children
+template <int MAXH, bool POW2>
+__global__ __launch_bounds__(256) void k_dense_resolve(Desc d, uint32_t* words, const u64* bits, u64 Wb, u64 L,
+                                                       DevState* st) {
+  const u64 W = d.W;
+  const uint32_t S = d.root_sum - (uint32_t)L;
+  uint32_t* mine = words + L * W;
+  const uint32_t* n1 = words + (L + 1) * W;  // only dereferenced when S >= 1
+  const uint32_t* n2 = words + (L + 2) * W;  // only dereferenced when S >= 2
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  constexpr uint32_t ABSENT = 0xFFFFFFFDu;  // "no such child" (register only)
+  constexpr uint32_t SKIP = 0xFFFFFFFCu;    // slot not resolved this round
+  u64 npos = 0, edges = 0, prims = 0;
+  uint32_t err = 0;
+  WaveDigits<MAXH, POW2> wd;
+  wd.init(d);
+  for (u64 p0 = (u64)blockIdx.x * blockDim.x + threadIdx.x; p0 < W; p0 += RESOLVE_UNROLL * stride) {
+    // gather the child words of RESOLVE_UNROLL rounds first (loads in flight together)
+    uint32_t c[RESOLVE_UNROLL][2 * MAXH];
+    uint32_t own[RESOLVE_UNROLL];
+#pragma unroll
+    for (int u = 0; u < RESOLVE_UNROLL; u++) {
+      const u64 p = p0 + u * stride;
+      own[u] = SKIP;
+#pragma unroll
+      for (int j = 0; j < 2 * MAXH; j++) c[u][j] = ABSENT;
+      if (p >= W) continue;
+      uint32_t h[MAXH];
+      uint32_t s = wd.digits(d, p & ~63ull, p, h);
+      if (s > S || S - s > d.heap[0]) continue;
+      if (!reach_bit(bits, L * Wb + p)) continue;
+      own[u] = 0;
+      if (S == 0) continue;  // the primitive: no children
+      const uint32_t h0 = S - s;
+      c[u][0] = h0 >= 1 ? n1[p] : ABSENT;
+      c[u][1] = h0 >= 2 ? n2[p] : ABSENT;
+#pragma unroll
+      for (int i = 1; i < MAXH; i++) {
+        const bool live = (MAXH <= 8) || i < d.nheaps;  // exact heap count when MAXH <= 8
+        c[u][2 * i] = (live && h[i] >= 1) ? n1[p - d.pstride[i]] : ABSENT;
+        c[u][2 * i + 1] = (live && h[i] >= 2) ? n2[p - 2 * d.pstride[i]] : ABSENT;
+      }
+    }
+    // ... then reduce: reference-canonical _res_red / _remote_red
+#pragma unroll
+    for (int u = 0; u < RESOLVE_UNROLL; u++) {
+      if (own[u] == SKIP) continue;
+      const u64 p = p0 + u * stride;
+      npos++;
+      uint32_t word;
+      if (S == 0) {  // all heaps empty: four_to_one.py:19-22 LOSS, remoteness 0
+        word = make_word(LOSS, 0);
+        prims++;
+      } else {
+        bool any_loss = false, any_tie = false, any_draw = false;
+        uint32_t min_loss = 0xFFFFFFFFu, max_all = 0;
+        int nch = 0;
+#pragma unroll
+        for (int j = 0; j < 2 * MAXH; j++) {
+          uint32_t w = c[u][j];
+          if (w == ABSENT) continue;
+          nch++;
+          if (w >= W_REACHED) { err |= ERR_CHILD_UNRESOLVED; continue; }
+          uint32_t v = w & 3u, r = w >> 2;
+          if (v == LOSS) { any_loss = true; min_loss = min(min_loss, r); }
+          any_tie |= (v == TIE);
+          any_draw |= (v == DRAW);
+          max_all = max(max_all, r);
+        }
+        edges += (u64)nch;
+        if (any_loss) word = make_word(WIN, min_loss + 1);
+        else word = make_word(any_tie ? TIE : any_draw ? DRAW : LOSS, max_all + 1);
+      }
+      mine[p] = word;
+    }
+  }
+  if (err) atomicOr(&st->err, err);
+  block_add(&st->cursor_front, npos);  // positions resolved
+  block_add(&st->edges, edges);
+  block_add(&st->prims, prims);
+}
+
+__global__ void k_dense_root(const Desc d, const uint32_t* words, const u64* bits, u64 root_p, DevState* st) {
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    st->root_word = reach_bit(bits, root_p) ? words[root_p] : NO_WORD;
+}
+
+__global__ void k_dense_query(Desc d, const uint32_t* words, const u64* bits, u64 Wb, const u64* keys, u64 n,
+                              uint32_t* out) {
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+    u64 slot, L, p;
+    uint32_t w = NO_WORD;
+    if (dense_slot_of(d, keys[i], &slot)) {
+      slot_split(d, slot, &L, &p);
+      if (reach_bit(bits, L * Wb + p)) w = words[slot];
+    }
+    out[i] = w;
+  }
+}
+
+// every reachable position -> its key (order arbitrary)
+__global__ void k_dense_positions(Desc d, const uint32_t* words, const u64* bits, u64 Wb, u64 nslots, u64* out,
+                                  u64 cap, u64* count) {
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < nslots; i += (u64)gridDim.x * blockDim.x) {
+    u64 L, p;
+    slot_split(d, i, &L, &p);
+    int64_t h0 = dense_h0(d, L, p);
+    if (h0 < 0 || !reach_bit(bits, L * Wb + p)) continue;
+    u64 k = atomicAdd(count, 1ull);
+    if (k < cap) out[k] = p * d.base[0] + (u64)h0;
+  }
+}

@@ -69,6 +69,14 @@ struct Desc {
   uint64_t full;   // all-cells mask
   uint64_t root;   // root key
   int max_levels;  // levels the pipeline must provision (root level = 0)
+  // K_SUM dense (perfect-hash) layout: slot = level * W + prefix, where
+  // prefix = rank / base[0] (heap digits 1..K-1) and heap 0 is recovered
+  // from the level: h0 = (root_sum - level) - digitsum(prefix).
+  int dense_ok;
+  int wshift;      // log2(W) when W is a power of two, else -1
+  uint64_t W;      // prefixes per level = prod_{i>=1} base[i]
+  uint64_t pstride[16];  // stride of heap digit i inside the prefix (i >= 1)
+  uint32_t pshift[16];   // log2(pstride[i]) when pow2
 };
 
 GM_HD int popc64(uint64_t v) {

@@ -85,6 +85,15 @@ enum : uint32_t {
 static std::mutex g_mu;
 static std::vector<Desc> g_games;
 
+// DENSE table = levels * W 32-bit words, then (256-B aligned) the reach
+// bitmap of levels * roundup(W, 64) bits
+static u64 dense_bitmap_offset(const Desc* d) {
+  return ((u64)d->max_levels * d->W * 4 + 255) & ~255ull;
+}
+static u64 dense_bitmap_bytes(const Desc* d) {
+  return (u64)d->max_levels * ((d->W + 63) & ~63ull) / 8;
+}
+
 static int kv(const char* params, const char* key, int dflt) {
   if (!params) return dflt;
   size_t kl = strlen(key);
@@ -135,8 +144,24 @@ static int build_desc(const char* name, const char* params, Desc* out) {
       stride *= d.base[i];
       if (stride > ((unsigned __int128)1 << 62)) return fail(GM_EINVAL, "state space exceeds 2^62");
     }
-    if (d.root_sum >= (1u << 30)) return fail(GM_EINVAL, "remoteness would exceed 30 bits");
+    if (d.root_sum >= (1u << 30) - 2) return fail(GM_EINVAL, "remoteness would exceed 30 bits");
     d.max_levels = (int)d.root_sum + 1;
+    // dense layout (see gm_dense.h)
+    d.W = 1;
+    for (int i = 1; i < d.nheaps; i++) {
+      d.pstride[i] = d.W;
+      int sh = 0;
+      while ((1ull << sh) < d.W) sh++;
+      d.pshift[i] = (uint32_t)sh;
+      d.W *= d.base[i];
+    }
+    d.wshift = -1;
+    if ((d.W & (d.W - 1)) == 0) {
+      int sh = 0;
+      while ((1ull << sh) < d.W) sh++;
+      d.wshift = sh;
+    }
+    d.dense_ok = 1;
   } else if (!strcmp(name, "tic_tac_toe_np") || !strcmp(name, "mttt")) {
     d.kind = K_TTT;
     d.variant = name[0] == 'm';
@@ -436,11 +461,18 @@ __global__ void k_owner(Desc d, const u64* keys, u64 n, uint32_t P, uint32_t* ow
   }
 }
 
+#include "gm_dense.h"
+
 // ---------------------------------------------------------------------------
 // solver object
 // ---------------------------------------------------------------------------
 struct gm_solver {
   Desc d;
+  uint32_t mode;
+  uint32_t* words;  // DENSE table: levels * W words ...
+  u64* bits;        // ... followed by the reach bitmap (levels * wb bits)
+  u64 wb;           // bitmap stride per level (W rounded up to 64)
+  u64 nslots;       // DENSE: levels * W
   gm_slot* tab;
   u64 mask;
   u64* lv;
@@ -492,6 +524,54 @@ static void do_resolve(gm_solver* s, int L) {
     case K_TOOT: enqueue_level_resolve<K_TOOT>(s, L); break;
     default: enqueue_level_resolve<K_OTHELLO>(s, L); break;
   }
+}
+
+template <int MAXH, bool POW2>
+static void dense_launch_pull_t(gm_solver* s, int grid, u64 L, u64 root_p) {
+  hipLaunchKernelGGL((k_dense_pull<MAXH, POW2>), dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->bits, s->wb, L,
+                     root_p);
+}
+template <int MAXH, bool POW2>
+static void dense_launch_resolve_t(gm_solver* s, int grid, u64 L) {
+  hipLaunchKernelGGL((k_dense_resolve<MAXH, POW2>), dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->words, s->bits,
+                     s->wb, L, s->st);
+}
+// kernels are instantiated per exact heap count 1..8 (16 = generic)
+template <bool POW2>
+static void dense_launch_pull_p(gm_solver* s, int grid, u64 L, u64 root_p) {
+  switch (s->d.nheaps) {
+    case 1: dense_launch_pull_t<1, POW2>(s, grid, L, root_p); break;
+    case 2: dense_launch_pull_t<2, POW2>(s, grid, L, root_p); break;
+    case 3: dense_launch_pull_t<3, POW2>(s, grid, L, root_p); break;
+    case 4: dense_launch_pull_t<4, POW2>(s, grid, L, root_p); break;
+    case 5: dense_launch_pull_t<5, POW2>(s, grid, L, root_p); break;
+    case 6: dense_launch_pull_t<6, POW2>(s, grid, L, root_p); break;
+    case 7: dense_launch_pull_t<7, POW2>(s, grid, L, root_p); break;
+    case 8: dense_launch_pull_t<8, POW2>(s, grid, L, root_p); break;
+    default: dense_launch_pull_t<16, POW2>(s, grid, L, root_p); break;
+  }
+}
+template <bool POW2>
+static void dense_launch_resolve_p(gm_solver* s, int grid, u64 L) {
+  switch (s->d.nheaps) {
+    case 1: dense_launch_resolve_t<1, POW2>(s, grid, L); break;
+    case 2: dense_launch_resolve_t<2, POW2>(s, grid, L); break;
+    case 3: dense_launch_resolve_t<3, POW2>(s, grid, L); break;
+    case 4: dense_launch_resolve_t<4, POW2>(s, grid, L); break;
+    case 5: dense_launch_resolve_t<5, POW2>(s, grid, L); break;
+    case 6: dense_launch_resolve_t<6, POW2>(s, grid, L); break;
+    case 7: dense_launch_resolve_t<7, POW2>(s, grid, L); break;
+    case 8: dense_launch_resolve_t<8, POW2>(s, grid, L); break;
+    default: dense_launch_resolve_t<16, POW2>(s, grid, L); break;
+  }
+}
+static void dense_launch_pull(gm_solver* s, int grid, u64 L, u64 root_p) {
+  if (s->d.pow2) dense_launch_pull_p<true>(s, grid, L, root_p);
+  else dense_launch_pull_p<false>(s, grid, L, root_p);
+}
+static void dense_launch_resolve(gm_solver* s, int grid, u64 L) {
+  if (s->d.pow2) dense_launch_resolve_p<true>(s, grid, L);
+  else dense_launch_resolve_p<false>(s, grid, L);
 }
 
 static std::string err_text(uint32_t e) {
@@ -684,35 +764,60 @@ int gm_owner_host(int game, const uint64_t* keys, size_t n, int world_size, uint
   return 0;
 }
 
-int gm_plan(int game, uint64_t positions, gm_plan_t* out) {
+int gm_plan(int game, uint64_t positions, uint32_t flags, uint64_t max_table_bytes, gm_plan_t* out) {
   const Desc* d = get_game(game);
   if (!d || !out) return fail(GM_EINVAL, "bad argument");
+  memset(out, 0, sizeof *out);
+  out->max_levels = (uint32_t)d->max_levels;
+  out->scratch_bytes = (devstate_bytes(d->max_levels) + 255) / 256 * 256;
+  if (d->dense_ok && !(flags & GM_F_FORCE_HASHED)) {
+    unsigned __int128 words = (unsigned __int128)d->max_levels * d->W;
+    unsigned __int128 bytes = (unsigned __int128)dense_bitmap_offset(d) + dense_bitmap_bytes(d);
+    if (max_table_bytes == 0 || bytes <= max_table_bytes) {
+      out->mode = GM_MODE_DENSE;
+      out->table_slots = (uint64_t)words;
+      out->table_bytes = (uint64_t)bytes;
+      out->level_capacity = 1;
+      return 0;
+    }
+  }
   if (positions == 0) {
     gm_game_info(game, &positions, nullptr, nullptr);
     if (positions == 0) return fail(GM_EINVAL, "no known position bound for this board; pass an estimate");
   }
   uint64_t slots = 1024;
   while (slots < 2 * positions) slots <<= 1;  // load factor <= 0.5
+  out->mode = GM_MODE_HASHED;
   out->table_slots = slots;
+  out->table_bytes = slots * sizeof(gm_slot);
   out->level_capacity = positions + 64;
-  out->scratch_bytes = (devstate_bytes(d->max_levels) + 255) / 256 * 256;
-  out->max_levels = (uint32_t)d->max_levels;
-  out->reserved = 0;
   return 0;
 }
 
 int gm_solver_create(int game, const gm_buffers* buf, gm_solver** out) {
   const Desc* d = get_game(game);
   if (!d || !buf || !out) return fail(GM_EINVAL, "bad argument");
-  if (!buf->table || !buf->levels || !buf->scratch) return fail(GM_EINVAL, "null device buffer");
-  if (buf->table_slots < 2 || (buf->table_slots & (buf->table_slots - 1)))
-    return fail(GM_EINVAL, "table_slots must be a power of two");
+  if (!buf->table || !buf->scratch) return fail(GM_EINVAL, "null device buffer");
   if (buf->scratch_bytes < devstate_bytes(d->max_levels)) return fail(GM_EINVAL, "scratch too small");
-  if (buf->level_capacity < 1) return fail(GM_EINVAL, "level capacity too small");
+  if (buf->mode == GM_MODE_DENSE) {
+    if (!d->dense_ok) return fail(GM_EINVAL, "game has no dense layout");
+    if (buf->table_slots != (u64)d->max_levels * d->W) return fail(GM_EINVAL, "dense table must hold levels * W words");
+  } else if (buf->mode == GM_MODE_HASHED) {
+    if (!buf->levels || buf->level_capacity < 1) return fail(GM_EINVAL, "null level store");
+    if (buf->table_slots < 2 || (buf->table_slots & (buf->table_slots - 1)))
+      return fail(GM_EINVAL, "table_slots must be a power of two");
+  } else {
+    return fail(GM_EINVAL, "unknown mode %u", buf->mode);
+  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(GM_ENOGPU, "no HIP device");
   gm_solver* s = new gm_solver();
   s->d = *d;
+  s->mode = buf->mode;
+  s->words = (uint32_t*)buf->table;
+  s->nslots = buf->table_slots;
+  s->wb = (d->W + 63) & ~63ull;
+  s->bits = (u64*)((char*)buf->table + dense_bitmap_offset(d));
   s->tab = (gm_slot*)buf->table;
   s->mask = buf->table_slots - 1;
   s->lv = (u64*)buf->levels;
@@ -741,9 +846,12 @@ void gm_solver_destroy(gm_solver* s) {
   delete s;
 }
 
+static int solve_dense(gm_solver* s, gm_result* out);
+
 int gm_solver_solve(gm_solver* s, gm_result* out) {
   if (!s || !out) return fail(GM_EINVAL, "bad argument");
   memset(out, 0, sizeof *out);
+  if (s->mode == GM_MODE_DENSE) return solve_dense(s, out);
   const int T = s->d.max_levels;
   const bool timing = s->flags & GM_F_KERNEL_TIMING;
   std::vector<hipEvent_t> ev;
@@ -837,12 +945,101 @@ int gm_solver_solve(gm_solver* s, gm_result* out) {
   return 0;
 }
 
+static int solve_dense(gm_solver* s, gm_result* out) {
+  const Desc& d = s->d;
+  const int T = d.max_levels;
+  const bool timing = s->flags & GM_F_KERNEL_TIMING;
+  std::vector<hipEvent_t> ev;
+  auto new_event = [&](hipEvent_t* e) -> int {
+    HIPCHK(hipEventCreate(e));
+    ev.push_back(*e);
+    return 0;
+  };
+  hipEvent_t e0, e1, e2;
+  if (new_event(&e0) || new_event(&e1) || new_event(&e2)) return GM_EHIP;
+  std::vector<hipEvent_t> kx, kr;
+  if (timing) {
+    kx.resize(2 * (size_t)T);
+    kr.resize(2 * (size_t)T);
+    for (auto& e : kx)
+      if (new_event(&e)) return GM_EHIP;
+    for (auto& e : kr)
+      if (new_event(&e)) return GM_EHIP;
+  }
+  const u64 root_slot = d.root / d.base[0];  // level 0, prefix of the root
+  // grid for per-level sweeps over W prefixes
+  const int lgrid = (int)std::min<u64>((d.W + kBlock - 1) / kBlock, (u64)s->grid);
+  auto t0 = std::chrono::steady_clock::now();
+  HIPCHK(hipEventRecord(e0, s->stream));
+  HIPCHK(hipMemsetAsync(s->st, 0, devstate_bytes(T), s->stream));
+  // forward (pull): level 0 .. T-1, each level's slab written exactly once
+  for (int L = 0; L < T; L++) {
+    if (timing) HIPCHK(hipEventRecord(kx[2 * L], s->stream));
+    dense_launch_pull(s, lgrid, (u64)L, root_slot);
+    if (timing) HIPCHK(hipEventRecord(kx[2 * L + 1], s->stream));
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(e1, s->stream));
+  for (int L = T - 1; L >= 0; L--) {
+    if (timing) HIPCHK(hipEventRecord(kr[2 * L], s->stream));
+    dense_launch_resolve(s, lgrid, (u64)L);
+    if (timing) HIPCHK(hipEventRecord(kr[2 * L + 1], s->stream));
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(e2, s->stream));
+  hipLaunchKernelGGL(k_dense_root, dim3(1), dim3(64), 0, s->stream, d, s->words, s->bits, root_slot, s->st);
+  std::vector<unsigned char> host(devstate_bytes(T));
+  HIPCHK(hipMemcpyAsync(host.data(), s->st, host.size(), hipMemcpyDeviceToHost, s->stream));
+  HIPCHK(hipStreamSynchronize(s->stream));
+  auto t1 = std::chrono::steady_clock::now();
+  const DevState* hs = (const DevState*)host.data();
+  float f = 0, b = 0;
+  HIPCHK(hipEventElapsedTime(&f, e0, e1));
+  HIPCHK(hipEventElapsedTime(&b, e1, e2));
+  out->ms_forward = f;
+  out->ms_backward = b;
+  out->ms_total = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  if (timing) {
+    double sx = 0, sr = 0;
+    for (int L = 0; L < T; L++) {
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, kx[2 * L], kx[2 * L + 1]));
+      sx += ms;
+    }
+    for (int L = 0; L < T; L++) {
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, kr[2 * L], kr[2 * L + 1]));
+      sr += ms;
+    }
+    out->ms_expand_kernels = sx;
+    out->ms_resolve_kernels = sr;
+    out->n_expand_launches = (uint64_t)T;
+    out->n_resolve_launches = (uint64_t)T;
+  }
+  for (auto e : ev) (void)hipEventDestroy(e);
+  out->positions = hs->cursor_front;
+  out->edges = hs->edges;
+  out->primitives = hs->prims;
+  out->levels = (uint32_t)T;
+  out->max_level_width = 0;
+  out->root_word = hs->root_word;
+  if (hs->err) return fail(GM_ECORRUPT, "solve failed:%s", err_text(hs->err).c_str());
+  if (hs->root_word == NO_WORD) return fail(GM_ECORRUPT, "root unresolved");
+  out->root_value = (int32_t)(hs->root_word & 3u);
+  out->root_remoteness = hs->root_word >> 2;
+  return 0;
+}
+
 int gm_solver_query(gm_solver* s, const uint64_t* keys_dev, uint64_t n, uint32_t* words_dev) {
   if (!s || (n && (!keys_dev || !words_dev))) return fail(GM_EINVAL, "bad argument");
   if (!n) return 0;
   int grid = (int)std::min<u64>((n + kBlock - 1) / kBlock, (u64)s->grid);
-  hipLaunchKernelGGL(k_query, dim3(grid), dim3(kBlock), 0, s->stream, s->tab, s->mask, (const u64*)keys_dev, n,
-                     words_dev);
+  if (s->mode == GM_MODE_DENSE)
+    hipLaunchKernelGGL(k_dense_query, dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->words, s->bits, s->wb,
+                       (const u64*)keys_dev, n, words_dev);
+  else
+    hipLaunchKernelGGL(k_query, dim3(grid), dim3(kBlock), 0, s->stream, s->tab, s->mask, (const u64*)keys_dev, n,
+                       words_dev);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(s->stream));
   return 0;
@@ -853,7 +1050,16 @@ int gm_solver_positions(gm_solver* s, uint64_t* keys_dev, uint64_t cap, uint64_t
   u64 cur[2];
   HIPCHK(hipStreamSynchronize(s->stream));
   HIPCHK(hipMemcpy(cur, s->st, sizeof cur, hipMemcpyDeviceToHost));
-  *n = cur[0] + cur[1];
+  *n = s->mode == GM_MODE_DENSE ? cur[0] : cur[0] + cur[1];
+  if (s->mode == GM_MODE_DENSE) {
+    if (*n > cap || !keys_dev) return cap < *n ? fail(GM_EFULL, "need %llu slots", (unsigned long long)*n) : 0;
+    HIPCHK(hipMemsetAsync(&s->st->cursor_back, 0, sizeof(u64), s->stream));
+    hipLaunchKernelGGL(k_dense_positions, dim3(s->grid), dim3(kBlock), 0, s->stream, s->d, s->words, s->bits, s->wb,
+                       s->nslots, (u64*)keys_dev, cap, &s->st->cursor_back);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return 0;
+  }
   if (*n > cap || !keys_dev) return cap < *n ? fail(GM_EFULL, "need %llu slots", (unsigned long long)*n) : 0;
   hipLaunchKernelGGL(k_gather_positions, dim3(s->grid), dim3(kBlock), 0, s->stream, s->lv, s->lcap, s->st,
                      (u64*)keys_dev);

@@ -46,7 +46,10 @@ class SolveResult:
 class Solver:
     """Owns the device buffers of one game's solve on one GPU."""
 
-    def __init__(self, spec, positions=0, device=None, kernel_timing=False):
+    def __init__(self, spec, positions=0, device=None, kernel_timing=False,
+                 layout="auto", max_table_bytes=0):
+        """layout: "auto" (dense when the descriptor supports it and the
+        table fits max_table_bytes, else hashed), "dense" or "hashed"."""
         import torch
         if not torch.cuda.is_available():
             raise RuntimeError("gamesmanmpi_amd needs a ROCm GPU (gfx950); "
@@ -55,6 +58,10 @@ class Solver:
         self.spec = spec if isinstance(spec, GameSpec) else GameSpec(*spec)
         self.device = torch.device(device if device is not None else "cuda")
         self.kernel_timing = kernel_timing
+        if layout not in ("auto", "dense", "hashed"):
+            raise ValueError("layout must be auto, dense or hashed")
+        self.layout = layout
+        self.max_table_bytes = int(max_table_bytes)
         self.positions_hint = int(positions or self.spec.positions_bound)
         self._h = None
         self._bufs = None
@@ -65,12 +72,17 @@ class Solver:
         L = _lib.load()
         self._free()
         plan = _lib.gm_plan_t()
-        _lib.check(L.gm_plan(self.spec.id, int(positions), ctypes.byref(plan)))
+        flags = _lib.GM_F_FORCE_HASHED if self.layout == "hashed" else 0
+        _lib.check(L.gm_plan(self.spec.id, int(positions), flags,
+                             self.max_table_bytes, ctypes.byref(plan)))
+        if self.layout == "dense" and plan.mode != _lib.GM_MODE_DENSE:
+            raise ValueError("%r has no dense layout (or it does not fit)"
+                             % (self.spec,))
         with torch.cuda.device(self.device):
-            table = torch.empty(plan.table_slots * 16, dtype=torch.uint8,
+            table = torch.empty(plan.table_bytes, dtype=torch.uint8,
                                 device=self.device)
-            levels = torch.empty(plan.level_capacity, dtype=torch.int64,
-                                 device=self.device)
+            levels = torch.empty(max(1, plan.level_capacity),
+                                 dtype=torch.int64, device=self.device)
             scratch = torch.empty(plan.scratch_bytes, dtype=torch.uint8,
                                   device=self.device)
             stream = torch.cuda.current_stream(self.device)
@@ -84,6 +96,7 @@ class Solver:
         b.scratch_bytes = plan.scratch_bytes
         b.stream = stream.cuda_stream
         b.flags = _lib.GM_F_KERNEL_TIMING if self.kernel_timing else 0
+        b.mode = plan.mode
         self._bufs = b
         self.plan = plan
         h = ctypes.c_void_p()
@@ -126,7 +139,10 @@ class Solver:
             ms_expand_kernels=r.ms_expand_kernels,
             ms_resolve_kernels=r.ms_resolve_kernels,
             n_expand_launches=r.n_expand_launches,
-            n_resolve_launches=r.n_resolve_launches)
+            n_resolve_launches=r.n_resolve_launches,
+            extra={"layout": "dense" if self.plan.mode == _lib.GM_MODE_DENSE
+                   else "hashed",
+                   "table_bytes": self.plan.table_bytes})
 
     # -- reading the table -------------------------------------------------
     def query(self, keys):

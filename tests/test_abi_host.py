@@ -123,5 +123,18 @@ def test_plan_sizes():
     assert s.positions_bound == 1 << 30
     assert s.max_levels == 187
     p = _lib.gm_plan_t()
-    _lib.check(_lib.load().gm_plan(s.id, 0, ctypes.byref(p)))
+    _lib.check(_lib.load().gm_plan(s.id, 0, _lib.GM_F_FORCE_HASHED, 0,
+                                   ctypes.byref(p)))
+    assert p.mode == _lib.GM_MODE_HASHED
     assert p.table_slots == 1 << 31 and p.level_capacity >= 1 << 30
+    assert p.table_bytes == 16 << 31
+    _lib.check(_lib.load().gm_plan(s.id, 0, 0, 0, ctypes.byref(p)))
+    assert p.mode == _lib.GM_MODE_DENSE
+    assert p.table_slots == 187 * 32 ** 5
+    assert p.table_bytes == 4 * 187 * 32 ** 5 + 187 * 32 ** 5 // 8  # words + reach bitmap
+    # a byte budget below the dense table falls back to the keyed table
+    _lib.check(_lib.load().gm_plan(s.id, 0, 0, 1 << 30, ctypes.byref(p)))
+    assert p.mode == _lib.GM_MODE_HASHED
+    t = GameSpec("toot_and_otto_bitstring", "length=4,height=4")
+    _lib.check(_lib.load().gm_plan(t.id, 0, 0, 0, ctypes.byref(p)))
+    assert p.mode == _lib.GM_MODE_HASHED

@@ -11,19 +11,26 @@ from conftest import CASES, load_table
 pytestmark = pytest.mark.gpu
 
 
-def _solve(stem, params, positions=0):
+def _solve(stem, params, positions=0, layout="auto"):
     from gamesmanmpi_amd.games import GameSpec
     from gamesmanmpi_amd.solver import Solver
     spec = GameSpec(stem, params)
-    s = Solver(spec, positions=positions)
+    s = Solver(spec, positions=positions, layout=layout)
     return spec, s, s.solve()
 
 
-@pytest.mark.parametrize("name", sorted(CASES))
-def test_gpu_solve_matches_golden(name, golden_summary):
+DENSE_GAMES = ("four_to_one", "sum_four_to_one")
+GOLDEN_RUNS = [(n, "hashed") for n in sorted(CASES)] + [
+    (n, "dense") for n in sorted(CASES) if CASES[n][0] in DENSE_GAMES]
+
+
+@pytest.mark.parametrize("name,layout", GOLDEN_RUNS)
+def test_gpu_solve_matches_golden(name, layout, golden_summary):
     info = golden_summary[name]
     stem, params = CASES[name]
-    spec, s, r = _solve(stem, params, positions=info["positions"])
+    spec, s, r = _solve(stem, params, positions=info["positions"],
+                        layout=layout)
+    assert r.extra["layout"] == layout
     assert r.positions == info["positions"]
     assert r.edges == info["edges"]
     assert r.primitives == info["primitives"]
@@ -47,10 +54,11 @@ def test_gpu_solve_matches_golden(name, golden_summary):
     np.testing.assert_array_equal(rem, t["remoteness"])
 
 
-def test_gpu_matches_oracle_sum_game():
+@pytest.mark.parametrize("layout", ["hashed", "dense"])
+def test_gpu_matches_oracle_sum_game(layout):
     """Mid-size synthetic (65,536 positions, 61 levels) vs the oracle."""
     from oracle.oracle import Game
-    spec, s, r = _solve("sum_four_to_one", "heaps=15:15:15:15")
+    spec, s, r = _solve("sum_four_to_one", "heaps=15:15:15:15", layout=layout)
     sol = Game("sum_four_to_one", "heaps=15:15:15:15").solve(1 << 17)
     assert (r.positions, r.edges) == (sol.count, sol.edges)
     assert r.root_line == sol.root_line
@@ -59,9 +67,10 @@ def test_gpu_matches_oracle_sum_game():
         assert sol.lookup(str(k).encode()) == (v, m), k
 
 
-def test_gpu_fto_chain_closed_form():
+@pytest.mark.parametrize("layout", ["hashed", "dense"])
+def test_gpu_fto_chain_closed_form(layout):
     """Four-To-One chain at N=3000: 3001 levels deep."""
-    spec, s, r = _solve("four_to_one", "start=3000")
+    spec, s, r = _solve("four_to_one", "start=3000", layout=layout)
     keys, val, rem = s.dump()
     x = keys.astype(np.int64)
     np.testing.assert_array_equal(val, np.where(x % 3 == 0, 1, 0))
@@ -81,9 +90,11 @@ def _sprague_grundy_check(keys, val, heaps):
     np.testing.assert_array_equal(val, np.where(g == 0, 1, 0).astype(np.uint8))
 
 
-def test_gpu_sum_game_sprague_grundy_1m():
+@pytest.mark.parametrize("layout", ["hashed", "dense"])
+def test_gpu_sum_game_sprague_grundy_1m(layout):
     heaps = (15, 15, 15, 15, 15)  # 1,048,576 positions
-    spec, s, r = _solve("sum_four_to_one", "heaps=" + ":".join(map(str, heaps)))
+    spec, s, r = _solve("sum_four_to_one", "heaps=" + ":".join(map(str, heaps)),
+                        layout=layout)
     assert r.positions == 16 ** 5
     keys, val, rem = s.dump()
     _sprague_grundy_check(keys, val, heaps)
@@ -112,3 +123,32 @@ def test_gpu_md5_owner_kernel():
                                             P, od.data_ptr(), None))
             got = od.cpu().numpy().tolist()
             assert got == [r["owners"][str(P)] for r in rs], (game, P)
+
+
+def test_gpu_dense_and_hashed_agree_nonpow2():
+    """Non-power-of-two heaps exercise the division paths of both layouts:
+    every word identical."""
+    _, a, ra = _solve("sum_four_to_one", "heaps=6:9:4:11", layout="dense")
+    _, b, rb = _solve("sum_four_to_one", "heaps=6:9:4:11", layout="hashed")
+    assert (ra.positions, ra.edges, ra.root_line) == (rb.positions, rb.edges, rb.root_line)
+    ka, va, ma = a.dump()
+    kb, vb, mb = b.dump()
+    oa, ob = np.argsort(ka), np.argsort(kb)
+    np.testing.assert_array_equal(ka[oa], kb[ob])
+    np.testing.assert_array_equal(va[oa], vb[ob])
+    np.testing.assert_array_equal(ma[oa], mb[ob])
+
+
+def test_gpu_full_size_synthetic_properties():
+    """BASELINE config 4 at full size (2^30 positions, dense): root line,
+    counts, and the Sprague-Grundy value rule on a 2^20 random sample."""
+    heaps = (31,) * 6
+    spec, s, r = _solve("sum_four_to_one", "heaps=" + ":".join(map(str, heaps)),
+                        layout="dense")
+    assert r.positions == 1 << 30
+    assert r.edges == 12280922112
+    assert r.root_line == "LOSS in 126 moves"  # XOR of 31%3=1 six times = 0
+    rng = np.random.default_rng(0)
+    keys = rng.integers(0, 1 << 30, size=1 << 20, dtype=np.uint64)
+    w = s.query(keys)
+    _sprague_grundy_check(keys, (w & 3).astype(np.uint8), heaps)
