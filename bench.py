@@ -6,7 +6,10 @@ A "step" is one complete strong solve from the root: table reset, forward
 expansion of every level, retrograde pass of every level, root word back on
 the host.  N=1 workload: heaps 31^6 = 2^30 = 1,073,741,824 positions,
 187 levels, 12,280,922,112 edges.  For N>1 (one process per GPU, launched by
-torch.distributed.run) every rank solves... see DESIGN.md §Multi-GPU.
+torch.distributed.run) the heaps are 31^5 x (32N-1): 2^30 positions per GPU,
+the ranks split the last heap's values and exchange two boundary slices per
+level over RCCL.  Every step's counts and root value
+are checked against closed forms; a wrong solve aborts the run.
 
 Prints ONE JSON line (rank 0).  Fields beyond the driver contract:
   roofline      dominant kernel's algorithmic bytes (SURVEY §8d model) per
@@ -27,23 +30,41 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
 
 
 def heaps_for(world):
-    """Weak scaling: 2^30 positions per GPU.  N=1: 31^6."""
-    base = [31] * 6
-    k = {1: 0, 2: 1, 4: 2, 8: 3}.get(world)
-    if k is None:
+    """Weak scaling, 2^30 positions per GPU: heaps 31^5 x (32N - 1).  N=1 is
+    SURVEY §8d's 31^6 (2^30 positions, 187 levels, b = 11.4375).  The last
+    heap is the one the ranks split (32 of its values each)."""
+    if world not in (1, 2, 4, 8):
         raise SystemExit("--gpus must be 1, 2, 4 or 8")
-    return [63] * k + base[k:]
+    return [31] * 5 + [32 * world - 1]
+
+
+def expected(heaps):
+    """Closed forms the solve must reproduce: positions = prod(h+1);
+    edges = sum_i P*(2h_i - 1)/(h_i + 1) (a heap h >= 2 has moves -1,-2, a
+    heap of 1 only -1); root value by Sprague-Grundy: each heap is the
+    subtraction game {1,2} with Grundy value h mod 3, so the root is a LOSS
+    iff the XOR of (h_i mod 3) is 0."""
+    P = 1
+    for h in heaps:
+        P *= h + 1
+    E = sum(P * (2 * h - 1) // (h + 1) for h in heaps if h >= 1)
+    g = 0
+    for h in heaps:
+        g ^= h % 3
+    return P, E, ("LOSS" if g == 0 else "WIN")
 
 
 def algorithmic_bytes(positions, edges, layout):
-    """Bytes a kernel family must move, per DESIGN.md §Roofline.
-    hashed (SURVEY §8d keyed model): forward 24 B/position + 8 B/edge,
-      backward 12 B/position + 12 B/edge (8-B keys, 4-B value words).
-    dense (level-major perfect hash, key implicit in the slot): forward
-      8 B/position (own word read + first-reach mark) + 4 B/edge (child word
-      probe); backward 8 B/position (own word read + write) + 4 B/edge."""
+    """Bytes each kernel family must move, per DESIGN.md §Roofline.
+    hashed (SURVEY §8d keyed model): expand 24 B/position + 8 B/edge,
+      resolve 12 B/position + 12 B/edge (8-B keys, 4-B value words).
+    dense (level-major perfect hash, key implicit in the slot):
+      pull: one reach bit per parent link + one written bit per position
+            = (edges + positions) / 8 B (parent links = edges);
+      resolve: own reach bit + 4-B word written per position, one 4-B child
+            word per edge = 4.125 B/position + 4 B/edge."""
     if layout == "dense":
-        return 8 * positions + 4 * edges, 8 * positions + 4 * edges
+        return (edges + positions) / 8.0, 4.125 * positions + 4 * edges
     return 24 * positions + 8 * edges, 12 * positions + 12 * edges
 
 
@@ -93,11 +114,14 @@ def main():
     from gamesmanmpi_amd.games import GameSpec
     from gamesmanmpi_amd.solver import Solver
 
-    heaps = args.heaps.split(":") if args.heaps else heaps_for(1)
+    heaps = [int(h) for h in args.heaps.split(":")] if args.heaps else heaps_for(world)
     params = "heaps=" + ":".join(str(h) for h in heaps)
     spec = GameSpec("sum_four_to_one", params)
-    solver = Solver(spec, device="cuda:%d" % local, kernel_timing=False,
-                    layout=args.layout)
+    if world > 1:
+        from gamesmanmpi_amd.dist import ShardedSolver
+        solver = ShardedSolver(spec, rank, world, device="cuda:%d" % local)
+    else:
+        solver = Solver(spec, device="cuda:%d" % local, layout=args.layout)
 
     def barrier():
         torch.cuda.synchronize()
@@ -118,23 +142,31 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     r = results[-1]
-    positions_total = r.positions * world
-
-    # roofline of the dominant kernel: one extra timed solve with HIP events
-    # around every launch (on the stream the kernels run on)
     layout = r.extra["layout"]
-    del solver
-    tsolver = Solver(spec, device="cuda:%d" % local, kernel_timing=True,
-                     layout=args.layout)
-    tr = tsolver.solve()
-    del tsolver
-    fwd_b, bwd_b = algorithmic_bytes(tr.positions, tr.edges, layout)
+    # whole-job position count: sharded results are already summed over ranks
+    positions_total = r.positions if world > 1 else r.positions
+    P, E, root_value = expected(heaps)
+    for x in results:
+        if (x.positions, x.edges) != (P, E) or x.root_line.split()[0] != root_value:
+            raise SystemExit("WRONG RESULT: %d positions, %d edges, %s; expected %d, %d, %s"
+                             % (x.positions, x.edges, x.root_line, P, E, root_value))
+
+    # roofline of the dominant kernel: one extra solve with HIP events
+    # around every launch, on the stream the kernels run on
+    solver.set_kernel_timing(True)
+    tr = solver.solve()
+    solver.set_kernel_timing(False)
+    if world > 1:
+        tr_pos, tr_edges = tr.positions // world, tr.edges // world  # per GPU
+    else:
+        tr_pos, tr_edges = tr.positions, tr.edges
+    fwd_b, bwd_b = algorithmic_bytes(tr_pos, tr_edges, layout)
     if tr.ms_resolve_kernels >= tr.ms_expand_kernels:
         kname, kb, kms, kn = ("k_dense_resolve" if layout == "dense"
                               else "k_resolve", bwd_b, tr.ms_resolve_kernels,
                               tr.n_resolve_launches)
     else:
-        kname, kb, kms, kn = ("k_dense_forward" if layout == "dense"
+        kname, kb, kms, kn = ("k_dense_pull" if layout == "dense"
                               else "k_expand", fwd_b, tr.ms_expand_kernels,
                               tr.n_expand_launches)
     achieved = (kb / kn) / (kms / kn / 1e3) / 1e9  # GB/s
@@ -152,10 +184,11 @@ def main():
         "dtype": "u64 keys / u32 words (integer)",
         "data": "synthetic: sum of Four-To-One heaps, fully determined state space",
         "config": {"workload": "sum_four_to_one heaps=%s" % ":".join(map(str, heaps)),
-                   "positions_per_gpu": r.positions, "edges_per_gpu": r.edges,
+                   "positions_per_gpu": r.positions // world, "edges_per_gpu": r.edges // world,
                    "levels": r.levels, "root": r.root_line,
                    "layout": layout,
-                   "parallelism": "md5 shards x%d" % world if world > 1 else "1 GPU"},
+                   "parallelism": ("top-heap blocks x%d, RCCL halo exchange" % world
+                                   if world > 1 else "1 GPU")},
         "roofline": {"bound": "hbm", "kernel": kname,
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
@@ -166,9 +199,9 @@ def main():
                      "expand_kernels": tr.ms_expand_kernels,
                      "resolve_kernels": tr.ms_resolve_kernels},
         "model_8d": {"bytes_per_position": model_8d_bytes(r.positions, r.edges) / r.positions,
-                     "equiv_GBps": model_8d_bytes(r.positions, r.edges) * world
+                     "equiv_GBps_per_gpu": model_8d_bytes(r.positions, r.edges) / world
                      * args.steps / elapsed / 1e9,
-                     "frac_of_peak": model_8d_bytes(r.positions, r.edges) * world
+                     "frac_of_peak": model_8d_bytes(r.positions, r.edges) / world
                      * args.steps / elapsed / 1e9 / HBM_PEAK_GBS},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

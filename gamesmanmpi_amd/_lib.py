@@ -16,6 +16,7 @@ GM_F_KERNEL_TIMING = 1
 GM_F_FORCE_HASHED = 2
 GM_MODE_HASHED, GM_MODE_DENSE = 0, 1
 GM_MAXCHILD = 32
+GM_COMM_ID_BYTES = 128
 GM_NO_WORD = 0xFFFFFFFF
 
 
@@ -74,6 +75,9 @@ EXPORTS = (
     "gm_encode_batch", "gm_decode_batch", "gm_str_utf8", "gm_host_expand", "gm_plan", "gm_solver_create",
     "gm_solver_solve", "gm_solver_query", "gm_solver_positions",
     "gm_solver_destroy", "gm_solve", "gm_owner", "gm_owner_host",
+    "gm_plan_shard", "gm_solver_create_shard", "gm_comm_unique_id",
+    "gm_solver_comm_init", "gm_solve_group", "gm_solver_set_flags",
+    "gm_shard_info",
     "gm_last_error", "gm_version",
 )
 
@@ -121,6 +125,15 @@ def load():
                      c.c_void_p],
         "gm_owner_host": [c.c_int, c.c_void_p, c.c_size_t, c.c_int,
                           c.c_void_p],
+        "gm_plan_shard": [c.c_int, c.c_int, c.c_int, c.c_uint32, c.c_uint64,
+                          P(gm_plan_t)],
+        "gm_solver_create_shard": [c.c_int, c.c_int, c.c_int, P(gm_buffers),
+                                   P(c.c_void_p)],
+        "gm_comm_unique_id": [c.c_void_p],
+        "gm_solver_comm_init": [c.c_void_p, c.c_void_p],
+        "gm_solve_group": [c.POINTER(c.c_void_p), c.c_int, P(gm_result)],
+        "gm_solver_set_flags": [c.c_void_p, c.c_uint32],
+        "gm_shard_info": [c.c_int, c.c_int, c.c_int, P(c.c_uint64)],
     }
     for name, args in sig.items():
         f = getattr(L, name)

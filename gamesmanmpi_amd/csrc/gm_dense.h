@@ -114,18 +114,13 @@ __device__ __forceinline__ bool dense_slot_of(const Desc& d, u64 key, u64* slot)
   return true;
 }
 
-// Reach marks live in a bitmap beside the words: level L's bit for prefix p
-// is bit (L * Wb + p), Wb = W rounded up to 64, so every 64-prefix group of
-// one level owns one 64-bit word (written whole by one lane after a ballot).
+// Reach marks live in a bitmap beside the words: level L's bit for local
+// prefix q is bit (L * Wbl + q), so every 64-prefix group of one level owns
+// one 64-bit word (written whole by one lane after a ballot).
 __device__ __forceinline__ bool reach_bit(const u64* bits, u64 pos) {
   return (bits[pos >> 6] >> (pos & 63)) & 1ull;
 }
 
-// Forward, PULL form, target level L: each non-hole slot of level L ORs the
-// reach bits of its parents -- the positions one move away, i.e. one heap +1
-// (level L-1) or +2 (level L-2), the undo-moves of four_to_one.py:10-17 --
-// and the wave writes its 64 bits at once.  Every bitmap word of a level is
-// written by exactly one lane: no initialisation, no races.
 // Grid-stride rounds each wave keeps in flight.  Measured on MI355X
 // (2^30-position solve): 1/1 -> 92 ms, pull 4 / resolve 2 -> 111 ms (the
 // extra registers cost occupancy: resolve 104 VGPRs, 4 waves/SIMD), so the
@@ -133,25 +128,32 @@ __device__ __forceinline__ bool reach_bit(const u64* bits, u64 pos) {
 constexpr int PULL_UNROLL = 1;
 constexpr int RESOLVE_UNROLL = 1;
 
+// Forward, PULL form, target level L: each non-hole slot of level L ORs the
+// reach bits of its parents -- the positions one move away, i.e. one heap +1
+// (level L-1) or +2 (level L-2), the undo-moves of four_to_one.py:10-17 --
+// and the wave writes its 64 bits at once.  Every bitmap word of a level is
+// written by exactly one lane: no initialisation, no races.
 template <int MAXH, bool POW2>
-__global__ __launch_bounds__(256) void k_dense_pull(Desc d, u64* bits, u64 Wb, u64 L, u64 root_p) {
-  const u64 W = d.W;
+__global__ __launch_bounds__(256) void k_dense_pull(Desc d, DenseView v, u64* bits, u64 L, u64 root_p) {
   const uint32_t S = d.root_sum - (uint32_t)L;
-  const u64 b0 = L * Wb, b1 = (L - 1) * Wb, b2 = (L - 2) * Wb;  // b1/b2 used only when L >= 1/2
+  const u64 b0 = L * v.Wbl, b1 = (L - 1) * v.Wbl, b2 = (L - 2) * v.Wbl;  // b1/b2 used only when L >= 1/2
   const u64 stride = (u64)gridDim.x * blockDim.x;
-  const u64 n = (W + 63) & ~63ull;  // whole waves: every lane reaches the ballot
+  // whole waves over [p_lo, p_hi rounded up to 64): every lane reaches the
+  // ballot (p_lo and base_off are multiples of 64)
+  const u64 n = (v.p_hi - v.p_lo + 63) & ~63ull;
   WaveDigits<MAXH, POW2> wd;
   wd.init(d);
-  for (u64 p0 = (u64)blockIdx.x * blockDim.x + threadIdx.x; p0 < n; p0 += PULL_UNROLL * stride) {
+  for (u64 i0 = (u64)blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += PULL_UNROLL * stride) {
     bool par[PULL_UNROLL][2 * MAXH];
     bool root_here[PULL_UNROLL];
 #pragma unroll
     for (int u = 0; u < PULL_UNROLL; u++) {
-      const u64 p = p0 + u * stride;
+      const u64 p = v.p_lo + i0 + u * stride;  // global prefix
+      const u64 q = p - v.base_off;            // local prefix
       root_here[u] = false;
 #pragma unroll
       for (int j = 0; j < 2 * MAXH; j++) par[u][j] = false;
-      if (p >= W) continue;
+      if (p >= v.p_hi) continue;
       uint32_t h[MAXH];
       uint32_t s = wd.digits(d, p & ~63ull, p, h);
       if (s > S || S - s > d.heap[0]) continue;  // hole
@@ -160,37 +162,37 @@ __global__ __launch_bounds__(256) void k_dense_pull(Desc d, u64* bits, u64 Wb, u
         continue;
       }
       const uint32_t h0 = S - s;
-      par[u][0] = h0 + 1 <= d.heap[0] && reach_bit(bits, b1 + p);
-      par[u][1] = L >= 2 && h0 + 2 <= d.heap[0] && reach_bit(bits, b2 + p);
+      par[u][0] = h0 + 1 <= d.heap[0] && reach_bit(bits, b1 + q);
+      par[u][1] = L >= 2 && h0 + 2 <= d.heap[0] && reach_bit(bits, b2 + q);
 #pragma unroll
       for (int i = 1; i < MAXH; i++) {
         const bool live = (MAXH <= 8) || i < d.nheaps;  // exact heap count when MAXH <= 8
-        par[u][2 * i] = live && h[i] + 1 <= d.heap[i] && reach_bit(bits, b1 + p + d.pstride[i]);
-        par[u][2 * i + 1] = live && L >= 2 && h[i] + 2 <= d.heap[i] && reach_bit(bits, b2 + p + 2 * d.pstride[i]);
+        par[u][2 * i] = live && h[i] + 1 <= d.heap[i] && reach_bit(bits, b1 + q + d.pstride[i]);
+        par[u][2 * i + 1] = live && L >= 2 && h[i] + 2 <= d.heap[i] && reach_bit(bits, b2 + q + 2 * d.pstride[i]);
       }
     }
 #pragma unroll
     for (int u = 0; u < PULL_UNROLL; u++) {
-      const u64 p = p0 + u * stride;
-      if (p >= n) break;  // wave-uniform: n and stride are multiples of 64
+      const u64 i = i0 + u * stride;
+      if (i >= n) break;  // wave-uniform: n and stride are multiples of 64
       bool reached = root_here[u];
 #pragma unroll
       for (int j = 0; j < 2 * MAXH; j++) reached |= par[u][j];
       u64 m = __ballot(reached);
-      if (__lane_id() == 0) bits[(b0 + (p & ~63ull)) >> 6] = m;
+      const u64 q = v.p_lo + i - v.base_off;
+      if (__lane_id() == 0) bits[(b0 + (q & ~63ull)) >> 6] = m;
     }
   }
 }
 
-// backward, level L: resolve every reached position from its children
+// backward, level L: resolve every reached owned position from its children
 template <int MAXH, bool POW2>
-__global__ __launch_bounds__(256) void k_dense_resolve(Desc d, uint32_t* words, const u64* bits, u64 Wb, u64 L,
+__global__ __launch_bounds__(256) void k_dense_resolve(Desc d, DenseView v, uint32_t* words, const u64* bits, u64 L,
                                                        DevState* st) {
-  const u64 W = d.W;
   const uint32_t S = d.root_sum - (uint32_t)L;
-  uint32_t* mine = words + L * W;
-  const uint32_t* n1 = words + (L + 1) * W;  // only dereferenced when S >= 1
-  const uint32_t* n2 = words + (L + 2) * W;  // only dereferenced when S >= 2
+  uint32_t* mine = words + L * v.Wl;
+  const uint32_t* n1 = words + (L + 1) * v.Wl;  // only dereferenced when S >= 1
+  const uint32_t* n2 = words + (L + 2) * v.Wl;  // only dereferenced when S >= 2
   const u64 stride = (u64)gridDim.x * blockDim.x;
   constexpr uint32_t ABSENT = 0xFFFFFFFDu;  // "no such child" (register only)
   constexpr uint32_t SKIP = 0xFFFFFFFCu;    // slot not resolved this round
@@ -198,38 +200,40 @@ __global__ __launch_bounds__(256) void k_dense_resolve(Desc d, uint32_t* words, 
   uint32_t err = 0;
   WaveDigits<MAXH, POW2> wd;
   wd.init(d);
-  for (u64 p0 = (u64)blockIdx.x * blockDim.x + threadIdx.x; p0 < W; p0 += RESOLVE_UNROLL * stride) {
-    // gather the child words of RESOLVE_UNROLL rounds first (loads in flight together)
+  const u64 n = v.p_hi - v.p_lo;
+  for (u64 i0 = (u64)blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += RESOLVE_UNROLL * stride) {
+    // gather the child words of RESOLVE_UNROLL rounds first
     uint32_t c[RESOLVE_UNROLL][2 * MAXH];
     uint32_t own[RESOLVE_UNROLL];
 #pragma unroll
     for (int u = 0; u < RESOLVE_UNROLL; u++) {
-      const u64 p = p0 + u * stride;
+      const u64 p = v.p_lo + i0 + u * stride;
+      const u64 q = p - v.base_off;
       own[u] = SKIP;
 #pragma unroll
       for (int j = 0; j < 2 * MAXH; j++) c[u][j] = ABSENT;
-      if (p >= W) continue;
+      if (p >= v.p_hi) continue;
       uint32_t h[MAXH];
       uint32_t s = wd.digits(d, p & ~63ull, p, h);
       if (s > S || S - s > d.heap[0]) continue;
-      if (!reach_bit(bits, L * Wb + p)) continue;
+      if (!reach_bit(bits, L * v.Wbl + q)) continue;
       own[u] = 0;
       if (S == 0) continue;  // the primitive: no children
       const uint32_t h0 = S - s;
-      c[u][0] = h0 >= 1 ? n1[p] : ABSENT;
-      c[u][1] = h0 >= 2 ? n2[p] : ABSENT;
+      c[u][0] = h0 >= 1 ? n1[q] : ABSENT;
+      c[u][1] = h0 >= 2 ? n2[q] : ABSENT;
 #pragma unroll
       for (int i = 1; i < MAXH; i++) {
-        const bool live = (MAXH <= 8) || i < d.nheaps;  // exact heap count when MAXH <= 8
-        c[u][2 * i] = (live && h[i] >= 1) ? n1[p - d.pstride[i]] : ABSENT;
-        c[u][2 * i + 1] = (live && h[i] >= 2) ? n2[p - 2 * d.pstride[i]] : ABSENT;
+        const bool live = (MAXH <= 8) || i < d.nheaps;
+        c[u][2 * i] = (live && h[i] >= 1) ? n1[q - d.pstride[i]] : ABSENT;
+        c[u][2 * i + 1] = (live && h[i] >= 2) ? n2[q - 2 * d.pstride[i]] : ABSENT;
       }
     }
     // ... then reduce: reference-canonical _res_red / _remote_red
 #pragma unroll
     for (int u = 0; u < RESOLVE_UNROLL; u++) {
       if (own[u] == SKIP) continue;
-      const u64 p = p0 + u * stride;
+      const u64 q = v.p_lo + i0 + u * stride - v.base_off;
       npos++;
       uint32_t word;
       if (S == 0) {  // all heaps empty: four_to_one.py:19-22 LOSS, remoteness 0
@@ -245,17 +249,17 @@ __global__ __launch_bounds__(256) void k_dense_resolve(Desc d, uint32_t* words, 
           if (w == ABSENT) continue;
           nch++;
           if (w >= W_REACHED) { err |= ERR_CHILD_UNRESOLVED; continue; }
-          uint32_t v = w & 3u, r = w >> 2;
-          if (v == LOSS) { any_loss = true; min_loss = min(min_loss, r); }
-          any_tie |= (v == TIE);
-          any_draw |= (v == DRAW);
+          uint32_t val = w & 3u, r = w >> 2;
+          if (val == LOSS) { any_loss = true; min_loss = min(min_loss, r); }
+          any_tie |= (val == TIE);
+          any_draw |= (val == DRAW);
           max_all = max(max_all, r);
         }
         edges += (u64)nch;
         if (any_loss) word = make_word(WIN, min_loss + 1);
         else word = make_word(any_tie ? TIE : any_draw ? DRAW : LOSS, max_all + 1);
       }
-      mine[p] = word;
+      mine[q] = word;
     }
   }
   if (err) atomicOr(&st->err, err);
@@ -264,32 +268,42 @@ __global__ __launch_bounds__(256) void k_dense_resolve(Desc d, uint32_t* words, 
   block_add(&st->prims, prims);
 }
 
-__global__ void k_dense_root(const Desc d, const uint32_t* words, const u64* bits, u64 root_p, DevState* st) {
-  if (blockIdx.x == 0 && threadIdx.x == 0)
-    st->root_word = reach_bit(bits, root_p) ? words[root_p] : NO_WORD;
+// root word (on the shard that owns the root; others report NO_WORD)
+__global__ void k_dense_root(DenseView v, const uint32_t* words, const u64* bits, u64 root_p, DevState* st) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    uint32_t w = NO_WORD;
+    if (root_p >= v.p_lo && root_p < v.p_hi) {
+      const u64 q = root_p - v.base_off;  // level 0
+      if (reach_bit(bits, q)) w = words[q];
+    }
+    st->root_word = w;
+  }
 }
 
-__global__ void k_dense_query(Desc d, const uint32_t* words, const u64* bits, u64 Wb, const u64* keys, u64 n,
+// word of each key this table owns (NO_WORD for unreachable / not owned)
+__global__ void k_dense_query(Desc d, DenseView v, const uint32_t* words, const u64* bits, const u64* keys, u64 n,
                               uint32_t* out) {
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
     u64 slot, L, p;
     uint32_t w = NO_WORD;
     if (dense_slot_of(d, keys[i], &slot)) {
       slot_split(d, slot, &L, &p);
-      if (reach_bit(bits, L * Wb + p)) w = words[slot];
+      if (p >= v.p_lo && p < v.p_hi) {
+        const u64 q = p - v.base_off;
+        if (reach_bit(bits, L * v.Wbl + q)) w = words[L * v.Wl + q];
+      }
     }
     out[i] = w;
   }
 }
 
-// every reachable position -> its key (order arbitrary)
-__global__ void k_dense_positions(Desc d, const uint32_t* words, const u64* bits, u64 Wb, u64 nslots, u64* out,
-                                  u64 cap, u64* count) {
-  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < nslots; i += (u64)gridDim.x * blockDim.x) {
-    u64 L, p;
-    slot_split(d, i, &L, &p);
+// every reachable owned position -> its key (order arbitrary)
+__global__ void k_dense_positions(Desc d, DenseView v, const u64* bits, u64 levels, u64* out, u64 cap, u64* count) {
+  const u64 n = v.p_hi - v.p_lo;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < levels * n; i += (u64)gridDim.x * blockDim.x) {
+    const u64 L = i / n, p = v.p_lo + (i - L * n);
     int64_t h0 = dense_h0(d, L, p);
-    if (h0 < 0 || !reach_bit(bits, L * Wb + p)) continue;
+    if (h0 < 0 || !reach_bit(bits, L * v.Wbl + (p - v.base_off))) continue;
     u64 k = atomicAdd(count, 1ull);
     if (k < cap) out[k] = p * d.base[0] + (u64)h0;
   }

@@ -79,6 +79,18 @@ struct Desc {
   uint32_t pshift[16];   // log2(pstride[i]) when pow2
 };
 
+// Which part of a DENSE table's global prefix space one table holds.  A
+// single-GPU solve holds everything; a shard owns the
+// prefixes whose TOP digit lies in [a, b) and keeps two halo slices of that
+// digit on each side: p_lo/p_hi bound the owned global prefixes, base_off
+// is the global prefix of local index 0, Wl the local words per level and
+// Wbl the local reach bits per level (Wl rounded up to 64).
+struct DenseView {
+  uint64_t p_lo, p_hi;
+  uint64_t base_off;
+  uint64_t Wl, Wbl;
+};
+
 GM_HD int popc64(uint64_t v) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return __popcll(v);

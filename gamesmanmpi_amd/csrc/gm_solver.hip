@@ -32,6 +32,7 @@
 // No host synchronisation inside the level loops: segment bounds travel
 // through device memory (k_finalize), so a whole solve is enqueued at once.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <chrono>
 #include <cstdarg>
@@ -85,14 +86,6 @@ enum : uint32_t {
 static std::mutex g_mu;
 static std::vector<Desc> g_games;
 
-// DENSE table = levels * W 32-bit words, then (256-B aligned) the reach
-// bitmap of levels * roundup(W, 64) bits
-static u64 dense_bitmap_offset(const Desc* d) {
-  return ((u64)d->max_levels * d->W * 4 + 255) & ~255ull;
-}
-static u64 dense_bitmap_bytes(const Desc* d) {
-  return (u64)d->max_levels * ((d->W + 63) & ~63ull) / 8;
-}
 
 static int kv(const char* params, const char* key, int dflt) {
   if (!params) return dflt;
@@ -225,6 +218,53 @@ static int build_desc(const char* name, const char* params, Desc* out) {
   return 0;
 }
 
+// Shard geometry of a dense table.  world == 1: the whole prefix space.
+// world > 1: the ranks split the values [0, E) of the TOP prefix digit
+// (heap K-1) into blocks of ceil(E / world) >= 2; rank r owns [a, b) and
+// keeps halo slices [a-2, a) (children of its positions: one move lowers a
+// heap by 1 or 2) and [b, b+2) (parents, for the pull-form forward pass).
+struct DenseGeom {
+  DenseView v;
+  u64 a, b, lo, hi, Z, E;
+};
+static int dense_geom(const Desc* d, int rank, int world, DenseGeom* g) {
+  memset(g, 0, sizeof *g);
+  if (world <= 1) {
+    g->v.p_lo = 0;
+    g->v.p_hi = d->W;
+    g->v.base_off = 0;
+    g->v.Wl = d->W;
+    g->v.Wbl = (d->W + 63) & ~63ull;
+    g->E = 1;
+    g->Z = d->W;
+    g->a = 0; g->b = 1; g->lo = 0; g->hi = 1;
+    return 0;
+  }
+  if (d->nheaps < 2) return fail(GM_EINVAL, "sharding needs at least 2 heaps");
+  const int k = d->nheaps - 1;
+  const u64 E = d->base[k], Z = d->pstride[k];
+  if (Z % 64) return fail(GM_EINVAL, "shard slices must hold a multiple of 64 prefixes (got %llu)", (unsigned long long)Z);
+  const u64 B = (E + world - 1) / world;
+  const u64 a = (u64)rank * B, b = std::min<u64>(E, a + B);
+  if (rank < 0 || rank >= world || a >= E || b - a < 2 || E - (u64)(world - 1) * B < 2)
+    return fail(GM_EINVAL, "top heap of %llu values cannot be split into %d blocks of >= 2", (unsigned long long)E, world);
+  g->a = a; g->b = b; g->E = E; g->Z = Z;
+  g->lo = a >= 2 ? a - 2 : 0;
+  g->hi = std::min<u64>(E, b + 2);
+  g->v.p_lo = a * Z;
+  g->v.p_hi = b * Z;
+  g->v.base_off = g->lo * Z;
+  g->v.Wl = (g->hi - g->lo) * Z;
+  g->v.Wbl = g->v.Wl;  // multiple of 64
+  return 0;
+}
+static u64 dense_words_bytes(const Desc* d, const DenseGeom& g) {
+  return ((u64)d->max_levels * g.v.Wl * 4 + 255) & ~255ull;
+}
+static u64 dense_bits_bytes(const Desc* d, const DenseGeom& g) {
+  return (u64)d->max_levels * g.v.Wbl / 8;
+}
+
 static const Desc* get_game(int id) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (id < 0 || id >= (int)g_games.size()) return nullptr;
@@ -246,6 +286,7 @@ struct DevState {
   u64 max_width;
   uint32_t err;
   uint32_t root_word;
+  u64 red[5];       // cross-shard reduction: positions, edges, prims, root word + 1, err
   LevelSeg seg[1];  // [max_levels + 2]
 };
 static size_t devstate_bytes(int max_levels) {
@@ -469,10 +510,14 @@ __global__ void k_owner(Desc d, const u64* keys, u64 n, uint32_t P, uint32_t* ow
 struct gm_solver {
   Desc d;
   uint32_t mode;
-  uint32_t* words;  // DENSE table: levels * W words ...
-  u64* bits;        // ... followed by the reach bitmap (levels * wb bits)
-  u64 wb;           // bitmap stride per level (W rounded up to 64)
-  u64 nslots;       // DENSE: levels * W
+  uint32_t* words;  // DENSE table: levels * Wl words ...
+  u64* bits;        // ... followed by the reach bitmap (levels * Wbl bits)
+  DenseView view;   // owned prefix range + local addressing
+  u64 nslots;       // DENSE: levels * Wl
+  // dense sharding over the top prefix digit
+  int rank, world;
+  u64 top_a, top_b, top_lo, top_hi, Z, E;
+  ncclComm_t comm;  // RCCL communicator (world > 1), or null
   gm_slot* tab;
   u64 mask;
   u64* lv;
@@ -528,13 +573,13 @@ static void do_resolve(gm_solver* s, int L) {
 
 template <int MAXH, bool POW2>
 static void dense_launch_pull_t(gm_solver* s, int grid, u64 L, u64 root_p) {
-  hipLaunchKernelGGL((k_dense_pull<MAXH, POW2>), dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->bits, s->wb, L,
+  hipLaunchKernelGGL((k_dense_pull<MAXH, POW2>), dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->view, s->bits, L,
                      root_p);
 }
 template <int MAXH, bool POW2>
 static void dense_launch_resolve_t(gm_solver* s, int grid, u64 L) {
-  hipLaunchKernelGGL((k_dense_resolve<MAXH, POW2>), dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->words, s->bits,
-                     s->wb, L, s->st);
+  hipLaunchKernelGGL((k_dense_resolve<MAXH, POW2>), dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->view, s->words,
+                     s->bits, L, s->st);
 }
 // kernels are instantiated per exact heap count 1..8 (16 = generic)
 template <bool POW2>
@@ -764,6 +809,46 @@ int gm_owner_host(int game, const uint64_t* keys, size_t n, int world_size, uint
   return 0;
 }
 
+static int plan_dense(const Desc* d, int rank, int world, uint64_t max_table_bytes, gm_plan_t* out, bool* fits) {
+  DenseGeom g;
+  int rc = dense_geom(d, rank, world, &g);
+  if (rc) return rc;
+  const u64 bytes = dense_words_bytes(d, g) + dense_bits_bytes(d, g);
+  *fits = max_table_bytes == 0 || bytes <= max_table_bytes;
+  out->mode = GM_MODE_DENSE;
+  out->table_slots = (u64)d->max_levels * g.v.Wl;
+  out->table_bytes = bytes;
+  out->level_capacity = 1;
+  return 0;
+}
+
+int gm_shard_info(int game, int rank, int world, uint64_t out[8]) {
+  const Desc* d = get_game(game);
+  if (!d || !out) return fail(GM_EINVAL, "bad argument");
+  if (!d->dense_ok) return fail(GM_EINVAL, "game has no dense layout");
+  DenseGeom g;
+  int rc = dense_geom(d, rank, world, &g);
+  if (rc) return rc;
+  const uint64_t v[8] = {g.a, g.b, g.lo, g.hi, g.Z, g.E, g.v.p_lo, g.v.p_hi};
+  memcpy(out, v, sizeof v);
+  return 0;
+}
+
+int gm_plan_shard(int game, int rank, int world, uint32_t flags, uint64_t max_table_bytes, gm_plan_t* out) {
+  const Desc* d = get_game(game);
+  if (!d || !out) return fail(GM_EINVAL, "bad argument");
+  memset(out, 0, sizeof *out);
+  out->max_levels = (uint32_t)d->max_levels;
+  out->scratch_bytes = (devstate_bytes(d->max_levels) + 255) / 256 * 256;
+  if (!d->dense_ok || (flags & GM_F_FORCE_HASHED))
+    return fail(GM_EINVAL, "only DENSE layouts shard by prefix blocks; keyed tables shard by md5 owner");
+  bool fits = false;
+  int rc = plan_dense(d, rank, world, max_table_bytes, out, &fits);
+  if (rc) return rc;
+  if (!fits) return fail(GM_EFULL, "dense shard needs %llu bytes", (unsigned long long)out->table_bytes);
+  return 0;
+}
+
 int gm_plan(int game, uint64_t positions, uint32_t flags, uint64_t max_table_bytes, gm_plan_t* out) {
   const Desc* d = get_game(game);
   if (!d || !out) return fail(GM_EINVAL, "bad argument");
@@ -771,15 +856,13 @@ int gm_plan(int game, uint64_t positions, uint32_t flags, uint64_t max_table_byt
   out->max_levels = (uint32_t)d->max_levels;
   out->scratch_bytes = (devstate_bytes(d->max_levels) + 255) / 256 * 256;
   if (d->dense_ok && !(flags & GM_F_FORCE_HASHED)) {
-    unsigned __int128 words = (unsigned __int128)d->max_levels * d->W;
-    unsigned __int128 bytes = (unsigned __int128)dense_bitmap_offset(d) + dense_bitmap_bytes(d);
-    if (max_table_bytes == 0 || bytes <= max_table_bytes) {
-      out->mode = GM_MODE_DENSE;
-      out->table_slots = (uint64_t)words;
-      out->table_bytes = (uint64_t)bytes;
-      out->level_capacity = 1;
-      return 0;
-    }
+    bool fits = false;
+    int rc = plan_dense(d, 0, 1, max_table_bytes, out, &fits);
+    if (rc) return rc;
+    if (fits) return 0;
+    memset(out, 0, sizeof *out);
+    out->max_levels = (uint32_t)d->max_levels;
+    out->scratch_bytes = (devstate_bytes(d->max_levels) + 255) / 256 * 256;
   }
   if (positions == 0) {
     gm_game_info(game, &positions, nullptr, nullptr);
@@ -794,15 +877,20 @@ int gm_plan(int game, uint64_t positions, uint32_t flags, uint64_t max_table_byt
   return 0;
 }
 
-int gm_solver_create(int game, const gm_buffers* buf, gm_solver** out) {
+int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf, gm_solver** out) {
   const Desc* d = get_game(game);
   if (!d || !buf || !out) return fail(GM_EINVAL, "bad argument");
   if (!buf->table || !buf->scratch) return fail(GM_EINVAL, "null device buffer");
   if (buf->scratch_bytes < devstate_bytes(d->max_levels)) return fail(GM_EINVAL, "scratch too small");
+  DenseGeom g;
+  memset(&g, 0, sizeof g);
   if (buf->mode == GM_MODE_DENSE) {
     if (!d->dense_ok) return fail(GM_EINVAL, "game has no dense layout");
-    if (buf->table_slots != (u64)d->max_levels * d->W) return fail(GM_EINVAL, "dense table must hold levels * W words");
+    int rc = dense_geom(d, rank, world, &g);
+    if (rc) return rc;
+    if (buf->table_slots != (u64)d->max_levels * g.v.Wl) return fail(GM_EINVAL, "dense table must hold levels * Wl words (use gm_plan_shard)");
   } else if (buf->mode == GM_MODE_HASHED) {
+    if (world != 1) return fail(GM_EINVAL, "keyed-table shards are driven by the md5 exchange (not yet in this ABI)");
     if (!buf->levels || buf->level_capacity < 1) return fail(GM_EINVAL, "null level store");
     if (buf->table_slots < 2 || (buf->table_slots & (buf->table_slots - 1)))
       return fail(GM_EINVAL, "table_slots must be a power of two");
@@ -816,8 +904,12 @@ int gm_solver_create(int game, const gm_buffers* buf, gm_solver** out) {
   s->mode = buf->mode;
   s->words = (uint32_t*)buf->table;
   s->nslots = buf->table_slots;
-  s->wb = (d->W + 63) & ~63ull;
-  s->bits = (u64*)((char*)buf->table + dense_bitmap_offset(d));
+  s->view = g.v;
+  s->bits = (u64*)((char*)buf->table + (buf->mode == GM_MODE_DENSE ? dense_words_bytes(d, g) : 0));
+  s->rank = rank;
+  s->world = world;
+  s->top_a = g.a; s->top_b = g.b; s->top_lo = g.lo; s->top_hi = g.hi; s->Z = g.Z; s->E = g.E;
+  s->comm = nullptr;
   s->tab = (gm_slot*)buf->table;
   s->mask = buf->table_slots - 1;
   s->lv = (u64*)buf->levels;
@@ -840,8 +932,40 @@ int gm_solver_create(int game, const gm_buffers* buf, gm_solver** out) {
   return 0;
 }
 
+int gm_solver_create(int game, const gm_buffers* buf, gm_solver** out) {
+  return gm_solver_create_shard(game, 0, 1, buf, out);
+}
+
+int gm_comm_unique_id(void* id_out) {
+  if (!id_out) return fail(GM_EINVAL, "null argument");
+  ncclUniqueId id;
+  ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) return fail(GM_EHIP, "ncclGetUniqueId: %s", ncclGetErrorString(r));
+  memcpy(id_out, &id, sizeof id);
+  return 0;
+}
+
+int gm_solver_comm_init(gm_solver* s, const void* id) {
+  if (!s || !id) return fail(GM_EINVAL, "bad argument");
+  if (s->world <= 1) return 0;
+  ncclUniqueId uid;
+  memcpy(&uid, id, sizeof uid);
+  ncclComm_t c;
+  ncclResult_t r = ncclCommInitRank(&c, s->world, uid, s->rank);
+  if (r != ncclSuccess) return fail(GM_EHIP, "ncclCommInitRank: %s", ncclGetErrorString(r));
+  s->comm = c;
+  return 0;
+}
+
+int gm_solver_set_flags(gm_solver* s, uint32_t flags) {
+  if (!s) return fail(GM_EINVAL, "null solver");
+  s->flags = flags;
+  return 0;
+}
+
 void gm_solver_destroy(gm_solver* s) {
   if (!s) return;
+  if (s->comm) (void)ncclCommDestroy(s->comm);
   if (s->own_stream) (void)hipStreamDestroy(s->stream);
   delete s;
 }
@@ -945,10 +1069,80 @@ int gm_solver_solve(gm_solver* s, gm_result* out) {
   return 0;
 }
 
-static int solve_dense(gm_solver* s, gm_result* out) {
-  const Desc& d = s->d;
+__global__ void k_fill_red(DevState* st) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st->red[0] = st->cursor_front;
+    st->red[1] = st->edges;
+    st->red[2] = st->prims;
+    st->red[3] = st->root_word == NO_WORD ? 0 : (u64)st->root_word + 1;
+    st->red[4] = st->err;
+  }
+}
+
+// halo regions of a dense shard (local addresses of top-digit slices)
+static u64* halo_bits(gm_solver* s, u64 L, u64 t0) {
+  return s->bits + (L * s->view.Wbl + (t0 - s->top_lo) * s->Z) / 64;
+}
+static uint32_t* halo_words(gm_solver* s, u64 L, u64 t0) {
+  return s->words + L * s->view.Wl + (t0 - s->top_lo) * s->Z;
+}
+
+// Exchange after pull(L): every shard's lowest two owned slices of level-L
+// reach bits go to the shard below (its parent halo).  mode: 1 = RCCL
+// (one process per GPU), 2 = in-process group (device-to-device copies).
+static int exchange_bits(std::vector<gm_solver*>& ss, u64 L, int mode) {
+  const u64 nbytes = 2 * ss[0]->Z / 8;
+  if (mode == 1) {
+    gm_solver* s = ss[0];
+    ncclGroupStart();
+    if (s->rank > 0) ncclSend(halo_bits(s, L, s->top_a), nbytes, ncclUint8, s->rank - 1, s->comm, s->stream);
+    if (s->rank + 1 < s->world) ncclRecv(halo_bits(s, L, s->top_b), nbytes, ncclUint8, s->rank + 1, s->comm, s->stream);
+    ncclResult_t r = ncclGroupEnd();
+    if (r != ncclSuccess) return fail(GM_EHIP, "RCCL bits halo: %s", ncclGetErrorString(r));
+    return 0;
+  }
+  for (size_t g = 1; g < ss.size(); g++)
+    HIPCHK(hipMemcpyAsync(halo_bits(ss[g - 1], L, ss[g]->top_a), halo_bits(ss[g], L, ss[g]->top_a), nbytes,
+                          hipMemcpyDeviceToDevice, ss[g]->stream));
+  return 0;
+}
+
+// Exchange after resolve(L): every shard's highest two owned slices of
+// level-L words go to the shard above (its child halo).
+static int exchange_words(std::vector<gm_solver*>& ss, u64 L, int mode) {
+  const u64 nbytes = 2 * ss[0]->Z * 4;
+  if (mode == 1) {
+    gm_solver* s = ss[0];
+    ncclGroupStart();
+    if (s->rank + 1 < s->world)
+      ncclSend(halo_words(s, L, s->top_b - 2), nbytes, ncclUint8, s->rank + 1, s->comm, s->stream);
+    if (s->rank > 0) ncclRecv(halo_words(s, L, s->top_a - 2), nbytes, ncclUint8, s->rank - 1, s->comm, s->stream);
+    ncclResult_t r = ncclGroupEnd();
+    if (r != ncclSuccess) return fail(GM_EHIP, "RCCL words halo: %s", ncclGetErrorString(r));
+    return 0;
+  }
+  for (size_t g = 0; g + 1 < ss.size(); g++)
+    HIPCHK(hipMemcpyAsync(halo_words(ss[g + 1], L, ss[g]->top_b - 2), halo_words(ss[g], L, ss[g]->top_b - 2), nbytes,
+                          hipMemcpyDeviceToDevice, ss[g]->stream));
+  return 0;
+}
+
+// Dense solve of one table (world 1), one shard of an RCCL job, or every
+// shard of an in-process group (all on one stream), level-synchronously.
+static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
+  gm_solver* s0 = ss[0];
+  const Desc& d = s0->d;
   const int T = d.max_levels;
-  const bool timing = s->flags & GM_F_KERNEL_TIMING;
+  const int mode = s0->world <= 1 ? 0 : (ss.size() == 1 ? 1 : 2);
+  if (mode == 1 && !s0->comm) return fail(GM_EINVAL, "shard %d/%d has no communicator (gm_solver_comm_init)", s0->rank, s0->world);
+  if (mode == 2) {
+    if ((int)ss.size() != s0->world) return fail(GM_EINVAL, "group solve needs all %d shards", s0->world);
+    for (size_t g = 0; g < ss.size(); g++)
+      if (ss[g]->rank != (int)g || ss[g]->stream != s0->stream || ss[g]->mode != GM_MODE_DENSE)
+        return fail(GM_EINVAL, "group shards must be ranks 0..n-1 on one stream");
+  }
+  const bool timing = s0->flags & GM_F_KERNEL_TIMING;
+  hipStream_t st = s0->stream;
   std::vector<hipEvent_t> ev;
   auto new_event = [&](hipEvent_t* e) -> int {
     HIPCHK(hipEventCreate(e));
@@ -957,7 +1151,7 @@ static int solve_dense(gm_solver* s, gm_result* out) {
   };
   hipEvent_t e0, e1, e2;
   if (new_event(&e0) || new_event(&e1) || new_event(&e2)) return GM_EHIP;
-  std::vector<hipEvent_t> kx, kr;
+  std::vector<hipEvent_t> kx, kr;  // per-level kernel start/stop (shard 0's launches)
   if (timing) {
     kx.resize(2 * (size_t)T);
     kr.resize(2 * (size_t)T);
@@ -966,33 +1160,57 @@ static int solve_dense(gm_solver* s, gm_result* out) {
     for (auto& e : kr)
       if (new_event(&e)) return GM_EHIP;
   }
-  const u64 root_slot = d.root / d.base[0];  // level 0, prefix of the root
-  // grid for per-level sweeps over W prefixes
-  const int lgrid = (int)std::min<u64>((d.W + kBlock - 1) / kBlock, (u64)s->grid);
+  const u64 root_p = d.root / d.base[0];  // global prefix of the root (level 0)
+  auto grid_of = [&](gm_solver* s) {
+    return (int)std::min<u64>((s->view.p_hi - s->view.p_lo + kBlock - 1) / kBlock, (u64)s->grid);
+  };
   auto t0 = std::chrono::steady_clock::now();
-  HIPCHK(hipEventRecord(e0, s->stream));
-  HIPCHK(hipMemsetAsync(s->st, 0, devstate_bytes(T), s->stream));
-  // forward (pull): level 0 .. T-1, each level's slab written exactly once
+  HIPCHK(hipEventRecord(e0, st));
+  for (gm_solver* s : ss) HIPCHK(hipMemsetAsync(s->st, 0, devstate_bytes(T), st));
+  // forward (pull): level 0 .. T-1, each level's bitmap written exactly once
   for (int L = 0; L < T; L++) {
-    if (timing) HIPCHK(hipEventRecord(kx[2 * L], s->stream));
-    dense_launch_pull(s, lgrid, (u64)L, root_slot);
-    if (timing) HIPCHK(hipEventRecord(kx[2 * L + 1], s->stream));
+    for (gm_solver* s : ss) {
+      if (timing && s == s0) HIPCHK(hipEventRecord(kx[2 * L], st));
+      dense_launch_pull(s, grid_of(s), (u64)L, root_p);
+      if (timing && s == s0) HIPCHK(hipEventRecord(kx[2 * L + 1], st));
+    }
+    if (mode) {
+      int rc = exchange_bits(ss, (u64)L, mode);
+      if (rc) return rc;
+    }
   }
   HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(e1, s->stream));
+  HIPCHK(hipEventRecord(e1, st));
   for (int L = T - 1; L >= 0; L--) {
-    if (timing) HIPCHK(hipEventRecord(kr[2 * L], s->stream));
-    dense_launch_resolve(s, lgrid, (u64)L);
-    if (timing) HIPCHK(hipEventRecord(kr[2 * L + 1], s->stream));
+    for (gm_solver* s : ss) {
+      if (timing && s == s0) HIPCHK(hipEventRecord(kr[2 * L], st));
+      dense_launch_resolve(s, grid_of(s), (u64)L);
+      if (timing && s == s0) HIPCHK(hipEventRecord(kr[2 * L + 1], st));
+    }
+    if (mode) {
+      int rc = exchange_words(ss, (u64)L, mode);
+      if (rc) return rc;
+    }
   }
   HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(e2, s->stream));
-  hipLaunchKernelGGL(k_dense_root, dim3(1), dim3(64), 0, s->stream, d, s->words, s->bits, root_slot, s->st);
-  std::vector<unsigned char> host(devstate_bytes(T));
-  HIPCHK(hipMemcpyAsync(host.data(), s->st, host.size(), hipMemcpyDeviceToHost, s->stream));
-  HIPCHK(hipStreamSynchronize(s->stream));
+  HIPCHK(hipEventRecord(e2, st));
+  for (gm_solver* s : ss) {
+    hipLaunchKernelGGL(k_dense_root, dim3(1), dim3(64), 0, st, s->view, s->words, s->bits, root_p, s->st);
+    hipLaunchKernelGGL(k_fill_red, dim3(1), dim3(64), 0, st, s->st);
+  }
+  if (mode == 1) {
+    ncclResult_t r = ncclAllReduce(s0->st->red, s0->st->red, 5, ncclUint64, ncclSum, s0->comm, st);
+    if (r != ncclSuccess) return fail(GM_EHIP, "RCCL allreduce: %s", ncclGetErrorString(r));
+  }
+  // totals (host): RCCL has already summed red[] across ranks; a group sums here
+  u64 red[5] = {0, 0, 0, 0, 0};
+  for (gm_solver* s : ss) {
+    u64 r[5];
+    HIPCHK(hipMemcpyAsync(r, s->st->red, sizeof r, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    for (int i = 0; i < 5; i++) red[i] = (i == 4) ? (red[i] | r[i]) : red[i] + r[i];
+  }
   auto t1 = std::chrono::steady_clock::now();
-  const DevState* hs = (const DevState*)host.data();
   float f = 0, b = 0;
   HIPCHK(hipEventElapsedTime(&f, e0, e1));
   HIPCHK(hipEventElapsedTime(&b, e1, e2));
@@ -1005,9 +1223,6 @@ static int solve_dense(gm_solver* s, gm_result* out) {
       float ms = 0;
       HIPCHK(hipEventElapsedTime(&ms, kx[2 * L], kx[2 * L + 1]));
       sx += ms;
-    }
-    for (int L = 0; L < T; L++) {
-      float ms = 0;
       HIPCHK(hipEventElapsedTime(&ms, kr[2 * L], kr[2 * L + 1]));
       sr += ms;
     }
@@ -1017,17 +1232,29 @@ static int solve_dense(gm_solver* s, gm_result* out) {
     out->n_resolve_launches = (uint64_t)T;
   }
   for (auto e : ev) (void)hipEventDestroy(e);
-  out->positions = hs->cursor_front;
-  out->edges = hs->edges;
-  out->primitives = hs->prims;
+  out->positions = red[0];
+  out->edges = red[1];
+  out->primitives = red[2];
   out->levels = (uint32_t)T;
   out->max_level_width = 0;
-  out->root_word = hs->root_word;
-  if (hs->err) return fail(GM_ECORRUPT, "solve failed:%s", err_text(hs->err).c_str());
-  if (hs->root_word == NO_WORD) return fail(GM_ECORRUPT, "root unresolved");
-  out->root_value = (int32_t)(hs->root_word & 3u);
-  out->root_remoteness = hs->root_word >> 2;
+  const uint32_t word = red[3] ? (uint32_t)(red[3] - 1) : NO_WORD;
+  out->root_word = word;
+  if (red[4]) return fail(GM_ECORRUPT, "solve failed:%s", err_text((uint32_t)red[4]).c_str());
+  if (word == NO_WORD) return fail(GM_ECORRUPT, "root unresolved");
+  out->root_value = (int32_t)(word & 3u);
+  out->root_remoteness = word >> 2;
   return 0;
+}
+
+static int solve_dense(gm_solver* s, gm_result* out) { return run_dense({s}, out); }
+
+int gm_solve_group(gm_solver** shards, int n, gm_result* out) {
+  if (!shards || n < 1 || !out) return fail(GM_EINVAL, "bad argument");
+  memset(out, 0, sizeof *out);
+  std::vector<gm_solver*> ss(shards, shards + n);
+  for (gm_solver* s : ss)
+    if (!s) return fail(GM_EINVAL, "null shard");
+  return run_dense(ss, out);
 }
 
 int gm_solver_query(gm_solver* s, const uint64_t* keys_dev, uint64_t n, uint32_t* words_dev) {
@@ -1035,7 +1262,7 @@ int gm_solver_query(gm_solver* s, const uint64_t* keys_dev, uint64_t n, uint32_t
   if (!n) return 0;
   int grid = (int)std::min<u64>((n + kBlock - 1) / kBlock, (u64)s->grid);
   if (s->mode == GM_MODE_DENSE)
-    hipLaunchKernelGGL(k_dense_query, dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->words, s->bits, s->wb,
+    hipLaunchKernelGGL(k_dense_query, dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->view, s->words, s->bits,
                        (const u64*)keys_dev, n, words_dev);
   else
     hipLaunchKernelGGL(k_query, dim3(grid), dim3(kBlock), 0, s->stream, s->tab, s->mask, (const u64*)keys_dev, n,
@@ -1054,8 +1281,8 @@ int gm_solver_positions(gm_solver* s, uint64_t* keys_dev, uint64_t cap, uint64_t
   if (s->mode == GM_MODE_DENSE) {
     if (*n > cap || !keys_dev) return cap < *n ? fail(GM_EFULL, "need %llu slots", (unsigned long long)*n) : 0;
     HIPCHK(hipMemsetAsync(&s->st->cursor_back, 0, sizeof(u64), s->stream));
-    hipLaunchKernelGGL(k_dense_positions, dim3(s->grid), dim3(kBlock), 0, s->stream, s->d, s->words, s->bits, s->wb,
-                       s->nslots, (u64*)keys_dev, cap, &s->st->cursor_back);
+    hipLaunchKernelGGL(k_dense_positions, dim3(s->grid), dim3(kBlock), 0, s->stream, s->d, s->view, s->bits,
+                       (u64)s->d.max_levels, (u64*)keys_dev, cap, &s->st->cursor_back);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(s->stream));
     return 0;

@@ -136,6 +136,15 @@ class GameSpec:
                                              out.ctypes.data))
         return out
 
+    def shard_info(self, rank, world):
+        """Geometry of dense shard `rank` of `world` (DESIGN.md
+        §Multi-GPU): dict a, b, lo, hi, Z, E, p_lo, p_hi."""
+        out = (_lib.ctypes.c_uint64 * 8)()
+        _lib.check(_lib.load().gm_shard_info(self.id, int(rank), int(world),
+                                             out))
+        return dict(zip(("a", "b", "lo", "hi", "Z", "E", "p_lo", "p_hi"),
+                        list(out)))
+
     # -- the drop-in guard -------------------------------------------------
     def verify(self, module, samples=200, seed=0):
         """Replay the module's own primitive/gen_moves/do_move on random

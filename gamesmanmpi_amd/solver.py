@@ -47,9 +47,12 @@ class Solver:
     """Owns the device buffers of one game's solve on one GPU."""
 
     def __init__(self, spec, positions=0, device=None, kernel_timing=False,
-                 layout="auto", max_table_bytes=0):
+                 layout="auto", max_table_bytes=0, rank=0, world=1,
+                 stream=None):
         """layout: "auto" (dense when the descriptor supports it and the
-        table fits max_table_bytes, else hashed), "dense" or "hashed"."""
+        table fits max_table_bytes, else hashed), "dense" or "hashed".
+        rank/world > 1: this object is one shard of a dense multi-GPU solve
+        (see gamesmanmpi_amd.dist); stream: a torch stream to run on."""
         import torch
         if not torch.cuda.is_available():
             raise RuntimeError("gamesmanmpi_amd needs a ROCm GPU (gfx950); "
@@ -62,6 +65,8 @@ class Solver:
             raise ValueError("layout must be auto, dense or hashed")
         self.layout = layout
         self.max_table_bytes = int(max_table_bytes)
+        self.rank, self.world = int(rank), int(world)
+        self.stream = stream
         self.positions_hint = int(positions or self.spec.positions_bound)
         self._h = None
         self._bufs = None
@@ -73,8 +78,13 @@ class Solver:
         self._free()
         plan = _lib.gm_plan_t()
         flags = _lib.GM_F_FORCE_HASHED if self.layout == "hashed" else 0
-        _lib.check(L.gm_plan(self.spec.id, int(positions), flags,
-                             self.max_table_bytes, ctypes.byref(plan)))
+        if self.world > 1:
+            _lib.check(L.gm_plan_shard(self.spec.id, self.rank, self.world,
+                                       flags, self.max_table_bytes,
+                                       ctypes.byref(plan)))
+        else:
+            _lib.check(L.gm_plan(self.spec.id, int(positions), flags,
+                                 self.max_table_bytes, ctypes.byref(plan)))
         if self.layout == "dense" and plan.mode != _lib.GM_MODE_DENSE:
             raise ValueError("%r has no dense layout (or it does not fit)"
                              % (self.spec,))
@@ -85,7 +95,7 @@ class Solver:
                                  dtype=torch.int64, device=self.device)
             scratch = torch.empty(plan.scratch_bytes, dtype=torch.uint8,
                                   device=self.device)
-            stream = torch.cuda.current_stream(self.device)
+            stream = self.stream or torch.cuda.current_stream(self.device)
         self._tensors = (table, levels, scratch)
         b = _lib.gm_buffers()
         b.table = table.data_ptr()
@@ -100,8 +110,9 @@ class Solver:
         self._bufs = b
         self.plan = plan
         h = ctypes.c_void_p()
-        _lib.check(L.gm_solver_create(self.spec.id, ctypes.byref(b),
-                                      ctypes.byref(h)))
+        _lib.check(L.gm_solver_create_shard(self.spec.id, self.rank,
+                                            self.world, ctypes.byref(b),
+                                            ctypes.byref(h)))
         self._h = h
 
     def _free(self):
@@ -116,10 +127,22 @@ class Solver:
         except Exception:  # noqa: BLE001 -- interpreter teardown
             pass
 
+    @property
+    def handle(self):
+        return self._h
+
+    def set_kernel_timing(self, on):
+        """Time every kernel launch with HIP events (on the solve stream)."""
+        self.kernel_timing = bool(on)
+        _lib.check(_lib.load().gm_solver_set_flags(
+            self._h, _lib.GM_F_KERNEL_TIMING if on else 0))
+
     def solve(self, max_retries=4):
         """Full solve from the root; grows the buffers on GM_EFULL."""
         L = _lib.load()
         r = _lib.gm_result()
+        if self.world > 1:
+            max_retries = 0  # shard tables are sized exactly
         for attempt in range(max_retries + 1):
             try:
                 with self.torch.cuda.device(self.device):
@@ -130,6 +153,9 @@ class Solver:
                     raise
                 self.positions_hint *= 2
                 self._alloc(self.positions_hint)
+        return self._result(r)
+
+    def _result(self, r):
         return SolveResult(
             root_value=r.root_value, root_remoteness=r.root_remoteness,
             positions=r.positions, edges=r.edges, primitives=r.primitives,
