@@ -1,0 +1,164 @@
+#!/usr/bin/env python3
+"""Drop-in for the reference's launcher (solver_launcher.py:1-98).
+
+    reference:  mpiexec -n P python solver_launcher.py GAME_FILE [--debug] [-sd DIR]
+    here:       python -m gamesmanmpi_amd.solver_launcher GAME_FILE [--debug] [-sd DIR]
+                torchrun --nproc-per-node N -m gamesmanmpi_amd.solver_launcher GAME_FILE
+
+Same positional argument and flags (solver_launcher.py:9-28), same game
+loading (imp.load_source + src.utils.game_module, :41-42), same validation
+of the four API functions (:55-66), and the same single output line on the
+root's rank: "<WIN|LOSS|TIE|DRAW> in <r> moves" (src/process.py:47-52).
+
+What differs, by design:
+  * the game file is paired with its device descriptor (by file stem) and
+    the pairing is verified by replaying the module's own functions on
+    sampled positions before solving (--no-verify skips it);
+  * one process per GPU via torch.distributed.run instead of mpiexec ranks;
+  * -sd writes the solution per rank as <DIR>/stats/<rank>/solution.npz
+    (keys, value, remoteness) plus meta.json -- the binary counterpart of the
+    reference's <DIR>/stats/<rank>/{resolved,remote} shelve files
+    (src/cache_dict.py:19-42);
+  * values are the order-independent reading of the reference's reduction
+    (DESIGN.md §Parity); results are deterministic.
+"""
+import argparse
+import importlib.util
+import json
+import logging
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+COMPAT = os.path.join(HERE, "compat")
+
+
+def ensure_src_utils():
+    """Game files `import src.utils` (e.g. four_to_one.py:5).  Use an
+    importable reference `src` package when there is one, otherwise our
+    compat copy of the constants (gamesmanmpi_amd/compat/src/utils.py)."""
+    try:
+        import src.utils  # noqa: F401
+    except ImportError:
+        for m in [m for m in sys.modules if m == "src" or m.startswith("src.")]:
+            del sys.modules[m]
+        sys.path.insert(0, COMPAT)
+        import src.utils  # noqa: F401
+    return sys.modules["src.utils"]
+
+
+def load_game(path):
+    """imp.load_source('game_module', path) (solver_launcher.py:41)."""
+    spec = importlib.util.spec_from_file_location("game_module", path)
+    if spec is None:
+        raise FileNotFoundError(path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def validate(mod):
+    """solver_launcher.py:55-66: the four API functions must exist."""
+    for name in ("initial_position", "do_move", "gen_moves", "primitive"):
+        try:
+            getattr(mod, name)
+        except AttributeError as e:
+            print("Could not find method", e.args[0])
+            raise
+
+
+def build_parser():
+    p = argparse.ArgumentParser(prog="gamesmanmpi_amd.solver_launcher")
+    p.add_argument("game_file", help="game to solve for")
+    p.add_argument("--debug", help="Enables or disables logging",
+                   action="store_true")
+    p.add_argument("-sd", "--statsdir",
+                   help="location to store statistics about game",
+                   action="store")
+    # additions
+    p.add_argument("--layout", choices=["auto", "dense", "hashed"],
+                   default="auto", help="table layout (DESIGN.md §Layout)")
+    p.add_argument("--positions", type=int, default=0,
+                   help="capacity estimate for boards without a known bound")
+    p.add_argument("--no-verify", action="store_true",
+                   help="skip replaying the module against its descriptor")
+    p.add_argument("--verify-samples", type=int, default=200)
+    p.add_argument("--json", action="store_true",
+                   help="also print a JSON line with counts and timings")
+    return p
+
+
+def write_stats(statsdir, rank, spec, solver, result):
+    """<statsdir>/stats/<rank>/solution.npz (+ meta.json)."""
+    import numpy as np
+    d = os.path.join(statsdir, "stats", str(rank))
+    os.makedirs(d, exist_ok=True)
+    keys, val, rem = solver.dump()
+    canon, lens = spec.decode_batch(keys, stride=32)
+    np.savez_compressed(os.path.join(d, "solution.npz"), keys=keys,
+                        canon=canon, clen=lens, value=val, remoteness=rem)
+    with open(os.path.join(d, "meta.json"), "w") as f:
+        json.dump({"game": spec.name, "params": spec.params,
+                   "root": result.root_line, "positions": len(keys),
+                   "owned_by_rank": rank,
+                   "value_codes": {"WIN": 0, "LOSS": 1, "TIE": 2, "DRAW": 3}},
+                  f, indent=1)
+
+
+def main(argv=None):
+    args = build_parser().parse_args(argv)
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.debug:  # src/debug.py:10-18: logging to logs/proc<rank>
+        os.makedirs("logs", exist_ok=True)
+        logging.basicConfig(filename="logs/proc%d" % rank, level=logging.DEBUG)
+
+    utils = ensure_src_utils()
+    game = load_game(args.game_file)
+    utils.game_module = game
+    validate(game)
+
+    root = os.path.dirname(HERE)
+    if root not in sys.path:
+        sys.path.insert(0, root)
+    from gamesmanmpi_amd.games import spec_for_module
+    spec = spec_for_module(game, os.path.splitext(
+        os.path.basename(args.game_file))[0])
+    if not args.no_verify:
+        n = spec.verify(game, samples=args.verify_samples)
+        logging.debug("descriptor %r verified on %d positions", spec, n)
+
+    import torch
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        from gamesmanmpi_amd.dist import ShardedSolver
+        solver = ShardedSolver(spec, rank, world, device="cuda:%d" % local)
+    else:
+        from gamesmanmpi_amd.solver import Solver
+        solver = Solver(spec, positions=args.positions,
+                        device="cuda:%d" % local, layout=args.layout)
+    result = solver.solve()
+    if rank == 0:
+        print(result.root_line, flush=True)  # src/process.py:47-52
+        if args.json:
+            print(json.dumps({"game": spec.name, "params": spec.params,
+                              "root": result.root_line,
+                              "positions": result.positions,
+                              "edges": result.edges,
+                              "ms_total": result.ms_total,
+                              "layout": result.extra.get("layout"),
+                              "ranks": world}), flush=True)
+    if args.statsdir:
+        write_stats(args.statsdir, rank, spec, solver, result)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

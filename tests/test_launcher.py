@@ -1,0 +1,154 @@
+"""The drop-in boundary: reference-API game files load, validate, map to
+their device descriptors and pass the descriptor-vs-module replay check
+(gamesmanmpi_amd/solver_launcher.py, games.spec_for_module/verify).
+
+CPU tests load the reference's OWN game files (only where /root/reference
+exists; third-party imports they need come from tests/golden/refstubs).  The
+GPU test runs the launcher end to end on a game file shipped here."""
+import importlib.util
+import io
+import os
+import shutil
+import sys
+from contextlib import redirect_stdout
+
+import numpy as np
+import pytest
+
+from conftest import REFERENCE, ROOT, has_reference
+
+STUBS = os.path.join(ROOT, "tests", "golden", "refstubs")
+OWN_SUM = os.path.join(ROOT, "gamesmanmpi_amd", "games", "sum_four_to_one.py")
+
+
+def _load(path, name, **overrides):
+    from gamesmanmpi_amd import solver_launcher as sl
+    if STUBS not in sys.path:
+        sys.path.insert(0, STUBS)
+    sl.ensure_src_utils()
+    spec = importlib.util.spec_from_file_location(name, path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    for k, v in overrides.items():
+        setattr(mod, k, v)
+    if "length" in overrides:
+        mod.area = mod.length * mod.height
+    sl.validate(mod)
+    return mod
+
+
+def test_compat_utils_semantics():
+    from gamesmanmpi_amd import solver_launcher as sl
+    sys.path.insert(0, os.path.join(ROOT, "gamesmanmpi_amd", "compat"))
+    spec = importlib.util.spec_from_file_location(
+        "compat_utils", os.path.join(ROOT, "gamesmanmpi_amd", "compat", "src",
+                                     "utils.py"))
+    u = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(u)
+    assert (u.WIN, u.LOSS, u.TIE, u.DRAW, u.UNDECIDED) == (0, 1, 2, 3, 4)
+    assert u.PRIMITIVES == (0, 1, 2, 3)
+    assert [u.negate(x) for x in range(5)] == [1, 0, 2, 3, 4]
+    assert [u.to_str(x) for x in range(5)] == ["WIN", "LOSS", "TIE", "DRAW",
+                                                "UNDECIDED"]
+    assert u.reduce_singleton(lambda a, b: (a, b), [7]) == (7, None)
+    assert u.reduce_singleton(lambda a, b: a + b, [1, 2, 3]) == 6
+    assert sl.COMPAT.endswith("compat")
+
+
+@pytest.mark.skipif(not has_reference(), reason="reference not mounted")
+def test_compat_utils_match_reference_module():
+    spec = importlib.util.spec_from_file_location(
+        "ref_utils", os.path.join(REFERENCE, "src", "utils.py"))
+    ref = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ref)
+    spec = importlib.util.spec_from_file_location(
+        "compat_utils2", os.path.join(ROOT, "gamesmanmpi_amd", "compat", "src",
+                                      "utils.py"))
+    ours = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ours)
+    for name in ("WIN", "LOSS", "TIE", "DRAW", "UNDECIDED", "PRIMITIVES",
+                 "PRIMITIVE_REMOTENESS", "UNKNOWN_REMOTENESS", "STATE_MAP"):
+        assert getattr(ours, name) == getattr(ref, name), name
+    for x in range(5):
+        assert ours.negate(x) == ref.negate(x)
+        assert ours.to_str(x) == ref.to_str(x)
+
+
+REF_GAMES = [
+    ("four_to_one.py", {}),
+    ("mttt.py", {}),
+    ("tic_tac_toe_np.py", {}),
+    ("toot_and_otto_bitstring.py", {}),                       # 6x4 as shipped
+    ("toot_and_otto_bitstring.py", {"length": 4, "height": 3}),
+    ("othello_bit_new.py", {"length": 4, "height": 4}),       # config 5 size
+]
+
+
+@pytest.mark.skipif(not has_reference(), reason="reference not mounted")
+@pytest.mark.parametrize("fname,overrides", REF_GAMES)
+def test_reference_game_files_map_and_verify(fname, overrides):
+    from gamesmanmpi_amd.games import spec_for_module
+    mod = _load(os.path.join(REFERENCE, "test_games", fname), "gm_launch_test",
+                **overrides)
+    spec = spec_for_module(mod, os.path.splitext(fname)[0])
+    assert spec.verify(mod, samples=150) == 150
+
+
+@pytest.mark.skipif(not has_reference(), reason="reference not mounted")
+def test_modified_game_file_is_refused():
+    """A game file whose rules differ from its descriptor must not be
+    silently solved with stale rules."""
+    from gamesmanmpi_amd.games import spec_for_module
+    mod = _load(os.path.join(REFERENCE, "test_games", "four_to_one.py"),
+                "gm_launch_mod")
+    mod.gen_moves = lambda x: [-1]  # a different game
+    spec = spec_for_module(mod, "four_to_one")
+    with pytest.raises(ValueError):
+        spec.verify(mod, samples=50)
+
+
+def test_unknown_game_file_is_refused():
+    from gamesmanmpi_amd.games import spec_for_module
+
+    class M:
+        __file__ = "/tmp/chess.py"
+    with pytest.raises(ValueError):
+        spec_for_module(M())
+
+
+def test_own_sum_game_file_verifies():
+    from gamesmanmpi_amd.games import spec_for_module
+    mod = _load(OWN_SUM, "gm_sum_launch", HEAPS=(5, 7, 3))
+    spec = spec_for_module(mod, "sum_four_to_one")
+    assert spec.params == "heaps=5:7:3"
+    assert spec.verify(mod, samples=200) == 200
+
+
+def test_missing_api_function_raises():
+    from gamesmanmpi_amd import solver_launcher as sl
+
+    class M:
+        initial_position = do_move = gen_moves = None
+    with pytest.raises(AttributeError):
+        sl.validate(M())
+
+
+@pytest.mark.gpu
+def test_launcher_end_to_end(tmp_path):
+    """Launcher on a game file (the shipped sum game with edited HEAPS):
+    prints the reference's root line and writes -sd output."""
+    from gamesmanmpi_amd import solver_launcher as sl
+    from oracle.oracle import Game
+    game = tmp_path / "sum_four_to_one.py"
+    src = open(OWN_SUM).read().replace(
+        "HEAPS = (31, 31, 31, 31, 31, 31)", "HEAPS = (4, 6, 3)")
+    game.write_text(src)
+    out = io.StringIO()
+    with redirect_stdout(out):
+        rc = sl.main([str(game), "-sd", str(tmp_path / "sd")])
+    assert rc == 0
+    want = Game("sum_four_to_one", "heaps=4:6:3").solve().root_line
+    assert out.getvalue().strip().splitlines()[0] == want
+    z = np.load(tmp_path / "sd" / "stats" / "0" / "solution.npz")
+    assert len(z["keys"]) == 5 * 7 * 4
+    shutil.rmtree(tmp_path / "sd")
