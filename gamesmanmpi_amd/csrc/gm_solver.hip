@@ -571,13 +571,64 @@ static void do_resolve(gm_solver* s, int L) {
   }
 }
 
+// Kernel choice for power-of-two dense layouts (measured on MI355X, 2^30
+// solve): pull -- word-parallel 4.2 ms vs per-lane 46 ms; resolve --
+// per-lane 44 ms vs mask-driven 64 / 79 / 181 ms (1 / 2 / 4 groups per
+// round).  GM_DENSE_PER_LANE=pull forces the per-lane pull,
+// GM_DENSE_RESOLVE=words selects the mask-driven resolve (A/B runs).
+static int dense_per_lane_mask() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("GM_DENSE_PER_LANE");
+    const char* r = getenv("GM_DENSE_RESOLVE");
+    v = 2;  // bit 0: per-lane pull, bit 1: per-lane resolve
+    if (e && !strcmp(e, "pull")) v |= 1;
+    if (e && atoi(e)) v |= 3;
+    if (r && !strcmp(r, "words")) v &= ~2;
+  }
+  return v;
+}
+
+// groups of 64 prefixes each resolve wave keeps in flight (measured; the
+// GM_RESOLVE_GROUPS environment variable overrides it for experiments)
+static int resolve_groups() {
+  static int g = 0;
+  if (!g) {
+    const char* e = getenv("GM_RESOLVE_GROUPS");
+    int v = e ? atoi(e) : 2;
+    g = (v == 1 || v == 4) ? v : 2;
+  }
+  return g;
+}
+
 template <int MAXH, bool POW2>
 static void dense_launch_pull_t(gm_solver* s, int grid, u64 L, u64 root_p) {
+  if (POW2 && !(dense_per_lane_mask() & 1)) {  // word-parallel form: one thread per 64-prefix group
+    const u64 groups = (s->view.p_hi - s->view.p_lo + 63) / 64;
+    const int g = (int)std::min<u64>((groups + kBlock - 1) / kBlock, (u64)s->grid);
+    hipLaunchKernelGGL((k_dense_pull_words<MAXH>), dim3(g), dim3(kBlock), 0, s->stream, s->d, s->view, s->bits, L,
+                       root_p);
+    return;
+  }
   hipLaunchKernelGGL((k_dense_pull<MAXH, POW2>), dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->view, s->bits, L,
                      root_p);
 }
 template <int MAXH, bool POW2>
 static void dense_launch_resolve_t(gm_solver* s, int grid, u64 L) {
+  if (POW2 && !(dense_per_lane_mask() & 2)) {  // mask-driven form: one wave per 64-prefix group
+    const u64 groups = (s->view.p_hi - s->view.p_lo + 63) / 64;
+    const int G = resolve_groups();
+    const u64 waves = (groups + G - 1) / G;
+    const int g = (int)std::min<u64>((waves + 3) / 4, (u64)s->grid);
+#define GM_RW(GR)                                                                                            \
+  hipLaunchKernelGGL((k_dense_resolve_words<MAXH, GR>), dim3(g), dim3(kBlock), 0, s->stream, s->d, s->view, \
+                     s->words, s->bits, L, s->st)
+    if (G == 1) GM_RW(1);
+    else if (G == 4) GM_RW(4);
+    else GM_RW(2);
+#undef GM_RW
+    return;
+  }
   hipLaunchKernelGGL((k_dense_resolve<MAXH, POW2>), dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->view, s->words,
                      s->bits, L, s->st);
 }
