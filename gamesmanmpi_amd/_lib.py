@@ -72,12 +72,15 @@ class gm_result(ctypes.Structure):
 # every symbol include/gamesman.h declares (tests check the exports)
 EXPORTS = (
     "gm_game_lookup", "gm_game_info", "gm_root", "gm_encode", "gm_decode",
-    "gm_encode_batch", "gm_decode_batch", "gm_str_utf8", "gm_host_expand", "gm_plan", "gm_solver_create",
+    "gm_encode_batch", "gm_decode_batch", "gm_str_utf8", "gm_host_expand", "gm_host_level", "gm_plan", "gm_solver_create",
     "gm_solver_solve", "gm_solver_query", "gm_solver_positions",
     "gm_solver_destroy", "gm_solve", "gm_owner", "gm_owner_host",
     "gm_plan_shard", "gm_solver_create_shard", "gm_comm_unique_id",
     "gm_solver_comm_init", "gm_solve_group", "gm_solver_set_flags",
     "gm_shard_info",
+    "gm_ks_begin", "gm_ks_level_size", "gm_ks_expand", "gm_ks_insert",
+    "gm_ks_finalize", "gm_ks_counts", "gm_ks_children", "gm_ks_reduce",
+    "gm_ks_end",
     "gm_last_error", "gm_version",
 )
 
@@ -112,6 +115,7 @@ def load():
                         P(c.c_size_t)],
         "gm_host_expand": [c.c_int, c.c_void_p, c.c_size_t, c.c_void_p,
                            c.c_void_p, c.c_void_p],
+        "gm_host_level": [c.c_int, c.c_void_p, c.c_size_t, c.c_void_p],
         "gm_plan": [c.c_int, c.c_uint64, c.c_uint32, c.c_uint64,
                     P(gm_plan_t)],
         "gm_solver_create": [c.c_int, P(gm_buffers), P(c.c_void_p)],
@@ -134,6 +138,17 @@ def load():
         "gm_solve_group": [c.POINTER(c.c_void_p), c.c_int, P(gm_result)],
         "gm_solver_set_flags": [c.c_void_p, c.c_uint32],
         "gm_shard_info": [c.c_int, c.c_int, c.c_int, P(c.c_uint64)],
+        "gm_ks_begin": [c.c_void_p, c.c_int],
+        "gm_ks_level_size": [c.c_void_p, c.c_int, P(c.c_uint64)],
+        "gm_ks_expand": [c.c_void_p, c.c_int, c.c_void_p, c.c_void_p,
+                         c.c_uint64, c.c_int, P(c.c_uint64)],
+        "gm_ks_insert": [c.c_void_p, c.c_int, c.c_void_p, c.c_uint64],
+        "gm_ks_finalize": [c.c_void_p, c.c_int],
+        "gm_ks_counts": [c.c_void_p, c.c_int, c.c_void_p],
+        "gm_ks_children": [c.c_void_p, c.c_int, c.c_void_p, c.c_void_p,
+                           c.c_void_p, c.c_int],
+        "gm_ks_reduce": [c.c_void_p, c.c_int, c.c_void_p, c.c_void_p],
+        "gm_ks_end": [c.c_void_p, P(gm_result)],
     }
     for name, args in sig.items():
         f = getattr(L, name)

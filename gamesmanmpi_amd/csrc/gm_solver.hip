@@ -286,7 +286,8 @@ struct DevState {
   u64 max_width;
   uint32_t err;
   uint32_t root_word;
-  u64 red[5];       // cross-shard reduction: positions, edges, prims, root word + 1, err
+  u64 ks_cursor;    // keyed shards: child pairs emitted by k_ks_expand
+  u64 red[5];     // cross-shard reduction: positions, edges, prims, root word + 1, err
   LevelSeg seg[1];  // [max_levels + 2]
 };
 static size_t devstate_bytes(int max_levels) {
@@ -503,6 +504,7 @@ __global__ void k_owner(Desc d, const u64* keys, u64 n, uint32_t P, uint32_t* ow
 }
 
 #include "gm_dense.h"
+#include "gm_keyed_shard.h"
 
 // ---------------------------------------------------------------------------
 // solver object
@@ -848,6 +850,13 @@ int gm_host_expand(int game, const uint64_t* keys, size_t n, uint64_t* children,
   return 0;
 }
 
+int gm_host_level(int game, const uint64_t* keys, size_t n, int32_t* levels) {
+  const Desc* d = get_game(game);
+  if (!d || (n && (!keys || !levels))) return fail(GM_EINVAL, "bad argument");
+  for (size_t i = 0; i < n; i++) levels[i] = any_level(*d, keys[i]);
+  return 0;
+}
+
 int gm_owner_host(int game, const uint64_t* keys, size_t n, int world_size, uint32_t* owners) {
   const Desc* d = get_game(game);
   if (!d || world_size < 1 || (n && (!keys || !owners))) return fail(GM_EINVAL, "bad argument");
@@ -941,7 +950,7 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
     if (rc) return rc;
     if (buf->table_slots != (u64)d->max_levels * g.v.Wl) return fail(GM_EINVAL, "dense table must hold levels * Wl words (use gm_plan_shard)");
   } else if (buf->mode == GM_MODE_HASHED) {
-    if (world != 1) return fail(GM_EINVAL, "keyed-table shards are driven by the md5 exchange (not yet in this ABI)");
+    if (world < 1 || rank < 0 || rank >= world) return fail(GM_EINVAL, "bad shard %d/%d", rank, world);
     if (!buf->levels || buf->level_capacity < 1) return fail(GM_EINVAL, "null level store");
     if (buf->table_slots < 2 || (buf->table_slots & (buf->table_slots - 1)))
       return fail(GM_EINVAL, "table_slots must be a power of two");
@@ -1027,6 +1036,7 @@ int gm_solver_solve(gm_solver* s, gm_result* out) {
   if (!s || !out) return fail(GM_EINVAL, "bad argument");
   memset(out, 0, sizeof *out);
   if (s->mode == GM_MODE_DENSE) return solve_dense(s, out);
+  if (s->world > 1) return fail(GM_EINVAL, "keyed-table shard %d/%d: drive it with gm_ks_* (md5 exchange)", s->rank, s->world);
   const int T = s->d.max_levels;
   const bool timing = s->flags & GM_F_KERNEL_TIMING;
   std::vector<hipEvent_t> ev;
@@ -1373,3 +1383,171 @@ int gm_owner(int game, const uint64_t* keys_dev, uint64_t n, int world_size, uin
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// md5-sharded keyed tables (gm_keyed_shard.h): the host moves keys/words
+// between ranks between these steps (gamesmanmpi_amd/keyed.py)
+// ---------------------------------------------------------------------------
+#define GM_KIND_DISPATCH(KERNEL, GRID, S, ...)                                                      \
+  switch ((S)->d.kind) {                                                                           \
+    case K_SUM: hipLaunchKernelGGL(KERNEL<K_SUM>, dim3(GRID), dim3(kBlock), 0, (S)->stream, __VA_ARGS__); break; \
+    case K_TTT: hipLaunchKernelGGL(KERNEL<K_TTT>, dim3(GRID), dim3(kBlock), 0, (S)->stream, __VA_ARGS__); break; \
+    case K_TOOT: hipLaunchKernelGGL(KERNEL<K_TOOT>, dim3(GRID), dim3(kBlock), 0, (S)->stream, __VA_ARGS__); break; \
+    default: hipLaunchKernelGGL(KERNEL<K_OTHELLO>, dim3(GRID), dim3(kBlock), 0, (S)->stream, __VA_ARGS__); break; \
+  }
+
+static int ks_check(gm_solver* s, int level) {
+  if (!s) return fail(GM_EINVAL, "null solver");
+  if (s->mode != GM_MODE_HASHED) return fail(GM_EINVAL, "gm_ks_* drive keyed (HASHED) tables only");
+  if (level < 0 || level >= s->d.max_levels) return fail(GM_EINVAL, "level %d out of range", level);
+  return 0;
+}
+
+static int ks_grid(gm_solver* s, u64 n) {
+  return (int)std::max<u64>(1, std::min<u64>((n + kBlock - 1) / kBlock, (u64)s->grid));
+}
+
+static int ks_errors(gm_solver* s) {
+  uint32_t err = 0;
+  HIPCHK(hipMemcpyAsync(&err, &s->st->err, sizeof err, hipMemcpyDeviceToHost, s->stream));
+  HIPCHK(hipStreamSynchronize(s->stream));
+  if (err) {
+    bool full = err & (ERR_TABLE_FULL | ERR_LEVELS_FULL);
+    return fail(full ? GM_EFULL : GM_ECORRUPT, "shard %d/%d:%s", s->rank, s->world, err_text(err).c_str());
+  }
+  return 0;
+}
+
+int gm_ks_begin(gm_solver* s, int root_owned) {
+  int rc = ks_check(s, 0);
+  if (rc) return rc;
+  HIPCHK(hipMemsetAsync(s->tab, 0xFF, (s->mask + 1) * sizeof(gm_slot), s->stream));
+  HIPCHK(hipMemsetAsync(s->st, 0, devstate_bytes(s->d.max_levels), s->stream));
+  hipLaunchKernelGGL(k_ks_seed, dim3(1), dim3(64), 0, s->stream, s->tab, s->mask, s->lv, s->st, s->d.root,
+                     root_owned ? 1 : 0);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int gm_ks_level_size(gm_solver* s, int level, uint64_t* n) {
+  int rc = ks_check(s, level);
+  if (rc) return rc;
+  if (!n) return fail(GM_EINVAL, "null argument");
+  LevelSeg g;
+  HIPCHK(hipMemcpyAsync(&g, &s->st->seg[level], sizeof g, hipMemcpyDeviceToHost, s->stream));
+  HIPCHK(hipStreamSynchronize(s->stream));
+  *n = (g.fe - g.fb) + (g.c2hi - g.c2lo);
+  return 0;
+}
+
+int gm_ks_expand(gm_solver* s, int level, uint64_t* keys_dev, uint32_t* owners_dev, uint64_t cap, int world,
+                 uint64_t* n) {
+  int rc = ks_check(s, level);
+  if (rc) return rc;
+  if (!n || world < 1 || (cap && (!keys_dev || !owners_dev))) return fail(GM_EINVAL, "bad argument");
+  uint64_t width = 0;
+  if ((rc = gm_ks_level_size(s, level, &width))) return rc;
+  HIPCHK(hipMemsetAsync(&s->st->ks_cursor, 0, sizeof(u64), s->stream));
+  GM_KIND_DISPATCH(k_ks_expand, ks_grid(s, width), s, s->d, s->lv, s->lcap, s->st, level, (u64*)keys_dev, owners_dev,
+                   cap, &s->st->ks_cursor, (uint32_t)world);
+  HIPCHK(hipGetLastError());
+  u64 got = 0;
+  HIPCHK(hipMemcpyAsync(&got, &s->st->ks_cursor, sizeof got, hipMemcpyDeviceToHost, s->stream));
+  HIPCHK(hipStreamSynchronize(s->stream));
+  *n = got;
+  if (got > cap) return fail(GM_EFULL, "expand of level %d emits %llu children (cap %llu)", level,
+                             (unsigned long long)got, (unsigned long long)cap);
+  return 0;
+}
+
+int gm_ks_insert(gm_solver* s, int level, const uint64_t* keys_dev, uint64_t n) {
+  int rc = ks_check(s, level);
+  if (rc) return rc;
+  if (n && !keys_dev) return fail(GM_EINVAL, "null keys");
+  if (n) GM_KIND_DISPATCH(k_ks_insert, ks_grid(s, n), s, s->d, s->tab, s->mask, s->lv, s->lcap, s->st, level,
+                          (const u64*)keys_dev, (u64)n);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int gm_ks_finalize(gm_solver* s, int level) {
+  int rc = ks_check(s, level);
+  if (rc) return rc;
+  if (level + 1 >= s->d.max_levels) return fail(GM_EINVAL, "level %d is the last level", level);
+  hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s->stream, s->st, level, s->lcap);
+  HIPCHK(hipGetLastError());
+  return ks_errors(s);
+}
+
+int gm_ks_counts(gm_solver* s, int level, uint64_t* counts_dev) {
+  int rc = ks_check(s, level);
+  if (rc) return rc;
+  uint64_t width = 0;
+  if ((rc = gm_ks_level_size(s, level, &width))) return rc;
+  if (!width) return 0;
+  if (!counts_dev) return fail(GM_EINVAL, "null counts");
+  GM_KIND_DISPATCH(k_ks_counts, ks_grid(s, width), s, s->d, s->lv, s->lcap, s->st, level, counts_dev);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int gm_ks_children(gm_solver* s, int level, const uint64_t* offsets_dev, uint64_t* keys_dev, uint32_t* owners_dev,
+                   int world) {
+  int rc = ks_check(s, level);
+  if (rc) return rc;
+  uint64_t width = 0;
+  if ((rc = gm_ks_level_size(s, level, &width))) return rc;
+  if (!width) return 0;
+  if (!offsets_dev || !keys_dev || !owners_dev || world < 1) return fail(GM_EINVAL, "bad argument");
+  GM_KIND_DISPATCH(k_ks_children, ks_grid(s, width), s, s->d, s->lv, s->lcap, s->st, level, offsets_dev,
+                   (u64*)keys_dev, owners_dev, (uint32_t)world);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int gm_ks_reduce(gm_solver* s, int level, const uint64_t* offsets_dev, const uint32_t* child_words_dev) {
+  int rc = ks_check(s, level);
+  if (rc) return rc;
+  uint64_t width = 0;
+  if ((rc = gm_ks_level_size(s, level, &width))) return rc;
+  if (!width) return 0;
+  if (!offsets_dev || !child_words_dev) return fail(GM_EINVAL, "bad argument");
+  GM_KIND_DISPATCH(k_ks_reduce, ks_grid(s, width), s, s->d, s->tab, s->mask, s->lv, s->lcap, s->st, level,
+                   offsets_dev, child_words_dev);
+  HIPCHK(hipGetLastError());
+  return ks_errors(s);
+}
+
+int gm_ks_end(gm_solver* s, gm_result* out) {
+  int rc = ks_check(s, 0);
+  if (rc) return rc;
+  if (!out) return fail(GM_EINVAL, "null result");
+  memset(out, 0, sizeof *out);
+  const int T = s->d.max_levels;
+  hipLaunchKernelGGL(k_root_word, dim3(1), dim3(64), 0, s->stream, s->tab, s->mask, s->d.root, s->st);
+  HIPCHK(hipGetLastError());
+  std::vector<unsigned char> host(devstate_bytes(T));
+  HIPCHK(hipMemcpyAsync(host.data(), s->st, host.size(), hipMemcpyDeviceToHost, s->stream));
+  HIPCHK(hipStreamSynchronize(s->stream));
+  const DevState* hs = (const DevState*)host.data();
+  out->positions = hs->cursor_front + hs->cursor_back;
+  out->edges = hs->edges;
+  out->primitives = hs->prims;
+  out->max_level_width = (uint32_t)hs->max_width;
+  uint32_t lv = 0;
+  for (int L = 0; L < T; L++) {
+    const LevelSeg& g = hs->seg[L];
+    if ((g.fe - g.fb) + (g.c2hi - g.c2lo) > 0) lv++;
+  }
+  out->levels = lv;
+  out->root_word = hs->root_word;  // NO_WORD on every rank but the root's owner
+  if (hs->root_word != NO_WORD) {
+    out->root_value = (int32_t)(hs->root_word & 3u);
+    out->root_remoteness = hs->root_word >> 2;
+  }
+  if (hs->err) {
+    bool full = hs->err & (ERR_TABLE_FULL | ERR_LEVELS_FULL);
+    return fail(full ? GM_EFULL : GM_ECORRUPT, "shard %d/%d:%s", s->rank, s->world, err_text(hs->err).c_str());
+  }
+  return 0;
+}

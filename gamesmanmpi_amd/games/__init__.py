@@ -127,6 +127,14 @@ class GameSpec:
             pr.ctypes.data))
         return pr, nc, ch
 
+    def host_level(self, keys):
+        """Tier of each key (int32[n]) from the descriptor, on the host."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        out = np.zeros(len(keys), np.int32)
+        _lib.check(_lib.load().gm_host_level(self.id, keys.ctypes.data,
+                                             len(keys), out.ctypes.data))
+        return out
+
     def owners_host(self, keys, world_size):
         """GameState.get_hash(world_size) (src/game_state.py:22-30)."""
         keys = np.ascontiguousarray(keys, dtype=np.uint64)

@@ -1,0 +1,308 @@
+"""md5-sharded solve of keyed (HASHED) tables (keyed).
+
+The reference partitions positions over MPI ranks by
+owner(pos) = md5(str(pos)) % world (GameState.get_hash,
+src/game_state.py:22-30) and sends one pickled LOOK_UP / RESOLVE message per
+tree edge (src/process.py:146-185).  Here the partition rule is the same,
+but each level moves its traffic in two bulk all-to-all(v) exchanges:
+
+  forward  (L = 0 .. T-2)  own level-L positions -> children + owners
+                           (gm_ks_expand), deduplicated, bucketed by owner,
+                           all-to-all, inserted by their owners (gm_ks_insert)
+  backward (L = T-1 .. 0)  own level-L positions -> children in gen_moves
+                           order (gm_ks_counts / gm_ks_children), queried at
+                           their owners (gm_solver_query), words sent back,
+                           reduced (gm_ks_reduce)
+
+`keyed_solve` is written once over the shards LOCAL to this process and an
+exchange object:
+  TorchExchange  one shard per process (torch.distributed.run); all_to_all
+                 _single over RCCL on GPUs (gloo in the CPU tests)
+  GroupExchange  every shard of a job in one process: the exchange is a
+                 transpose of the send lists (runs the md5 job on one GPU)
+A shard is `GpuShard` (libgamesman_hip.so, this module); the CPU tests drive
+the same loop with a host shard built on the descriptor's host functions.
+"""
+import contextlib
+import ctypes
+import time
+
+from . import _lib
+from .games import GameSpec
+from .solver import SolveResult, Solver
+
+
+# ---------------------------------------------------------------------------
+# exchanges
+# ---------------------------------------------------------------------------
+class GroupExchange:
+    """All shards in this process: recv[dst][src] = send[src][dst]."""
+
+    def all_to_all(self, send):
+        n = len(send)
+        return [[send[src][dst] for src in range(n)] for dst in range(n)]
+
+    def allreduce_sum(self, values):
+        return [sum(col) for col in zip(*values)]
+
+
+class TorchExchange:
+    """One shard per process over the initialised torch.distributed default
+    group; tensors live on `device` (cuda for RCCL, cpu for gloo)."""
+
+    def __init__(self, device):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist, self.device = torch, dist, device
+
+    def all_to_all(self, send):
+        torch, dist = self.torch, self.dist
+        (lists,) = send
+        in_sizes = [int(t.numel()) for t in lists]
+        sizes = torch.tensor(in_sizes, dtype=torch.int64, device=self.device)
+        got = torch.empty_like(sizes)
+        dist.all_to_all_single(got, sizes)
+        out_sizes = [int(x) for x in got.tolist()]
+        inp = torch.cat(lists)
+        out = torch.empty(sum(out_sizes), dtype=inp.dtype, device=self.device)
+        dist.all_to_all_single(out, inp, out_sizes, in_sizes)
+        return [list(torch.split(out, out_sizes))]
+
+    def allreduce_sum(self, values):
+        (v,) = values
+        t = self.torch.tensor(v, dtype=self.torch.int64, device=self.device)
+        self.dist.all_reduce(t)
+        return [int(x) for x in t.tolist()]
+
+
+# ---------------------------------------------------------------------------
+# the GPU shard
+# ---------------------------------------------------------------------------
+class GpuShard:
+    """Rank `rank`'s keyed table on a GPU: a HASHED Solver driven step by
+    step through gm_ks_*.  `positions`: bound on this shard's positions
+    (default: 2x its md5 share of the game's bound)."""
+
+    def __init__(self, spec, rank, world, device=None, positions=0,
+                 stream=None):
+        import torch
+        self.torch = torch
+        self.spec = spec if isinstance(spec, GameSpec) else GameSpec(*spec)
+        self.rank, self.world = int(rank), int(world)
+        if not positions:
+            positions = 2 * self.spec.positions_bound // self.world + 4096
+        dev = torch.device(device if device is not None else "cuda")
+        self.stream = stream or torch.cuda.Stream(device=dev)
+        self.solver = Solver(self.spec, positions=positions, device=dev,
+                             layout="hashed", rank=self.rank,
+                             world=self.world, stream=self.stream)
+        self.device = self.solver.device
+        self.h = self.solver.handle
+        self.L = _lib.load()
+        self.fanout = float(_lib.GM_MAXCHILD)  # children per position seen
+
+    def context(self):
+        torch = self.torch
+        stack = contextlib.ExitStack()
+        stack.enter_context(torch.cuda.device(self.device))
+        stack.enter_context(torch.cuda.stream(self.stream))
+        return stack
+
+    def begin(self, root_owned):
+        _lib.check(self.L.gm_ks_begin(self.h, 1 if root_owned else 0))
+
+    def level_size(self, level):
+        n = ctypes.c_uint64()
+        _lib.check(self.L.gm_ks_level_size(self.h, level, ctypes.byref(n)))
+        return n.value
+
+    def expand(self, level):
+        """(child keys int64, owners int32) of the own level-L positions, in
+        no particular order (duplicates included)."""
+        torch = self.torch
+        width = self.level_size(level)
+        cap = int(width * min(self.fanout * 1.25 + 1, _lib.GM_MAXCHILD)) + 64
+        n = ctypes.c_uint64()
+        while True:
+            keys = torch.empty(cap, dtype=torch.int64, device=self.device)
+            owners = torch.empty(cap, dtype=torch.int32, device=self.device)
+            rc = self.L.gm_ks_expand(self.h, level, keys.data_ptr(),
+                                     owners.data_ptr(), cap, self.world,
+                                     ctypes.byref(n))
+            if rc == _lib.GM_EFULL and n.value > cap:
+                cap = n.value  # exact size now known: expand again
+                continue
+            _lib.check(rc)
+            break
+        if width:
+            self.fanout = max(1.0, n.value / width)
+        return keys[:n.value], owners[:n.value]
+
+    def insert(self, level, keys):
+        keys = keys.contiguous()
+        if keys.numel():
+            _lib.check(self.L.gm_ks_insert(self.h, level, keys.data_ptr(),
+                                           keys.numel()))
+
+    def finalize(self, level):
+        _lib.check(self.L.gm_ks_finalize(self.h, level))
+
+    def children(self, level):
+        """(offsets int64[n+1], child keys, owners) of the own level-L
+        positions, children of position i at [offsets[i], offsets[i+1])."""
+        torch = self.torch
+        n = self.level_size(level)
+        offsets = torch.zeros(n + 1, dtype=torch.int64, device=self.device)
+        if n == 0:
+            empty = torch.empty(0, dtype=torch.int64, device=self.device)
+            return offsets, empty, empty.to(torch.int32)
+        counts = torch.empty(n, dtype=torch.int64, device=self.device)
+        _lib.check(self.L.gm_ks_counts(self.h, level, counts.data_ptr()))
+        offsets[1:] = torch.cumsum(counts, 0)
+        total = int(offsets[-1].item())
+        keys = torch.empty(max(1, total), dtype=torch.int64,
+                           device=self.device)
+        owners = torch.empty(max(1, total), dtype=torch.int32,
+                             device=self.device)
+        if total:
+            _lib.check(self.L.gm_ks_children(
+                self.h, level, offsets.data_ptr(), keys.data_ptr(),
+                owners.data_ptr(), self.world))
+        return offsets, keys[:total], owners[:total]
+
+    def lookup(self, keys):
+        """Words of keys this shard owns (GM_NO_WORD if absent)."""
+        torch = self.torch
+        keys = keys.contiguous()
+        words = torch.empty(keys.numel(), dtype=torch.int32,
+                            device=self.device)
+        if keys.numel():
+            _lib.check(self.L.gm_solver_query(self.h, keys.data_ptr(),
+                                              keys.numel(),
+                                              words.data_ptr()))
+        return words
+
+    def reduce(self, level, offsets, words):
+        if offsets.numel() <= 1:
+            return
+        words = words.contiguous()
+        if words.numel() == 0:  # every position primitive: any valid address
+            words = self.torch.zeros(1, dtype=self.torch.int32,
+                                     device=self.device)
+        _lib.check(self.L.gm_ks_reduce(self.h, level, offsets.data_ptr(),
+                                       words.data_ptr()))
+
+    def end(self):
+        r = _lib.gm_result()
+        _lib.check(self.L.gm_ks_end(self.h, ctypes.byref(r)))
+        return r
+
+    def dump(self):
+        """(keys, value, remoteness) of the positions this shard owns."""
+        return self.solver.dump()
+
+
+# ---------------------------------------------------------------------------
+# the level loop
+# ---------------------------------------------------------------------------
+def _bucket(torch, keys, owners, world):
+    """keys grouped by owner: (list of `world` tensors, permutation such
+    that cat(list) == keys[perm])."""
+    perm = torch.argsort(owners, stable=True)
+    counts = torch.bincount(owners.long(), minlength=world).tolist()
+    return list(torch.split(keys[perm], counts)), perm
+
+
+def keyed_solve(shards, exchange):
+    """Solve the job whose LOCAL shards are `shards` (every rank for a
+    group, this rank's one shard under torch.distributed).  Returns the
+    whole job's SolveResult (the same on every rank)."""
+    s0 = shards[0]
+    torch, spec, world = s0.torch, s0.spec, s0.world
+    T = spec.max_levels
+    root_owner = int(spec.owners_host([spec.root_key], world)[0])
+    widths = [[0] * T for _ in shards]
+    ctx = [sh.context() for sh in shards]
+    with contextlib.ExitStack() as stack:
+        for c in ctx:
+            stack.enter_context(c)
+        t0 = time.perf_counter()
+        for sh in shards:
+            sh.begin(sh.rank == root_owner)
+        for L in range(T - 1):
+            send = []
+            for sh in shards:
+                keys, owners = sh.expand(L)
+                if keys.numel():  # duplicates need not travel
+                    keys, inv = torch.unique(keys, return_inverse=True)
+                    own = torch.empty(keys.numel(), dtype=owners.dtype,
+                                      device=owners.device)
+                    own[inv] = owners
+                    owners = own
+                send.append(_bucket(torch, keys, owners, world)[0])
+            for sh, lists in zip(shards, exchange.all_to_all(send)):
+                sh.insert(L, torch.cat(lists))
+                sh.finalize(L)
+        t1 = time.perf_counter()
+        for L in range(T - 1, -1, -1):
+            queries, state = [], []
+            for g, sh in enumerate(shards):
+                offsets, keys, owners = sh.children(L)
+                widths[g][L] = offsets.numel() - 1
+                lists, perm = _bucket(torch, keys, owners, world)
+                queries.append(lists)
+                state.append((offsets, perm, keys.numel()))
+            replies = []
+            for sh, lists in zip(shards, exchange.all_to_all(queries)):
+                sizes = [int(t.numel()) for t in lists]
+                replies.append(list(torch.split(sh.lookup(torch.cat(lists)),
+                                                sizes)))
+            answers = exchange.all_to_all(replies)
+            for sh, lists, (offsets, perm, n) in zip(shards, answers, state):
+                words = torch.empty(n, dtype=torch.int32, device=sh.device)
+                words[perm] = torch.cat(lists)
+                sh.reduce(L, offsets, words)
+        t2 = time.perf_counter()
+        res = [sh.end() for sh in shards]
+    local = []
+    for r, w in zip(res, widths):
+        owned_root = (r.root_word + 1) if r.root_word != _lib.GM_NO_WORD else 0
+        local.append([r.positions, r.edges, r.primitives, owned_root] + w)
+    tot = exchange.allreduce_sum(local)
+    t3 = time.perf_counter()
+    if tot[3] == 0:
+        raise _lib.GmError(_lib.GM_ECORRUPT, "root unresolved")
+    word = tot[3] - 1
+    per_level = tot[4:]
+    return SolveResult(
+        root_value=word & 3, root_remoteness=word >> 2, positions=tot[0],
+        edges=tot[1], primitives=tot[2],
+        levels=sum(1 for x in per_level if x),
+        max_level_width=max(per_level), ms_total=(t3 - t0) * 1e3,
+        ms_forward=(t1 - t0) * 1e3, ms_backward=(t2 - t1) * 1e3,
+        extra={"layout": "hashed", "partition": "md5", "world": world,
+               "root_owner": root_owner})
+
+
+def group_keyed_solve(spec, world, device=None):
+    """Every md5 shard of a `world`-rank job in this process, on one GPU
+    and one stream.  Returns (SolveResult, [GpuShard])."""
+    import torch
+    spec = spec if isinstance(spec, GameSpec) else GameSpec(*spec)
+    dev = torch.device(device if device is not None else "cuda")
+    stream = torch.cuda.Stream(device=dev)
+    shards = [GpuShard(spec, g, world, device=dev, stream=stream)
+              for g in range(world)]
+    return keyed_solve(shards, GroupExchange()), shards
+
+
+def dist_keyed_solve(spec, device=None, positions=0):
+    """This process's shard of an md5-sharded job over the initialised
+    torch.distributed default group; `positions`: bound for the whole job
+    (0: the game's own).  Returns (SolveResult, GpuShard)."""
+    import torch.distributed as dist
+    world = dist.get_world_size()
+    per_shard = 2 * int(positions) // world + 4096 if positions else 0
+    shard = GpuShard(spec, dist.get_rank(), world, device=device,
+                     positions=per_shard)
+    return keyed_solve([shard], TorchExchange(shard.device)), shard

@@ -52,7 +52,9 @@ class Solver:
         """layout: "auto" (dense when the descriptor supports it and the
         table fits max_table_bytes, else hashed), "dense" or "hashed".
         rank/world > 1: this object is one shard of a dense multi-GPU solve
-        (see gamesmanmpi_amd.dist); stream: a torch stream to run on."""
+        (gamesmanmpi_amd.dist), or with layout="hashed" one md5 shard of a
+        keyed solve (gamesmanmpi_amd.keyed; `positions` is then this
+        shard's bound); stream: a torch stream to run on."""
         import torch
         if not torch.cuda.is_available():
             raise RuntimeError("gamesmanmpi_amd needs a ROCm GPU (gfx950); "
@@ -78,7 +80,7 @@ class Solver:
         self._free()
         plan = _lib.gm_plan_t()
         flags = _lib.GM_F_FORCE_HASHED if self.layout == "hashed" else 0
-        if self.world > 1:
+        if self.world > 1 and self.layout != "hashed":
             _lib.check(L.gm_plan_shard(self.spec.id, self.rank, self.world,
                                        flags, self.max_table_bytes,
                                        ctypes.byref(plan)))

@@ -88,6 +88,9 @@ def build_parser():
     return p
 
 
+DENSE_STEMS = ("four_to_one", "sum_four_to_one")  # rank-indexable descriptors
+
+
 def write_stats(statsdir, rank, spec, solver, result):
     """<statsdir>/stats/<rank>/solution.npz (+ meta.json)."""
     import numpy as np
@@ -134,13 +137,22 @@ def main(argv=None):
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        from gamesmanmpi_amd.dist import ShardedSolver
-        solver = ShardedSolver(spec, rank, world, device="cuda:%d" % local)
+        if spec.name in DENSE_STEMS and args.layout != "hashed":
+            # top-heap blocks, RCCL halo exchange (gamesmanmpi_amd.dist)
+            from gamesmanmpi_amd.dist import ShardedSolver
+            solver = ShardedSolver(spec, rank, world, device="cuda:%d" % local)
+            result = solver.solve()
+        else:
+            # the reference's md5 partition, all-to-all per level (keyed.py)
+            from gamesmanmpi_amd.keyed import dist_keyed_solve
+            result, shard = dist_keyed_solve(spec, device="cuda:%d" % local,
+                                             positions=args.positions)
+            solver = shard.solver
     else:
         from gamesmanmpi_amd.solver import Solver
         solver = Solver(spec, positions=args.positions,
                         device="cuda:%d" % local, layout=args.layout)
-    result = solver.solve()
+        result = solver.solve()
     if rank == 0:
         print(result.root_line, flush=True)  # src/process.py:47-52
         if args.json:
