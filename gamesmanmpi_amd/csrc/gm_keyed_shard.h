@@ -46,23 +46,31 @@ __global__ void k_ks_seed(gm_slot* tab, u64 mask, u64* lv, DevState* st, u64 roo
   }
 }
 
+// children of the own level-L positions (LDS-staged appends at `cursor`);
+// owners are filled afterwards by k_owner over the emitted keys
 template <int KIND>
 __global__ __launch_bounds__(256) void k_ks_expand(Desc d, const u64* lv, u64 lcap, DevState* st, int L,
-                                                   u64* keys_out, uint32_t* owners_out, u64 cap, u64* cursor,
-                                                   uint32_t P) {
+                                                   u64* keys_out, u64 cap, u64* cursor) {
+  __shared__ StageLDS stage;
+  stage_init(stage);
   const LevelSeg s = st->seg[L];
   const u64 n = (s.fe - s.fb) + (s.c2hi - s.c2lo);
-  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
-    const u64 key = level_key(lv, lcap, s, i);
-    if (Game<KIND>::prim(d, key) != UNDECIDED) continue;
-    Game<KIND>::children(d, key, [&](u64 child, int) {
-      const u64 j = atomicAdd(cursor, 1ull);
-      if (j < cap) {
-        keys_out[j] = child;
-        owners_out[j] = owner_of(d, child, P);
-      }
-    });
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  auto store = [&](int, u64 g, u64 key) {
+    if (g < cap) keys_out[g] = key;
+  };
+  for (u64 base = (u64)blockIdx.x * blockDim.x; base < n; base += stride) {  // block-uniform
+    const u64 i = base + threadIdx.x;
+    if (i < n) {
+      const u64 key = level_key(lv, lcap, s, i);
+      if (Game<KIND>::prim(d, key) == UNDECIDED)
+        Game<KIND>::children(d, key, [&](u64 child, int) {
+          if (!stage_push(stage, 0, child)) store(0, atomicAdd(cursor, 1ull), child);
+        });
+    }
+    if (stage_should_flush(stage)) stage_flush(stage, cursor, cursor, store);
   }
+  stage_flush(stage, cursor, cursor, store);
 }
 
 // insert received keys (all owned by this rank); new ones join the level
@@ -70,21 +78,29 @@ __global__ __launch_bounds__(256) void k_ks_expand(Desc d, const u64* lv, u64 lc
 template <int KIND>
 __global__ __launch_bounds__(256) void k_ks_insert(Desc d, gm_slot* tab, u64 mask, u64* lv, u64 lcap, DevState* st,
                                                    int L, const u64* keys, u64 n) {
+  __shared__ StageLDS stage;
+  stage_init(stage);
   uint32_t err = 0;
-  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
-    const u64 key = keys[i];
-    if (!table_insert(tab, mask, key, &st->err)) continue;
-    const int step = Game<KIND>::level(d, key) - L;
-    if (step == 1) {
-      const u64 f = atomicAdd(&st->cursor_front, 1ull);
-      if (f < lcap) lv[f] = key;
-    } else if (step == 2) {
-      const u64 b = atomicAdd(&st->cursor_back, 1ull);
-      if (b < lcap) lv[lcap - 1 - b] = key;
-    } else {
-      err |= ERR_BAD_STEP;
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  auto store = [&](int q, u64 g, u64 key) { level_store(lv, lcap, q, g, key); };
+  for (u64 base = (u64)blockIdx.x * blockDim.x; base < n; base += stride) {  // block-uniform
+    const u64 i = base + threadIdx.x;
+    if (i < n) {
+      const u64 key = keys[i];
+      if (table_insert(tab, mask, key, &st->err)) {
+        const int step = Game<KIND>::level(d, key) - L;
+        if (step == 1 || step == 2) {
+          const int q = step - 1;
+          if (!stage_push(stage, q, key))
+            store(q, atomicAdd(q ? &st->cursor_back : &st->cursor_front, 1ull), key);
+        } else {
+          err |= ERR_BAD_STEP;
+        }
+      }
     }
+    if (stage_should_flush(stage)) stage_flush(stage, &st->cursor_front, &st->cursor_back, store);
   }
+  stage_flush(stage, &st->cursor_front, &st->cursor_back, store);
   if (err) atomicOr(&st->err, err);
 }
 

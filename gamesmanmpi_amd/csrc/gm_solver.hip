@@ -286,7 +286,7 @@ struct DevState {
   u64 max_width;
   uint32_t err;
   uint32_t root_word;
-  u64 ks_cursor;    // keyed shards: child pairs emitted by k_ks_expand
+  u64 ks_cursor;    // keyed shards: children emitted by k_ks_expand
   u64 red[5];     // cross-shard reduction: positions, edges, prims, root word + 1, err
   LevelSeg seg[1];  // [max_levels + 2]
 };
@@ -367,6 +367,63 @@ __device__ __forceinline__ void block_add(u64* dst, u64 v) {
   __syncthreads();
 }
 
+// Block-staged appends to up to two global stacks (Guideline 12).  Every
+// new key used to cost one wave-aggregated atomic on ONE global cursor; a
+// device-scope counter saturates near 90 adds/us, which bounded the hashed
+// forward (toot 6x4: 324 ms on the widest level).  Keys now go to LDS with
+// LDS atomics and a block reserves global space once per flush.  A key that
+// finds its LDS queue full is appended straight to global memory (rare).
+constexpr uint32_t kStageCap = 1024;  // keys per queue (2 queues: 16 KB, 8+ blocks per CU)
+struct StageLDS {
+  u64 key[2][kStageCap];
+  uint32_t n[2];
+  u64 base[2];
+};
+
+__device__ __forceinline__ void stage_init(StageLDS& s) {
+  if (threadIdx.x == 0) s.n[0] = s.n[1] = 0;
+  __syncthreads();
+}
+
+// queue q: true if staged, false if the caller must append directly
+__device__ __forceinline__ bool stage_push(StageLDS& s, int q, u64 key) {
+  const uint32_t j = atomicAdd(&s.n[q], 1u);
+  if (j < kStageCap) {
+    s.key[q][j] = key;
+    return true;
+  }
+  return false;
+}
+
+// Block-uniform: true when a queue is at least 3/4 full.  Both barriers
+// are needed so every thread reads the same counts before the next pushes.
+__device__ __forceinline__ bool stage_should_flush(StageLDS& s) {
+  __syncthreads();
+  const bool f = s.n[0] >= kStageCap * 3 / 4 || s.n[1] >= kStageCap * 3 / 4;
+  __syncthreads();
+  return f;
+}
+
+// Reserve [base, base + n) on cursor q with one atomic per queue and copy
+// the staged keys out with coalesced stores: store(q, global_index, key).
+template <class Store>
+__device__ __forceinline__ void stage_flush(StageLDS& s, u64* cur0, u64* cur1, Store store) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int q = 0; q < 2; q++) {
+      const uint32_t c = min(s.n[q], kStageCap);
+      s.n[q] = c;
+      s.base[q] = c ? atomicAdd(q ? cur1 : cur0, (u64)c) : 0;
+    }
+  }
+  __syncthreads();
+  for (int q = 0; q < 2; q++)
+    for (uint32_t j = threadIdx.x; j < s.n[q]; j += blockDim.x) store(q, s.base[q] + j, s.key[q][j]);
+  __syncthreads();
+  if (threadIdx.x == 0) s.n[0] = s.n[1] = 0;
+  __syncthreads();
+}
+
 // ---------------------------------------------------------------------------
 // kernels
 // ---------------------------------------------------------------------------
@@ -385,32 +442,43 @@ __global__ void k_seed(gm_slot* tab, u64 mask, u64* lv, DevState* st, u64 root) 
   }
 }
 
-// K1+K2: expand level L, insert children, append new ones to L+1 / L+2.
-// The per-thread atomicAdd on a wave-uniform cursor is combined into one
-// atomic per wave by the AMDGPU atomic optimizer (Guideline 12).
+// append a new level-(L+1) key (q = 0, front stack) or level-(L+2) key
+// (q = 1, back stack) at global stack index g
+__device__ __forceinline__ void level_store(u64* lv, u64 lcap, int q, u64 g, u64 key) {
+  if (g < lcap) lv[q ? lcap - 1 - g : g] = key;
+}
+
+// K1+K2: expand level L, insert children, append new ones to L+1 / L+2
+// through the block's LDS stage (one global atomic per block flush).
 template <int KIND>
 __global__ __launch_bounds__(256) void k_expand(Desc d, gm_slot* tab, u64 mask, u64* lv, u64 lcap,
                                                 DevState* st, int L) {
+  __shared__ StageLDS stage;
+  stage_init(stage);
   const LevelSeg s = st->seg[L];
   const u64 n = (s.fe - s.fb) + (s.c2hi - s.c2lo);
   const u64 stride = (u64)gridDim.x * blockDim.x;
   uint32_t err = 0;
-  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    u64 key = level_key(lv, lcap, s, i);
-    if (Game<KIND>::prim(d, key) != UNDECIDED) continue;  // lookup(): primitive, no children
-    Game<KIND>::children(d, key, [&](u64 child, int step) {
-      if (!table_insert(tab, mask, child, &st->err)) return;
-      if (step == 1) {
-        u64 f = atomicAdd(&st->cursor_front, 1ull);
-        if (f < lcap) lv[f] = child;
-      } else if (step == 2) {
-        u64 b = atomicAdd(&st->cursor_back, 1ull);
-        if (b < lcap) lv[lcap - 1 - b] = child;
-      } else {
-        err |= ERR_BAD_STEP;
-      }
-    });
+  auto store = [&](int q, u64 g, u64 key) { level_store(lv, lcap, q, g, key); };
+  for (u64 base = (u64)blockIdx.x * blockDim.x; base < n; base += stride) {  // block-uniform
+    const u64 i = base + threadIdx.x;
+    if (i < n) {
+      const u64 key = level_key(lv, lcap, s, i);
+      if (Game<KIND>::prim(d, key) == UNDECIDED)  // lookup(): primitive, no children
+        Game<KIND>::children(d, key, [&](u64 child, int step) {
+          if (!table_insert(tab, mask, child, &st->err)) return;
+          if (step != 1 && step != 2) {
+            err |= ERR_BAD_STEP;
+            return;
+          }
+          const int q = step - 1;
+          if (!stage_push(stage, q, child))
+            store(q, atomicAdd(q ? &st->cursor_back : &st->cursor_front, 1ull), child);
+        });
+    }
+    if (stage_should_flush(stage)) stage_flush(stage, &st->cursor_front, &st->cursor_back, store);
   }
+  stage_flush(stage, &st->cursor_front, &st->cursor_back, store);
   if (err) atomicOr(&st->err, err);
 }
 
@@ -1448,8 +1516,8 @@ int gm_ks_expand(gm_solver* s, int level, uint64_t* keys_dev, uint32_t* owners_d
   uint64_t width = 0;
   if ((rc = gm_ks_level_size(s, level, &width))) return rc;
   HIPCHK(hipMemsetAsync(&s->st->ks_cursor, 0, sizeof(u64), s->stream));
-  GM_KIND_DISPATCH(k_ks_expand, ks_grid(s, width), s, s->d, s->lv, s->lcap, s->st, level, (u64*)keys_dev, owners_dev,
-                   cap, &s->st->ks_cursor, (uint32_t)world);
+  GM_KIND_DISPATCH(k_ks_expand, ks_grid(s, width), s, s->d, s->lv, s->lcap, s->st, level, (u64*)keys_dev, cap,
+                   &s->st->ks_cursor);
   HIPCHK(hipGetLastError());
   u64 got = 0;
   HIPCHK(hipMemcpyAsync(&got, &s->st->ks_cursor, sizeof got, hipMemcpyDeviceToHost, s->stream));
@@ -1457,6 +1525,10 @@ int gm_ks_expand(gm_solver* s, int level, uint64_t* keys_dev, uint32_t* owners_d
   *n = got;
   if (got > cap) return fail(GM_EFULL, "expand of level %d emits %llu children (cap %llu)", level,
                              (unsigned long long)got, (unsigned long long)cap);
+  if (got)
+    hipLaunchKernelGGL(k_owner, dim3(ks_grid(s, got)), dim3(kBlock), 0, s->stream, s->d, (const u64*)keys_dev, got,
+                       (uint32_t)world, owners_dev);
+  HIPCHK(hipGetLastError());
   return 0;
 }
 
