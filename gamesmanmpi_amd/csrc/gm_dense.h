@@ -122,11 +122,9 @@ __device__ __forceinline__ bool reach_bit(const u64* bits, u64 pos) {
 }
 
 // Grid-stride rounds each wave keeps in flight.  Measured on MI355X
-// (2^30-position solve): 1/1 -> 92 ms, pull 4 / resolve 2 -> 111 ms (the
-// extra registers cost occupancy: resolve 104 VGPRs, 4 waves/SIMD), so the
-// loads of one round per wave are what the memory system sees.
+// (2^30-position solve): 1 -> 92 ms, pull 4 / resolve 2 -> 111 ms (the
+// extra registers cost occupancy), so one round per wave it is.
 constexpr int PULL_UNROLL = 1;
-constexpr int RESOLVE_UNROLL = 1;
 
 // Forward, PULL form, target level L: each non-hole slot of level L ORs the
 // reach bits of its parents -- the positions one move away, i.e. one heap +1
@@ -418,82 +416,116 @@ __global__ __launch_bounds__(256) void k_dense_resolve_words(Desc d, DenseView v
   block_add(&st->prims, prims);
 }
 
-// backward, level L: resolve every reached owned position from its children
-template <int MAXH, bool POW2>
+// XCD-aware split of [0, n) (MI355X dispatches workgroup b to XCD b % 8):
+// the blocks of one XCD grid-stride over one contiguous, 64-aligned chunk,
+// so the child words that neighbouring prefixes share are fetched into ONE
+// XCD's L2 instead of all eight.  Grids that are not a multiple of 8 blocks
+// fall back to one plain grid-stride range.
+constexpr uint32_t kXcds = 8;
+struct XcdRange {
+  u64 first, end, stride;
+};
+__device__ __forceinline__ XcdRange xcd_range(u64 n) {
+  const uint32_t G = gridDim.x;
+  const uint32_t nx = (G >= kXcds && G % kXcds == 0) ? kXcds : 1;
+  const uint32_t x = blockIdx.x % nx, lb = blockIdx.x / nx;
+  const u64 chunk = ((n + nx - 1) / nx + 63) & ~63ull;
+  const u64 b = min(n, (u64)x * chunk);
+  XcdRange r;
+  r.end = min(n, b + chunk);
+  r.first = b + (u64)lb * blockDim.x + threadIdx.x;
+  r.stride = (u64)(G / nx) * blockDim.x;
+  return r;
+}
+
+// One level row of words for child loads.  BUF: a raw buffer resource
+// (32-bit byte offsets, hardware range check): an absent child is given an
+// out-of-range offset and reads 0 with no memory access; a missing row
+// (level past the table) has zero records.  !BUF: 64-bit global loads for
+// rows of 2^30 words or more.
+template <bool BUF>
+struct WordRow;
+template <>
+struct WordRow<true> {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ __forceinline__ void init(const uint32_t* base, u64 nwords) {
+    r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(uint32_t)(nwords * 4u), 0x00020000);
+  }
+  __device__ __forceinline__ uint32_t at(u64 idx, bool ok) const {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, ok ? (uint32_t)idx * 4u : 0xFFFFFFFCu, 0, 0);
+  }
+};
+template <>
+struct WordRow<false> {
+  const uint32_t* p;
+  __device__ __forceinline__ void init(const uint32_t* base, u64 nwords) { p = nwords ? base : nullptr; }
+  __device__ __forceinline__ uint32_t at(u64 idx, bool ok) const { return ok ? p[idx] : 0u; }
+};
+
+// backward, level L: resolve every reached owned position from its children.
+// Absent children read as 0 (= WIN, remoteness 0, which no resolved
+// position holds), neutral for every term of the reduction, so each child
+// costs a load and four ALU ops:
+//   value       WIN if any child LOSS, else TIE if any TIE, else DRAW if any
+//               DRAW, else LOSS                      (flag bits of child values)
+//   remoteness  WIN: 1 + min rem over LOSS children  (min of LOSS words)
+//               else 1 + max rem over all children   (max of words, rem = w>>2)
+// The reach-bit word is loaded with the child words (children of a non-hole
+// slot are never holes), so a round costs one memory latency.
+template <int MAXH, bool POW2, bool BUF>
 __global__ __launch_bounds__(256) void k_dense_resolve(Desc d, DenseView v, uint32_t* words, const u64* bits, u64 L,
                                                        DevState* st) {
   const uint32_t S = d.root_sum - (uint32_t)L;
   uint32_t* mine = words + L * v.Wl;
-  const uint32_t* n1 = words + (L + 1) * v.Wl;  // only dereferenced when S >= 1
-  const uint32_t* n2 = words + (L + 2) * v.Wl;  // only dereferenced when S >= 2
-  const u64 stride = (u64)gridDim.x * blockDim.x;
-  constexpr uint32_t ABSENT = 0xFFFFFFFDu;  // "no such child" (register only)
-  constexpr uint32_t SKIP = 0xFFFFFFFCu;    // slot not resolved this round
+  WordRow<BUF> n1, n2;  // levels L+1, L+2 (empty rows past the last level)
+  n1.init(words + (L + 1) * v.Wl, S >= 1 ? v.Wl : 0);
+  n2.init(words + (L + 2) * v.Wl, S >= 2 ? v.Wl : 0);
   u64 npos = 0, edges = 0, prims = 0;
   uint32_t err = 0;
   WaveDigits<MAXH, POW2> wd;
   wd.init(d);
-  const u64 n = v.p_hi - v.p_lo;
-  for (u64 i0 = (u64)blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += RESOLVE_UNROLL * stride) {
-    // gather the child words of RESOLVE_UNROLL rounds first
-    uint32_t c[RESOLVE_UNROLL][2 * MAXH];
-    uint32_t own[RESOLVE_UNROLL];
+  const XcdRange r = xcd_range(v.p_hi - v.p_lo);
+  for (u64 i0 = r.first; i0 < r.end; i0 += r.stride) {
+    const u64 p = v.p_lo + i0;
+    const u64 q = p - v.base_off;
+    uint32_t h[MAXH];
+    const uint32_t s = wd.digits(d, p & ~63ull, p, h);
+    const bool valid = s <= S && S - s <= d.heap[0];  // not a hole
+    const u64 rw = valid ? bits[(L * v.Wbl + q) >> 6] : 0ull;
+    const uint32_t h0 = S - s;
+    uint32_t c[2 * MAXH];
+    int nch = 0;
+    c[0] = n1.at(q, valid && h0 >= 1);
+    c[1] = n2.at(q, valid && h0 >= 2);
+    nch += (h0 >= 1) + (h0 >= 2);
 #pragma unroll
-    for (int u = 0; u < RESOLVE_UNROLL; u++) {
-      const u64 p = v.p_lo + i0 + u * stride;
-      const u64 q = p - v.base_off;
-      own[u] = SKIP;
-#pragma unroll
-      for (int j = 0; j < 2 * MAXH; j++) c[u][j] = ABSENT;
-      if (p >= v.p_hi) continue;
-      uint32_t h[MAXH];
-      uint32_t s = wd.digits(d, p & ~63ull, p, h);
-      if (s > S || S - s > d.heap[0]) continue;
-      if (!reach_bit(bits, L * v.Wbl + q)) continue;
-      own[u] = 0;
-      if (S == 0) continue;  // the primitive: no children
-      const uint32_t h0 = S - s;
-      c[u][0] = h0 >= 1 ? n1[q] : ABSENT;
-      c[u][1] = h0 >= 2 ? n2[q] : ABSENT;
-#pragma unroll
-      for (int i = 1; i < MAXH; i++) {
-        const bool live = (MAXH <= 8) || i < d.nheaps;
-        c[u][2 * i] = (live && h[i] >= 1) ? n1[q - d.pstride[i]] : ABSENT;
-        c[u][2 * i + 1] = (live && h[i] >= 2) ? n2[q - 2 * d.pstride[i]] : ABSENT;
-      }
+    for (int i = 1; i < MAXH; i++) {
+      const bool live = valid && ((MAXH <= 8) || i < d.nheaps);
+      c[2 * i] = n1.at(q - d.pstride[i], live && h[i] >= 1);
+      c[2 * i + 1] = n2.at(q - 2 * d.pstride[i], live && h[i] >= 2);
+      nch += live ? (h[i] >= 1) + (h[i] >= 2) : 0;
     }
-    // ... then reduce: reference-canonical _res_red / _remote_red
+    if (!((rw >> (q & 63)) & 1ull)) continue;  // hole or not reached
+    npos++;
+    uint32_t word;
+    if (S == 0) {  // all heaps empty: four_to_one.py:19-22 LOSS, remoteness 0
+      word = make_word(LOSS, 0);
+      prims++;
+    } else {
+      uint32_t mn = 0xFFFFFFFFu, mx = 0, fl = 0;
 #pragma unroll
-    for (int u = 0; u < RESOLVE_UNROLL; u++) {
-      if (own[u] == SKIP) continue;
-      const u64 q = v.p_lo + i0 + u * stride - v.base_off;
-      npos++;
-      uint32_t word;
-      if (S == 0) {  // all heaps empty: four_to_one.py:19-22 LOSS, remoteness 0
-        word = make_word(LOSS, 0);
-        prims++;
-      } else {
-        bool any_loss = false, any_tie = false, any_draw = false;
-        uint32_t min_loss = 0xFFFFFFFFu, max_all = 0;
-        int nch = 0;
-#pragma unroll
-        for (int j = 0; j < 2 * MAXH; j++) {
-          uint32_t w = c[u][j];
-          if (w == ABSENT) continue;
-          nch++;
-          if (w >= W_REACHED) { err |= ERR_CHILD_UNRESOLVED; continue; }
-          uint32_t val = w & 3u, r = w >> 2;
-          if (val == LOSS) { any_loss = true; min_loss = min(min_loss, r); }
-          any_tie |= (val == TIE);
-          any_draw |= (val == DRAW);
-          max_all = max(max_all, r);
-        }
-        edges += (u64)nch;
-        if (any_loss) word = make_word(WIN, min_loss + 1);
-        else word = make_word(any_tie ? TIE : any_draw ? DRAW : LOSS, max_all + 1);
+      for (int j = 0; j < 2 * MAXH; j++) {
+        const uint32_t w = c[j];
+        mx = max(mx, w);
+        fl |= 1u << (w & 3u);
+        mn = min(mn, (w & 3u) == LOSS ? w : 0xFFFFFFFFu);
       }
-      mine[q] = word;
+      if (mx >= W_REACHED) err |= ERR_CHILD_UNRESOLVED;
+      edges += (u64)nch;
+      if (fl & (1u << LOSS)) word = make_word(WIN, (mn >> 2) + 1);
+      else word = make_word((fl & (1u << TIE)) ? TIE : (fl & (1u << DRAW)) ? DRAW : LOSS, (mx >> 2) + 1);
     }
+    mine[q] = word;
   }
   if (err) atomicOr(&st->err, err);
   block_add(&st->cursor_front, npos);  // positions resolved

@@ -699,8 +699,13 @@ static void dense_launch_resolve_t(gm_solver* s, int grid, u64 L) {
 #undef GM_RW
     return;
   }
-  hipLaunchKernelGGL((k_dense_resolve<MAXH, POW2>), dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->view, s->words,
-                     s->bits, L, s->st);
+  // buffer loads need every row's byte offsets to fit 32 bits
+  if (s->view.Wl * 4 <= 0xFFFFFFF0ull)
+    hipLaunchKernelGGL((k_dense_resolve<MAXH, POW2, true>), dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->view,
+                       s->words, s->bits, L, s->st);
+  else
+    hipLaunchKernelGGL((k_dense_resolve<MAXH, POW2, false>), dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->view,
+                       s->words, s->bits, L, s->st);
 }
 // kernels are instantiated per exact heap count 1..8 (16 = generic)
 template <bool POW2>
