@@ -672,26 +672,26 @@ static int resolve_groups() {
 }
 
 template <int MAXH, bool POW2>
-static void dense_launch_pull_t(gm_solver* s, int grid, u64 L, u64 root_p) {
+static void dense_launch_pull_t(gm_solver* s, const DenseView& v, int grid, u64 L, u64 root_p) {
   if (POW2 && !(dense_per_lane_mask() & 1)) {  // word-parallel form: one thread per 64-prefix group
-    const u64 groups = (s->view.p_hi - s->view.p_lo + 63) / 64;
+    const u64 groups = (v.p_hi - v.p_lo + 63) / 64;
     const int g = (int)std::min<u64>((groups + kBlock - 1) / kBlock, (u64)s->grid);
-    hipLaunchKernelGGL((k_dense_pull_words<MAXH>), dim3(g), dim3(kBlock), 0, s->stream, s->d, s->view, s->bits, L,
+    hipLaunchKernelGGL((k_dense_pull_words<MAXH>), dim3(g), dim3(kBlock), 0, s->stream, s->d, v, s->bits, L,
                        root_p);
     return;
   }
-  hipLaunchKernelGGL((k_dense_pull<MAXH, POW2>), dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->view, s->bits, L,
+  hipLaunchKernelGGL((k_dense_pull<MAXH, POW2>), dim3(grid), dim3(kBlock), 0, s->stream, s->d, v, s->bits, L,
                      root_p);
 }
 template <int MAXH, bool POW2>
-static void dense_launch_resolve_t(gm_solver* s, int grid, u64 L) {
+static void dense_launch_resolve_t(gm_solver* s, const DenseView& v, int grid, u64 L) {
   if (POW2 && !(dense_per_lane_mask() & 2)) {  // mask-driven form: one wave per 64-prefix group
-    const u64 groups = (s->view.p_hi - s->view.p_lo + 63) / 64;
+    const u64 groups = (v.p_hi - v.p_lo + 63) / 64;
     const int G = resolve_groups();
     const u64 waves = (groups + G - 1) / G;
     const int g = (int)std::min<u64>((waves + 3) / 4, (u64)s->grid);
 #define GM_RW(GR)                                                                                            \
-  hipLaunchKernelGGL((k_dense_resolve_words<MAXH, GR>), dim3(g), dim3(kBlock), 0, s->stream, s->d, s->view, \
+  hipLaunchKernelGGL((k_dense_resolve_words<MAXH, GR>), dim3(g), dim3(kBlock), 0, s->stream, s->d, v, \
                      s->words, s->bits, L, s->st)
     if (G == 1) GM_RW(1);
     else if (G == 4) GM_RW(4);
@@ -700,49 +700,49 @@ static void dense_launch_resolve_t(gm_solver* s, int grid, u64 L) {
     return;
   }
   // buffer loads need every row's byte offsets to fit 32 bits
-  if (s->view.Wl * 4 <= 0xFFFFFFF0ull)
-    hipLaunchKernelGGL((k_dense_resolve<MAXH, POW2, true>), dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->view,
+  if (v.Wl * 4 <= 0xFFFFFFF0ull)
+    hipLaunchKernelGGL((k_dense_resolve<MAXH, POW2, true>), dim3(grid), dim3(kBlock), 0, s->stream, s->d, v,
                        s->words, s->bits, L, s->st);
   else
-    hipLaunchKernelGGL((k_dense_resolve<MAXH, POW2, false>), dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->view,
+    hipLaunchKernelGGL((k_dense_resolve<MAXH, POW2, false>), dim3(grid), dim3(kBlock), 0, s->stream, s->d, v,
                        s->words, s->bits, L, s->st);
 }
 // kernels are instantiated per exact heap count 1..8 (16 = generic)
 template <bool POW2>
-static void dense_launch_pull_p(gm_solver* s, int grid, u64 L, u64 root_p) {
+static void dense_launch_pull_p(gm_solver* s, const DenseView& v, int grid, u64 L, u64 root_p) {
   switch (s->d.nheaps) {
-    case 1: dense_launch_pull_t<1, POW2>(s, grid, L, root_p); break;
-    case 2: dense_launch_pull_t<2, POW2>(s, grid, L, root_p); break;
-    case 3: dense_launch_pull_t<3, POW2>(s, grid, L, root_p); break;
-    case 4: dense_launch_pull_t<4, POW2>(s, grid, L, root_p); break;
-    case 5: dense_launch_pull_t<5, POW2>(s, grid, L, root_p); break;
-    case 6: dense_launch_pull_t<6, POW2>(s, grid, L, root_p); break;
-    case 7: dense_launch_pull_t<7, POW2>(s, grid, L, root_p); break;
-    case 8: dense_launch_pull_t<8, POW2>(s, grid, L, root_p); break;
-    default: dense_launch_pull_t<16, POW2>(s, grid, L, root_p); break;
+    case 1: dense_launch_pull_t<1, POW2>(s, v, grid, L, root_p); break;
+    case 2: dense_launch_pull_t<2, POW2>(s, v, grid, L, root_p); break;
+    case 3: dense_launch_pull_t<3, POW2>(s, v, grid, L, root_p); break;
+    case 4: dense_launch_pull_t<4, POW2>(s, v, grid, L, root_p); break;
+    case 5: dense_launch_pull_t<5, POW2>(s, v, grid, L, root_p); break;
+    case 6: dense_launch_pull_t<6, POW2>(s, v, grid, L, root_p); break;
+    case 7: dense_launch_pull_t<7, POW2>(s, v, grid, L, root_p); break;
+    case 8: dense_launch_pull_t<8, POW2>(s, v, grid, L, root_p); break;
+    default: dense_launch_pull_t<16, POW2>(s, v, grid, L, root_p); break;
   }
 }
 template <bool POW2>
-static void dense_launch_resolve_p(gm_solver* s, int grid, u64 L) {
+static void dense_launch_resolve_p(gm_solver* s, const DenseView& v, int grid, u64 L) {
   switch (s->d.nheaps) {
-    case 1: dense_launch_resolve_t<1, POW2>(s, grid, L); break;
-    case 2: dense_launch_resolve_t<2, POW2>(s, grid, L); break;
-    case 3: dense_launch_resolve_t<3, POW2>(s, grid, L); break;
-    case 4: dense_launch_resolve_t<4, POW2>(s, grid, L); break;
-    case 5: dense_launch_resolve_t<5, POW2>(s, grid, L); break;
-    case 6: dense_launch_resolve_t<6, POW2>(s, grid, L); break;
-    case 7: dense_launch_resolve_t<7, POW2>(s, grid, L); break;
-    case 8: dense_launch_resolve_t<8, POW2>(s, grid, L); break;
-    default: dense_launch_resolve_t<16, POW2>(s, grid, L); break;
+    case 1: dense_launch_resolve_t<1, POW2>(s, v, grid, L); break;
+    case 2: dense_launch_resolve_t<2, POW2>(s, v, grid, L); break;
+    case 3: dense_launch_resolve_t<3, POW2>(s, v, grid, L); break;
+    case 4: dense_launch_resolve_t<4, POW2>(s, v, grid, L); break;
+    case 5: dense_launch_resolve_t<5, POW2>(s, v, grid, L); break;
+    case 6: dense_launch_resolve_t<6, POW2>(s, v, grid, L); break;
+    case 7: dense_launch_resolve_t<7, POW2>(s, v, grid, L); break;
+    case 8: dense_launch_resolve_t<8, POW2>(s, v, grid, L); break;
+    default: dense_launch_resolve_t<16, POW2>(s, v, grid, L); break;
   }
 }
-static void dense_launch_pull(gm_solver* s, int grid, u64 L, u64 root_p) {
-  if (s->d.pow2) dense_launch_pull_p<true>(s, grid, L, root_p);
-  else dense_launch_pull_p<false>(s, grid, L, root_p);
+static void dense_launch_pull(gm_solver* s, const DenseView& v, int grid, u64 L, u64 root_p) {
+  if (s->d.pow2) dense_launch_pull_p<true>(s, v, grid, L, root_p);
+  else dense_launch_pull_p<false>(s, v, grid, L, root_p);
 }
-static void dense_launch_resolve(gm_solver* s, int grid, u64 L) {
-  if (s->d.pow2) dense_launch_resolve_p<true>(s, grid, L);
-  else dense_launch_resolve_p<false>(s, grid, L);
+static void dense_launch_resolve(gm_solver* s, const DenseView& v, int grid, u64 L) {
+  if (s->d.pow2) dense_launch_resolve_p<true>(s, v, grid, L);
+  else dense_launch_resolve_p<false>(s, v, grid, L);
 }
 
 static std::string err_text(uint32_t e) {
@@ -1261,6 +1261,38 @@ static int exchange_words(std::vector<gm_solver*>& ss, u64 L, int mode) {
   return 0;
 }
 
+// Band of level L: every non-hole slot has digit sum s(p) in [S - H0, S]
+// (S = root_sum - L), so its prefix lies between the smallest prefix with
+// s >= S - H0 (fill the low digits first) and the largest with s <= S (fill
+// the high digits first).  Narrowing a launch to the band skips whole
+// stretches of holes at both ends of the tier sequence.  Returns the view
+// clipped to the band (64-aligned start) or one with p_lo == p_hi.
+static DenseView dense_band(const Desc& d, const DenseView& v, u64 L) {
+  const int64_t S = (int64_t)d.root_sum - (int64_t)L;
+  int64_t T = S - (int64_t)d.heap[0];
+  u64 pmin = 0, pmax = 0;
+  int64_t rem = S;
+  for (int i = d.nheaps - 1; i >= 1; i--) {
+    const int64_t h = std::min<int64_t>(rem, d.heap[i]);
+    pmax += (u64)h * d.pstride[i];
+    rem -= h;
+  }
+  for (int i = 1; i < d.nheaps && T > 0; i++) {
+    const int64_t h = std::min<int64_t>(T, d.heap[i]);
+    pmin += (u64)h * d.pstride[i];
+    T -= h;
+  }
+  DenseView b = v;
+  if (S < 0 || T > 0) {  // no slot of this level exists
+    b.p_hi = b.p_lo;
+    return b;
+  }
+  b.p_lo = std::max<u64>(v.p_lo, pmin & ~63ull);
+  b.p_hi = std::min<u64>(v.p_hi, pmax + 1);
+  if (b.p_hi < b.p_lo) b.p_hi = b.p_lo;
+  return b;
+}
+
 // Dense solve of one table (world 1), one shard of an RCCL job, or every
 // shard of an in-process group (all on one stream), level-synchronously.
 static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
@@ -1295,8 +1327,11 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
       if (new_event(&e)) return GM_EHIP;
   }
   const u64 root_p = d.root / d.base[0];  // global prefix of the root (level 0)
-  auto grid_of = [&](gm_solver* s) {
-    return (int)std::min<u64>((s->view.p_hi - s->view.p_lo + kBlock - 1) / kBlock, (u64)s->grid);
+  // launches cover only the level's band of prefixes (dense_band); the
+  // grid is a multiple of 8 blocks for the XCD-chunked kernels
+  auto grid_of = [&](gm_solver* s, const DenseView& b) {
+    const u64 blocks = (b.p_hi - b.p_lo + kBlock - 1) / kBlock;
+    return (int)std::min<u64>((blocks + 7) & ~7ull, (u64)s->grid);
   };
   auto t0 = std::chrono::steady_clock::now();
   HIPCHK(hipEventRecord(e0, st));
@@ -1305,7 +1340,8 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
   for (int L = 0; L < T; L++) {
     for (gm_solver* s : ss) {
       if (timing && s == s0) HIPCHK(hipEventRecord(kx[2 * L], st));
-      dense_launch_pull(s, grid_of(s), (u64)L, root_p);
+      const DenseView b = dense_band(d, s->view, (u64)L);
+      if (b.p_hi > b.p_lo) dense_launch_pull(s, b, grid_of(s, b), (u64)L, root_p);
       if (timing && s == s0) HIPCHK(hipEventRecord(kx[2 * L + 1], st));
     }
     if (mode) {
@@ -1318,7 +1354,8 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
   for (int L = T - 1; L >= 0; L--) {
     for (gm_solver* s : ss) {
       if (timing && s == s0) HIPCHK(hipEventRecord(kr[2 * L], st));
-      dense_launch_resolve(s, grid_of(s), (u64)L);
+      const DenseView b = dense_band(d, s->view, (u64)L);
+      if (b.p_hi > b.p_lo) dense_launch_resolve(s, b, grid_of(s, b), (u64)L);
       if (timing && s == s0) HIPCHK(hipEventRecord(kr[2 * L + 1], st));
     }
     if (mode) {

@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 PMC passes (tools/pmc_passes.sh) per kernel: launch
+count and per-launch means of every counter, plus derived HBM-side bytes
+(FETCH_SIZE is in KB and, on gfx950, half the bytes of wide coalesced
+reads -- MI355X_MICROARCH.md §HBM) and the L2 hit rate.
+
+  python tools/pmc_summary.py gpurun_out/pmc2 [kernel-substring ...]
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def load(root):
+    per = defaultdict(lambda: defaultdict(float))
+    launches = defaultdict(set)
+    for path in glob.glob(os.path.join(root, "*", "run_counter_collection.csv")):
+        for r in csv.DictReader(open(path)):
+            name = r["Kernel_Name"]
+            key = (os.path.basename(os.path.dirname(path)), r["Dispatch_Id"])
+            launches[name].add(key)
+            per[name][r["Counter_Name"]] += float(r["Counter_Value"])
+    return per, launches
+
+
+def main():
+    root = sys.argv[1]
+    subs = sys.argv[2:] or ["k_dense_resolve", "k_dense_pull", "k_expand", "k_resolve"]
+    per, launches = load(root)
+    out = {}
+    for name, ctr in per.items():
+        if not any(s in name for s in subs):
+            continue
+        short = name.split("(")[0]
+        passes = {p for p, _ in launches[name]}
+        n = len(launches[name]) / max(1, len(passes))  # launches per pass
+        row = {"launches_per_pass": n}
+        for c, v in sorted(ctr.items()):
+            row[c + "_per_launch"] = v / n
+        if "FETCH_SIZE" in ctr:
+            row["fetch_bytes_per_launch_x2"] = ctr["FETCH_SIZE"] * 1024 * 2 / n
+        if "WRITE_SIZE" in ctr:
+            row["write_bytes_per_launch"] = ctr["WRITE_SIZE"] * 1024 / n
+        if "TCC_HIT_sum" in ctr:
+            row["l2_hit_rate"] = ctr["TCC_HIT_sum"] / max(1.0, ctr["TCC_HIT_sum"] + ctr["TCC_MISS_sum"])
+        out[short] = row
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
