@@ -458,18 +458,23 @@ struct WordRow<true> {
 template <>
 struct WordRow<false> {
   const uint32_t* p;
-  __device__ __forceinline__ void init(const uint32_t* base, u64 nwords) { p = nwords ? base : nullptr; }
-  __device__ __forceinline__ uint32_t at(u64 idx, bool ok) const { return ok ? p[idx] : 0u; }
+  u64 n;
+  __device__ __forceinline__ void init(const uint32_t* base, u64 nwords) {
+    p = base;
+    n = nwords;
+  }
+  // the range check mirrors the buffer form (wrapped indices read 0)
+  __device__ __forceinline__ uint32_t at(u64 idx, bool ok) const { return (ok && idx < n) ? p[idx] : 0u; }
 };
 
 // backward, level L: resolve every reached owned position from its children.
 // Absent children read as 0 (= WIN, remoteness 0, which no resolved
 // position holds), neutral for every term of the reduction, so each child
-// costs a load and four ALU ops:
+// costs a load and a few ALU ops (reference-canonical _res_red/_remote_red):
 //   value       WIN if any child LOSS, else TIE if any TIE, else DRAW if any
-//               DRAW, else LOSS                      (flag bits of child values)
-//   remoteness  WIN: 1 + min rem over LOSS children  (min of LOSS words)
-//               else 1 + max rem over all children   (max of words, rem = w>>2)
+//               DRAW, else LOSS      (min / max of the remapped value codes)
+//   remoteness  WIN: 1 + min rem over LOSS children, else 1 + max rem over
+//               all children         (min of LOSS words, max of words)
 // The reach-bit word is loaded with the child words (children of a non-hole
 // slot are never holes), so a round costs one memory latency.
 template <int MAXH, bool POW2, bool BUF>
@@ -491,19 +496,22 @@ __global__ __launch_bounds__(256) void k_dense_resolve(Desc d, DenseView v, uint
     uint32_t h[MAXH];
     const uint32_t s = wd.digits(d, p & ~63ull, p, h);
     const bool valid = s <= S && S - s <= d.heap[0];  // not a hole
+    if (!__ballot(valid)) continue;                   // a wave of holes
     const u64 rw = valid ? bits[(L * v.Wbl + q) >> 6] : 0ull;
+    // Child loads need no `valid` guard: a hole lane's result is dropped
+    // below, and its offsets either wrap out of range (read 0) or land on
+    // the lines its wave reads anyway.
     const uint32_t h0 = S - s;
     uint32_t c[2 * MAXH];
-    int nch = 0;
-    c[0] = n1.at(q, valid && h0 >= 1);
-    c[1] = n2.at(q, valid && h0 >= 2);
-    nch += (h0 >= 1) + (h0 >= 2);
+    uint32_t nch = min(h0, 2u);
+    c[0] = n1.at(q, h0 >= 1);
+    c[1] = n2.at(q, h0 >= 2);
 #pragma unroll
     for (int i = 1; i < MAXH; i++) {
-      const bool live = valid && ((MAXH <= 8) || i < d.nheaps);
+      const bool live = (MAXH <= 8) || i < d.nheaps;
       c[2 * i] = n1.at(q - d.pstride[i], live && h[i] >= 1);
       c[2 * i + 1] = n2.at(q - 2 * d.pstride[i], live && h[i] >= 2);
-      nch += live ? (h[i] >= 1) + (h[i] >= 2) : 0;
+      nch += live ? min(h[i], 2u) : 0u;
     }
     if (!((rw >> (q & 63)) & 1ull)) continue;  // hole or not reached
     npos++;
@@ -512,18 +520,22 @@ __global__ __launch_bounds__(256) void k_dense_resolve(Desc d, DenseView v, uint
       word = make_word(LOSS, 0);
       prims++;
     } else {
-      uint32_t mn = 0xFFFFFFFFu, mx = 0, fl = 0;
+      // x = rotr(w ^ 1, 2): value code on top, remapped so LOSS < WIN < DRAW
+      // < TIE (LOSS 00, WIN 01, DRAW 10, TIE 11); an absent child (w = 0)
+      // is a WIN of remoteness 0 and changes no term below
+      uint32_t mn = 0xFFFFFFFFu, mxx = 0, mxw = 0;
 #pragma unroll
       for (int j = 0; j < 2 * MAXH; j++) {
         const uint32_t w = c[j];
-        mx = max(mx, w);
-        fl |= 1u << (w & 3u);
-        mn = min(mn, (w & 3u) == LOSS ? w : 0xFFFFFFFFu);
+        const uint32_t x = __builtin_amdgcn_alignbit(w ^ 1u, w ^ 1u, 2);
+        mn = min(mn, x);
+        mxx = max(mxx, x);
+        mxw = max(mxw, w);
       }
-      if (mx >= W_REACHED) err |= ERR_CHILD_UNRESOLVED;
+      if (mxw >= W_REACHED) err |= ERR_CHILD_UNRESOLVED;
       edges += (u64)nch;
-      if (fl & (1u << LOSS)) word = make_word(WIN, (mn >> 2) + 1);
-      else word = make_word((fl & (1u << TIE)) ? TIE : (fl & (1u << DRAW)) ? DRAW : LOSS, (mx >> 2) + 1);
+      if (mn < 0x40000000u) word = make_word(WIN, (mn & 0x3FFFFFFFu) + 1);  // a LOSS child
+      else word = make_word(mxx >= 0xC0000000u ? TIE : mxx >= 0x80000000u ? DRAW : LOSS, (mxw >> 2) + 1);
     }
     mine[q] = word;
   }
