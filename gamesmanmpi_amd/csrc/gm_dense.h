@@ -497,10 +497,10 @@ __global__ __launch_bounds__(256) void k_dense_resolve(Desc d, DenseView v, uint
     const uint32_t s = wd.digits(d, p & ~63ull, p, h);
     const bool valid = s <= S && S - s <= d.heap[0];  // not a hole
     if (!__ballot(valid)) continue;                   // a wave of holes
-    const u64 rw = valid ? bits[(L * v.Wbl + q) >> 6] : 0ull;
-    // Child loads need no `valid` guard: a hole lane's result is dropped
-    // below, and its offsets either wrap out of range (read 0) or land on
-    // the lines its wave reads anyway.
+    if (!valid) continue;
+    // the wave's 64 reach bits (one uniform word), loaded with the children
+    const u64 rw = bits[__builtin_amdgcn_readfirstlane((uint32_t)((L * v.Wbl + q) >> 6)) |
+                        ((u64)__builtin_amdgcn_readfirstlane((uint32_t)(((L * v.Wbl + q) >> 6) >> 32)) << 32)];
     const uint32_t h0 = S - s;
     uint32_t c[2 * MAXH];
     uint32_t nch = min(h0, 2u);
@@ -513,31 +513,33 @@ __global__ __launch_bounds__(256) void k_dense_resolve(Desc d, DenseView v, uint
       c[2 * i + 1] = n2.at(q - 2 * d.pstride[i], live && h[i] >= 2);
       nch += live ? min(h[i], 2u) : 0u;
     }
-    if (!((rw >> (q & 63)) & 1ull)) continue;  // hole or not reached
-    npos++;
-    uint32_t word;
-    if (S == 0) {  // all heaps empty: four_to_one.py:19-22 LOSS, remoteness 0
-      word = make_word(LOSS, 0);
-      prims++;
-    } else {
-      // x = rotr(w ^ 1, 2): value code on top, remapped so LOSS < WIN < DRAW
-      // < TIE (LOSS 00, WIN 01, DRAW 10, TIE 11); an absent child (w = 0)
-      // is a WIN of remoteness 0 and changes no term below
-      uint32_t mn = 0xFFFFFFFFu, mxx = 0, mxw = 0;
+    // x = rotr(w ^ 1, 2): value code on top, remapped so LOSS < WIN < DRAW
+    // < TIE (LOSS 00, WIN 01, DRAW 10, TIE 11); an absent child (w = 0) is a
+    // WIN of remoteness 0 and changes no term below
+    uint32_t mn = 0xFFFFFFFFu, mxx = 0, mxw = 0;
 #pragma unroll
-      for (int j = 0; j < 2 * MAXH; j++) {
-        const uint32_t w = c[j];
-        const uint32_t x = __builtin_amdgcn_alignbit(w ^ 1u, w ^ 1u, 2);
-        mn = min(mn, x);
-        mxx = max(mxx, x);
-        mxw = max(mxw, w);
-      }
-      if (mxw >= W_REACHED) err |= ERR_CHILD_UNRESOLVED;
-      edges += (u64)nch;
-      if (mn < 0x40000000u) word = make_word(WIN, (mn & 0x3FFFFFFFu) + 1);  // a LOSS child
-      else word = make_word(mxx >= 0xC0000000u ? TIE : mxx >= 0x80000000u ? DRAW : LOSS, (mxw >> 2) + 1);
+    for (int j = 0; j < 2 * MAXH; j++) {
+      const uint32_t w = c[j];
+      const uint32_t x = __builtin_amdgcn_alignbit(w ^ 1u, w ^ 1u, 2);
+      mn = min(mn, x);
+      mxx = max(mxx, x);
+      mxw = max(mxw, w);
     }
-    mine[q] = word;
+    uint32_t word;
+    if (S == 0) word = make_word(LOSS, 0);  // all heaps empty: four_to_one.py:19-22
+    else if (mn < 0x40000000u) word = make_word(WIN, (mn & 0x3FFFFFFFu) + 1);  // a LOSS child
+    else word = make_word(mxx >= 0xC0000000u ? TIE : mxx >= 0x80000000u ? DRAW : LOSS, (mxw >> 2) + 1);
+    // Every non-hole slot is written (the word is consumed unconditionally,
+    // so the child loads issue together with the reach word); unreached
+    // slots get W_UNREACHED and are never read as children.
+    const bool reached = (rw >> (q & 63)) & 1ull;
+    mine[q] = reached ? word : W_UNREACHED;
+    if (reached) {
+      npos++;
+      edges += (u64)nch;
+      prims += S == 0;
+      if (S != 0 && mxw >= W_REACHED) err |= ERR_CHILD_UNRESOLVED;
+    }
   }
   if (err) atomicOr(&st->err, err);
   block_add(&st->cursor_front, npos);  // positions resolved
