@@ -68,14 +68,30 @@ def algorithmic_bytes(positions, edges, layout):
     return 24 * positions + 8 * edges, 12 * positions + 12 * edges
 
 
+def pmc_traffic(kernel, workload):
+    """HBM bytes per launch of `kernel` from the committed PMC summary
+    (profiles/pmc_traffic.json, written by tools/pmc_summary.py --traffic
+    from separate rocprofv3 --pmc passes of this bench), or None when no
+    pass of this workload is recorded."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as fh:
+            row = json.load(fh).get(kernel)
+    except (OSError, ValueError):
+        return None, None
+    if not row or row.get("workload") != workload:
+        return None, None
+    return row["bytes_per_launch"], "profiles/pmc_traffic.json (%s)" % row.get("source", "?")
+
+
 def model_8d_bytes(positions, edges):
     """SURVEY §8d per-position figure 36 + 20*b (whole solve)."""
     return 36 * positions + 20 * edges
 
 
-def cpu_baseline(sample_heaps="31:31:31:31:15"):
+def cpu_baseline(sample_heaps="31:31:31:31:31"):
     """Oracle (one core, scalar C port) on a bounded sample: the same game
-    family at 2^24 positions (about 10-15 s)."""
+    family at 2^25 positions (about 10-20 s)."""
     from oracle.oracle import Game
     g = Game("sum_four_to_one", "heaps=" + sample_heaps)
     t0 = time.perf_counter()
@@ -170,6 +186,8 @@ def main():
                               else "k_expand", fwd_b, tr.ms_expand_kernels,
                               tr.n_expand_launches)
     achieved = (kb / kn) / (kms / kn / 1e3) / 1e9  # GB/s
+    workload = "sum_four_to_one heaps=%s" % ":".join(map(str, heaps))
+    traffic, traffic_src = pmc_traffic(kname, workload)
     line = {
         "metric": "positions solved/sec (node)",
         "value": positions_total * args.steps / elapsed,
@@ -183,7 +201,7 @@ def main():
         "vs_baseline": None,
         "dtype": "u64 keys / u32 words (integer)",
         "data": "synthetic: sum of Four-To-One heaps, fully determined state space",
-        "config": {"workload": "sum_four_to_one heaps=%s" % ":".join(map(str, heaps)),
+        "config": {"workload": workload,
                    "positions_per_gpu": r.positions // world, "edges_per_gpu": r.edges // world,
                    "levels": r.levels, "root": r.root_line,
                    "layout": layout,
@@ -191,8 +209,15 @@ def main():
                                    if world > 1 else "1 GPU")},
         "roofline": {"bound": "hbm", "kernel": kname,
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_unit": "HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE)",
+                     "traffic_source": traffic_src,
+                     "algorithmic_bytes_per_launch": kb / kn,
+                     "model": ("dense: resolve 4.125 B/position + 4 B/edge, pull (edges + positions)/8 B"
+                               if layout == "dense" else
+                               "SURVEY 8d keyed: expand 24 B/position + 8 B/edge, resolve 12 B/position + 12 B/edge"),
                      "launches": kn, "ms_kernel_total": kms,
+                     "ms_per_launch": kms / kn,
                      "algorithmic_bytes_total": kb},
         "phase_ms": {"forward": r.ms_forward, "backward": r.ms_backward,
                      "solve_wall": r.ms_total,

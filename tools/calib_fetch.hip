@@ -1,0 +1,69 @@
+// Calibration of rocprofv3's FETCH_SIZE / WRITE_SIZE for the access widths
+// the solver's kernels use (MI355X_MICROARCH.md §HBM: only 16-B-per-lane
+// streaming reads are calibrated there).  Each kernel touches a known byte
+// count of a 1 GiB buffer (past the 256 MiB Infinity Cache); the PMC pass
+// divides the counter by that count.
+//   hipcc --offload-arch=gfx950 -O3 tools/calib_fetch.hip -o tools/calib_fetch
+//   rocprofv3 --pmc FETCH_SIZE -- tools/calib_fetch
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+
+#define CHK(x)                                                        \
+  do {                                                                \
+    hipError_t e_ = (x);                                              \
+    if (e_ != hipSuccess) {                                           \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));         \
+      return 1;                                                       \
+    }                                                                 \
+  } while (0)
+
+// 4 B per lane, contiguous per wave (the dense resolve's child loads)
+__global__ void read_b32(const uint32_t* __restrict__ p, size_t n, uint32_t* out) {
+  uint32_t acc = 0;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    acc ^= p[i];
+  if (acc == 0x12345678u) out[0] = acc;
+}
+// 8 B per lane (bitmap words, hashed-table keys)
+__global__ void read_b64(const uint64_t* __restrict__ p, size_t n, uint32_t* out) {
+  uint64_t acc = 0;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    acc ^= p[i];
+  if (acc == 0x12345678u) out[0] = (uint32_t)acc;
+}
+// 16 B per lane (the guide's calibrated case)
+__global__ void read_b128(const uint4* __restrict__ p, size_t n, uint32_t* out) {
+  uint32_t acc = 0;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    uint4 v = p[i];
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+// 4 B per lane stores (the resolve's word stores)
+__global__ void write_b32(uint32_t* __restrict__ p, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    p[i] = (uint32_t)i;
+}
+
+int main() {
+  const size_t bytes = (size_t)1 << 30;
+  void* buf = nullptr;
+  uint32_t* out = nullptr;
+  CHK(hipMalloc(&buf, bytes));
+  CHK(hipMalloc(&out, 64));
+  CHK(hipMemset(buf, 1, bytes));
+  const int grid = 256 * 8, block = 256;
+  for (int rep = 0; rep < 2; rep++) {
+    hipLaunchKernelGGL(read_b32, dim3(grid), dim3(block), 0, 0, (const uint32_t*)buf, bytes / 4, out);
+    hipLaunchKernelGGL(read_b64, dim3(grid), dim3(block), 0, 0, (const uint64_t*)buf, bytes / 8, out);
+    hipLaunchKernelGGL(read_b128, dim3(grid), dim3(block), 0, 0, (const uint4*)buf, bytes / 16, out);
+    hipLaunchKernelGGL(write_b32, dim3(grid), dim3(block), 0, 0, (uint32_t*)buf, bytes / 4);
+  }
+  CHK(hipDeviceSynchronize());
+  printf("{\"bytes_per_kernel\": %zu}\n", bytes);
+  CHK(hipFree(buf));
+  CHK(hipFree(out));
+  return 0;
+}

@@ -5,6 +5,12 @@ count and per-launch means of every counter, plus derived HBM-side bytes
 reads -- MI355X_MICROARCH.md §HBM) and the L2 hit rate.
 
   python tools/pmc_summary.py gpurun_out/pmc2 [kernel-substring ...]
+  python tools/pmc_summary.py --traffic WORKLOAD OUT.json gpurun_out/pmc2
+      writes {kernel: {workload, bytes_per_launch, fetch_bytes_per_launch,
+      write_bytes_per_launch, l2_hit_rate, source}} for bench.py's
+      roofline.traffic (FETCH_SIZE x 2: calibrated on gfx950 with
+      tools/calib_fetch.hip for 4-, 8- and 16-B-per-lane reads; WRITE_SIZE
+      exact for 4-B stores).
 """
 import csv
 import glob
@@ -26,7 +32,30 @@ def load(root):
     return per, launches
 
 
+def traffic(workload, out_path, root):
+    per, launches = load(root)
+    res = {}
+    for name, ctr in per.items():
+        if "FETCH_SIZE" not in ctr or "WRITE_SIZE" not in ctr:
+            continue
+        short = name.split("(")[0].replace("void ", "").split("<")[0]
+        n = len(launches[name]) / max(1, len({p for p, _ in launches[name]}))
+        f = ctr["FETCH_SIZE"] * 1024 * 2 / n
+        w = ctr["WRITE_SIZE"] * 1024 / n
+        row = {"workload": workload, "bytes_per_launch": f + w,
+               "fetch_bytes_per_launch": f, "write_bytes_per_launch": w,
+               "launches": n, "source": root}
+        if "TCC_HIT_sum" in ctr:
+            row["l2_hit_rate"] = ctr["TCC_HIT_sum"] / max(1.0, ctr["TCC_HIT_sum"] + ctr["TCC_MISS_sum"])
+        res[short] = row
+    with open(out_path, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res, indent=1))
+
+
 def main():
+    if sys.argv[1] == "--traffic":
+        return traffic(sys.argv[2], sys.argv[3], sys.argv[4])
     root = sys.argv[1]
     subs = sys.argv[2:] or ["k_dense_resolve", "k_dense_pull", "k_expand", "k_resolve"]
     per, launches = load(root)
