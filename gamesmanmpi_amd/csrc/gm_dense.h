@@ -188,7 +188,7 @@ __global__ __launch_bounds__(256) void k_dense_pull(Desc d, DenseView v, u64* bi
 // i.e. per output bitmap word.  With pow2 bases and a 64-aligned group base
 // pg, digit_i(pg + j) = digit_i(pg) + digit_i(j) for j < 64, so every
 // per-prefix condition of the group is a 64-bit mask read from small
-// per-block tables indexed by the group's (uniform) digits:
+// tables (staged in LDS) indexed by the group's (uniform) digits:
 //   TS[t]    = { j : sum_i digit_i(j) <= t }      (slot validity, heap-0 moves)
 //   TD[i][t] = { j : digit_i(j) <= t }            (heap-i moves, i >= 1)
 // and each parent kind contributes (64 parent bits, one or two word loads)
@@ -207,30 +207,15 @@ __device__ __forceinline__ u64 bits64_at(const u64* bits, u64 pos) {
 }
 
 template <int MAXH>
-__global__ __launch_bounds__(256) void k_dense_pull_words(Desc d, DenseView v, u64* bits, u64 L, u64 root_p) {
-  __shared__ u64 TS[64];
-  __shared__ u64 TD[MAXH][64];
-  // tables from wave 0: lane j evaluates its digits, one ballot per entry
-  if (threadIdx.x < 64) {
-    const uint32_t j = threadIdx.x;
-    uint32_t dj[MAXH], sj = 0;
-#pragma unroll
-    for (int i = 1; i < MAXH; i++) {
-      const bool live = (MAXH <= 8) || i < d.nheaps;
-      dj[i] = live ? (uint32_t)((j >> d.pshift[i]) & (d.base[i] - 1)) : 0u;
-      sj += dj[i];
-    }
-    for (int t = 0; t < 64; t++) {
-      u64 m = __ballot(sj <= (uint32_t)t);
-      if (j == 0) TS[t] = m;
-#pragma unroll
-      for (int i = 1; i < MAXH; i++) {
-        u64 mi = __ballot(dj[i] <= (uint32_t)t);
-        if (j == 0) TD[i][t] = mi;
-      }
-    }
-  }
+__global__ __launch_bounds__(256) void k_dense_pull_words(Desc d, DenseView v, u64* bits, u64 L, u64 root_p,
+                                                          const u64* __restrict__ masks) {
+  // mask tables (built once on the host at solver creation, gm_solver.hip
+  // build_mask_tables): M[0..63] = TS, M[64 (i + 1) + t] = TD[i][t]
+  __shared__ u64 M[64 * (MAXH + 1)];
+  for (int k = threadIdx.x; k < 64 * (MAXH + 1); k += blockDim.x) M[k] = masks[k];
   __syncthreads();
+  const u64* TS = M;
+#define TD(i) (M + 64 * ((i) + 1))
   const int S = (int)(d.root_sum - (uint32_t)L);
   const int H0 = (int)d.heap[0];
   const u64 ngroups = (v.p_hi - v.p_lo + 63) >> 6;
@@ -265,10 +250,10 @@ __global__ __launch_bounds__(256) void k_dense_pull_words(Desc d, DenseView v, u
         if (!live) continue;
         // heap i +1 / +2: exists iff dg + dj <= H_i - d
         const int Hi = (int)d.heap[i];
-        const u64 m1 = mask_le(TD[i], Hi - 1 - dg[i]);
+        const u64 m1 = mask_le(TD(i), Hi - 1 - dg[i]);
         if (m1) reached |= bits64_at(bits, b1 + d.pstride[i]) & m1;
         if (L >= 2) {
-          const u64 m2 = mask_le(TD[i], Hi - 2 - dg[i]);
+          const u64 m2 = mask_le(TD(i), Hi - 2 - dg[i]);
           if (m2) reached |= bits64_at(bits, b2 + 2 * d.pstride[i]) & m2;
         }
       }
@@ -276,145 +261,7 @@ __global__ __launch_bounds__(256) void k_dense_pull_words(Desc d, DenseView v, u
     bits[(L * v.Wbl + q) >> 6] = reached & V;
   }
 }
-
-// ---------------------------------------------------------------------------
-// Mask-driven resolve (power-of-two layouts): one WAVE per 64-prefix group,
-// lane j <-> prefix pg + j.  Slot validity, the group's reach bits and, per
-// child kind, "this child exists" are wave-uniform 64-bit masks (tables as
-// in k_dense_pull_words), so hole groups cost a few scalar instructions and
-// lanes only test a bit before each coalesced 4-B child load.  GROUPS groups
-// per round keep more loads in flight per wave.
-// ---------------------------------------------------------------------------
-template <int MAXH, int RESOLVE_GROUPS>
-__global__ __launch_bounds__(256) void k_dense_resolve_words(Desc d, DenseView v, uint32_t* words, const u64* bits,
-                                                             u64 L, DevState* st) {
-  __shared__ u64 TS[64];
-  __shared__ u64 TD[MAXH][64];
-  const uint32_t lane = __lane_id();
-  if (threadIdx.x < 64) {
-    uint32_t dj[MAXH], sj = 0;
-#pragma unroll
-    for (int i = 1; i < MAXH; i++) {
-      const bool live = (MAXH <= 8) || i < d.nheaps;
-      dj[i] = live ? (uint32_t)((lane >> d.pshift[i]) & (d.base[i] - 1)) : 0u;
-      sj += dj[i];
-    }
-    for (int t = 0; t < 64; t++) {
-      u64 m = __ballot(sj <= (uint32_t)t);
-      if (lane == 0) TS[t] = m;
-#pragma unroll
-      for (int i = 1; i < MAXH; i++) {
-        u64 mi = __ballot(dj[i] <= (uint32_t)t);
-        if (lane == 0) TD[i][t] = mi;
-      }
-    }
-  }
-  __syncthreads();
-  const int S = (int)(d.root_sum - (uint32_t)L);
-  const int H0 = (int)d.heap[0];
-  uint32_t* mine = words + L * v.Wl;
-  const uint32_t* n1 = words + (L + 1) * v.Wl;  // only dereferenced when S >= 1
-  const uint32_t* n2 = words + (L + 2) * v.Wl;  // only dereferenced when S >= 2
-  const u64 ngroups = (v.p_hi - v.p_lo + 63) >> 6;
-  const u64 nwaves = (u64)gridDim.x * (blockDim.x >> 6);
-  // Masks stay in vector registers.  A variant that moved them to scalar
-  // registers (readfirstlane of the wave index and of every mask) counted
-  // 4,672 reached positions for the 4,096 reach bits set on heaps 7:7:7:7
-  // on MI355X / ROCm 7.2, so it was removed.
-  const u64 wave0 = (u64)blockIdx.x * (blockDim.x >> 6) + (u64)(threadIdx.x >> 6);
-  constexpr int NK = 2 * MAXH;  // child kinds: (heap i, step 1|2)
-  u64 npos = 0, edges = 0, prims = 0;
-  uint32_t err = 0;
-  for (u64 g0 = wave0; g0 < ngroups; g0 += RESOLVE_GROUPS * nwaves) {
-    uint32_t c[RESOLVE_GROUPS][NK];
-    u64 em[RESOLVE_GROUPS][NK];  // child-exists masks (equal in every lane)
-    u64 act[RESOLVE_GROUPS];
-    u64 qv[RESOLVE_GROUPS];
-#pragma unroll
-    for (int u = 0; u < RESOLVE_GROUPS; u++) {
-      const u64 gi = g0 + (u64)u * nwaves;
-      act[u] = 0;
-      qv[u] = 0;
-#pragma unroll
-      for (int k = 0; k < NK; k++) {
-        c[u][k] = 0;
-        em[u][k] = 0;
-      }
-      if (gi >= ngroups) continue;
-      const u64 pg = v.p_lo + (gi << 6);
-      const u64 q = pg - v.base_off;
-      qv[u] = q;
-      int dg[MAXH];
-      int sg = 0;
-#pragma unroll
-      for (int i = 1; i < MAXH; i++) {
-        const bool live = (MAXH <= 8) || i < d.nheaps;
-        dg[i] = live ? (int)((pg >> d.pshift[i]) & (d.base[i] - 1)) : 0;
-        sg += dg[i];
-      }
-      const int hi_s = S - sg, lo_s = S - H0 - sg;
-      u64 V = (mask_le(TS, hi_s) & ~mask_le(TS, lo_s - 1));
-      if (pg + 64 > v.p_hi) V &= (1ull << (v.p_hi - pg)) - 1;
-      if (!V) continue;
-      const u64 A = (V & bits[(L * v.Wbl + q) >> 6]);  // valid and reached
-      act[u] = A;
-      if (!A || S == 0) continue;
-      // heap 0 -1 / -2: exists iff h0 >= d  <=>  sj <= hi_s - d
-      em[u][0] = (A & mask_le(TS, hi_s - 1));
-      em[u][1] = (A & mask_le(TS, hi_s - 2));
-#pragma unroll
-      for (int i = 1; i < MAXH; i++) {
-        const bool live = (MAXH <= 8) || i < d.nheaps;
-        if (!live) continue;
-        // heap i -1 / -2: exists iff dg + dj >= d  <=>  NOT(dj <= d - 1 - dg)
-        em[u][2 * i] = (A & ~mask_le(TD[i], -dg[i]));
-        em[u][2 * i + 1] = (A & ~mask_le(TD[i], 1 - dg[i]));
-      }
-      // coalesced child loads, one per existing (lane, kind)
-      c[u][0] = ((em[u][0] >> lane) & 1) ? n1[q + lane] : 0u;
-      c[u][1] = ((em[u][1] >> lane) & 1) ? n2[q + lane] : 0u;
-#pragma unroll
-      for (int i = 1; i < MAXH; i++) {
-        c[u][2 * i] = ((em[u][2 * i] >> lane) & 1) ? n1[q + lane - d.pstride[i]] : 0u;
-        c[u][2 * i + 1] = ((em[u][2 * i + 1] >> lane) & 1) ? n2[q + lane - 2 * d.pstride[i]] : 0u;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < RESOLVE_GROUPS; u++) {
-      const u64 A = act[u];
-      if (!((A >> lane) & 1)) continue;
-      npos++;  // per-lane tallies, summed by block_add
-      uint32_t word;
-      if (S == 0) {
-        word = make_word(LOSS, 0);  // four_to_one.py:19-22
-        prims++;
-      } else {
-        bool any_loss = false, any_tie = false, any_draw = false;
-        uint32_t min_loss = 0xFFFFFFFFu, max_all = 0;
-#pragma unroll
-        for (int k = 0; k < NK; k++) {
-          if (!((em[u][k] >> lane) & 1)) continue;
-          edges++;
-          const uint32_t w = c[u][k];
-          if (w >= W_REACHED) { err |= ERR_CHILD_UNRESOLVED; continue; }
-          const uint32_t val = w & 3u, r = w >> 2;
-          if (val == LOSS) { any_loss = true; min_loss = min(min_loss, r); }
-          any_tie |= (val == TIE);
-          any_draw |= (val == DRAW);
-          max_all = max(max_all, r);
-        }
-        // reference-canonical _res_red / _remote_red
-        if (any_loss) word = make_word(WIN, min_loss + 1);
-        else word = make_word(any_tie ? TIE : any_draw ? DRAW : LOSS, max_all + 1);
-      }
-      mine[qv[u] + lane] = word;
-    }
-  }
-  if (err) atomicOr(&st->err, err);
-  block_add(&st->cursor_front, npos);
-  block_add(&st->edges, edges);
-  block_add(&st->prims, prims);
-}
+#undef TD
 
 // XCD-aware split of [0, n) (MI355X dispatches workgroup b to XCD b % 8):
 // the blocks of one XCD grid-stride over one contiguous, 64-aligned chunk,

@@ -293,6 +293,13 @@ struct DevState {
 static size_t devstate_bytes(int max_levels) {
   return sizeof(DevState) + sizeof(LevelSeg) * (size_t)(max_levels + 2);
 }
+// Scratch = DevState (cleared per solve) + the dense mask tables (written
+// once at solver creation): TS[64] then TD[16][64], u64 each.
+constexpr size_t kMaskTableWords = 64 * 17;
+static size_t mask_tables_offset(int max_levels) { return (devstate_bytes(max_levels) + 255) / 256 * 256; }
+static size_t scratch_bytes_for(int max_levels) {
+  return mask_tables_offset(max_levels) + kMaskTableWords * sizeof(u64);
+}
 
 __device__ __forceinline__ u64 mix64(u64 x) {  // splitmix64 finaliser
   x ^= x >> 31;
@@ -593,6 +600,7 @@ struct gm_solver {
   u64* lv;
   u64 lcap;
   DevState* st;
+  const u64* masks;  // dense pow2 mask tables in scratch (k_dense_pull_words)
   hipStream_t stream;
   bool own_stream;
   uint32_t flags;
@@ -642,42 +650,24 @@ static void do_resolve(gm_solver* s, int L) {
 }
 
 // Kernel choice for power-of-two dense layouts (measured on MI355X, 2^30
-// solve): pull -- word-parallel 4.2 ms vs per-lane 46 ms; resolve --
-// per-lane 44 ms vs mask-driven 64 / 79 / 181 ms (1 / 2 / 4 groups per
-// round).  GM_DENSE_PER_LANE=pull forces the per-lane pull,
-// GM_DENSE_RESOLVE=words selects the mask-driven resolve (A/B runs).
-static int dense_per_lane_mask() {
+// solve): pull -- word-parallel 4.2 ms vs per-lane 46 ms.
+// GM_DENSE_PER_LANE=pull forces the per-lane pull (A/B runs).
+static bool dense_per_lane_pull() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("GM_DENSE_PER_LANE");
-    const char* r = getenv("GM_DENSE_RESOLVE");
-    v = 2;  // bit 0: per-lane pull, bit 1: per-lane resolve
-    if (e && !strcmp(e, "pull")) v |= 1;
-    if (e && atoi(e)) v |= 3;
-    if (r && !strcmp(r, "words")) v &= ~2;
+    v = (e && (!strcmp(e, "pull") || atoi(e))) ? 1 : 0;
   }
-  return v;
-}
-
-// groups of 64 prefixes each resolve wave keeps in flight (measured; the
-// GM_RESOLVE_GROUPS environment variable overrides it for experiments)
-static int resolve_groups() {
-  static int g = 0;
-  if (!g) {
-    const char* e = getenv("GM_RESOLVE_GROUPS");
-    int v = e ? atoi(e) : 2;
-    g = (v == 1 || v == 4) ? v : 2;
-  }
-  return g;
+  return v == 1;
 }
 
 template <int MAXH, bool POW2>
 static void dense_launch_pull_t(gm_solver* s, const DenseView& v, int grid, u64 L, u64 root_p) {
-  if (POW2 && !(dense_per_lane_mask() & 1)) {  // word-parallel form: one thread per 64-prefix group
+  if (POW2 && !dense_per_lane_pull()) {  // word-parallel form: one thread per 64-prefix group
     const u64 groups = (v.p_hi - v.p_lo + 63) / 64;
     const int g = (int)std::min<u64>((groups + kBlock - 1) / kBlock, (u64)s->grid);
     hipLaunchKernelGGL((k_dense_pull_words<MAXH>), dim3(g), dim3(kBlock), 0, s->stream, s->d, v, s->bits, L,
-                       root_p);
+                       root_p, s->masks);
     return;
   }
   hipLaunchKernelGGL((k_dense_pull<MAXH, POW2>), dim3(grid), dim3(kBlock), 0, s->stream, s->d, v, s->bits, L,
@@ -685,20 +675,6 @@ static void dense_launch_pull_t(gm_solver* s, const DenseView& v, int grid, u64 
 }
 template <int MAXH, bool POW2>
 static void dense_launch_resolve_t(gm_solver* s, const DenseView& v, int grid, u64 L) {
-  if (POW2 && !(dense_per_lane_mask() & 2)) {  // mask-driven form: one wave per 64-prefix group
-    const u64 groups = (v.p_hi - v.p_lo + 63) / 64;
-    const int G = resolve_groups();
-    const u64 waves = (groups + G - 1) / G;
-    const int g = (int)std::min<u64>((waves + 3) / 4, (u64)s->grid);
-#define GM_RW(GR)                                                                                            \
-  hipLaunchKernelGGL((k_dense_resolve_words<MAXH, GR>), dim3(g), dim3(kBlock), 0, s->stream, s->d, v, \
-                     s->words, s->bits, L, s->st)
-    if (G == 1) GM_RW(1);
-    else if (G == 4) GM_RW(4);
-    else GM_RW(2);
-#undef GM_RW
-    return;
-  }
   // buffer loads need every row's byte offsets to fit 32 bits
   if (v.Wl * 4 <= 0xFFFFFFF0ull)
     hipLaunchKernelGGL((k_dense_resolve<MAXH, POW2, true>), dim3(grid), dim3(kBlock), 0, s->stream, s->d, v,
@@ -972,7 +948,7 @@ int gm_plan_shard(int game, int rank, int world, uint32_t flags, uint64_t max_ta
   if (!d || !out) return fail(GM_EINVAL, "bad argument");
   memset(out, 0, sizeof *out);
   out->max_levels = (uint32_t)d->max_levels;
-  out->scratch_bytes = (devstate_bytes(d->max_levels) + 255) / 256 * 256;
+  out->scratch_bytes = scratch_bytes_for(d->max_levels);
   if (!d->dense_ok || (flags & GM_F_FORCE_HASHED))
     return fail(GM_EINVAL, "only DENSE layouts shard by prefix blocks; keyed tables shard by md5 owner");
   bool fits = false;
@@ -987,7 +963,7 @@ int gm_plan(int game, uint64_t positions, uint32_t flags, uint64_t max_table_byt
   if (!d || !out) return fail(GM_EINVAL, "bad argument");
   memset(out, 0, sizeof *out);
   out->max_levels = (uint32_t)d->max_levels;
-  out->scratch_bytes = (devstate_bytes(d->max_levels) + 255) / 256 * 256;
+  out->scratch_bytes = scratch_bytes_for(d->max_levels);
   if (d->dense_ok && !(flags & GM_F_FORCE_HASHED)) {
     bool fits = false;
     int rc = plan_dense(d, 0, 1, max_table_bytes, out, &fits);
@@ -995,7 +971,7 @@ int gm_plan(int game, uint64_t positions, uint32_t flags, uint64_t max_table_byt
     if (fits) return 0;
     memset(out, 0, sizeof *out);
     out->max_levels = (uint32_t)d->max_levels;
-    out->scratch_bytes = (devstate_bytes(d->max_levels) + 255) / 256 * 256;
+    out->scratch_bytes = scratch_bytes_for(d->max_levels);
   }
   if (positions == 0) {
     gm_game_info(game, &positions, nullptr, nullptr);
@@ -1010,11 +986,32 @@ int gm_plan(int game, uint64_t positions, uint32_t flags, uint64_t max_table_byt
   return 0;
 }
 
+// Per-lane condition masks of a 64-prefix group for power-of-two layouts
+// (k_dense_pull_words): with j the lane's offset in the group,
+//   M[t]              = { j : sum_i digit_i(j) <= t }   (TS)
+//   M[64 (i + 1) + t] = { j : digit_i(j) <= t }         (TD[i], i >= 1)
+// They depend only on the descriptor, so they are built once here.
+static void build_mask_tables(const Desc& d, u64* M) {
+  memset(M, 0, kMaskTableWords * sizeof(u64));
+  for (int j = 0; j < 64; j++) {
+    uint32_t dj[16] = {0}, sj = 0;
+    for (int i = 1; i < d.nheaps; i++) {
+      dj[i] = (uint32_t)((j >> d.pshift[i]) & (d.base[i] - 1));
+      sj += dj[i];
+    }
+    for (int t = 0; t < 64; t++) {
+      if (sj <= (uint32_t)t) M[t] |= 1ull << j;
+      for (int i = 1; i < d.nheaps; i++)
+        if (dj[i] <= (uint32_t)t) M[64 * (i + 1) + t] |= 1ull << j;
+    }
+  }
+}
+
 int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf, gm_solver** out) {
   const Desc* d = get_game(game);
   if (!d || !buf || !out) return fail(GM_EINVAL, "bad argument");
   if (!buf->table || !buf->scratch) return fail(GM_EINVAL, "null device buffer");
-  if (buf->scratch_bytes < devstate_bytes(d->max_levels)) return fail(GM_EINVAL, "scratch too small");
+  if (buf->scratch_bytes < scratch_bytes_for(d->max_levels)) return fail(GM_EINVAL, "scratch too small (use gm_plan)");
   DenseGeom g;
   memset(&g, 0, sizeof g);
   if (buf->mode == GM_MODE_DENSE) {
@@ -1048,6 +1045,7 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
   s->lv = (u64*)buf->levels;
   s->lcap = buf->level_capacity;
   s->st = (DevState*)buf->scratch;
+  s->masks = (const u64*)((char*)buf->scratch + mask_tables_offset(d->max_levels));
   s->flags = buf->flags;
   s->grid = launch_grid();
   if (buf->stream) {
@@ -1060,6 +1058,15 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
       return fail(GM_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
     }
     s->own_stream = true;
+  }
+  if (s->mode == GM_MODE_DENSE && d->pow2) {
+    std::vector<u64> m(kMaskTableWords);
+    build_mask_tables(*d, m.data());
+    hipError_t e = hipMemcpy((void*)s->masks, m.data(), m.size() * sizeof(u64), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      gm_solver_destroy(s);
+      return fail(GM_EHIP, "mask tables: %s", hipGetErrorString(e));
+    }
   }
   *out = s;
   return 0;
