@@ -324,7 +324,7 @@ struct WordRow<false> {
 //               all children         (min of LOSS words, max of words)
 // The reach-bit word is loaded with the child words (children of a non-hole
 // slot are never holes), so a round costs one memory latency.
-template <int MAXH, bool POW2, bool BUF>
+template <int MAXH, bool POW2, bool BUF, int U>
 __global__ __launch_bounds__(256) void k_dense_resolve(Desc d, DenseView v, uint32_t* words, const u64* bits, u64 L,
                                                        DevState* st) {
   const uint32_t S = d.root_sum - (uint32_t)L;
@@ -337,55 +337,74 @@ __global__ __launch_bounds__(256) void k_dense_resolve(Desc d, DenseView v, uint
   WaveDigits<MAXH, POW2> wd;
   wd.init(d);
   const XcdRange r = xcd_range(v.p_hi - v.p_lo);
-  for (u64 i0 = r.first; i0 < r.end; i0 += r.stride) {
-    const u64 p = v.p_lo + i0;
-    const u64 q = p - v.base_off;
-    uint32_t h[MAXH];
-    const uint32_t s = wd.digits(d, p & ~63ull, p, h);
-    const bool valid = s <= S && S - s <= d.heap[0];  // not a hole
-    if (!__ballot(valid)) continue;                   // a wave of holes
-    if (!valid) continue;
-    // the wave's 64 reach bits (one uniform word), loaded with the children
-    const u64 rw = bits[__builtin_amdgcn_readfirstlane((uint32_t)((L * v.Wbl + q) >> 6)) |
-                        ((u64)__builtin_amdgcn_readfirstlane((uint32_t)(((L * v.Wbl + q) >> 6) >> 32)) << 32)];
-    const uint32_t h0 = S - s;
-    uint32_t c[2 * MAXH];
-    uint32_t nch = min(h0, 2u);
-    c[0] = n1.at(q, h0 >= 1);
-    c[1] = n2.at(q, h0 >= 2);
+  for (u64 i0 = r.first; i0 < r.end; i0 += U * r.stride) {
+    // U grid-stride rounds per iteration: all their loads issue before the
+    // first wait
+    uint32_t c[U][2 * MAXH];
+    u64 rw[U], qs[U];
+    uint32_t nch[U];
+    bool ok[U];
 #pragma unroll
-    for (int i = 1; i < MAXH; i++) {
-      const bool live = (MAXH <= 8) || i < d.nheaps;
-      c[2 * i] = n1.at(q - d.pstride[i], live && h[i] >= 1);
-      c[2 * i + 1] = n2.at(q - 2 * d.pstride[i], live && h[i] >= 2);
-      nch += live ? min(h[i], 2u) : 0u;
-    }
-    // x = rotr(w ^ 1, 2): value code on top, remapped so LOSS < WIN < DRAW
-    // < TIE (LOSS 00, WIN 01, DRAW 10, TIE 11); an absent child (w = 0) is a
-    // WIN of remoteness 0 and changes no term below
-    uint32_t mn = 0xFFFFFFFFu, mxx = 0, mxw = 0;
+    for (int u = 0; u < U; u++) {
+      ok[u] = false;
+      rw[u] = 0;
+      nch[u] = 0;
+      const u64 iu = i0 + (u64)u * r.stride;
+      const u64 p = v.p_lo + iu;
+      const u64 q = p - v.base_off;
+      qs[u] = q;
+      uint32_t h[MAXH];
+      const uint32_t s = wd.digits(d, p & ~63ull, p, h);
+      const bool valid = iu < r.end && s <= S && S - s <= d.heap[0];  // not a hole
+      if (!__ballot(valid)) continue;                                 // a wave of holes
+      if (!valid) continue;
+      ok[u] = true;
+      // the wave's 64 reach bits (one uniform word), loaded with the children
+      rw[u] = bits[__builtin_amdgcn_readfirstlane((uint32_t)((L * v.Wbl + q) >> 6)) |
+                   ((u64)__builtin_amdgcn_readfirstlane((uint32_t)(((L * v.Wbl + q) >> 6) >> 32)) << 32)];
+      const uint32_t h0 = S - s;
+      nch[u] = min(h0, 2u);
+      c[u][0] = n1.at(q, h0 >= 1);
+      c[u][1] = n2.at(q, h0 >= 2);
 #pragma unroll
-    for (int j = 0; j < 2 * MAXH; j++) {
-      const uint32_t w = c[j];
-      const uint32_t x = __builtin_amdgcn_alignbit(w ^ 1u, w ^ 1u, 2);
-      mn = min(mn, x);
-      mxx = max(mxx, x);
-      mxw = max(mxw, w);
+      for (int i = 1; i < MAXH; i++) {
+        const bool live = (MAXH <= 8) || i < d.nheaps;
+        c[u][2 * i] = n1.at(q - d.pstride[i], live && h[i] >= 1);
+        c[u][2 * i + 1] = n2.at(q - 2 * d.pstride[i], live && h[i] >= 2);
+        nch[u] += live ? min(h[i], 2u) : 0u;
+      }
     }
-    uint32_t word;
-    if (S == 0) word = make_word(LOSS, 0);  // all heaps empty: four_to_one.py:19-22
-    else if (mn < 0x40000000u) word = make_word(WIN, (mn & 0x3FFFFFFFu) + 1);  // a LOSS child
-    else word = make_word(mxx >= 0xC0000000u ? TIE : mxx >= 0x80000000u ? DRAW : LOSS, (mxw >> 2) + 1);
-    // Every non-hole slot is written (the word is consumed unconditionally,
-    // so the child loads issue together with the reach word); unreached
-    // slots get W_UNREACHED and are never read as children.
-    const bool reached = (rw >> (q & 63)) & 1ull;
-    mine[q] = reached ? word : W_UNREACHED;
-    if (reached) {
-      npos++;
-      edges += (u64)nch;
-      prims += S == 0;
-      if (S != 0 && mxw >= W_REACHED) err |= ERR_CHILD_UNRESOLVED;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if (!ok[u]) continue;
+      // x = rotr(w ^ 1, 2): value code on top, remapped so LOSS < WIN <
+      // DRAW < TIE (LOSS 00, WIN 01, DRAW 10, TIE 11); an absent child
+      // (w = 0) is a WIN of remoteness 0 and changes no term below
+      uint32_t mn = 0xFFFFFFFFu, mxx = 0, mxw = 0;
+#pragma unroll
+      for (int j = 0; j < 2 * MAXH; j++) {
+        const uint32_t w = c[u][j];
+        const uint32_t x = __builtin_amdgcn_alignbit(w ^ 1u, w ^ 1u, 2);
+        mn = min(mn, x);
+        mxx = max(mxx, x);
+        mxw = max(mxw, w);
+      }
+      uint32_t word;
+      if (S == 0) word = make_word(LOSS, 0);  // all heaps empty: four_to_one.py:19-22
+      else if (mn < 0x40000000u) word = make_word(WIN, (mn & 0x3FFFFFFFu) + 1);  // a LOSS child
+      else word = make_word(mxx >= 0xC0000000u ? TIE : mxx >= 0x80000000u ? DRAW : LOSS, (mxw >> 2) + 1);
+      // Every non-hole slot is written (the word is consumed unconditionally,
+      // so the child loads issue together with the reach word); unreached
+      // slots get W_UNREACHED and are never read as children.
+      const u64 q = qs[u];
+      const bool reached = (rw[u] >> (q & 63)) & 1ull;
+      mine[q] = reached ? word : W_UNREACHED;
+      if (reached) {
+        npos++;
+        edges += (u64)nch[u];
+        prims += S == 0;
+        if (S != 0 && mxw >= W_REACHED) err |= ERR_CHILD_UNRESOLVED;
+      }
     }
   }
   if (err) atomicOr(&st->err, err);

@@ -676,12 +676,15 @@ static void dense_launch_pull_t(gm_solver* s, const DenseView& v, int grid, u64 
 template <int MAXH, bool POW2>
 static void dense_launch_resolve_t(gm_solver* s, const DenseView& v, int grid, u64 L) {
   // buffer loads need every row's byte offsets to fit 32 bits
-  if (v.Wl * 4 <= 0xFFFFFFF0ull)
-    hipLaunchKernelGGL((k_dense_resolve<MAXH, POW2, true>), dim3(grid), dim3(kBlock), 0, s->stream, s->d, v,
+  if (v.Wl * 4 <= 0xFFFFFFF0ull) {
+    // one grid-stride round per iteration: two rounds (24 loads in flight,
+    // fewer waves per SIMD) measured 21.6 vs 17.4 ms per 2^30 resolve
+    hipLaunchKernelGGL((k_dense_resolve<MAXH, POW2, true, 1>), dim3(grid), dim3(kBlock), 0, s->stream, s->d, v,
                        s->words, s->bits, L, s->st);
-  else
-    hipLaunchKernelGGL((k_dense_resolve<MAXH, POW2, false>), dim3(grid), dim3(kBlock), 0, s->stream, s->d, v,
+  } else {
+    hipLaunchKernelGGL((k_dense_resolve<MAXH, POW2, false, 1>), dim3(grid), dim3(kBlock), 0, s->stream, s->d, v,
                        s->words, s->bits, L, s->st);
+  }
 }
 // kernels are instantiated per exact heap count 1..8 (16 = generic)
 template <bool POW2>
