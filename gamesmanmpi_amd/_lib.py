@@ -80,7 +80,7 @@ EXPORTS = (
     "gm_shard_info",
     "gm_ks_begin", "gm_ks_level_size", "gm_ks_expand", "gm_ks_insert",
     "gm_ks_finalize", "gm_ks_counts", "gm_ks_children", "gm_ks_reduce",
-    "gm_ks_end",
+    "gm_ks_end", "gm_graph_solve",
     "gm_last_error", "gm_version",
 )
 
@@ -149,6 +149,9 @@ def load():
                            c.c_void_p, c.c_int],
         "gm_ks_reduce": [c.c_void_p, c.c_int, c.c_void_p, c.c_void_p],
         "gm_ks_end": [c.c_void_p, P(gm_result)],
+        "gm_graph_solve": [c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint64,
+                           c.c_uint64, c.c_void_p, c.c_void_p, c.c_void_p,
+                           P(gm_result)],
     }
     for name, args in sig.items():
         f = getattr(L, name)

@@ -1675,3 +1675,107 @@ int gm_ks_end(gm_solver* s, gm_result* out) {
   }
   return 0;
 }
+
+// ---------------------------------------------------------------------------
+// Explicit-graph retrograde for game files without a device descriptor
+// (SURVEY §8f row 3): the host enumerates the positions with the module's
+// own gen_moves/do_move/primitive (gamesmanmpi_amd/generic.py) and hands
+// over a CSR graph; the device resolves it in rounds.  A round resolves
+// every position whose children are all resolved (any order of positions
+// inside a round is fine: a word, once written, is final), so the number of
+// rounds is the height of the DAG.  No progress with the root unresolved
+// means a cycle (the reference's job loop would never finish either).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_graph_round(const uint8_t* prim, const uint64_t* offsets,
+                                                     const uint32_t* children, uint64_t n, uint32_t* words,
+                                                     DevState* st) {
+  u64 done = 0, edges = 0, prims = 0;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+    if (words[i] != NO_WORD) continue;
+    const int p = prim[i];
+    uint32_t word;
+    if (p != UNDECIDED) {
+      word = make_word(p, 0);  // process.py:120-123: primitive, remoteness 0
+      prims++;
+    } else {
+      const u64 a = offsets[i], b = offsets[i + 1];
+      bool ready = true, any_loss = false, any_tie = false, any_draw = false;
+      uint32_t min_loss = 0xFFFFFFFFu, max_all = 0;
+      for (u64 j = a; j < b && ready; j++) {
+        const uint32_t w = __hip_atomic_load(&words[children[j]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (w == NO_WORD) {
+          ready = false;
+          break;
+        }
+        const uint32_t v = w & 3u, r = w >> 2;
+        if (v == LOSS) { any_loss = true; min_loss = min(min_loss, r); }
+        any_tie |= (v == TIE);
+        any_draw |= (v == DRAW);
+        max_all = max(max_all, r);
+      }
+      if (!ready) continue;
+      if (a == b) {  // no moves but not primitive: the reference's job never resolves
+        atomicOr(&st->err, ERR_NO_MOVES);
+        continue;
+      }
+      // reference-canonical _res_red / _remote_red
+      if (any_loss) word = make_word(WIN, min_loss + 1);
+      else word = make_word(any_tie ? TIE : any_draw ? DRAW : LOSS, max_all + 1);
+      edges += b - a;
+    }
+    __hip_atomic_store(&words[i], word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    done++;
+  }
+  block_add(&st->cursor_front, done);
+  block_add(&st->edges, edges);
+  block_add(&st->prims, prims);
+}
+
+int gm_graph_solve(const uint8_t* prim_dev, const uint64_t* offsets_dev, const uint32_t* children_dev, uint64_t n,
+                   uint64_t root, uint32_t* words_dev, void* scratch_dev, void* stream, gm_result* out) {
+  if (!out || !n || root >= n || !prim_dev || !offsets_dev || !words_dev || !scratch_dev)
+    return fail(GM_EINVAL, "bad argument");
+  memset(out, 0, sizeof *out);
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(GM_ENOGPU, "no HIP device");
+  hipStream_t s = (hipStream_t)stream;
+  DevState* st = (DevState*)scratch_dev;
+  const int grid = (int)std::max<u64>(1, std::min<u64>((n + kBlock - 1) / kBlock, (u64)launch_grid()));
+  auto t0 = std::chrono::steady_clock::now();
+  HIPCHK(hipMemsetAsync(words_dev, 0xFF, n * sizeof(uint32_t), s));
+  HIPCHK(hipMemsetAsync(st, 0, sizeof(DevState), s));
+  u64 resolved = 0, rounds = 0;
+  uint32_t root_word = NO_WORD;
+  for (;;) {
+    hipLaunchKernelGGL(k_graph_round, dim3(grid), dim3(kBlock), 0, s, prim_dev, offsets_dev, children_dev, n,
+                       words_dev, st);
+    HIPCHK(hipGetLastError());
+    rounds++;
+    u64 now = 0;
+    uint32_t err = 0;
+    HIPCHK(hipMemcpyAsync(&now, &st->cursor_front, sizeof now, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&err, &st->err, sizeof err, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (err) return fail(GM_ECORRUPT, "graph solve:%s", err_text(err).c_str());
+    if (now == resolved) break;  // no progress: done, or a cycle
+    resolved = now;
+    if (resolved == n) break;
+  }
+  HIPCHK(hipMemcpyAsync(&root_word, words_dev + root, sizeof root_word, hipMemcpyDeviceToHost, s));
+  DevState hs;
+  HIPCHK(hipMemcpyAsync(&hs, st, sizeof hs, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  out->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  out->positions = hs.cursor_front;
+  out->edges = hs.edges;
+  out->primitives = hs.prims;
+  out->levels = (uint32_t)rounds;
+  out->n_resolve_launches = rounds;
+  out->root_word = root_word;
+  if (resolved != n)
+    return fail(GM_ECORRUPT, "%llu of %llu positions never resolve (cycle)", (unsigned long long)(n - resolved),
+                (unsigned long long)n);
+  out->root_value = (int32_t)(root_word & 3u);
+  out->root_remoteness = root_word >> 2;
+  return 0;
+}

@@ -76,8 +76,10 @@ def build_parser():
                    help="location to store statistics about game",
                    action="store")
     # additions
-    p.add_argument("--layout", choices=["auto", "dense", "hashed"],
-                   default="auto", help="table layout (DESIGN.md §Layout)")
+    p.add_argument("--layout", choices=["auto", "dense", "hashed", "graph"],
+                   default="auto",
+                   help="table layout (DESIGN.md §Layout); graph = host-"
+                        "enumerated positions, for files without a descriptor")
     p.add_argument("--positions", type=int, default=0,
                    help="capacity estimate for boards without a known bound")
     p.add_argument("--no-verify", action="store_true",
@@ -108,6 +110,41 @@ def write_stats(statsdir, rank, spec, solver, result):
                   f, indent=1)
 
 
+def solve_generic(args, game, rank, world, local):
+    """Game files without a device descriptor: the
+    module's own functions enumerate the positions on the host
+    (gamesmanmpi_amd/generic.py), the GPU runs the retrograde.  One GPU:
+    under torchrun only rank 0 solves."""
+    import torch
+    from gamesmanmpi_amd.generic import solve_module
+    if rank == 0:
+        torch.cuda.set_device(local)
+        result, solver = solve_module(game, device="cuda:%d" % local)
+        print(result.root_line, flush=True)  # src/process.py:47-52
+        if args.json:
+            print(json.dumps({"game": os.path.basename(args.game_file),
+                              "root": result.root_line,
+                              "positions": result.positions,
+                              "edges": result.edges,
+                              "ms_total": result.ms_total,
+                              "host_enumeration_s": result.extra["host_enumeration_s"],
+                              "layout": "graph", "ranks": 1}), flush=True)
+        if args.statsdir:
+            import numpy as np
+            d = os.path.join(args.statsdir, "stats", "0")
+            os.makedirs(d, exist_ok=True)
+            names, val, rem = solver.dump()
+            np.savez_compressed(os.path.join(d, "solution.npz"),
+                                names=np.array(names), value=val, remoteness=rem)
+            with open(os.path.join(d, "meta.json"), "w") as f:
+                json.dump({"game": os.path.basename(args.game_file),
+                           "root": result.root_line, "positions": len(names),
+                           "layout": "graph", "key": "str(position)",
+                           "value_codes": {"WIN": 0, "LOSS": 1, "TIE": 2, "DRAW": 3}},
+                          f, indent=1)
+    return 0
+
+
 def main(argv=None):
     args = build_parser().parse_args(argv)
     rank = int(os.environ.get("RANK", "0"))
@@ -126,8 +163,16 @@ def main(argv=None):
     if root not in sys.path:
         sys.path.insert(0, root)
     from gamesmanmpi_amd.games import spec_for_module
-    spec = spec_for_module(game, os.path.splitext(
-        os.path.basename(args.game_file))[0])
+    try:
+        spec = spec_for_module(game, os.path.splitext(
+            os.path.basename(args.game_file))[0])
+    except ValueError as e:  # no device descriptor for this file
+        if args.layout not in ("auto", "graph"):
+            raise
+        logging.debug("%s: solving through the host-enumerated graph", e)
+        return solve_generic(args, game, rank, world, local)
+    if args.layout == "graph":
+        return solve_generic(args, game, rank, world, local)
     if not args.no_verify:
         n = spec.verify(game, samples=args.verify_samples)
         logging.debug("descriptor %r verified on %d positions", spec, n)

@@ -152,3 +152,19 @@ def test_launcher_end_to_end(tmp_path):
     z = np.load(tmp_path / "sd" / "stats" / "0" / "solution.npz")
     assert len(z["keys"]) == 5 * 7 * 4
     shutil.rmtree(tmp_path / "sd")
+
+
+@pytest.mark.gpu
+def test_launcher_graph_path_for_file_without_descriptor(tmp_path):
+    """A game file with no device descriptor (tests/games/grid_tictactoe.py)
+    is enumerated on the host with its own functions and solved on the GPU:
+    same root line as the reference's tic_tac_toe_np (TIE in 9 moves)."""
+    from gamesmanmpi_amd import solver_launcher as sl
+    game = os.path.join(ROOT, "tests", "games", "grid_tictactoe.py")
+    out = io.StringIO()
+    with redirect_stdout(out):
+        rc = sl.main([game, "-sd", str(tmp_path / "sd")])
+    assert rc == 0
+    assert out.getvalue().strip().splitlines()[0] == "TIE in 9 moves"
+    z = np.load(tmp_path / "sd" / "stats" / "0" / "solution.npz")
+    assert len(z["names"]) == 5478
