@@ -48,29 +48,33 @@ class GroupExchange:
 
 class TorchExchange:
     """One shard per process over the initialised torch.distributed default
-    group; tensors live on `device` (cuda for RCCL, cpu for gloo)."""
+    group.  Tensors live on `device` (cuda for RCCL, cpu for gloo);
+    `stage` = a device to run the collectives on instead (e.g. cpu with gloo
+    when several ranks share one GPU in tests -- RCCL needs one GPU per
+    rank)."""
 
-    def __init__(self, device):
+    def __init__(self, device, stage=None):
         import torch
         import torch.distributed as dist
         self.torch, self.dist, self.device = torch, dist, device
+        self.stage = torch.device(stage) if stage is not None else device
 
     def all_to_all(self, send):
         torch, dist = self.torch, self.dist
         (lists,) = send
         in_sizes = [int(t.numel()) for t in lists]
-        sizes = torch.tensor(in_sizes, dtype=torch.int64, device=self.device)
+        sizes = torch.tensor(in_sizes, dtype=torch.int64, device=self.stage)
         got = torch.empty_like(sizes)
         dist.all_to_all_single(got, sizes)
         out_sizes = [int(x) for x in got.tolist()]
-        inp = torch.cat(lists)
-        out = torch.empty(sum(out_sizes), dtype=inp.dtype, device=self.device)
+        inp = torch.cat(lists).to(self.stage)
+        out = torch.empty(sum(out_sizes), dtype=inp.dtype, device=self.stage)
         dist.all_to_all_single(out, inp, out_sizes, in_sizes)
-        return [list(torch.split(out, out_sizes))]
+        return [list(torch.split(out.to(self.device), out_sizes))]
 
     def allreduce_sum(self, values):
         (v,) = values
-        t = self.torch.tensor(v, dtype=self.torch.int64, device=self.device)
+        t = self.torch.tensor(v, dtype=self.torch.int64, device=self.stage)
         self.dist.all_reduce(t)
         return [int(x) for x in t.tolist()]
 
@@ -296,7 +300,7 @@ def group_keyed_solve(spec, world, device=None):
     return keyed_solve(shards, GroupExchange()), shards
 
 
-def dist_keyed_solve(spec, device=None, positions=0):
+def dist_keyed_solve(spec, device=None, positions=0, stage=None):
     """This process's shard of an md5-sharded job over the initialised
     torch.distributed default group; `positions`: bound for the whole job
     (0: the game's own).  Returns (SolveResult, GpuShard)."""
@@ -305,4 +309,4 @@ def dist_keyed_solve(spec, device=None, positions=0):
     per_shard = 2 * int(positions) // world + 4096 if positions else 0
     shard = GpuShard(spec, dist.get_rank(), world, device=device,
                      positions=per_shard)
-    return keyed_solve([shard], TorchExchange(shard.device)), shard
+    return keyed_solve([shard], TorchExchange(shard.device, stage)), shard
