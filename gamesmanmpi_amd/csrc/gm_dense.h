@@ -263,6 +263,36 @@ __global__ __launch_bounds__(256) void k_dense_pull_words(Desc d, DenseView v, u
 }
 #undef TD
 
+// Packed word halo (sharded power-of-two tables, gm_solver.hip
+// exchange_words): the non-hole words of two consecutive top-value slices
+// of one level move between a slice pair and a dense buffer.  One wave per
+// 64-slot group; the group's non-hole mask is the pull's TS-window mask for
+// x = S - t, its packed offset comes from the host-built table off[x][g]
+// (both ends of a halo use the same order).  pack = 1: slices -> buf.
+__global__ __launch_bounds__(256) void k_halo_move(Desc d, const u64* __restrict__ masks,
+                                                   const uint32_t* __restrict__ off, u64 G, int XN,
+                                                   uint32_t* slices, u64 Z, int64_t x0, uint32_t tot0,
+                                                   uint32_t* buf, int pack) {
+  const uint32_t lane = __lane_id();
+  const int H0 = (int)d.heap[0];
+  const u64 nwaves = (u64)gridDim.x * (blockDim.x >> 6);
+  const u64 w0 = (u64)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  for (u64 w = w0; w < 2 * G; w += nwaves) {
+    const u64 slice = w / G, g = w - slice * G;
+    const int64_t x = x0 - (int64_t)slice;
+    if (x < 0 || x >= XN) continue;
+    const u64 r0 = g * 64;
+    int sg = 0;
+    for (int i = 1; i < d.nheaps; i++) sg += (int)((r0 >> d.pshift[i]) & (d.base[i] - 1));
+    const u64 V = mask_le(masks, (int)x - sg) & ~mask_le(masks, (int)x - H0 - 1 - sg);
+    if (!((V >> lane) & 1ull)) continue;
+    const u64 idx = (slice ? tot0 : 0) + off[(u64)x * G + g] + (u64)__popcll(V & ((1ull << lane) - 1ull));
+    uint32_t* slot = slices + slice * Z + r0 + lane;
+    if (pack) buf[idx] = *slot;
+    else *slot = buf[idx];
+  }
+}
+
 // XCD-aware split of [0, n) (MI355X dispatches workgroup b to XCD b % 8):
 // the blocks of one XCD grid-stride over one contiguous, 64-aligned chunk,
 // so the child words that neighbouring prefixes share are fetched into ONE

@@ -300,6 +300,32 @@ static size_t mask_tables_offset(int max_levels) { return (devstate_bytes(max_le
 static size_t scratch_bytes_for(int max_levels) {
   return mask_tables_offset(max_levels) + kMaskTableWords * sizeof(u64);
 }
+// Packed word halos of sharded power-of-two dense tables (exchange_words):
+// after the mask tables, the group offset table off[XN][G] (u32; G = Z/64
+// groups of a slice, XN = values of x = S - t that leave any slot valid),
+// then a send and a receive buffer of 2 slices of words each.
+struct HaloGeom {
+  u64 G = 0, Z = 0;
+  int XN = 0;
+  bool on = false;
+};
+static HaloGeom halo_geom(const Desc* d, int world) {
+  HaloGeom h;
+  if (world <= 1 || !d->pow2 || d->nheaps < 2) return h;
+  const int k = d->nheaps - 1;
+  h.Z = d->pstride[k];
+  if (h.Z % 64) return h;
+  h.G = h.Z / 64;
+  int slow = 0;
+  for (int i = 1; i < k; i++) slow += (int)d->heap[i];
+  h.XN = slow + (int)d->heap[0] + 1;
+  h.on = true;
+  return h;
+}
+static size_t halo_bytes(const HaloGeom& h) {
+  if (!h.on) return 0;
+  return ((size_t)h.XN * h.G * 4 + 255) / 256 * 256 + 2 * (2 * h.Z * 4);
+}
 
 __device__ __forceinline__ u64 mix64(u64 x) {  // splitmix64 finaliser
   x ^= x >> 31;
@@ -601,6 +627,16 @@ struct gm_solver {
   u64 lcap;
   DevState* st;
   const u64* masks;  // dense pow2 mask tables in scratch (k_dense_pull_words)
+  // sharded dense solves: halo exchanges run on their own stream, ordered
+  // against the compute stream by events (created on first use)
+  hipStream_t cstream = nullptr;
+  std::vector<hipEvent_t> pev;
+  // packed word halos (HaloGeom): device offset table, buffers, host totals
+  HaloGeom hg;
+  const uint32_t* halo_off = nullptr;
+  uint32_t* halo_send = nullptr;
+  uint32_t* halo_recv = nullptr;
+  std::vector<uint32_t> halo_tot;
   hipStream_t stream;
   bool own_stream;
   uint32_t flags;
@@ -951,7 +987,7 @@ int gm_plan_shard(int game, int rank, int world, uint32_t flags, uint64_t max_ta
   if (!d || !out) return fail(GM_EINVAL, "bad argument");
   memset(out, 0, sizeof *out);
   out->max_levels = (uint32_t)d->max_levels;
-  out->scratch_bytes = scratch_bytes_for(d->max_levels);
+  out->scratch_bytes = scratch_bytes_for(d->max_levels) + halo_bytes(halo_geom(d, world));
   if (!d->dense_ok || (flags & GM_F_FORCE_HASHED))
     return fail(GM_EINVAL, "only DENSE layouts shard by prefix blocks; keyed tables shard by md5 owner");
   bool fits = false;
@@ -1007,6 +1043,35 @@ static void build_mask_tables(const Desc& d, u64* M) {
       for (int i = 1; i < d.nheaps; i++)
         if (dj[i] <= (uint32_t)t) M[64 * (i + 1) + t] |= 1ull << j;
     }
+  }
+}
+
+// Slot r of a top-value slice is a non-hole at level L iff the digit sum
+// of r (all prefix digits below the top) lies in [x - heap0, x], x = S - t.
+// For every x and every 64-slot group g of a slice: the packed offset of the
+// group's first non-hole (exclusive prefix over groups in slot order) and,
+// per x, the slice's non-hole total.  Sender and receiver of a halo compute
+// the same order, so packed slots need no index.
+static u64 host_mask_le(const u64* T, int t) { return t < 0 ? 0ull : (t >= 63 ? ~0ull : T[t]); }
+static void build_halo_offsets(const Desc& d, const u64* M, const HaloGeom& h, std::vector<uint32_t>& off,
+                               std::vector<uint32_t>& tot) {
+  off.assign((size_t)h.XN * h.G, 0);
+  tot.assign((size_t)h.XN, 0);
+  std::vector<int> sg(h.G);
+  for (u64 g = 0; g < h.G; g++) {
+    int sum = 0;
+    for (int i = 1; i < d.nheaps; i++) sum += (int)(((g * 64) >> d.pshift[i]) & (d.base[i] - 1));
+    sg[g] = sum;
+  }
+  const int H0 = (int)d.heap[0];
+  for (int x = 0; x < h.XN; x++) {
+    uint32_t run = 0;
+    for (u64 g = 0; g < h.G; g++) {
+      off[(size_t)x * h.G + g] = run;
+      const u64 V = host_mask_le(M, x - sg[g]) & ~host_mask_le(M, x - H0 - 1 - sg[g]);
+      run += (uint32_t)__builtin_popcountll(V);
+    }
+    tot[x] = run;
   }
 }
 
@@ -1070,6 +1135,23 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
       gm_solver_destroy(s);
       return fail(GM_EHIP, "mask tables: %s", hipGetErrorString(e));
     }
+    s->hg = halo_geom(d, world);
+    if (s->hg.on && buf->scratch_bytes >= scratch_bytes_for(d->max_levels) + halo_bytes(s->hg)) {
+      char* base = (char*)buf->scratch + scratch_bytes_for(d->max_levels);
+      const size_t tab = ((size_t)s->hg.XN * s->hg.G * 4 + 255) / 256 * 256;
+      s->halo_off = (const uint32_t*)base;
+      s->halo_send = (uint32_t*)(base + tab);
+      s->halo_recv = s->halo_send + 2 * s->hg.Z;
+      std::vector<uint32_t> off;
+      build_halo_offsets(*d, m.data(), s->hg, off, s->halo_tot);
+      e = hipMemcpy((void*)s->halo_off, off.data(), off.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+      if (e != hipSuccess) {
+        gm_solver_destroy(s);
+        return fail(GM_EHIP, "halo offsets: %s", hipGetErrorString(e));
+      }
+    } else {
+      s->hg.on = false;  // scratch from an older plan: whole-slice halos
+    }
   }
   *out = s;
   return 0;
@@ -1108,6 +1190,8 @@ int gm_solver_set_flags(gm_solver* s, uint32_t flags) {
 
 void gm_solver_destroy(gm_solver* s) {
   if (!s) return;
+  for (hipEvent_t e : s->pev) (void)hipEventDestroy(e);
+  if (s->cstream) (void)hipStreamDestroy(s->cstream);
   if (s->comm) (void)ncclCommDestroy(s->comm);
   if (s->own_stream) (void)hipStreamDestroy(s->stream);
   delete s;
@@ -1223,54 +1307,6 @@ __global__ void k_fill_red(DevState* st) {
   }
 }
 
-// halo regions of a dense shard (local addresses of top-digit slices)
-static u64* halo_bits(gm_solver* s, u64 L, u64 t0) {
-  return s->bits + (L * s->view.Wbl + (t0 - s->top_lo) * s->Z) / 64;
-}
-static uint32_t* halo_words(gm_solver* s, u64 L, u64 t0) {
-  return s->words + L * s->view.Wl + (t0 - s->top_lo) * s->Z;
-}
-
-// Exchange after pull(L): every shard's lowest two owned slices of level-L
-// reach bits go to the shard below (its parent halo).  mode: 1 = RCCL
-// (one process per GPU), 2 = in-process group (device-to-device copies).
-static int exchange_bits(std::vector<gm_solver*>& ss, u64 L, int mode) {
-  const u64 nbytes = 2 * ss[0]->Z / 8;
-  if (mode == 1) {
-    gm_solver* s = ss[0];
-    ncclGroupStart();
-    if (s->rank > 0) ncclSend(halo_bits(s, L, s->top_a), nbytes, ncclUint8, s->rank - 1, s->comm, s->stream);
-    if (s->rank + 1 < s->world) ncclRecv(halo_bits(s, L, s->top_b), nbytes, ncclUint8, s->rank + 1, s->comm, s->stream);
-    ncclResult_t r = ncclGroupEnd();
-    if (r != ncclSuccess) return fail(GM_EHIP, "RCCL bits halo: %s", ncclGetErrorString(r));
-    return 0;
-  }
-  for (size_t g = 1; g < ss.size(); g++)
-    HIPCHK(hipMemcpyAsync(halo_bits(ss[g - 1], L, ss[g]->top_a), halo_bits(ss[g], L, ss[g]->top_a), nbytes,
-                          hipMemcpyDeviceToDevice, ss[g]->stream));
-  return 0;
-}
-
-// Exchange after resolve(L): every shard's highest two owned slices of
-// level-L words go to the shard above (its child halo).
-static int exchange_words(std::vector<gm_solver*>& ss, u64 L, int mode) {
-  const u64 nbytes = 2 * ss[0]->Z * 4;
-  if (mode == 1) {
-    gm_solver* s = ss[0];
-    ncclGroupStart();
-    if (s->rank + 1 < s->world)
-      ncclSend(halo_words(s, L, s->top_b - 2), nbytes, ncclUint8, s->rank + 1, s->comm, s->stream);
-    if (s->rank > 0) ncclRecv(halo_words(s, L, s->top_a - 2), nbytes, ncclUint8, s->rank - 1, s->comm, s->stream);
-    ncclResult_t r = ncclGroupEnd();
-    if (r != ncclSuccess) return fail(GM_EHIP, "RCCL words halo: %s", ncclGetErrorString(r));
-    return 0;
-  }
-  for (size_t g = 0; g + 1 < ss.size(); g++)
-    HIPCHK(hipMemcpyAsync(halo_words(ss[g + 1], L, ss[g]->top_b - 2), halo_words(ss[g], L, ss[g]->top_b - 2), nbytes,
-                          hipMemcpyDeviceToDevice, ss[g]->stream));
-  return 0;
-}
-
 // Band of level L: every non-hole slot has digit sum s(p) in [S - H0, S]
 // (S = root_sum - L), so its prefix lies between the smallest prefix with
 // s >= S - H0 (fill the low digits first) and the largest with s <= S (fill
@@ -1301,6 +1337,134 @@ static DenseView dense_band(const Desc& d, const DenseView& v, u64 L) {
   b.p_hi = std::min<u64>(v.p_hi, pmax + 1);
   if (b.p_hi < b.p_lo) b.p_hi = b.p_lo;
   return b;
+}
+
+// Halo exchanges of a dense shard group.  Only the part of the two slices
+// that lies in level L's band (dense_band) travels: bits of [t0, t0+2)
+// slices as whole 64-bit words, words as 4-B runs.  `cs` is the stream the
+// copies / RCCL calls are enqueued on.  mode: 1 = RCCL (one process per
+// GPU), 2 = in-process group (device-to-device copies).
+static bool band_slice(const gm_solver* s, const DenseView& band, u64 t0, u64* lo, u64* hi) {
+  // global prefixes of slices [t0, t0 + 2) clipped to the level band
+  const u64 a = std::max<u64>(t0 * s->Z, band.p_lo), b = std::min<u64>((t0 + 2) * s->Z, band.p_hi);
+  if (b <= a) return false;
+  *lo = a;
+  *hi = b;
+  return true;
+}
+
+// after pull(L): every shard's lowest two owned slices of level-L reach
+// bits go to the shard below (its parent halo)
+static int exchange_bits(std::vector<gm_solver*>& ss, u64 L, int mode, hipStream_t cs) {
+  const Desc& d = ss[0]->d;
+  if (mode == 1) {
+    gm_solver* s = ss[0];
+    u64 lo, hi;
+    ncclGroupStart();
+    // what this rank sends (its bottom slices) and receives (the rank above's
+    // bottom slices = its halo) cover the same band of global prefixes
+    if (s->rank > 0 && band_slice(s, dense_band(d, DenseView{0, ~0ull, 0, 0, 0}, L), s->top_a, &lo, &hi)) {
+      lo &= ~63ull;
+      hi = (hi + 63) & ~63ull;
+      ncclSend(s->bits + (L * s->view.Wbl + lo - s->view.base_off) / 64, (hi - lo) / 8, ncclUint8, s->rank - 1,
+               s->comm, cs);
+    }
+    if (s->rank + 1 < s->world && band_slice(s, dense_band(d, DenseView{0, ~0ull, 0, 0, 0}, L), s->top_b, &lo, &hi)) {
+      lo &= ~63ull;
+      hi = (hi + 63) & ~63ull;
+      ncclRecv(s->bits + (L * s->view.Wbl + lo - s->view.base_off) / 64, (hi - lo) / 8, ncclUint8, s->rank + 1,
+               s->comm, cs);
+    }
+    ncclResult_t r = ncclGroupEnd();
+    if (r != ncclSuccess) return fail(GM_EHIP, "RCCL bits halo: %s", ncclGetErrorString(r));
+    return 0;
+  }
+  for (size_t g = 1; g < ss.size(); g++) {
+    u64 lo, hi;
+    if (!band_slice(ss[g], dense_band(d, DenseView{0, ~0ull, 0, 0, 0}, L), ss[g]->top_a, &lo, &hi)) continue;
+    lo &= ~63ull;
+    hi = (hi + 63) & ~63ull;
+    HIPCHK(hipMemcpyAsync(ss[g - 1]->bits + (L * ss[g - 1]->view.Wbl + lo - ss[g - 1]->view.base_off) / 64,
+                          ss[g]->bits + (L * ss[g]->view.Wbl + lo - ss[g]->view.base_off) / 64, (hi - lo) / 8,
+                          hipMemcpyDeviceToDevice, cs));
+  }
+  return 0;
+}
+
+// packed halo helpers: non-hole words of slices (t0, t0 + 1) at level L
+static uint32_t halo_total(const gm_solver* s, int64_t x) {
+  return (x < 0 || x >= s->hg.XN) ? 0u : s->halo_tot[(size_t)x];
+}
+static void halo_move(gm_solver* s, u64 L, u64 t0, uint32_t* buf, int pack, hipStream_t cs) {
+  const int64_t x0 = (int64_t)s->d.root_sum - (int64_t)L - (int64_t)t0;
+  const u64 waves = 2 * s->hg.G;
+  const int grid = (int)std::max<u64>(1, std::min<u64>((waves + 3) / 4, (u64)s->grid));
+  hipLaunchKernelGGL(k_halo_move, dim3(grid), dim3(kBlock), 0, cs, s->d, s->masks, s->halo_off, s->hg.G, s->hg.XN,
+                     s->words + L * s->view.Wl + (t0 * s->Z - s->view.base_off), s->Z, x0, halo_total(s, x0), buf,
+                     pack);
+}
+static uint32_t halo_count(const gm_solver* s, u64 L, u64 t0) {
+  const int64_t x0 = (int64_t)s->d.root_sum - (int64_t)L - (int64_t)t0;
+  return halo_total(s, x0) + halo_total(s, x0 - 1);
+}
+
+// after resolve(L): every shard's highest two owned slices of level-L words
+// go to the shard above (its child halo).  Power-of-two tables send only the
+// non-hole words (k_halo_move): about a fifth of the two slices, averaged
+// over the levels.
+static int exchange_words(std::vector<gm_solver*>& ss, u64 L, int mode, hipStream_t cs) {
+  const Desc& d = ss[0]->d;
+  bool packed = true;
+  for (gm_solver* s : ss) packed = packed && s->hg.on;
+  if (packed && mode == 1) {
+    gm_solver* s = ss[0];
+    const bool up = s->rank + 1 < s->world, down = s->rank > 0;
+    const uint32_t nsend = up ? halo_count(s, L, s->top_b - 2) : 0;
+    const uint32_t nrecv = down ? halo_count(s, L, s->top_a - 2) : 0;
+    if (nsend) halo_move(s, L, s->top_b - 2, s->halo_send, 1, cs);
+    ncclGroupStart();
+    if (nsend) ncclSend(s->halo_send, (size_t)nsend * 4, ncclUint8, s->rank + 1, s->comm, cs);
+    if (nrecv) ncclRecv(s->halo_recv, (size_t)nrecv * 4, ncclUint8, s->rank - 1, s->comm, cs);
+    ncclResult_t r = ncclGroupEnd();
+    if (r != ncclSuccess) return fail(GM_EHIP, "RCCL words halo: %s", ncclGetErrorString(r));
+    if (nrecv) halo_move(s, L, s->top_a - 2, s->halo_recv, 0, cs);
+    HIPCHK(hipGetLastError());
+    return 0;
+  }
+  if (packed) {
+    for (size_t g = 0; g + 1 < ss.size(); g++) {
+      const u64 t0 = ss[g]->top_b - 2;
+      const uint32_t n = halo_count(ss[g], L, t0);
+      if (!n) continue;
+      halo_move(ss[g], L, t0, ss[g]->halo_send, 1, cs);
+      HIPCHK(hipMemcpyAsync(ss[g + 1]->halo_recv, ss[g]->halo_send, (size_t)n * 4, hipMemcpyDeviceToDevice, cs));
+      halo_move(ss[g + 1], L, t0, ss[g + 1]->halo_recv, 0, cs);
+    }
+    HIPCHK(hipGetLastError());
+    return 0;
+  }
+  if (mode == 1) {
+    gm_solver* s = ss[0];
+    u64 lo, hi;
+    ncclGroupStart();
+    if (s->rank + 1 < s->world && band_slice(s, dense_band(d, DenseView{0, ~0ull, 0, 0, 0}, L), s->top_b - 2, &lo, &hi))
+      ncclSend(s->words + L * s->view.Wl + (lo - s->view.base_off), (hi - lo) * 4, ncclUint8, s->rank + 1, s->comm,
+               cs);
+    if (s->rank > 0 && band_slice(s, dense_band(d, DenseView{0, ~0ull, 0, 0, 0}, L), s->top_a - 2, &lo, &hi))
+      ncclRecv(s->words + L * s->view.Wl + (lo - s->view.base_off), (hi - lo) * 4, ncclUint8, s->rank - 1, s->comm,
+               cs);
+    ncclResult_t r = ncclGroupEnd();
+    if (r != ncclSuccess) return fail(GM_EHIP, "RCCL words halo: %s", ncclGetErrorString(r));
+    return 0;
+  }
+  for (size_t g = 0; g + 1 < ss.size(); g++) {
+    u64 lo, hi;
+    if (!band_slice(ss[g], dense_band(d, DenseView{0, ~0ull, 0, 0, 0}, L), ss[g]->top_b - 2, &lo, &hi)) continue;
+    HIPCHK(hipMemcpyAsync(ss[g + 1]->words + L * ss[g + 1]->view.Wl + (lo - ss[g + 1]->view.base_off),
+                          ss[g]->words + L * ss[g]->view.Wl + (lo - ss[g]->view.base_off), (hi - lo) * 4,
+                          hipMemcpyDeviceToDevice, cs));
+  }
+  return 0;
 }
 
 // Dense solve of one table (world 1), one shard of an RCCL job, or every
@@ -1346,34 +1510,105 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
   auto t0 = std::chrono::steady_clock::now();
   HIPCHK(hipEventRecord(e0, st));
   for (gm_solver* s : ss) HIPCHK(hipMemsetAsync(s->st, 0, devstate_bytes(T), st));
-  // forward (pull): level 0 .. T-1, each level's bitmap written exactly once
+  // Sharded solves overlap each level's halo exchange with compute: a
+  // level's launch is split into the part whose parents (pull) / children
+  // (resolve) lie inside the shard's own block -- which includes the two
+  // slices the exchange sends -- and the two boundary slices that read the
+  // halo.  Per level: own part -> event -> exchange on the comm stream ->
+  // event; the boundary part of the NEXT level waits for that exchange.  A
+  // block narrower than 4 top values has no such split: exchange in order.
+  bool pipe = mode != 0;
+  for (gm_solver* s : ss)
+    if (s->top_b - s->top_a < 4) pipe = false;
+  hipStream_t cs = st;
+  hipEvent_t* E = nullptr;  // [0, T): own part done, [T, 2T): exchange done (forward); reused backward
+  if (pipe) {
+    if (!s0->cstream) HIPCHK(hipStreamCreateWithFlags(&s0->cstream, hipStreamNonBlocking));
+    while (s0->pev.size() < 2 * (size_t)T) {
+      hipEvent_t e;
+      HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      s0->pev.push_back(e);
+    }
+    cs = s0->cstream;
+    E = s0->pev.data();
+  }
+  auto clip = [](const DenseView& v, u64 lo, u64 hi) {
+    DenseView c = v;
+    c.p_lo = std::max<uint64_t>(v.p_lo, lo);
+    c.p_hi = std::min<uint64_t>(v.p_hi, hi);
+    if (c.p_hi < c.p_lo) c.p_hi = c.p_lo;
+    return c;
+  };
+  // forward (pull): level 0 .. T-1, each level's bitmap written exactly once.
+  // Parents are one or two top values ABOVE: the boundary is the top two
+  // slices [b-2, b), whose parents sit in the halo [b, b+2) sent down by the
+  // rank above.
   for (int L = 0; L < T; L++) {
+    if (timing) HIPCHK(hipEventRecord(kx[2 * L], st));
     for (gm_solver* s : ss) {
-      if (timing && s == s0) HIPCHK(hipEventRecord(kx[2 * L], st));
       const DenseView b = dense_band(d, s->view, (u64)L);
-      if (b.p_hi > b.p_lo) dense_launch_pull(s, b, grid_of(s, b), (u64)L, root_p);
-      if (timing && s == s0) HIPCHK(hipEventRecord(kx[2 * L + 1], st));
+      const DenseView own = pipe ? clip(b, 0, (s->top_b - 2) * s->Z) : b;
+      if (own.p_hi > own.p_lo) dense_launch_pull(s, own, grid_of(s, own), (u64)L, root_p);
     }
     if (mode) {
-      int rc = exchange_bits(ss, (u64)L, mode);
+      if (pipe) {
+        HIPCHK(hipEventRecord(E[L], st));
+        HIPCHK(hipStreamWaitEvent(cs, E[L], 0));
+      }
+      int rc = exchange_bits(ss, (u64)L, mode, cs);
       if (rc) return rc;
+      if (pipe) {
+        HIPCHK(hipEventRecord(E[T + L], cs));
+        if (L >= 1) HIPCHK(hipStreamWaitEvent(st, E[T + L - 1], 0));  // halos of L-1 (L-2 waited before)
+        for (gm_solver* s : ss) {
+          const DenseView b = dense_band(d, s->view, (u64)L);
+          const DenseView bd = clip(b, (s->top_b - 2) * s->Z, ~0ull);
+          if (bd.p_hi > bd.p_lo) dense_launch_pull(s, bd, grid_of(s, bd), (u64)L, root_p);
+        }
+      }
     }
+    if (timing) HIPCHK(hipEventRecord(kx[2 * L + 1], st));
   }
   HIPCHK(hipGetLastError());
+  if (pipe) {  // the backward pass reuses the events: drain the forward exchanges first
+    HIPCHK(hipEventRecord(E[0], cs));
+    HIPCHK(hipStreamWaitEvent(st, E[0], 0));
+  }
   HIPCHK(hipEventRecord(e1, st));
+  // backward (resolve): children are one or two top values BELOW: the
+  // boundary is the bottom two slices [a, a+2), whose children sit in the
+  // halo [a-2, a) sent up by the rank below.
   for (int L = T - 1; L >= 0; L--) {
+    if (timing) HIPCHK(hipEventRecord(kr[2 * L], st));
     for (gm_solver* s : ss) {
-      if (timing && s == s0) HIPCHK(hipEventRecord(kr[2 * L], st));
       const DenseView b = dense_band(d, s->view, (u64)L);
-      if (b.p_hi > b.p_lo) dense_launch_resolve(s, b, grid_of(s, b), (u64)L);
-      if (timing && s == s0) HIPCHK(hipEventRecord(kr[2 * L + 1], st));
+      const DenseView own = pipe ? clip(b, (s->top_a + 2) * s->Z, ~0ull) : b;
+      if (own.p_hi > own.p_lo) dense_launch_resolve(s, own, grid_of(s, own), (u64)L);
     }
     if (mode) {
-      int rc = exchange_words(ss, (u64)L, mode);
+      if (pipe) {
+        HIPCHK(hipEventRecord(E[L], st));
+        HIPCHK(hipStreamWaitEvent(cs, E[L], 0));
+      }
+      int rc = exchange_words(ss, (u64)L, mode, cs);
       if (rc) return rc;
+      if (pipe) {
+        HIPCHK(hipEventRecord(E[T + L], cs));
+        if (L + 1 < T) HIPCHK(hipStreamWaitEvent(st, E[T + L + 1], 0));  // halos of L+1 (L+2 waited before)
+        for (gm_solver* s : ss) {
+          const DenseView b = dense_band(d, s->view, (u64)L);
+          const DenseView bd = clip(b, 0, (s->top_a + 2) * s->Z);
+          if (bd.p_hi > bd.p_lo) dense_launch_resolve(s, bd, grid_of(s, bd), (u64)L);
+        }
+      }
     }
+    if (timing) HIPCHK(hipEventRecord(kr[2 * L + 1], st));
   }
   HIPCHK(hipGetLastError());
+  if (pipe) {  // every exchange done before the reduction and the host read-back
+    HIPCHK(hipEventRecord(E[0], cs));
+    HIPCHK(hipStreamWaitEvent(st, E[0], 0));
+  }
   HIPCHK(hipEventRecord(e2, st));
   for (gm_solver* s : ss) {
     hipLaunchKernelGGL(k_dense_root, dim3(1), dim3(64), 0, st, s->view, s->words, s->bits, root_p, s->st);

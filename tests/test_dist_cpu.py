@@ -52,8 +52,9 @@ def _run(world, params):
 
 
 @pytest.mark.parametrize("world,params", [
-    (2, "heaps=31:31:31:31:31:63"),   # bench N=2 workload
-    (4, "heaps=31:31:31:31:31:127"),  # bench N=4 workload
+    (2, "heaps=31:31:31:31:31:3:15"),  # bench N=2 workload
+    (4, "heaps=31:31:31:31:31:3:31"),  # bench N=4 workload
+    (8, "heaps=31:31:31:31:31:3:63"),  # bench N=8 workload
     (2, "heaps=7:7:7:15"),
 ])
 def test_gloo_bootstrap_and_geometry(world, params):
@@ -74,6 +75,8 @@ def test_gloo_bootstrap_and_geometry(world, params):
             assert prev["b"] == i["a"]                 # blocks tile [0, E)
             assert i["lo"] == i["a"] - 2               # child halo = prev's top 2
             assert prev["hi"] == min(E, prev["b"] + 2)  # parent halo = my bottom 2
-    if world == 2 and E == 64:
-        # 2^30 positions per GPU: 32 top values x 32^5 prefixes... x 32 heap-0
-        assert [i["b"] - i["a"] for i in infos] == [32, 32]
+    if E == 8 * world and "3:" in params:
+        # bench shape: 8 top values per rank, 32^4 x 4 prefixes per value,
+        # x 32 heap-0 values = 2^30 positions per GPU
+        assert [i["b"] - i["a"] for i in infos] == [8] * world
+        assert Z == 32 ** 4 * 4

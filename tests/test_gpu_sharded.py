@@ -62,15 +62,16 @@ def test_group_matches_oracle():
 
 
 def test_bench_geometry_two_shards():
-    """The N=2 bench workload's geometry (top heap 63, slices of 2^20
-    prefixes) at one GPU's scale: 31:31:31:31:63 = 2^26 positions."""
-    params = "heaps=31:31:31:31:63"
+    """The N=2 bench workload's shape (31^k x 3 x 15: 8 top values per rank,
+    packed word halos) at one GPU's scale: 31:31:31:31:3:15 = 2^26
+    positions."""
+    params = "heaps=31:31:31:31:3:15"
     r1, s1 = _single(params)
     rg, shards = _group(params, 2)
     assert (rg.positions, rg.edges, rg.root_line) == (r1.positions, r1.edges,
                                                       r1.root_line)
     rng = np.random.default_rng(1)
-    keys = rng.integers(0, 32 ** 4 * 64, size=1 << 16, dtype=np.uint64)
+    keys = rng.integers(0, 32 ** 4 * 4 * 16, size=1 << 16, dtype=np.uint64)
     w, hits = _words_by_owner(shards, keys)
     assert (hits == 1).all()
     np.testing.assert_array_equal(w, s1.query(keys))
@@ -80,3 +81,24 @@ def test_bad_geometry_is_refused():
     from gamesmanmpi_amd import _lib
     with pytest.raises(_lib.GmError):
         _group("heaps=7:7:7:15", 16)  # blocks of 1 top value: halo spans ranks
+
+
+@pytest.mark.parametrize("world,params,npos", [
+    (3, "heaps=31:31:31:31:127", 32 ** 4 * 128),
+    (4, "heaps=31:31:31:31:127", 32 ** 4 * 128),
+    (4, "heaps=31:31:31:3:31", 32 ** 3 * 4 * 32),   # the N=4 bench shape, smaller
+    (8, "heaps=31:31:31:3:63", 32 ** 3 * 4 * 64),   # the N=8 bench shape, smaller
+])
+def test_pipelined_halo_exchange_wide_blocks(world, params, npos):
+    """Blocks of >= 4 top values take the overlapped schedule (own part,
+    exchange on the comm stream, boundary slices after the previous level's
+    halo arrived) with packed word halos; every sampled word equal to the
+    unsharded solve's."""
+    r1, s1 = _single(params)
+    rg, shards = _group(params, world)
+    assert (rg.positions, rg.edges, rg.root_line) == (r1.positions, r1.edges, r1.root_line)
+    rng = np.random.default_rng(world)
+    keys = rng.integers(0, npos, size=1 << 18, dtype=np.uint64)
+    w, hits = _words_by_owner(shards, keys)
+    assert (hits == 1).all()
+    np.testing.assert_array_equal(w, s1.query(keys))
