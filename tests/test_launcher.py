@@ -151,6 +151,12 @@ def test_launcher_end_to_end(tmp_path):
     assert out.getvalue().strip().splitlines()[0] == want
     z = np.load(tmp_path / "sd" / "stats" / "0" / "solution.npz")
     assert len(z["keys"]) == 5 * 7 * 4
+    # the solution database answers for the initial position (db.py)
+    from gamesmanmpi_amd.db import main as db_main
+    out = io.StringIO()
+    with redirect_stdout(out):
+        assert db_main([str(tmp_path / "sd"), "--game", str(game)]) == 0
+    assert out.getvalue().strip().endswith(want)
     shutil.rmtree(tmp_path / "sd")
 
 
