@@ -6,9 +6,10 @@ A "step" is one complete strong solve from the root: table reset, forward
 expansion of every level, retrograde pass of every level, root word back on
 the host.  N=1 workload: heaps 31^6 = 2^30 = 1,073,741,824 positions,
 187 levels, 12,280,922,112 edges.  For N>1 (one process per GPU, launched by
-torch.distributed.run) the heaps are 31^5 x 3 x (8N-1): 2^30 positions per
-GPU, the ranks split the last heap's values (8 each) and exchange two
-boundary slices per level over RCCL.  Every step's counts and root value
+torch.distributed.run) the heaps are 31^5 x (32N-1): 2^30 positions per
+GPU; the ranks split the last heap's values into blocks of 8 dealt round
+robin and exchange two boundary slices per block and level over RCCL
+(DESIGN.md §Multi-GPU).  Every step's counts and root value
 are checked against closed forms; a wrong solve aborts the run.
 
 Prints ONE JSON line (rank 0).  Fields beyond the driver contract:
@@ -31,18 +32,15 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
 
 
 def heaps_for(world):
-    """Weak scaling, 2^30 positions per GPU.  N=1 is SURVEY §8d's 31^6
-    (2^30 positions, 187 levels, b = 11.4375).  N>1: 31^5 x 3 x (8N - 1):
-    the ranks split the last heap, 8 of its values each (DESIGN.md
-    §Multi-GPU: a position's children lie one or two values below, so a
-    rank's halo is 2 of its 8 slices; narrower blocks than the 32 of a
-    31^5 x (32N-1) layout keep the ranks' per-level work within 1.15 / 1.44
-    / 2.04x of the mean at N = 2 / 4 / 8 instead of 1.51 / 2.53 / 4.58x)."""
+    """Weak scaling, 2^30 positions per GPU: heaps 31^5 x (32N - 1).  N=1 is
+    SURVEY §8d's 31^6 (2^30 positions, 187 levels, b = 11.4375).  The ranks
+    split the last heap into blocks of 8 values dealt round robin, four per
+    rank (round robin keeps the ranks' per-level work
+    within 1.11 / 1.19 / 1.41x of the mean at N = 2 / 4 / 8; one contiguous
+    block of 32 per rank would give 1.51 / 2.53 / 4.58x)."""
     if world not in (1, 2, 4, 8):
         raise SystemExit("--gpus must be 1, 2, 4 or 8")
-    if world == 1:
-        return [31] * 6
-    return [31] * 5 + [3, 8 * world - 1]
+    return [31] * 5 + [32 * world - 1]
 
 
 def expected(heaps):
@@ -212,7 +210,7 @@ def main():
                    "positions_per_gpu": r.positions // world, "edges_per_gpu": r.edges // world,
                    "levels": r.levels, "root": r.root_line,
                    "layout": layout,
-                   "parallelism": ("top-heap blocks x%d, RCCL halo exchange" % world
+                   "parallelism": ("round-robin top-heap blocks x%d, RCCL halo exchange" % world
                                    if world > 1 else "1 GPU")},
         "roofline": {"bound": "hbm", "kernel": kname,
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

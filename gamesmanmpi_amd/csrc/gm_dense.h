@@ -121,10 +121,6 @@ __device__ __forceinline__ bool reach_bit(const u64* bits, u64 pos) {
   return (bits[pos >> 6] >> (pos & 63)) & 1ull;
 }
 
-// Grid-stride rounds each wave keeps in flight.  Measured on MI355X
-// (2^30-position solve): 1 -> 92 ms, pull 4 / resolve 2 -> 111 ms (the
-// extra registers cost occupancy), so one round per wave it is.
-constexpr int PULL_UNROLL = 1;
 
 // Forward, PULL form, target level L: each non-hole slot of level L ORs the
 // reach bits of its parents -- the positions one move away, i.e. one heap +1
@@ -137,49 +133,39 @@ __global__ __launch_bounds__(256) void k_dense_pull(Desc d, DenseView v, u64* bi
   const u64 b0 = L * v.Wbl, b1 = (L - 1) * v.Wbl, b2 = (L - 2) * v.Wbl;  // b1/b2 used only when L >= 1/2
   const u64 stride = (u64)gridDim.x * blockDim.x;
   // whole waves over [p_lo, p_hi rounded up to 64): every lane reaches the
-  // ballot (p_lo and base_off are multiples of 64)
+  // ballot (p_lo is a multiple of 64)
   const u64 n = (v.p_hi - v.p_lo + 63) & ~63ull;
   WaveDigits<MAXH, POW2> wd;
   wd.init(d);
-  for (u64 i0 = (u64)blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += PULL_UNROLL * stride) {
-    bool par[PULL_UNROLL][2 * MAXH];
-    bool root_here[PULL_UNROLL];
-#pragma unroll
-    for (int u = 0; u < PULL_UNROLL; u++) {
-      const u64 p = v.p_lo + i0 + u * stride;  // global prefix
-      const u64 q = p - v.base_off;            // local prefix
-      root_here[u] = false;
-#pragma unroll
-      for (int j = 0; j < 2 * MAXH; j++) par[u][j] = false;
-      if (p >= v.p_hi) continue;
-      uint32_t h[MAXH];
-      uint32_t s = wd.digits(d, p & ~63ull, p, h);
-      if (s > S || S - s > d.heap[0]) continue;  // hole
+  for (u64 i0 = (u64)blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += stride) {
+    const u64 q = v.p_lo + i0;  // local prefix
+    const u64 qw = q & ~63ull;
+    bool run;
+    const u64 pw = dense_global(v, __builtin_amdgcn_readfirstlane((uint32_t)qw) |
+                                       ((u64)__builtin_amdgcn_readfirstlane((uint32_t)(qw >> 32)) << 32),
+                                &run);
+    if (!run) continue;  // wave-uniform: another launch's slice, or a halo
+    const u64 p = pw + (q - qw);  // global prefix
+    bool reached = false;
+    uint32_t h[MAXH];
+    const uint32_t s = wd.digits(d, pw, p, h);
+    if (q < v.p_hi && s <= S && S - s <= d.heap[0]) {  // not a hole
       if (L == 0) {
-        root_here[u] = p == root_p;  // level 0 holds only the root
-        continue;
-      }
-      const uint32_t h0 = S - s;
-      par[u][0] = h0 + 1 <= d.heap[0] && reach_bit(bits, b1 + q);
-      par[u][1] = L >= 2 && h0 + 2 <= d.heap[0] && reach_bit(bits, b2 + q);
+        reached = p == root_p;  // level 0 holds only the root
+      } else {
+        const uint32_t h0 = S - s;
+        reached = (h0 + 1 <= d.heap[0] && reach_bit(bits, b1 + q)) ||
+                  (L >= 2 && h0 + 2 <= d.heap[0] && reach_bit(bits, b2 + q));
 #pragma unroll
-      for (int i = 1; i < MAXH; i++) {
-        const bool live = (MAXH <= 8) || i < d.nheaps;  // exact heap count when MAXH <= 8
-        par[u][2 * i] = live && h[i] + 1 <= d.heap[i] && reach_bit(bits, b1 + q + d.pstride[i]);
-        par[u][2 * i + 1] = live && L >= 2 && h[i] + 2 <= d.heap[i] && reach_bit(bits, b2 + q + 2 * d.pstride[i]);
+        for (int i = 1; i < MAXH; i++) {
+          const bool live = (MAXH <= 8) || i < d.nheaps;  // exact heap count when MAXH <= 8
+          reached = reached || (live && h[i] + 1 <= d.heap[i] && reach_bit(bits, b1 + q + d.pstride[i])) ||
+                    (live && L >= 2 && h[i] + 2 <= d.heap[i] && reach_bit(bits, b2 + q + 2 * d.pstride[i]));
+        }
       }
     }
-#pragma unroll
-    for (int u = 0; u < PULL_UNROLL; u++) {
-      const u64 i = i0 + u * stride;
-      if (i >= n) break;  // wave-uniform: n and stride are multiples of 64
-      bool reached = root_here[u];
-#pragma unroll
-      for (int j = 0; j < 2 * MAXH; j++) reached |= par[u][j];
-      u64 m = __ballot(reached);
-      const u64 q = v.p_lo + i - v.base_off;
-      if (__lane_id() == 0) bits[(b0 + (q & ~63ull)) >> 6] = m;
-    }
+    const u64 m = __ballot(reached);
+    if (__lane_id() == 0) bits[(b0 + qw) >> 6] = m;
   }
 }
 
@@ -221,8 +207,10 @@ __global__ __launch_bounds__(256) void k_dense_pull_words(Desc d, DenseView v, u
   const u64 ngroups = (v.p_hi - v.p_lo + 63) >> 6;
   const u64 stride = (u64)gridDim.x * blockDim.x;
   for (u64 gi = (u64)blockIdx.x * blockDim.x + threadIdx.x; gi < ngroups; gi += stride) {
-    const u64 pg = v.p_lo + (gi << 6);  // global prefix of lane-bit 0
-    const u64 q = pg - v.base_off;      // local prefix (multiple of 64)
+    const u64 q = v.p_lo + (gi << 6);  // local prefix of lane-bit 0 (multiple of 64)
+    bool run;
+    const u64 pg = dense_global(v, q, &run);  // global prefix of lane-bit 0
+    if (!run) continue;  // another launch's slice, or a halo
     int dg[MAXH];
     int sg = 0;
 #pragma unroll
@@ -234,7 +222,7 @@ __global__ __launch_bounds__(256) void k_dense_pull_words(Desc d, DenseView v, u
     // valid: S - H0 <= sg + sj <= S
     const int lo_s = S - H0 - sg, hi_s = S - sg;
     u64 V = mask_le(TS, hi_s) & ~mask_le(TS, lo_s - 1);
-    if (pg + 64 > v.p_hi) V &= (1ull << (v.p_hi - pg)) - 1;
+    if (q + 64 > v.p_hi) V &= (1ull << (v.p_hi - q)) - 1;
     u64 reached = 0;
     if (L == 0) {
       if (root_p >= pg && root_p < pg + 64) reached = 1ull << (root_p - pg);
@@ -354,7 +342,7 @@ struct WordRow<false> {
 //               all children         (min of LOSS words, max of words)
 // The reach-bit word is loaded with the child words (children of a non-hole
 // slot are never holes), so a round costs one memory latency.
-template <int MAXH, bool POW2, bool BUF, int U>
+template <int MAXH, bool POW2, bool BUF, int U, bool BLK>
 __global__ __launch_bounds__(256) void k_dense_resolve(Desc d, DenseView v, uint32_t* words, const u64* bits, u64 L,
                                                        DevState* st) {
   const uint32_t S = d.root_sum - (uint32_t)L;
@@ -380,12 +368,19 @@ __global__ __launch_bounds__(256) void k_dense_resolve(Desc d, DenseView v, uint
       rw[u] = 0;
       nch[u] = 0;
       const u64 iu = i0 + (u64)u * r.stride;
-      const u64 p = v.p_lo + iu;
-      const u64 q = p - v.base_off;
+      const u64 q = v.p_lo + iu;  // local prefix
+      const u64 qw = q & ~63ull;
       qs[u] = q;
+      bool run = true;
+      u64 pw = qw;  // world 1: local = global
+      if (BLK)
+        pw = dense_global(v, __builtin_amdgcn_readfirstlane((uint32_t)qw) |
+                                 ((u64)__builtin_amdgcn_readfirstlane((uint32_t)(qw >> 32)) << 32),
+                          &run);
+      const u64 p = pw + (q - qw);  // global prefix
       uint32_t h[MAXH];
-      const uint32_t s = wd.digits(d, p & ~63ull, p, h);
-      const bool valid = iu < r.end && s <= S && S - s <= d.heap[0];  // not a hole
+      const uint32_t s = wd.digits(d, pw, p, h);
+      const bool valid = run && iu < r.end && s <= S && S - s <= d.heap[0];  // not a hole
       if (!__ballot(valid)) continue;                                 // a wave of holes
       if (!valid) continue;
       ok[u] = true;
@@ -443,14 +438,12 @@ __global__ __launch_bounds__(256) void k_dense_resolve(Desc d, DenseView v, uint
   block_add(&st->prims, prims);
 }
 
-// root word (on the shard that owns the root; others report NO_WORD)
-__global__ void k_dense_root(DenseView v, const uint32_t* words, const u64* bits, u64 root_p, DevState* st) {
+// root word (on the shard that owns the root, root_q = its local prefix;
+// others pass ~0 and report NO_WORD)
+__global__ void k_dense_root(DenseView v, const uint32_t* words, const u64* bits, u64 root_q, DevState* st) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     uint32_t w = NO_WORD;
-    if (root_p >= v.p_lo && root_p < v.p_hi) {
-      const u64 q = root_p - v.base_off;  // level 0
-      if (reach_bit(bits, q)) w = words[q];
-    }
+    if (root_q != ~0ull && reach_bit(bits, root_q)) w = words[root_q];  // level 0
     st->root_word = w;
   }
 }
@@ -463,22 +456,24 @@ __global__ void k_dense_query(Desc d, DenseView v, const uint32_t* words, const 
     uint32_t w = NO_WORD;
     if (dense_slot_of(d, keys[i], &slot)) {
       slot_split(d, slot, &L, &p);
-      if (p >= v.p_lo && p < v.p_hi) {
-        const u64 q = p - v.base_off;
-        if (reach_bit(bits, L * v.Wbl + q)) w = words[L * v.Wl + q];
-      }
+      uint64_t q;
+      if (dense_local(v, p, &q) && reach_bit(bits, L * v.Wbl + q)) w = words[L * v.Wl + q];
     }
     out[i] = w;
   }
 }
 
-// every reachable owned position -> its key (order arbitrary)
+// every reachable owned position -> its key (order arbitrary); v sweeps the
+// whole local range with the own-slice filter
 __global__ void k_dense_positions(Desc d, DenseView v, const u64* bits, u64 levels, u64* out, u64 cap, u64* count) {
-  const u64 n = v.p_hi - v.p_lo;
+  const u64 n = v.Wl;
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < levels * n; i += (u64)gridDim.x * blockDim.x) {
-    const u64 L = i / n, p = v.p_lo + (i - L * n);
+    const u64 L = i / n, q = i - L * n;
+    bool run;
+    const u64 p = dense_global(v, q, &run);
+    if (!run) continue;
     int64_t h0 = dense_h0(d, L, p);
-    if (h0 < 0 || !reach_bit(bits, L * v.Wbl + (p - v.base_off))) continue;
+    if (h0 < 0 || !reach_bit(bits, L * v.Wbl + q)) continue;
     u64 k = atomicAdd(count, 1ull);
     if (k < cap) out[k] = p * d.base[0] + (u64)h0;
   }

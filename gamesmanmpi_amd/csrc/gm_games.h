@@ -79,17 +79,54 @@ struct Desc {
   uint32_t pshift[16];   // log2(pstride[i]) when pow2
 };
 
-// Which part of a DENSE table's global prefix space one table holds.  A
-// single-GPU solve holds everything; a shard owns the
-// prefixes whose TOP digit lies in [a, b) and keeps two halo slices of that
-// digit on each side: p_lo/p_hi bound the owned global prefixes, base_off
-// is the global prefix of local index 0, Wl the local words per level and
-// Wbl the local reach bits per level (Wl rounded up to 64).
+// Which part of a DENSE table's global prefix space one table holds, and
+// which part a launch sweeps.  A single-GPU table holds everything (local
+// prefix = global prefix).  A shard (blk = 1) owns
+// BLOCKS of B consecutive values of the TOP prefix digit, block k owned by
+// rank k mod world, and lays them out one after another, each as
+// [2 halo slices | B own slices | 2 halo slices] of Z prefixes (Z = the top
+// digit's stride): local slice u is slice o = u mod (B + 4) of its rank's
+// block j = u / (B + 4), i.e. top value t = (rank + j world) B + o - 2.
+// p_lo/p_hi bound the local prefixes a launch sweeps; a launch processes
+// only slices with olo <= o < ohi (own slices: [2, B + 2)).  Wl = local
+// words per level, Wbl = local reach bits per level (Wl rounded up to 64).
 struct DenseView {
   uint64_t p_lo, p_hi;
-  uint64_t base_off;
+  uint64_t base_off;  // always 0 (local addressing starts at 0)
   uint64_t Wl, Wbl;
+  uint32_t blk, B, world, rank;
+  uint64_t Z, E;
+  int32_t zshift;     // log2(Z) when Z is a power of two, else -1
+  uint32_t olo, ohi;
 };
+
+// global prefix of local prefix q; *run = this launch processes its slice
+// (q's slice must be the same for every lane of a wave: Z % 64 == 0)
+GM_HD uint64_t dense_global(const DenseView& v, uint64_t q, bool* run) {
+  if (!v.blk) {
+    *run = true;
+    return q;
+  }
+  const uint64_t u = v.zshift >= 0 ? (q >> v.zshift) : q / v.Z;
+  const uint32_t j = (uint32_t)u / (v.B + 4), o = (uint32_t)u - j * (v.B + 4);
+  const int64_t t = (int64_t)(((uint64_t)v.rank + (uint64_t)j * v.world) * v.B + o) - 2;
+  *run = o >= v.olo && o < v.ohi && t >= 0 && (uint64_t)t < v.E;
+  return (uint64_t)t * v.Z + (q - u * v.Z);
+}
+
+// local prefix of global prefix p, if this table owns it
+GM_HD bool dense_local(const DenseView& v, uint64_t p, uint64_t* q) {
+  if (!v.blk) {
+    if (p >= v.Wl) return false;
+    *q = p;
+    return true;
+  }
+  const uint64_t t = p / v.Z, k = t / v.B;
+  if (t >= v.E || k % v.world != v.rank) return false;
+  const uint64_t u = (k / v.world) * (v.B + 4) + 2 + (t - k * v.B);
+  *q = u * v.Z + (p - t * v.Z);
+  return true;
+}
 
 GM_HD int popc64(uint64_t v) {
 #if defined(__HIP_DEVICE_COMPILE__)

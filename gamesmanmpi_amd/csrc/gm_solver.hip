@@ -219,43 +219,59 @@ static int build_desc(const char* name, const char* params, Desc* out) {
 }
 
 // Shard geometry of a dense table.  world == 1: the whole prefix space.
-// world > 1: the ranks split the values [0, E) of the TOP prefix digit
-// (heap K-1) into blocks of ceil(E / world) >= 2; rank r owns [a, b) and
-// keeps halo slices [a-2, a) (children of its positions: one move lowers a
-// heap by 1 or 2) and [b, b+2) (parents, for the pull-form forward pass).
+// world > 1: the values [0, E) of the TOP prefix digit (heap K-1) are cut
+// into blocks of B and block k is owned by rank k mod world (round robin:
+// every rank's top values spread over the whole range, so the ranks'
+// per-level work stays close -- DESIGN.md §Multi-GPU).  Each block keeps
+// halo slices [kB-2, kB) (children: one move lowers a heap by 1 or 2) and
+// [kB+B, kB+B+2) (parents, for the pull-form forward pass).  B = 8 when
+// every rank gets at least two blocks, else ceil(E / world) (one block per
+// rank); GM_SHARD_BLOCK overrides.
 struct DenseGeom {
   DenseView v;
-  u64 a, b, lo, hi, Z, E;
+  u64 nblocks, nb;
 };
 static int dense_geom(const Desc* d, int rank, int world, DenseGeom* g) {
   memset(g, 0, sizeof *g);
   if (world <= 1) {
     g->v.p_lo = 0;
     g->v.p_hi = d->W;
-    g->v.base_off = 0;
     g->v.Wl = d->W;
     g->v.Wbl = (d->W + 63) & ~63ull;
-    g->E = 1;
-    g->Z = d->W;
-    g->a = 0; g->b = 1; g->lo = 0; g->hi = 1;
+    g->v.world = 1;
+    g->v.zshift = -1;
+    g->nblocks = g->nb = 1;
     return 0;
   }
   if (d->nheaps < 2) return fail(GM_EINVAL, "sharding needs at least 2 heaps");
+  if (rank < 0 || rank >= world) return fail(GM_EINVAL, "bad shard %d/%d", rank, world);
   const int k = d->nheaps - 1;
   const u64 E = d->base[k], Z = d->pstride[k];
   if (Z % 64) return fail(GM_EINVAL, "shard slices must hold a multiple of 64 prefixes (got %llu)", (unsigned long long)Z);
-  const u64 B = (E + world - 1) / world;
-  const u64 a = (u64)rank * B, b = std::min<u64>(E, a + B);
-  if (rank < 0 || rank >= world || a >= E || b - a < 2 || E - (u64)(world - 1) * B < 2)
-    return fail(GM_EINVAL, "top heap of %llu values cannot be split into %d blocks of >= 2", (unsigned long long)E, world);
-  g->a = a; g->b = b; g->E = E; g->Z = Z;
-  g->lo = a >= 2 ? a - 2 : 0;
-  g->hi = std::min<u64>(E, b + 2);
-  g->v.p_lo = a * Z;
-  g->v.p_hi = b * Z;
-  g->v.base_off = g->lo * Z;
-  g->v.Wl = (g->hi - g->lo) * Z;
-  g->v.Wbl = g->v.Wl;  // multiple of 64
+  u64 B = E >= 16 * (u64)world ? 8 : (E + world - 1) / world;
+  if (const char* e = getenv("GM_SHARD_BLOCK")) B = (u64)atoll(e);
+  const u64 nblocks = B ? (E + B - 1) / B : 0;
+  if (B < 2 || nblocks < (u64)world)
+    return fail(GM_EINVAL, "top heap of %llu values cannot give %d ranks blocks of >= 2", (unsigned long long)E, world);
+  g->nblocks = nblocks;
+  g->nb = (nblocks - (u64)rank + world - 1) / world;
+  DenseView& v = g->v;
+  v.blk = 1;
+  v.B = (uint32_t)B;
+  v.world = (uint32_t)world;
+  v.rank = (uint32_t)rank;
+  v.Z = Z;
+  v.E = E;
+  v.zshift = (Z & (Z - 1)) ? -1 : __builtin_ctzll(Z);
+  v.olo = 2;
+  v.ohi = (uint32_t)B + 2;
+  v.Wl = g->nb * (B + 4) * Z;
+  v.Wbl = v.Wl;  // multiple of 64
+  if (v.Wl * 4 > 0xFFFFFFF0ull)  // the shard resolve addresses a level with 32-bit buffer offsets
+    return fail(GM_EINVAL, "shard of %llu prefixes per level: more than 2^30 (use more ranks)",
+                (unsigned long long)v.Wl);
+  v.p_lo = 0;
+  v.p_hi = v.Wl;
   return 0;
 }
 static u64 dense_words_bytes(const Desc* d, const DenseGeom& g) {
@@ -305,26 +321,28 @@ static size_t scratch_bytes_for(int max_levels) {
 // groups of a slice, XN = values of x = S - t that leave any slot valid),
 // then a send and a receive buffer of 2 slices of words each.
 struct HaloGeom {
-  u64 G = 0, Z = 0;
+  u64 G = 0, Z = 0, nb = 0;
   int XN = 0;
   bool on = false;
 };
-static HaloGeom halo_geom(const Desc* d, int world) {
+static HaloGeom halo_geom(const Desc* d, int world, u64 nb) {
   HaloGeom h;
   if (world <= 1 || !d->pow2 || d->nheaps < 2) return h;
   const int k = d->nheaps - 1;
   h.Z = d->pstride[k];
   if (h.Z % 64) return h;
   h.G = h.Z / 64;
+  h.nb = nb;
   int slow = 0;
   for (int i = 1; i < k; i++) slow += (int)d->heap[i];
   h.XN = slow + (int)d->heap[0] + 1;
   h.on = true;
   return h;
 }
+// offset table + send and receive buffers of 2 slices per local block
 static size_t halo_bytes(const HaloGeom& h) {
   if (!h.on) return 0;
-  return ((size_t)h.XN * h.G * 4 + 255) / 256 * 256 + 2 * (2 * h.Z * 4);
+  return ((size_t)h.XN * h.G * 4 + 255) / 256 * 256 + 2 * (h.nb * 2 * h.Z * 4);
 }
 
 __device__ __forceinline__ u64 mix64(u64 x) {  // splitmix64 finaliser
@@ -619,7 +637,7 @@ struct gm_solver {
   u64 nslots;       // DENSE: levels * Wl
   // dense sharding over the top prefix digit
   int rank, world;
-  u64 top_a, top_b, top_lo, top_hi, Z, E;
+  u64 nblocks;  // blocks of the top digit over all ranks (view.B values each)
   ncclComm_t comm;  // RCCL communicator (world > 1), or null
   gm_slot* tab;
   u64 mask;
@@ -712,15 +730,19 @@ static void dense_launch_pull_t(gm_solver* s, const DenseView& v, int grid, u64 
 template <int MAXH, bool POW2>
 static void dense_launch_resolve_t(gm_solver* s, const DenseView& v, int grid, u64 L) {
   // buffer loads need every row's byte offsets to fit 32 bits
-  if (v.Wl * 4 <= 0xFFFFFFF0ull) {
-    // one grid-stride round per iteration: two rounds (24 loads in flight,
-    // fewer waves per SIMD) measured 21.6 vs 17.4 ms per 2^30 resolve
-    hipLaunchKernelGGL((k_dense_resolve<MAXH, POW2, true, 1>), dim3(grid), dim3(kBlock), 0, s->stream, s->d, v,
-                       s->words, s->bits, L, s->st);
-  } else {
-    hipLaunchKernelGGL((k_dense_resolve<MAXH, POW2, false, 1>), dim3(grid), dim3(kBlock), 0, s->stream, s->d, v,
-                       s->words, s->bits, L, s->st);
-  }
+  // one grid-stride round per iteration: two rounds (24 loads in flight,
+  // fewer waves per SIMD) measured 21.6 vs 17.4 ms per 2^30 resolve.  The
+  // block-layout mapping (shards) is a separate instantiation so the
+  // single-table kernel carries none of it.
+  if (v.blk)
+    hipLaunchKernelGGL((k_dense_resolve<MAXH, POW2, true, 1, true>), dim3(grid), dim3(kBlock), 0, s->stream, s->d,
+                       v, s->words, s->bits, L, s->st);
+  else if (v.Wl * 4 <= 0xFFFFFFF0ull)
+    hipLaunchKernelGGL((k_dense_resolve<MAXH, POW2, true, 1, false>), dim3(grid), dim3(kBlock), 0, s->stream, s->d,
+                       v, s->words, s->bits, L, s->st);
+  else
+    hipLaunchKernelGGL((k_dense_resolve<MAXH, POW2, false, 1, false>), dim3(grid), dim3(kBlock), 0, s->stream, s->d,
+                       v, s->words, s->bits, L, s->st);
 }
 // kernels are instantiated per exact heap count 1..8 (16 = generic)
 template <bool POW2>
@@ -977,7 +999,7 @@ int gm_shard_info(int game, int rank, int world, uint64_t out[8]) {
   DenseGeom g;
   int rc = dense_geom(d, rank, world, &g);
   if (rc) return rc;
-  const uint64_t v[8] = {g.a, g.b, g.lo, g.hi, g.Z, g.E, g.v.p_lo, g.v.p_hi};
+  const uint64_t v[8] = {g.v.B, g.nblocks, g.nb, (uint64_t)rank, g.v.Z, g.v.E, g.v.Wl, (uint64_t)world};
   memcpy(out, v, sizeof v);
   return 0;
 }
@@ -987,9 +1009,13 @@ int gm_plan_shard(int game, int rank, int world, uint32_t flags, uint64_t max_ta
   if (!d || !out) return fail(GM_EINVAL, "bad argument");
   memset(out, 0, sizeof *out);
   out->max_levels = (uint32_t)d->max_levels;
-  out->scratch_bytes = scratch_bytes_for(d->max_levels) + halo_bytes(halo_geom(d, world));
+  out->scratch_bytes = scratch_bytes_for(d->max_levels);
   if (!d->dense_ok || (flags & GM_F_FORCE_HASHED))
     return fail(GM_EINVAL, "only DENSE layouts shard by prefix blocks; keyed tables shard by md5 owner");
+  DenseGeom g;
+  int grc = dense_geom(d, rank, world, &g);
+  if (grc) return grc;
+  out->scratch_bytes += halo_bytes(halo_geom(d, world, g.nb));
   bool fits = false;
   int rc = plan_dense(d, rank, world, max_table_bytes, out, &fits);
   if (rc) return rc;
@@ -1106,7 +1132,7 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
   s->bits = (u64*)((char*)buf->table + (buf->mode == GM_MODE_DENSE ? dense_words_bytes(d, g) : 0));
   s->rank = rank;
   s->world = world;
-  s->top_a = g.a; s->top_b = g.b; s->top_lo = g.lo; s->top_hi = g.hi; s->Z = g.Z; s->E = g.E;
+  s->nblocks = g.nblocks;
   s->comm = nullptr;
   s->tab = (gm_slot*)buf->table;
   s->mask = buf->table_slots - 1;
@@ -1135,13 +1161,13 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
       gm_solver_destroy(s);
       return fail(GM_EHIP, "mask tables: %s", hipGetErrorString(e));
     }
-    s->hg = halo_geom(d, world);
+    s->hg = halo_geom(d, world, (u64)(s->view.blk ? s->view.Wl / ((s->view.B + 4) * s->view.Z) : 1));
     if (s->hg.on && buf->scratch_bytes >= scratch_bytes_for(d->max_levels) + halo_bytes(s->hg)) {
       char* base = (char*)buf->scratch + scratch_bytes_for(d->max_levels);
       const size_t tab = ((size_t)s->hg.XN * s->hg.G * 4 + 255) / 256 * 256;
       s->halo_off = (const uint32_t*)base;
       s->halo_send = (uint32_t*)(base + tab);
-      s->halo_recv = s->halo_send + 2 * s->hg.Z;
+      s->halo_recv = s->halo_send + s->hg.nb * 2 * s->hg.Z;
       std::vector<uint32_t> off;
       build_halo_offsets(*d, m.data(), s->hg, off, s->halo_tot);
       e = hipMemcpy((void*)s->halo_off, off.data(), off.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
@@ -1339,131 +1365,185 @@ static DenseView dense_band(const Desc& d, const DenseView& v, u64 L) {
   return b;
 }
 
-// Halo exchanges of a dense shard group.  Only the part of the two slices
-// that lies in level L's band (dense_band) travels: bits of [t0, t0+2)
-// slices as whole 64-bit words, words as 4-B runs.  `cs` is the stream the
-// copies / RCCL calls are enqueued on.  mode: 1 = RCCL (one process per
+// Halo exchanges of a dense shard group (block layout, DenseView).  Block
+// k's bottom two own slices (top values kB, kB+1) are the upper halo of
+// block k-1 (reach bits, after the pull); its top two own slices are the
+// lower halo of block k+1 (words, after the resolve).  With blocks dealt
+// round robin every block of rank r sends to the same neighbour rank
+// (r -/+ 1 mod world), in block order, and the receiver walks its blocks in
+// the same order.  Only the part of a slice pair inside level L's band
+// travels: bits as whole 64-bit words, words packed to their non-hole slots
+// (power-of-two tables, k_halo_move) or as the band's 4-B run.  `cs` is the
+// stream the copies / RCCL calls run on.  mode: 1 = RCCL (one process per
 // GPU), 2 = in-process group (device-to-device copies).
-static bool band_slice(const gm_solver* s, const DenseView& band, u64 t0, u64* lo, u64* hi) {
-  // global prefixes of slices [t0, t0 + 2) clipped to the level band
-  const u64 a = std::max<u64>(t0 * s->Z, band.p_lo), b = std::min<u64>((t0 + 2) * s->Z, band.p_hi);
+
+// local slice index of slice o of local block j
+static u64 blk_slice(const gm_solver* s, u64 j, u64 o) { return j * (s->view.B + 4) + o; }
+// global top value of slice o of local block j
+static int64_t blk_top(const gm_solver* s, u64 j, u64 o) {
+  return (int64_t)(((u64)s->view.rank + j * s->view.world) * s->view.B + o) - 2;
+}
+static u64 blk_count(const gm_solver* s) { return s->view.Wl / ((s->view.B + 4) * s->view.Z); }
+static u64 blk_global(const gm_solver* s, u64 j) { return (u64)s->view.rank + j * s->view.world; }
+
+// prefixes [lo, hi) (offsets inside the slice pair starting at top value
+// t0) of level L's band; false if none
+static bool band_pair(const gm_solver* s, u64 L, int64_t t0, u64* lo, u64* hi) {
+  const DenseView all{0, ~0ull, 0, 0, 0};
+  const DenseView band = dense_band(s->d, all, L);
+  const int64_t Z = (int64_t)s->view.Z;
+  const int64_t a = std::max<int64_t>(t0 * Z, (int64_t)band.p_lo);
+  const int64_t b = std::min<int64_t>((t0 + 2) * Z, (int64_t)std::min<u64>(band.p_hi, (u64)INT64_MAX));
   if (b <= a) return false;
-  *lo = a;
-  *hi = b;
+  *lo = (u64)(a - t0 * Z);
+  *hi = (u64)(b - t0 * Z);
   return true;
 }
 
-// after pull(L): every shard's lowest two owned slices of level-L reach
-// bits go to the shard below (its parent halo)
+// after pull(L): bits of every block's bottom two own slices go down
 static int exchange_bits(std::vector<gm_solver*>& ss, u64 L, int mode, hipStream_t cs) {
-  const Desc& d = ss[0]->d;
+  auto bits_at = [&](gm_solver* s, u64 j, u64 o, u64 off) {
+    return s->bits + (L * s->view.Wbl + blk_slice(s, j, o) * s->view.Z + off) / 64;
+  };
   if (mode == 1) {
     gm_solver* s = ss[0];
-    u64 lo, hi;
+    const int down = (s->rank + s->world - 1) % s->world, up = (s->rank + 1) % s->world;
+    const u64 nb = blk_count(s), B = s->view.B;
     ncclGroupStart();
-    // what this rank sends (its bottom slices) and receives (the rank above's
-    // bottom slices = its halo) cover the same band of global prefixes
-    if (s->rank > 0 && band_slice(s, dense_band(d, DenseView{0, ~0ull, 0, 0, 0}, L), s->top_a, &lo, &hi)) {
-      lo &= ~63ull;
-      hi = (hi + 63) & ~63ull;
-      ncclSend(s->bits + (L * s->view.Wbl + lo - s->view.base_off) / 64, (hi - lo) / 8, ncclUint8, s->rank - 1,
-               s->comm, cs);
+    for (u64 j = 0; j < nb; j++) {
+      u64 lo, hi;
+      if (blk_global(s, j) >= 1 && band_pair(s, L, blk_top(s, j, 2), &lo, &hi)) {  // to block k-1
+        lo &= ~63ull;
+        hi = (hi + 63) & ~63ull;
+        ncclSend(bits_at(s, j, 2, lo), (hi - lo) / 8, ncclUint8, down, s->comm, cs);
+      }
     }
-    if (s->rank + 1 < s->world && band_slice(s, dense_band(d, DenseView{0, ~0ull, 0, 0, 0}, L), s->top_b, &lo, &hi)) {
-      lo &= ~63ull;
-      hi = (hi + 63) & ~63ull;
-      ncclRecv(s->bits + (L * s->view.Wbl + lo - s->view.base_off) / 64, (hi - lo) / 8, ncclUint8, s->rank + 1,
-               s->comm, cs);
+    for (u64 j = 0; j < nb; j++) {
+      u64 lo, hi;
+      if (blk_global(s, j) + 1 < s->nblocks && band_pair(s, L, blk_top(s, j, B + 2), &lo, &hi)) {  // from block k+1
+        lo &= ~63ull;
+        hi = (hi + 63) & ~63ull;
+        ncclRecv(bits_at(s, j, B + 2, lo), (hi - lo) / 8, ncclUint8, up, s->comm, cs);
+      }
     }
     ncclResult_t r = ncclGroupEnd();
     if (r != ncclSuccess) return fail(GM_EHIP, "RCCL bits halo: %s", ncclGetErrorString(r));
     return 0;
   }
-  for (size_t g = 1; g < ss.size(); g++) {
-    u64 lo, hi;
-    if (!band_slice(ss[g], dense_band(d, DenseView{0, ~0ull, 0, 0, 0}, L), ss[g]->top_a, &lo, &hi)) continue;
-    lo &= ~63ull;
-    hi = (hi + 63) & ~63ull;
-    HIPCHK(hipMemcpyAsync(ss[g - 1]->bits + (L * ss[g - 1]->view.Wbl + lo - ss[g - 1]->view.base_off) / 64,
-                          ss[g]->bits + (L * ss[g]->view.Wbl + lo - ss[g]->view.base_off) / 64, (hi - lo) / 8,
-                          hipMemcpyDeviceToDevice, cs));
+  const int W = (int)ss.size();
+  for (gm_solver* s : ss) {
+    const u64 nb = blk_count(s), B = s->view.B;
+    for (u64 j = 0; j < nb; j++) {
+      const u64 k = blk_global(s, j);
+      u64 lo, hi;
+      if (k < 1 || !band_pair(s, L, blk_top(s, j, 2), &lo, &hi)) continue;
+      gm_solver* dst = ss[(k - 1) % W];
+      const u64 jd = (k - 1) / W;
+      lo &= ~63ull;
+      hi = (hi + 63) & ~63ull;
+      HIPCHK(hipMemcpyAsync(bits_at(dst, jd, B + 2, lo), bits_at(s, j, 2, lo), (hi - lo) / 8,
+                            hipMemcpyDeviceToDevice, cs));
+    }
   }
   return 0;
 }
 
-// packed halo helpers: non-hole words of slices (t0, t0 + 1) at level L
+// packed halo helpers: non-hole words of the slice pair whose first slice
+// has top value t0 at level L (local slice u0)
 static uint32_t halo_total(const gm_solver* s, int64_t x) {
   return (x < 0 || x >= s->hg.XN) ? 0u : s->halo_tot[(size_t)x];
 }
-static void halo_move(gm_solver* s, u64 L, u64 t0, uint32_t* buf, int pack, hipStream_t cs) {
-  const int64_t x0 = (int64_t)s->d.root_sum - (int64_t)L - (int64_t)t0;
+static uint32_t halo_count(const gm_solver* s, u64 L, int64_t t0) {
+  const int64_t x0 = (int64_t)s->d.root_sum - (int64_t)L - t0;
+  return halo_total(s, x0) + halo_total(s, x0 - 1);
+}
+static void halo_move(gm_solver* s, u64 L, u64 u0, int64_t t0, uint32_t* buf, int pack, hipStream_t cs) {
+  const int64_t x0 = (int64_t)s->d.root_sum - (int64_t)L - t0;
   const u64 waves = 2 * s->hg.G;
   const int grid = (int)std::max<u64>(1, std::min<u64>((waves + 3) / 4, (u64)s->grid));
   hipLaunchKernelGGL(k_halo_move, dim3(grid), dim3(kBlock), 0, cs, s->d, s->masks, s->halo_off, s->hg.G, s->hg.XN,
-                     s->words + L * s->view.Wl + (t0 * s->Z - s->view.base_off), s->Z, x0, halo_total(s, x0), buf,
-                     pack);
-}
-static uint32_t halo_count(const gm_solver* s, u64 L, u64 t0) {
-  const int64_t x0 = (int64_t)s->d.root_sum - (int64_t)L - (int64_t)t0;
-  return halo_total(s, x0) + halo_total(s, x0 - 1);
+                     s->words + L * s->view.Wl + u0 * s->view.Z, s->view.Z, x0, halo_total(s, x0), buf, pack);
 }
 
-// after resolve(L): every shard's highest two owned slices of level-L words
-// go to the shard above (its child halo).  Power-of-two tables send only the
-// non-hole words (k_halo_move): about a fifth of the two slices, averaged
-// over the levels.
+// after resolve(L): words of every block's top two own slices go up.
+// Power-of-two tables send only the non-hole words (about a fifth of the
+// two slices, averaged over the levels).
 static int exchange_words(std::vector<gm_solver*>& ss, u64 L, int mode, hipStream_t cs) {
-  const Desc& d = ss[0]->d;
   bool packed = true;
   for (gm_solver* s : ss) packed = packed && s->hg.on;
-  if (packed && mode == 1) {
-    gm_solver* s = ss[0];
-    const bool up = s->rank + 1 < s->world, down = s->rank > 0;
-    const uint32_t nsend = up ? halo_count(s, L, s->top_b - 2) : 0;
-    const uint32_t nrecv = down ? halo_count(s, L, s->top_a - 2) : 0;
-    if (nsend) halo_move(s, L, s->top_b - 2, s->halo_send, 1, cs);
-    ncclGroupStart();
-    if (nsend) ncclSend(s->halo_send, (size_t)nsend * 4, ncclUint8, s->rank + 1, s->comm, cs);
-    if (nrecv) ncclRecv(s->halo_recv, (size_t)nrecv * 4, ncclUint8, s->rank - 1, s->comm, cs);
-    ncclResult_t r = ncclGroupEnd();
-    if (r != ncclSuccess) return fail(GM_EHIP, "RCCL words halo: %s", ncclGetErrorString(r));
-    if (nrecv) halo_move(s, L, s->top_a - 2, s->halo_recv, 0, cs);
-    HIPCHK(hipGetLastError());
-    return 0;
-  }
-  if (packed) {
-    for (size_t g = 0; g + 1 < ss.size(); g++) {
-      const u64 t0 = ss[g]->top_b - 2;
-      const uint32_t n = halo_count(ss[g], L, t0);
-      if (!n) continue;
-      halo_move(ss[g], L, t0, ss[g]->halo_send, 1, cs);
-      HIPCHK(hipMemcpyAsync(ss[g + 1]->halo_recv, ss[g]->halo_send, (size_t)n * 4, hipMemcpyDeviceToDevice, cs));
-      halo_move(ss[g + 1], L, t0, ss[g + 1]->halo_recv, 0, cs);
-    }
-    HIPCHK(hipGetLastError());
-    return 0;
-  }
+  auto words_at = [&](gm_solver* s, u64 j, u64 o, u64 off) {
+    return s->words + L * s->view.Wl + blk_slice(s, j, o) * s->view.Z + off;
+  };
   if (mode == 1) {
     gm_solver* s = ss[0];
-    u64 lo, hi;
+    const int down = (s->rank + s->world - 1) % s->world, up = (s->rank + 1) % s->world;
+    const u64 nb = blk_count(s), B = s->view.B;
+    if (packed) {
+      u64 nsend = 0, nrecv = 0;
+      for (u64 j = 0; j < nb; j++) {
+        if (blk_global(s, j) + 1 < s->nblocks) {  // to block k+1
+          const int64_t t0 = blk_top(s, j, B);
+          const uint32_t n = halo_count(s, L, t0);
+          if (n) halo_move(s, L, blk_slice(s, j, B), t0, s->halo_send + nsend, 1, cs);
+          nsend += n;
+        }
+        if (blk_global(s, j) >= 1) nrecv += halo_count(s, L, blk_top(s, j, 0));  // from block k-1
+      }
+      ncclGroupStart();
+      if (nsend) ncclSend(s->halo_send, nsend * 4, ncclUint8, up, s->comm, cs);
+      if (nrecv) ncclRecv(s->halo_recv, nrecv * 4, ncclUint8, down, s->comm, cs);
+      ncclResult_t r = ncclGroupEnd();
+      if (r != ncclSuccess) return fail(GM_EHIP, "RCCL words halo: %s", ncclGetErrorString(r));
+      u64 at = 0;
+      for (u64 j = 0; j < nb; j++) {
+        if (blk_global(s, j) < 1) continue;
+        const int64_t t0 = blk_top(s, j, 0);
+        const uint32_t n = halo_count(s, L, t0);
+        if (n) halo_move(s, L, blk_slice(s, j, 0), t0, s->halo_recv + at, 0, cs);
+        at += n;
+      }
+      HIPCHK(hipGetLastError());
+      return 0;
+    }
     ncclGroupStart();
-    if (s->rank + 1 < s->world && band_slice(s, dense_band(d, DenseView{0, ~0ull, 0, 0, 0}, L), s->top_b - 2, &lo, &hi))
-      ncclSend(s->words + L * s->view.Wl + (lo - s->view.base_off), (hi - lo) * 4, ncclUint8, s->rank + 1, s->comm,
-               cs);
-    if (s->rank > 0 && band_slice(s, dense_band(d, DenseView{0, ~0ull, 0, 0, 0}, L), s->top_a - 2, &lo, &hi))
-      ncclRecv(s->words + L * s->view.Wl + (lo - s->view.base_off), (hi - lo) * 4, ncclUint8, s->rank - 1, s->comm,
-               cs);
+    for (u64 j = 0; j < nb; j++) {
+      u64 lo, hi;
+      if (blk_global(s, j) + 1 < s->nblocks && band_pair(s, L, blk_top(s, j, B), &lo, &hi))
+        ncclSend(words_at(s, j, B, lo), (hi - lo) * 4, ncclUint8, up, s->comm, cs);
+    }
+    for (u64 j = 0; j < nb; j++) {
+      u64 lo, hi;
+      if (blk_global(s, j) >= 1 && band_pair(s, L, blk_top(s, j, 0), &lo, &hi))
+        ncclRecv(words_at(s, j, 0, lo), (hi - lo) * 4, ncclUint8, down, s->comm, cs);
+    }
     ncclResult_t r = ncclGroupEnd();
     if (r != ncclSuccess) return fail(GM_EHIP, "RCCL words halo: %s", ncclGetErrorString(r));
     return 0;
   }
-  for (size_t g = 0; g + 1 < ss.size(); g++) {
-    u64 lo, hi;
-    if (!band_slice(ss[g], dense_band(d, DenseView{0, ~0ull, 0, 0, 0}, L), ss[g]->top_b - 2, &lo, &hi)) continue;
-    HIPCHK(hipMemcpyAsync(ss[g + 1]->words + L * ss[g + 1]->view.Wl + (lo - ss[g + 1]->view.base_off),
-                          ss[g]->words + L * ss[g]->view.Wl + (lo - ss[g]->view.base_off), (hi - lo) * 4,
-                          hipMemcpyDeviceToDevice, cs));
+  const int W = (int)ss.size();
+  for (gm_solver* s : ss) {
+    const u64 nb = blk_count(s), B = s->view.B;
+    for (u64 j = 0; j < nb; j++) {
+      const u64 k = blk_global(s, j);
+      if (k + 1 >= s->nblocks) continue;
+      gm_solver* dst = ss[(k + 1) % W];
+      const u64 jd = (k + 1) / W;
+      const int64_t t0 = blk_top(s, j, B);
+      if (packed) {
+        const uint32_t n = halo_count(s, L, t0);
+        if (!n) continue;
+        halo_move(s, L, blk_slice(s, j, B), t0, s->halo_send, 1, cs);
+        HIPCHK(hipMemcpyAsync(dst->halo_recv, s->halo_send, (size_t)n * 4, hipMemcpyDeviceToDevice, cs));
+        halo_move(dst, L, blk_slice(dst, jd, 0), t0, dst->halo_recv, 0, cs);
+      } else {
+        u64 lo, hi;
+        if (!band_pair(s, L, t0, &lo, &hi)) continue;
+        HIPCHK(hipMemcpyAsync(words_at(dst, jd, 0, lo), words_at(s, j, B, lo), (hi - lo) * 4,
+                              hipMemcpyDeviceToDevice, cs));
+      }
+    }
   }
+  HIPCHK(hipGetLastError());
   return 0;
 }
 
@@ -1519,7 +1599,7 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
   // block narrower than 4 top values has no such split: exchange in order.
   bool pipe = mode != 0;
   for (gm_solver* s : ss)
-    if (s->top_b - s->top_a < 4) pipe = false;
+    if (s->view.B < 4) pipe = false;
   hipStream_t cs = st;
   hipEvent_t* E = nullptr;  // [0, T): own part done, [T, 2T): exchange done (forward); reused backward
   if (pipe) {
@@ -1532,11 +1612,14 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
     cs = s0->cstream;
     E = s0->pev.data();
   }
-  auto clip = [](const DenseView& v, u64 lo, u64 hi) {
-    DenseView c = v;
-    c.p_lo = std::max<uint64_t>(v.p_lo, lo);
-    c.p_hi = std::min<uint64_t>(v.p_hi, hi);
-    if (c.p_hi < c.p_lo) c.p_hi = c.p_lo;
+  // the launch view of level L: world 1 sweeps the level's band; a shard
+  // sweeps its whole local range, processing the own slices o in [olo, ohi)
+  // of every block
+  auto level_view = [&](gm_solver* s, int L, uint32_t olo, uint32_t ohi) {
+    if (!s->view.blk) return dense_band(d, s->view, (u64)L);
+    DenseView c = s->view;
+    c.olo = olo;
+    c.ohi = ohi;
     return c;
   };
   // forward (pull): level 0 .. T-1, each level's bitmap written exactly once.
@@ -1546,8 +1629,8 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
   for (int L = 0; L < T; L++) {
     if (timing) HIPCHK(hipEventRecord(kx[2 * L], st));
     for (gm_solver* s : ss) {
-      const DenseView b = dense_band(d, s->view, (u64)L);
-      const DenseView own = pipe ? clip(b, 0, (s->top_b - 2) * s->Z) : b;
+      const uint32_t B = s->view.B;  // pull: the top two own slices read the upper halo
+      const DenseView own = level_view(s, L, 2, pipe ? B : B + 2);
       if (own.p_hi > own.p_lo) dense_launch_pull(s, own, grid_of(s, own), (u64)L, root_p);
     }
     if (mode) {
@@ -1561,8 +1644,7 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
         HIPCHK(hipEventRecord(E[T + L], cs));
         if (L >= 1) HIPCHK(hipStreamWaitEvent(st, E[T + L - 1], 0));  // halos of L-1 (L-2 waited before)
         for (gm_solver* s : ss) {
-          const DenseView b = dense_band(d, s->view, (u64)L);
-          const DenseView bd = clip(b, (s->top_b - 2) * s->Z, ~0ull);
+          const DenseView bd = level_view(s, L, s->view.B, s->view.B + 2);
           if (bd.p_hi > bd.p_lo) dense_launch_pull(s, bd, grid_of(s, bd), (u64)L, root_p);
         }
       }
@@ -1581,8 +1663,8 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
   for (int L = T - 1; L >= 0; L--) {
     if (timing) HIPCHK(hipEventRecord(kr[2 * L], st));
     for (gm_solver* s : ss) {
-      const DenseView b = dense_band(d, s->view, (u64)L);
-      const DenseView own = pipe ? clip(b, (s->top_a + 2) * s->Z, ~0ull) : b;
+      const uint32_t B = s->view.B;  // resolve: the bottom two own slices read the lower halo
+      const DenseView own = level_view(s, L, pipe ? 4 : 2, B + 2);
       if (own.p_hi > own.p_lo) dense_launch_resolve(s, own, grid_of(s, own), (u64)L);
     }
     if (mode) {
@@ -1596,8 +1678,7 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
         HIPCHK(hipEventRecord(E[T + L], cs));
         if (L + 1 < T) HIPCHK(hipStreamWaitEvent(st, E[T + L + 1], 0));  // halos of L+1 (L+2 waited before)
         for (gm_solver* s : ss) {
-          const DenseView b = dense_band(d, s->view, (u64)L);
-          const DenseView bd = clip(b, 0, (s->top_a + 2) * s->Z);
+          const DenseView bd = level_view(s, L, 2, 4);
           if (bd.p_hi > bd.p_lo) dense_launch_resolve(s, bd, grid_of(s, bd), (u64)L);
         }
       }
@@ -1611,7 +1692,9 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
   }
   HIPCHK(hipEventRecord(e2, st));
   for (gm_solver* s : ss) {
-    hipLaunchKernelGGL(k_dense_root, dim3(1), dim3(64), 0, st, s->view, s->words, s->bits, root_p, s->st);
+    uint64_t root_q = ~0ull;
+    if (!dense_local(s->view, root_p, &root_q)) root_q = ~0ull;
+    hipLaunchKernelGGL(k_dense_root, dim3(1), dim3(64), 0, st, s->view, s->words, s->bits, root_q, s->st);
     hipLaunchKernelGGL(k_fill_red, dim3(1), dim3(64), 0, st, s->st);
   }
   if (mode == 1) {

@@ -146,12 +146,15 @@ class GameSpec:
 
     def shard_info(self, rank, world):
         """Geometry of dense shard `rank` of `world` (DESIGN.md
-        §Multi-GPU): dict a, b, lo, hi, Z, E, p_lo, p_hi."""
+        §Multi-GPU): dict B (block width in top-heap values), nblocks (over
+        all ranks), nb (blocks of this rank: k = rank, rank + world, ...),
+        rank, Z (prefixes per top value), E (top values), Wl (local
+        prefixes per level), world."""
         out = (_lib.ctypes.c_uint64 * 8)()
         _lib.check(_lib.load().gm_shard_info(self.id, int(rank), int(world),
                                              out))
-        return dict(zip(("a", "b", "lo", "hi", "Z", "E", "p_lo", "p_hi"),
-                        list(out)))
+        return dict(zip(("B", "nblocks", "nb", "rank", "Z", "E", "Wl",
+                         "world"), list(out)))
 
     # -- the drop-in guard -------------------------------------------------
     def verify(self, module, samples=200, seed=0):

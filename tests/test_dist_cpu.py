@@ -52,10 +52,11 @@ def _run(world, params):
 
 
 @pytest.mark.parametrize("world,params", [
-    (2, "heaps=31:31:31:31:31:3:15"),  # bench N=2 workload
-    (4, "heaps=31:31:31:31:31:3:31"),  # bench N=4 workload
-    (8, "heaps=31:31:31:31:31:3:63"),  # bench N=8 workload
+    (2, "heaps=31:31:31:31:31:63"),   # bench N=2 workload
+    (4, "heaps=31:31:31:31:31:127"),  # bench N=4 workload
+    (8, "heaps=31:31:31:31:31:255"),  # bench N=8 workload
     (2, "heaps=7:7:7:15"),
+    (3, "heaps=7:7:7:15"),
 ])
 def test_gloo_bootstrap_and_geometry(world, params):
     out = _run(world, params)
@@ -63,20 +64,16 @@ def test_gloo_bootstrap_and_geometry(world, params):
         assert uid == bytes(range(128))
         assert infos == out[0][2]  # every rank sees the same geometry
     infos = out[0][2]
-    E, Z = infos[0]["E"], infos[0]["Z"]
-    assert Z % 64 == 0
-    assert infos[0]["a"] == 0 and infos[-1]["b"] == E
-    for g in range(world):
-        i = infos[g]
-        assert i["b"] - i["a"] >= 2
-        assert i["p_lo"] == i["a"] * Z and i["p_hi"] == i["b"] * Z
-        if g > 0:
-            prev = infos[g - 1]
-            assert prev["b"] == i["a"]                 # blocks tile [0, E)
-            assert i["lo"] == i["a"] - 2               # child halo = prev's top 2
-            assert prev["hi"] == min(E, prev["b"] + 2)  # parent halo = my bottom 2
-    if E == 8 * world and "3:" in params:
-        # bench shape: 8 top values per rank, 32^4 x 4 prefixes per value,
-        # x 32 heap-0 values = 2^30 positions per GPU
-        assert [i["b"] - i["a"] for i in infos] == [8] * world
-        assert Z == 32 ** 4 * 4
+    B, nblocks, Z, E = (infos[0][k] for k in ("B", "nblocks", "Z", "E"))
+    assert Z % 64 == 0 and B >= 2
+    assert nblocks == -(-E // B) and nblocks >= world
+    for r, i in enumerate(infos):
+        assert (i["B"], i["nblocks"], i["Z"], i["E"], i["rank"], i["world"]) == (B, nblocks, Z, E, r, world)
+        # round robin: rank r owns blocks r, r + world, ...
+        assert i["nb"] == len(range(r, nblocks, world))
+        assert i["Wl"] == i["nb"] * (B + 4) * Z  # two halo slices each side
+    assert sum(i["nb"] for i in infos) == nblocks
+    if "31:31:31:31:31:" in params:
+        # bench shape: 2^30 positions per GPU, blocks of 8, four per rank
+        assert (B, nblocks, Z) == (8, 4 * world, 32 ** 4)
+        assert all(i["nb"] == 4 for i in infos)

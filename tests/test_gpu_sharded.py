@@ -62,19 +62,37 @@ def test_group_matches_oracle():
 
 
 def test_bench_geometry_two_shards():
-    """The N=2 bench workload's shape (31^k x 3 x 15: 8 top values per rank,
-    packed word halos) at one GPU's scale: 31:31:31:31:3:15 = 2^26
-    positions."""
-    params = "heaps=31:31:31:31:3:15"
+    """The N=2 bench workload's shape (31^k x 63: blocks of 8 top values,
+    four per rank, round robin, packed word halos) at one GPU's scale:
+    31:31:31:31:63 = 2^26 positions."""
+    params = "heaps=31:31:31:31:63"
     r1, s1 = _single(params)
     rg, shards = _group(params, 2)
     assert (rg.positions, rg.edges, rg.root_line) == (r1.positions, r1.edges,
                                                       r1.root_line)
     rng = np.random.default_rng(1)
-    keys = rng.integers(0, 32 ** 4 * 4 * 16, size=1 << 16, dtype=np.uint64)
+    keys = rng.integers(0, 32 ** 4 * 64, size=1 << 16, dtype=np.uint64)
     w, hits = _words_by_owner(shards, keys)
     assert (hits == 1).all()
     np.testing.assert_array_equal(w, s1.query(keys))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_non_pow2_round_robin_blocks(world):
+    """A top heap of 48 values (not a power of two: per-lane kernels,
+    division-based block mapping, unpacked band-clipped word halos), blocks
+    of 8 dealt round robin; every position's word equal to the unsharded
+    solve's."""
+    params = "heaps=3:7:15:47"
+    r1, s1 = _single(params)
+    rg, shards = _group(params, world)
+    assert (rg.positions, rg.edges, rg.primitives, rg.root_line) == (
+        r1.positions, r1.edges, r1.primitives, r1.root_line)
+    keys, val, rem = s1.dump()
+    w, hits = _words_by_owner(shards, keys)
+    assert (hits == 1).all()
+    np.testing.assert_array_equal(w & 3, val)
+    np.testing.assert_array_equal(w >> 2, rem)
 
 
 def test_bad_geometry_is_refused():
@@ -84,10 +102,10 @@ def test_bad_geometry_is_refused():
 
 
 @pytest.mark.parametrize("world,params,npos", [
-    (3, "heaps=31:31:31:31:127", 32 ** 4 * 128),
-    (4, "heaps=31:31:31:31:127", 32 ** 4 * 128),
-    (4, "heaps=31:31:31:3:31", 32 ** 3 * 4 * 32),   # the N=4 bench shape, smaller
-    (8, "heaps=31:31:31:3:63", 32 ** 3 * 4 * 64),   # the N=8 bench shape, smaller
+    (3, "heaps=31:31:31:31:127", 32 ** 4 * 128),   # 16 blocks: 6 / 5 / 5 per rank
+    (4, "heaps=31:31:31:31:127", 32 ** 4 * 128),   # the N=4 bench shape, smaller
+    (8, "heaps=31:31:31:255", 32 ** 3 * 256),      # the N=8 bench shape, smaller
+    (2, "heaps=31:31:31:3:15", 32 ** 3 * 4 * 16),  # one block per rank
 ])
 def test_pipelined_halo_exchange_wide_blocks(world, params, npos):
     """Blocks of >= 4 top values take the overlapped schedule (own part,
