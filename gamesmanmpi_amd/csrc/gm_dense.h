@@ -138,18 +138,19 @@ __global__ __launch_bounds__(256) void k_dense_pull(Desc d, DenseView v, u64* bi
   WaveDigits<MAXH, POW2> wd;
   wd.init(d);
   for (u64 i0 = (u64)blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += stride) {
-    const u64 q = v.p_lo + i0;  // local prefix
-    const u64 qw = q & ~63ull;
+    const u64 qi = v.p_lo + i0;  // sweep index
+    const u64 qiw = __builtin_amdgcn_readfirstlane((uint32_t)(qi & ~63ull)) |
+                    ((u64)__builtin_amdgcn_readfirstlane((uint32_t)(qi >> 32)) << 32);
+    uint64_t qw;  // local prefix of the wave's lane 0
     bool run;
-    const u64 pw = dense_global(v, __builtin_amdgcn_readfirstlane((uint32_t)qw) |
-                                       ((u64)__builtin_amdgcn_readfirstlane((uint32_t)(qw >> 32)) << 32),
-                                &run);
+    const u64 pw = dense_sweep(v, qiw, &qw, &run);
+    const u64 q = qw + (qi - qiw);
     if (!run) continue;  // wave-uniform: another launch's slice, or a halo
     const u64 p = pw + (q - qw);  // global prefix
     bool reached = false;
     uint32_t h[MAXH];
     const uint32_t s = wd.digits(d, pw, p, h);
-    if (q < v.p_hi && s <= S && S - s <= d.heap[0]) {  // not a hole
+    if (qi < v.p_hi && s <= S && S - s <= d.heap[0]) {  // not a hole
       if (L == 0) {
         reached = p == root_p;  // level 0 holds only the root
       } else {
@@ -207,9 +208,10 @@ __global__ __launch_bounds__(256) void k_dense_pull_words(Desc d, DenseView v, u
   const u64 ngroups = (v.p_hi - v.p_lo + 63) >> 6;
   const u64 stride = (u64)gridDim.x * blockDim.x;
   for (u64 gi = (u64)blockIdx.x * blockDim.x + threadIdx.x; gi < ngroups; gi += stride) {
-    const u64 q = v.p_lo + (gi << 6);  // local prefix of lane-bit 0 (multiple of 64)
+    const u64 qi = v.p_lo + (gi << 6);  // sweep index of lane-bit 0
+    uint64_t q;  // local prefix of lane-bit 0 (multiple of 64)
     bool run;
-    const u64 pg = dense_global(v, q, &run);  // global prefix of lane-bit 0
+    const u64 pg = dense_sweep(v, qi, &q, &run);  // global prefix of lane-bit 0
     if (!run) continue;  // another launch's slice, or a halo
     int dg[MAXH];
     int sg = 0;
@@ -222,7 +224,7 @@ __global__ __launch_bounds__(256) void k_dense_pull_words(Desc d, DenseView v, u
     // valid: S - H0 <= sg + sj <= S
     const int lo_s = S - H0 - sg, hi_s = S - sg;
     u64 V = mask_le(TS, hi_s) & ~mask_le(TS, lo_s - 1);
-    if (q + 64 > v.p_hi) V &= (1ull << (v.p_hi - q)) - 1;
+    if (qi + 64 > v.p_hi) V &= (1ull << (v.p_hi - qi)) - 1;
     u64 reached = 0;
     if (L == 0) {
       if (root_p >= pg && root_p < pg + 64) reached = 1ull << (root_p - pg);
@@ -252,32 +254,48 @@ __global__ __launch_bounds__(256) void k_dense_pull_words(Desc d, DenseView v, u
 #undef TD
 
 // Packed word halo (sharded power-of-two tables, gm_solver.hip
-// exchange_words): the non-hole words of two consecutive top-value slices
-// of one level move between a slice pair and a dense buffer.  One wave per
-// 64-slot group; the group's non-hole mask is the pull's TS-window mask for
-// x = S - t, its packed offset comes from the host-built table off[x][g]
-// (both ends of a halo use the same order).  pack = 1: slices -> buf.
-__global__ __launch_bounds__(256) void k_halo_move(Desc d, const u64* __restrict__ masks,
-                                                   const uint32_t* __restrict__ off, u64 G, int XN,
-                                                   uint32_t* slices, u64 Z, int64_t x0, uint32_t tot0,
+// exchange_words): the non-hole words of slice pairs of one level move
+// between the table and a dense buffer, one job per pair (a rank's blocks
+// in one launch).  One wave per 64-slot group; the group's non-hole mask
+// vmask[x][g] and packed offset off[x][g] (x = S - t) come from host-built
+// tables, so both ends of a halo use the same order.  pack = 1: table -> buf.
+constexpr int kMaxHaloJobs = 32;
+struct HaloJobs {
+  uint32_t n;
+  uint32_t u0[kMaxHaloJobs];    // local slice of the pair's first slice
+  int32_t x0[kMaxHaloJobs];     // S - t of the first slice
+  uint32_t base[kMaxHaloJobs];  // buffer offset of the pair's first word
+  uint32_t tot0[kMaxHaloJobs];  // non-hole words of the first slice
+};
+__global__ __launch_bounds__(256) void k_halo_move(const u64* __restrict__ vmask, const uint32_t* __restrict__ off,
+                                                   u64 G, int XN, uint32_t* level_words, u64 Z, HaloJobs jobs,
                                                    uint32_t* buf, int pack) {
   const uint32_t lane = __lane_id();
-  const int H0 = (int)d.heap[0];
   const u64 nwaves = (u64)gridDim.x * (blockDim.x >> 6);
-  const u64 w0 = (u64)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  for (u64 w = w0; w < 2 * G; w += nwaves) {
-    const u64 slice = w / G, g = w - slice * G;
-    const int64_t x = x0 - (int64_t)slice;
-    if (x < 0 || x >= XN) continue;
-    const u64 r0 = g * 64;
-    int sg = 0;
-    for (int i = 1; i < d.nheaps; i++) sg += (int)((r0 >> d.pshift[i]) & (d.base[i] - 1));
-    const u64 V = mask_le(masks, (int)x - sg) & ~mask_le(masks, (int)x - H0 - 1 - sg);
-    if (!((V >> lane) & 1ull)) continue;
-    const u64 idx = (slice ? tot0 : 0) + off[(u64)x * G + g] + (u64)__popcll(V & ((1ull << lane) - 1ull));
-    uint32_t* slot = slices + slice * Z + r0 + lane;
-    if (pack) buf[idx] = *slot;
-    else *slot = buf[idx];
+  const u64 w0 = __builtin_amdgcn_readfirstlane((uint32_t)((u64)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
+  // four groups per round: their mask/offset loads and word moves overlap
+  for (u64 wb = w0 * 4; wb < (u64)jobs.n * 2 * G; wb += nwaves * 4) {
+    u64 V[4], idx[4], slot[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      V[k] = 0;
+      const u64 w = wb + k;
+      if (w >= (u64)jobs.n * 2 * G) continue;
+      const u64 job = w / (2 * G), rem = w - job * 2 * G;
+      const u64 slice = rem / G, g = rem - slice * G;
+      const int64_t x = (int64_t)jobs.x0[job] - (int64_t)slice;
+      if (x < 0 || x >= XN) continue;
+      V[k] = vmask[(u64)x * G + g];
+      idx[k] = jobs.base[job] + (slice ? jobs.tot0[job] : 0) + off[(u64)x * G + g];
+      slot[k] = ((u64)jobs.u0[job] + slice) * Z + g * 64 + lane;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (!((V[k] >> lane) & 1ull)) continue;
+      const u64 i = idx[k] + (u64)__popcll(V[k] & ((1ull << lane) - 1ull));
+      if (pack) buf[i] = level_words[slot[k]];
+      else level_words[slot[k]] = buf[i];
+    }
   }
 }
 
@@ -368,15 +386,19 @@ __global__ __launch_bounds__(256) void k_dense_resolve(Desc d, DenseView v, uint
       rw[u] = 0;
       nch[u] = 0;
       const u64 iu = i0 + (u64)u * r.stride;
-      const u64 q = v.p_lo + iu;  // local prefix
-      const u64 qw = q & ~63ull;
-      qs[u] = q;
+      u64 q = v.p_lo + iu;  // local prefix (world 1) / sweep index (shards)
+      u64 qw = q & ~63ull;
       bool run = true;
       u64 pw = qw;  // world 1: local = global
-      if (BLK)
-        pw = dense_global(v, __builtin_amdgcn_readfirstlane((uint32_t)qw) |
-                                 ((u64)__builtin_amdgcn_readfirstlane((uint32_t)(qw >> 32)) << 32),
-                          &run);
+      if (BLK) {
+        const u64 qiw = __builtin_amdgcn_readfirstlane((uint32_t)qw) |
+                        ((u64)__builtin_amdgcn_readfirstlane((uint32_t)(qw >> 32)) << 32);
+        uint64_t lq;
+        pw = dense_sweep(v, qiw, &lq, &run);
+        q = lq + (q - qw);
+        qw = lq;
+      }
+      qs[u] = q;
       const u64 p = pw + (q - qw);  // global prefix
       uint32_t h[MAXH];
       const uint32_t s = wd.digits(d, pw, p, h);

@@ -90,6 +90,7 @@ struct Desc {
 // p_lo/p_hi bound the local prefixes a launch sweeps; a launch processes
 // only slices with olo <= o < ohi (own slices: [2, B + 2)).  Wl = local
 // words per level, Wbl = local reach bits per level (Wl rounded up to 64).
+constexpr int kMaxSweepSlices = 192;
 struct DenseView {
   uint64_t p_lo, p_hi;
   uint64_t base_off;  // always 0 (local addressing starts at 0)
@@ -98,7 +99,40 @@ struct DenseView {
   uint64_t Z, E;
   int32_t zshift;     // log2(Z) when Z is a power of two, else -1
   uint32_t olo, ohi;
+  // compact sweep (blk, nsl > 0): a launch sweeps only the nsl local slices
+  // listed in sl[] -- sweep index i is slice sl[i / Z], prefix i % Z
+  uint32_t nsl;
+  uint16_t sl[kMaxSweepSlices];  // local slice
+  uint16_t st[kMaxSweepSlices];  // its global top value
 };
+
+// local prefix of sweep index i (identity unless the view lists slices)
+GM_HD uint64_t dense_sweep_q(const DenseView& v, uint64_t i) {
+  if (!v.nsl) return i;
+  const uint64_t si = v.zshift >= 0 ? (i >> v.zshift) : i / v.Z;
+  return (uint64_t)v.sl[si] * v.Z + (i - si * v.Z);
+}
+
+// sweep index qi -> local prefix *q and global prefix (returned); *run =
+// this launch processes the slice.  Listed slices carry their global top
+// value, so the common case is two table reads and shifts.
+GM_HD uint64_t dense_global(const DenseView& v, uint64_t q, bool* run);
+GM_HD uint64_t dense_sweep(const DenseView& v, uint64_t qi, uint64_t* q, bool* run) {
+  if (v.nsl) {
+    const uint64_t si = v.zshift >= 0 ? (qi >> v.zshift) : qi / v.Z;
+    const uint64_t base = v.zshift >= 0 ? (si << v.zshift) : si * v.Z;
+    const uint64_t r = qi - base;
+    *run = true;
+    if (v.zshift >= 0) {
+      *q = ((uint64_t)v.sl[si] << v.zshift) + r;
+      return ((uint64_t)v.st[si] << v.zshift) + r;
+    }
+    *q = (uint64_t)v.sl[si] * v.Z + r;
+    return (uint64_t)v.st[si] * v.Z + r;
+  }
+  *q = qi;
+  return dense_global(v, qi, run);
+}
 
 // global prefix of local prefix q; *run = this launch processes its slice
 // (q's slice must be the same for every lane of a wave: Z % 64 == 0)

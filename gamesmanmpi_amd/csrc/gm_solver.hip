@@ -339,10 +339,14 @@ static HaloGeom halo_geom(const Desc* d, int world, u64 nb) {
   h.on = true;
   return h;
 }
-// offset table + send and receive buffers of 2 slices per local block
+// mask table (u64) + offset table (u32) + send and receive buffers of 2
+// slices per local block
+static size_t halo_tab_bytes(const HaloGeom& h) {
+  return ((size_t)h.XN * h.G * 8 + 255) / 256 * 256 + ((size_t)h.XN * h.G * 4 + 255) / 256 * 256;
+}
 static size_t halo_bytes(const HaloGeom& h) {
   if (!h.on) return 0;
-  return ((size_t)h.XN * h.G * 4 + 255) / 256 * 256 + 2 * (h.nb * 2 * h.Z * 4);
+  return halo_tab_bytes(h) + 2 * (h.nb * 2 * h.Z * 4);
 }
 
 __device__ __forceinline__ u64 mix64(u64 x) {  // splitmix64 finaliser
@@ -651,6 +655,7 @@ struct gm_solver {
   std::vector<hipEvent_t> pev;
   // packed word halos (HaloGeom): device offset table, buffers, host totals
   HaloGeom hg;
+  const u64* halo_vmask = nullptr;
   const uint32_t* halo_off = nullptr;
   uint32_t* halo_send = nullptr;
   uint32_t* halo_recv = nullptr;
@@ -1080,8 +1085,9 @@ static void build_mask_tables(const Desc& d, u64* M) {
 // the same order, so packed slots need no index.
 static u64 host_mask_le(const u64* T, int t) { return t < 0 ? 0ull : (t >= 63 ? ~0ull : T[t]); }
 static void build_halo_offsets(const Desc& d, const u64* M, const HaloGeom& h, std::vector<uint32_t>& off,
-                               std::vector<uint32_t>& tot) {
+                               std::vector<u64>& vm, std::vector<uint32_t>& tot) {
   off.assign((size_t)h.XN * h.G, 0);
+  vm.assign((size_t)h.XN * h.G, 0);
   tot.assign((size_t)h.XN, 0);
   std::vector<int> sg(h.G);
   for (u64 g = 0; g < h.G; g++) {
@@ -1095,6 +1101,7 @@ static void build_halo_offsets(const Desc& d, const u64* M, const HaloGeom& h, s
     for (u64 g = 0; g < h.G; g++) {
       off[(size_t)x * h.G + g] = run;
       const u64 V = host_mask_le(M, x - sg[g]) & ~host_mask_le(M, x - H0 - 1 - sg[g]);
+      vm[(size_t)x * h.G + g] = V;
       run += (uint32_t)__builtin_popcountll(V);
     }
     tot[x] = run;
@@ -1164,13 +1171,17 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
     s->hg = halo_geom(d, world, (u64)(s->view.blk ? s->view.Wl / ((s->view.B + 4) * s->view.Z) : 1));
     if (s->hg.on && buf->scratch_bytes >= scratch_bytes_for(d->max_levels) + halo_bytes(s->hg)) {
       char* base = (char*)buf->scratch + scratch_bytes_for(d->max_levels);
-      const size_t tab = ((size_t)s->hg.XN * s->hg.G * 4 + 255) / 256 * 256;
-      s->halo_off = (const uint32_t*)base;
-      s->halo_send = (uint32_t*)(base + tab);
+      const size_t vbytes = ((size_t)s->hg.XN * s->hg.G * 8 + 255) / 256 * 256;
+      s->halo_vmask = (const u64*)base;
+      s->halo_off = (const uint32_t*)(base + vbytes);
+      s->halo_send = (uint32_t*)(base + halo_tab_bytes(s->hg));
       s->halo_recv = s->halo_send + s->hg.nb * 2 * s->hg.Z;
       std::vector<uint32_t> off;
-      build_halo_offsets(*d, m.data(), s->hg, off, s->halo_tot);
-      e = hipMemcpy((void*)s->halo_off, off.data(), off.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+      std::vector<u64> vm;
+      build_halo_offsets(*d, m.data(), s->hg, off, vm, s->halo_tot);
+      e = hipMemcpy((void*)s->halo_vmask, vm.data(), vm.size() * sizeof(u64), hipMemcpyHostToDevice);
+      if (e == hipSuccess)
+        e = hipMemcpy((void*)s->halo_off, off.data(), off.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
       if (e != hipSuccess) {
         gm_solver_destroy(s);
         return fail(GM_EHIP, "halo offsets: %s", hipGetErrorString(e));
@@ -1449,7 +1460,7 @@ static int exchange_bits(std::vector<gm_solver*>& ss, u64 L, int mode, hipStream
 }
 
 // packed halo helpers: non-hole words of the slice pair whose first slice
-// has top value t0 at level L (local slice u0)
+// has top value t0 at level L
 static uint32_t halo_total(const gm_solver* s, int64_t x) {
   return (x < 0 || x >= s->hg.XN) ? 0u : s->halo_tot[(size_t)x];
 }
@@ -1457,12 +1468,47 @@ static uint32_t halo_count(const gm_solver* s, u64 L, int64_t t0) {
   const int64_t x0 = (int64_t)s->d.root_sum - (int64_t)L - t0;
   return halo_total(s, x0) + halo_total(s, x0 - 1);
 }
-static void halo_move(gm_solver* s, u64 L, u64 u0, int64_t t0, uint32_t* buf, int pack, hipStream_t cs) {
-  const int64_t x0 = (int64_t)s->d.root_sum - (int64_t)L - t0;
-  const u64 waves = 2 * s->hg.G;
-  const int grid = (int)std::max<u64>(1, std::min<u64>((waves + 3) / 4, (u64)s->grid));
-  hipLaunchKernelGGL(k_halo_move, dim3(grid), dim3(kBlock), 0, cs, s->d, s->masks, s->halo_off, s->hg.G, s->hg.XN,
-                     s->words + L * s->view.Wl + u0 * s->view.Z, s->view.Z, x0, halo_total(s, x0), buf, pack);
+// Pack (send side: every block's top pair, o = B) or unpack (receive side:
+// every block's lower halo, o = 0) all of a rank's halo pairs of level L
+// between the table and buf; returns the words moved.  Blocks without a
+// neighbour on that side are skipped, in the same order on both ends.
+static u64 halo_move_all(gm_solver* s, u64 L, int pack, uint32_t* buf, hipStream_t cs) {
+  const u64 nb = blk_count(s), B = s->view.B;
+  const int64_t S = (int64_t)s->d.root_sum - (int64_t)L;
+  HaloJobs jobs;
+  memset(&jobs, 0, sizeof jobs);
+  u64 at = 0;
+  auto flush = [&]() {
+    if (!jobs.n) return;
+    const u64 waves = ((u64)jobs.n * 2 * s->hg.G + 3) / 4;  // four groups per wave round
+    const int grid = (int)std::max<u64>(1, std::min<u64>((waves + 3) / 4, (u64)s->grid));
+    hipLaunchKernelGGL(k_halo_move, dim3(grid), dim3(kBlock), 0, cs, s->halo_vmask, s->halo_off, s->hg.G,
+                       s->hg.XN, s->words + L * s->view.Wl, s->view.Z, jobs, buf, pack);
+    jobs.n = 0;
+  };
+  for (u64 j = 0; j < nb; j++) {
+    const u64 k = blk_global(s, j);
+    if (pack ? k + 1 >= s->nblocks : k < 1) continue;
+    const u64 o = pack ? B : 0;
+    const int64_t t0 = blk_top(s, j, o), x0 = S - t0;
+    const uint32_t n = halo_count(s, L, t0);
+    if (!n) continue;
+    jobs.u0[jobs.n] = (uint32_t)blk_slice(s, j, o);
+    jobs.x0[jobs.n] = (int32_t)x0;
+    jobs.base[jobs.n] = (uint32_t)at;
+    jobs.tot0[jobs.n] = halo_total(s, x0);
+    jobs.n++;
+    at += n;
+    if (jobs.n == kMaxHaloJobs) flush();
+  }
+  flush();
+  return at;
+}
+static u64 halo_recv_count(const gm_solver* s, u64 L) {
+  u64 n = 0;
+  for (u64 j = 0; j < blk_count(s); j++)
+    if (blk_global(s, j) >= 1) n += halo_count(s, L, blk_top(s, j, 0));
+  return n;
 }
 
 // after resolve(L): words of every block's top two own slices go up.
@@ -1479,29 +1525,14 @@ static int exchange_words(std::vector<gm_solver*>& ss, u64 L, int mode, hipStrea
     const int down = (s->rank + s->world - 1) % s->world, up = (s->rank + 1) % s->world;
     const u64 nb = blk_count(s), B = s->view.B;
     if (packed) {
-      u64 nsend = 0, nrecv = 0;
-      for (u64 j = 0; j < nb; j++) {
-        if (blk_global(s, j) + 1 < s->nblocks) {  // to block k+1
-          const int64_t t0 = blk_top(s, j, B);
-          const uint32_t n = halo_count(s, L, t0);
-          if (n) halo_move(s, L, blk_slice(s, j, B), t0, s->halo_send + nsend, 1, cs);
-          nsend += n;
-        }
-        if (blk_global(s, j) >= 1) nrecv += halo_count(s, L, blk_top(s, j, 0));  // from block k-1
-      }
+      const u64 nsend = halo_move_all(s, L, 1, s->halo_send, cs);
+      const u64 nrecv = halo_recv_count(s, L);
       ncclGroupStart();
       if (nsend) ncclSend(s->halo_send, nsend * 4, ncclUint8, up, s->comm, cs);
       if (nrecv) ncclRecv(s->halo_recv, nrecv * 4, ncclUint8, down, s->comm, cs);
       ncclResult_t r = ncclGroupEnd();
       if (r != ncclSuccess) return fail(GM_EHIP, "RCCL words halo: %s", ncclGetErrorString(r));
-      u64 at = 0;
-      for (u64 j = 0; j < nb; j++) {
-        if (blk_global(s, j) < 1) continue;
-        const int64_t t0 = blk_top(s, j, 0);
-        const uint32_t n = halo_count(s, L, t0);
-        if (n) halo_move(s, L, blk_slice(s, j, 0), t0, s->halo_recv + at, 0, cs);
-        at += n;
-      }
+      if (nrecv) halo_move_all(s, L, 0, s->halo_recv, cs);
       HIPCHK(hipGetLastError());
       return 0;
     }
@@ -1521,6 +1552,18 @@ static int exchange_words(std::vector<gm_solver*>& ss, u64 L, int mode, hipStrea
     return 0;
   }
   const int W = (int)ss.size();
+  if (packed) {
+    // every block of shard g sends to shard g + 1 (mod W): pack straight
+    // into the receiver's buffer, then unpack there -- the RCCL path's
+    // kernels and order, with the transfer left out
+    for (int g = 0; g < W; g++) {
+      gm_solver* dst = ss[(g + 1) % W];
+      const u64 n = halo_move_all(ss[g], L, 1, dst->halo_recv, cs);
+      if (n) halo_move_all(dst, L, 0, dst->halo_recv, cs);
+    }
+    HIPCHK(hipGetLastError());
+    return 0;
+  }
   for (gm_solver* s : ss) {
     const u64 nb = blk_count(s), B = s->view.B;
     for (u64 j = 0; j < nb; j++) {
@@ -1529,18 +1572,10 @@ static int exchange_words(std::vector<gm_solver*>& ss, u64 L, int mode, hipStrea
       gm_solver* dst = ss[(k + 1) % W];
       const u64 jd = (k + 1) / W;
       const int64_t t0 = blk_top(s, j, B);
-      if (packed) {
-        const uint32_t n = halo_count(s, L, t0);
-        if (!n) continue;
-        halo_move(s, L, blk_slice(s, j, B), t0, s->halo_send, 1, cs);
-        HIPCHK(hipMemcpyAsync(dst->halo_recv, s->halo_send, (size_t)n * 4, hipMemcpyDeviceToDevice, cs));
-        halo_move(dst, L, blk_slice(dst, jd, 0), t0, dst->halo_recv, 0, cs);
-      } else {
-        u64 lo, hi;
-        if (!band_pair(s, L, t0, &lo, &hi)) continue;
-        HIPCHK(hipMemcpyAsync(words_at(dst, jd, 0, lo), words_at(s, j, B, lo), (hi - lo) * 4,
-                              hipMemcpyDeviceToDevice, cs));
-      }
+      u64 lo, hi;
+      if (!band_pair(s, L, t0, &lo, &hi)) continue;
+      HIPCHK(hipMemcpyAsync(words_at(dst, jd, 0, lo), words_at(s, j, B, lo), (hi - lo) * 4,
+                            hipMemcpyDeviceToDevice, cs));
     }
   }
   HIPCHK(hipGetLastError());
@@ -1600,6 +1635,8 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
   bool pipe = mode != 0;
   for (gm_solver* s : ss)
     if (s->view.B < 4) pipe = false;
+  if (const char* e = getenv("GM_SHARD_NOPIPE"))  // A/B: exchange in order
+    if (atoi(e)) pipe = false;
   hipStream_t cs = st;
   hipEvent_t* E = nullptr;  // [0, T): own part done, [T, 2T): exchange done (forward); reused backward
   if (pipe) {
@@ -1615,11 +1652,37 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
   // the launch view of level L: world 1 sweeps the level's band; a shard
   // sweeps its whole local range, processing the own slices o in [olo, ohi)
   // of every block
+  int slow = 0;  // largest digit sum of the prefix digits below the top
+  for (int i = 1; i + 1 < d.nheaps; i++) slow += (int)d.heap[i];
   auto level_view = [&](gm_solver* s, int L, uint32_t olo, uint32_t ohi) {
     if (!s->view.blk) return dense_band(d, s->view, (u64)L);
+    // a shard sweeps only the listed slices of its blocks that hold a
+    // non-hole at level L: top value t with 0 <= S - t <= slow + heap0
     DenseView c = s->view;
     c.olo = olo;
     c.ohi = ohi;
+    const int64_t S = (int64_t)d.root_sum - L;
+    uint32_t n = 0;
+    bool over = false;
+    for (u64 j = 0; j < blk_count(s); j++)
+      for (uint32_t o = olo; o < ohi; o++) {
+        const int64_t t = blk_top(s, j, o);
+        if (t < 0 || (u64)t >= c.E || S - t < 0 || S - t > slow + (int64_t)d.heap[0]) continue;
+        if (n == (uint32_t)kMaxSweepSlices || t > 0xFFFF || blk_slice(s, j, o) > 0xFFFF) {
+          over = true;
+        } else {
+          c.sl[n] = (uint16_t)blk_slice(s, j, o);
+          c.st[n++] = (uint16_t)t;
+        }
+      }
+    c.p_lo = 0;
+    if (over) {  // too many to list: sweep everything, filter per wave
+      c.nsl = 0;
+      c.p_hi = c.Wl;
+    } else {
+      c.nsl = n;
+      c.p_hi = (u64)n * c.Z;
+    }
     return c;
   };
   // forward (pull): level 0 .. T-1, each level's bitmap written exactly once.
