@@ -89,6 +89,15 @@ def pmc_traffic(kernel, workload):
     return row["bytes_per_launch"], "profiles/pmc_traffic.json (%s)" % row.get("source", "?")
 
 
+def dense_resolve_kernel():
+    """Name of the dense resolve kernel the library launches for the bench
+    shape (power-of-two heaps, base >= 4): the four-prefixes-per-lane form
+    unless GM_DENSE_RESOLVE=scalar selects the one-prefix form (A/B)."""
+    if os.environ.get("GM_DENSE_RESOLVE") == "scalar":
+        return "k_dense_resolve"
+    return "k_dense_resolve4"
+
+
 def model_8d_bytes(positions, edges):
     """SURVEY §8d per-position figure 36 + 20*b (whole solve)."""
     return 36 * positions + 20 * edges
@@ -183,7 +192,7 @@ def main():
         tr_pos, tr_edges = tr.positions, tr.edges
     fwd_b, bwd_b = algorithmic_bytes(tr_pos, tr_edges, layout)
     if tr.ms_resolve_kernels >= tr.ms_expand_kernels:
-        kname, kb, kms, kn = ("k_dense_resolve" if layout == "dense"
+        kname, kb, kms, kn = (dense_resolve_kernel() if layout == "dense"
                               else "k_resolve", bwd_b, tr.ms_resolve_kernels,
                               tr.n_resolve_launches)
     else:

@@ -460,6 +460,177 @@ __global__ __launch_bounds__(256) void k_dense_resolve(Desc d, DenseView v, uint
   block_add(&st->prims, prims);
 }
 
+// ---------------------------------------------------------------------------
+// Four prefixes per lane (power-of-two tables with base[1] >= 4): a lane
+// resolves prefixes q..q+3 (q 4-aligned), which share every digit but the
+// lowest (h1 + e), so every child stream of the lane is ONE 16-B load:
+//   heap 0 -d : row L+d words [q, q+4)                      (A_d)
+//   heap 1 -d : row L+d words [q-d, q-d+4) = tail of the aligned quad
+//               [q-4, q) (P_d) followed by the head of A_d
+//   heap i -d : row L+d words [q - d stride_i, +4)           (i >= 2, aligned)
+// 2K+1 memory instructions per four positions instead of per position, and
+// four times the bytes in flight per instruction: the k_dense_resolve
+// kernel is latency/issue-bound, this one is not.  Per
+// element e the digit sum is s + e, so validity (not a hole) and child
+// existence are per-element compares; quads touching hole slots are loaded
+// whole and the hole words (never written, so garbage) masked to 0 before
+// the reduction.  Stores are one 16-B store when all four are non-holes,
+// else per-element stores (holes stay untouched).
+// ---------------------------------------------------------------------------
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// a level's live-group list split into 8 XCD shares: share x = entries
+// [o[x], o[x + 1]) (blocks b with b % 8 == x sweep it)
+struct XcdShares {
+  uint32_t o[9];
+};
+
+struct WordRow4 {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ __forceinline__ void init(const uint32_t* base, u64 nwords) {
+    r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(uint32_t)(nwords * 4u), 0x00020000);
+  }
+  // words [idx, idx + 4), idx 4-aligned; !ok reads zeros with no memory access
+  __device__ __forceinline__ u32x4 at(u64 idx, bool ok) const {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, ok ? (uint32_t)idx * 4u : 0xFFFFFFF0u, 0, 0);
+  }
+};
+
+template <int MAXH, bool BLK>
+__global__ __launch_bounds__(256) void k_dense_resolve4(Desc d, DenseView v, uint32_t* words, const u64* bits, u64 L,
+                                                        DevState* st, const uint32_t* __restrict__ glist,
+                                                        XcdShares xs) {
+  const uint32_t S = d.root_sum - (uint32_t)L;
+  const uint32_t H0 = d.heap[0];
+  uint32_t* mine = words + L * v.Wl;
+  WordRow4 n1, n2;  // levels L+1, L+2 (empty rows past the last level)
+  n1.init(words + (L + 1) * v.Wl, S >= 1 ? v.Wl : 0);
+  n2.init(words + (L + 2) * v.Wl, S >= 2 ? v.Wl : 0);
+  u64 npos = 0, edges = 0, prims = 0;
+  uint32_t err = 0;
+  // digits of the lane's first prefix offset 4 * lane (pow2 digit split)
+  const uint32_t lane = __lane_id();
+  uint32_t hl[MAXH], sl = 0;
+#pragma unroll
+  for (int i = 1; i < MAXH; i++) {
+    hl[i] = ((MAXH <= 8) || i < d.nheaps) ? (((4u * lane) >> d.pshift[i]) & (d.base[i] - 1)) : 0u;
+    sl += hl[i];
+  }
+  // units of four prefixes over [p_lo rounded down to 256, p_hi), or over
+  // the level's live 256-prefix groups (glist, 64 units each)
+  const u64 lo = v.p_lo & ~255ull;
+  XcdRange r;
+  if (glist) {  // grid is a multiple of 8 blocks (host)
+    const uint32_t x = blockIdx.x % kXcds;
+    r.first = (u64)xs.o[x] * 64 + (u64)(blockIdx.x / kXcds) * blockDim.x + threadIdx.x;
+    r.end = (u64)xs.o[x + 1] * 64;
+    r.stride = (u64)(gridDim.x / kXcds) * blockDim.x;
+  } else {
+    r = xcd_range((v.p_hi - lo + 3) >> 2);
+  }
+  for (u64 iu = r.first; iu < r.end; iu += r.stride) {
+    // sweep index of element 0 (the wave's 64 units are one group)
+    const u64 qi = glist ? ((u64)glist[__builtin_amdgcn_readfirstlane((uint32_t)(iu >> 6))] << 8) + 4 * (iu & 63)
+                         : lo + 4 * iu;
+    const u64 qiw = __builtin_amdgcn_readfirstlane((uint32_t)(qi & ~255ull)) |
+                    ((u64)__builtin_amdgcn_readfirstlane((uint32_t)(qi >> 32)) << 32);
+    u64 qw = qiw, pw = qiw;  // local / global prefix of the wave's element 0
+    bool run = true;
+    if (BLK) {
+      uint64_t lq;
+      pw = dense_sweep(v, qiw, &lq, &run);
+      qw = lq;
+    }
+    if (!run) continue;  // wave-uniform: another launch's slice, or a halo
+    const u64 q = qw + (qi - qiw);
+    uint32_t h[MAXH];
+    uint32_t s = sl;
+#pragma unroll
+    for (int i = 1; i < MAXH; i++) {
+      const uint32_t hb = ((MAXH <= 8) || i < d.nheaps) ? (uint32_t)((pw >> d.pshift[i]) & (d.base[i] - 1)) : 0u;
+      h[i] = hb + hl[i];
+      s += hb;
+    }
+    // element e: digit sum s + e, heap 0 = S - s - e
+    uint32_t valid = 0;
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const uint32_t se = s + e;
+      const bool ok = qi + e >= v.p_lo && qi + e < v.p_hi && se <= S && S - se <= H0;
+      valid |= (uint32_t)ok << e;
+    }
+    if (!__ballot(valid != 0)) continue;  // a wave of holes
+    if (!valid) continue;
+    const u64 bw = (L * v.Wbl + q) >> 6;
+    const uint32_t rbits = (uint32_t)(bits[bw] >> ((L * v.Wbl + q) & 63)) & 15u;
+    u32x4 A1 = n1.at(q, true), A2 = n2.at(q, true);
+    u32x4 P1 = n1.at(q - 4, q >= 4), P2 = n2.at(q - 4, q >= 4);
+    u32x4 C1[MAXH], C2[MAXH];
+#pragma unroll
+    for (int i = 2; i < MAXH; i++) {
+      const bool live = (MAXH <= 8) || i < d.nheaps;
+      C1[i] = n1.at(q - d.pstride[i], live && h[i] >= 1);
+      C2[i] = n2.at(q - 2 * d.pstride[i], live && h[i] >= 2);
+    }
+    uint32_t nch_hi = 0;  // children through heaps >= 2 (same for the four)
+#pragma unroll
+    for (int i = 2; i < MAXH; i++) nch_hi += ((MAXH <= 8) || i < d.nheaps) ? min(h[i], 2u) : 0u;
+    uint32_t out[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const uint32_t h0 = S - (s + e), h1 = h[1] + e;
+      // heap 0: same prefix; heap 1: one / two prefixes down
+      const uint32_t c[4] = {h0 >= 1 ? A1[e] : 0u, h0 >= 2 ? A2[e] : 0u,
+                             h1 >= 1 ? (e >= 1 ? A1[e - 1] : P1[3]) : 0u,
+                             h1 >= 2 ? (e >= 2 ? A2[e - 2] : P2[2 + e]) : 0u};
+      uint32_t mn = 0xFFFFFFFFu, mxx = 0, mxw = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t w = c[j];
+        const uint32_t x = __builtin_amdgcn_alignbit(w ^ 1u, w ^ 1u, 2);
+        mn = min(mn, x);
+        mxx = max(mxx, x);
+        mxw = max(mxw, w);
+      }
+#pragma unroll
+      for (int i = 2; i < MAXH; i++) {
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+          const uint32_t w = k ? C2[i][e] : C1[i][e];
+          const uint32_t x = __builtin_amdgcn_alignbit(w ^ 1u, w ^ 1u, 2);
+          mn = min(mn, x);
+          mxx = max(mxx, x);
+          mxw = max(mxw, w);
+        }
+      }
+      uint32_t word;
+      if (S == 0) word = make_word(LOSS, 0);  // all heaps empty: four_to_one.py:19-22
+      else if (mn < 0x40000000u) word = make_word(WIN, (mn & 0x3FFFFFFFu) + 1);
+      else word = make_word(mxx >= 0xC0000000u ? TIE : mxx >= 0x80000000u ? DRAW : LOSS, (mxw >> 2) + 1);
+      const bool reached = (rbits >> e) & 1u;
+      out[e] = reached ? word : W_UNREACHED;
+      if (reached && ((valid >> e) & 1u)) {
+        npos++;
+        edges += (u64)(min(h0, 2u) + min(h1, 2u) + nch_hi);
+        prims += S == 0;
+        if (S != 0 && mxw >= W_REACHED) err |= ERR_CHILD_UNRESOLVED;
+      }
+    }
+    if (valid == 15u) {
+      u32x4 o4 = {out[0], out[1], out[2], out[3]};
+      *(u32x4*)(mine + q) = o4;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; e++)
+        if ((valid >> e) & 1u) mine[q + e] = out[e];
+    }
+  }
+  if (err) atomicOr(&st->err, err);
+  block_add(&st->cursor_front, npos);  // positions resolved
+  block_add(&st->edges, edges);
+  block_add(&st->prims, prims);
+}
+
 // root word (on the shard that owns the root, root_q = its local prefix;
 // others pass ~0 and report NO_WORD)
 __global__ void k_dense_root(DenseView v, const uint32_t* words, const u64* bits, u64 root_q, DevState* st) {

@@ -349,6 +349,68 @@ static size_t halo_bytes(const HaloGeom& h) {
   return halo_tab_bytes(h) + 2 * (h.nb * 2 * h.Z * 4);
 }
 
+// Active-group lists of single-table power-of-two dense layouts
+// (k_dense_resolve4): per level, the 256-prefix groups holding at least one
+// non-hole.  A level's band (dense_band) is a loose bound -- at the narrow
+// ends of the tier sequence it spans nearly the whole row while a few
+// percent of its groups hold positions -- and XCD chunks of a band split the
+// level's work unevenly; a launch over the list sweeps only live groups.
+// Group g (base 256 g) holds digit sums [gs, gs + mj] with gs =
+// digitsum(256 g), mj = digitsum(255) (pow2 digits are bit fields), so it is
+// live at level L iff [gs, gs + mj] meets [S - heap0, S].
+//
+// Order (L2 reuse): a group's children lie in the same group or in groups
+// one or two steps down one digit.  With g = column + top * C (C = groups
+// per top-digit slice), the level's columns are cut into 8 contiguous
+// ranges of equal live-group count, one per XCD, and each XCD walks its
+// range TOP-MAJOR (all its columns at top value t, then t + 1, ...): the
+// top-digit children (4-8 MB away in address order) were touched one or two
+// steps earlier, the other digits' children are neighbouring columns of the
+// same step -- both still in that XCD's L2.  Tables without a top digit
+// above the group fall back to address order in 8 equal shares.
+struct GroupGeom {
+  bool on = false;
+  u64 groups = 0;
+  int mj = 0;
+};
+static GroupGeom group_geom(const Desc* d, int world) {
+  GroupGeom g;
+  if (world != 1 || !d->pow2 || d->nheaps < 2 || d->base[1] < 4 || d->W % 256 || d->W * 4 > 0xFFFFFFF0ull)
+    return g;
+  g.groups = d->W / 256;
+  for (int i = 1; i < d->nheaps; i++) g.mj += (int)((255u >> d->pshift[i]) & (d->base[i] - 1));
+  g.on = true;
+  return g;
+}
+static void group_sums(const Desc* d, const GroupGeom& g, std::vector<uint16_t>& gs) {
+  gs.resize(g.groups);
+  for (u64 k = 0; k < g.groups; k++) {
+    int s = 0;
+    for (int i = 1; i < d->nheaps; i++) s += (int)(((k * 256) >> d->pshift[i]) & (d->base[i] - 1));
+    gs[k] = (uint16_t)s;
+  }
+}
+static bool group_live(const Desc* d, const GroupGeom& g, int gs, int L) {
+  const int S = (int)d->root_sum - L;
+  return gs <= S && gs + g.mj >= S - (int)d->heap[0];
+}
+static u64 group_entries(const Desc* d, const GroupGeom& g) {
+  if (!g.on) return 0;
+  std::vector<uint16_t> gs;
+  group_sums(d, g, gs);
+  std::vector<u64> hist(1 << 16, 0);
+  for (uint16_t x : gs) hist[x]++;
+  u64 n = 0;
+  for (int L = 0; L < d->max_levels; L++)
+    for (int x = 0; x < (1 << 16); x++)
+      if (hist[x] && group_live(d, g, x, L)) n += hist[x];
+  return n;
+}
+static size_t group_bytes(const Desc* d, int world) {
+  const GroupGeom g = group_geom(d, world);
+  return g.on ? (group_entries(d, g) * 4 + 255) / 256 * 256 : 0;
+}
+
 __device__ __forceinline__ u64 mix64(u64 x) {  // splitmix64 finaliser
   x ^= x >> 31;
   x *= 0x7fb5d329728ea185ull;
@@ -660,6 +722,11 @@ struct gm_solver {
   uint32_t* halo_send = nullptr;
   uint32_t* halo_recv = nullptr;
   std::vector<uint32_t> halo_tot;
+  // active-group lists (GroupGeom): device list, per-level offsets and
+  // per-level XCD shares (host)
+  const uint32_t* glist = nullptr;
+  std::vector<u64> goff;
+  std::vector<uint32_t> gxcd;  // [L * 9 + x]: share x of level L starts at entry gxcd (relative to goff[L])
   hipStream_t stream;
   bool own_stream;
   uint32_t flags;
@@ -719,6 +786,16 @@ static bool dense_per_lane_pull() {
   }
   return v == 1;
 }
+// resolve: four prefixes per lane (k_dense_resolve4) unless
+// GM_DENSE_RESOLVE=scalar (A/B runs)
+static bool dense_scalar_resolve() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("GM_DENSE_RESOLVE");
+    v = (e && !strcmp(e, "scalar")) ? 1 : 0;
+  }
+  return v == 1;
+}
 
 template <int MAXH, bool POW2>
 static void dense_launch_pull_t(gm_solver* s, const DenseView& v, int grid, u64 L, u64 root_p) {
@@ -739,6 +816,50 @@ static void dense_launch_resolve_t(gm_solver* s, const DenseView& v, int grid, u
   // fewer waves per SIMD) measured 21.6 vs 17.4 ms per 2^30 resolve.  The
   // block-layout mapping (shards) is a separate instantiation so the
   // single-table kernel carries none of it.
+  // quad form: pow2 digits with base[1] >= 4 (the four prefixes of a lane
+  // share every digit but the lowest), 32-bit row offsets, and waves of 256
+  // prefixes that never straddle a slice of a block layout
+  if constexpr (POW2 && MAXH >= 2) {
+  if (s->d.nheaps >= 2 && s->d.base[1] >= 4 && v.Wl * 4 <= 0xFFFFFFF0ull && (!v.blk || v.Z % 256 == 0) &&
+      !dense_scalar_resolve()) {
+    const uint32_t* gl = nullptr;
+    u64 units = (v.p_hi - (v.p_lo & ~255ull) + 3) / 4;
+    if (s->glist && !v.blk) {  // live groups of level L, 64 units each
+      gl = s->glist + s->goff[L];
+      units = (s->goff[L + 1] - s->goff[L]) * 64;
+      if (!units) return;
+    }
+    // a grid of exactly the blocks that fit at once (a multiple of 8):
+    // blocks that start late would sweep their grid-stride items out of the
+    // list order the L2 reuse relies on
+    static int resident = 0;
+    if (!resident) {
+      int per_cu = 0, dev = 0, cus = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_dense_resolve4<MAXH, false>, kBlock,
+                                                       0) != hipSuccess ||
+          per_cu < 1)
+        per_cu = 4;
+      (void)hipGetDevice(&dev);
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+        cus = 256;
+      resident = std::max(8, (per_cu * cus) & ~7);
+    }
+    const int g = (int)std::min<u64>(((units + kBlock - 1) / kBlock + 7) & ~7ull, (u64)resident);
+    if (gl) {
+      XcdShares xs;
+      for (int x = 0; x < 9; x++) xs.o[x] = s->gxcd[(size_t)L * 9 + x];
+      hipLaunchKernelGGL((k_dense_resolve4<MAXH, false>), dim3(g), dim3(kBlock), 0, s->stream, s->d, v, s->words,
+                         s->bits, L, s->st, gl, xs);
+    }
+    else if (v.blk)
+      hipLaunchKernelGGL((k_dense_resolve4<MAXH, true>), dim3(g), dim3(kBlock), 0, s->stream, s->d, v, s->words,
+                         s->bits, L, s->st, nullptr, XcdShares{});
+    else
+      hipLaunchKernelGGL((k_dense_resolve4<MAXH, false>), dim3(g), dim3(kBlock), 0, s->stream, s->d, v, s->words,
+                         s->bits, L, s->st, nullptr, XcdShares{});
+    return;
+  }
+  }
   if (v.blk)
     hipLaunchKernelGGL((k_dense_resolve<MAXH, POW2, true, 1, true>), dim3(grid), dim3(kBlock), 0, s->stream, s->d,
                        v, s->words, s->bits, L, s->st);
@@ -1038,6 +1159,7 @@ int gm_plan(int game, uint64_t positions, uint32_t flags, uint64_t max_table_byt
     bool fits = false;
     int rc = plan_dense(d, 0, 1, max_table_bytes, out, &fits);
     if (rc) return rc;
+    out->scratch_bytes += group_bytes(d, 1);
     if (fits) return 0;
     memset(out, 0, sizeof *out);
     out->max_levels = (uint32_t)d->max_levels;
@@ -1188,6 +1310,61 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
       }
     } else {
       s->hg.on = false;  // scratch from an older plan: whole-slice halos
+    }
+    const GroupGeom gg = group_geom(d, world);
+    const size_t gbytes = gg.on ? (group_entries(d, gg) * 4 + 255) / 256 * 256 : 0;
+    if (gg.on && !s->view.blk && buf->scratch_bytes >= scratch_bytes_for(d->max_levels) + gbytes) {
+      std::vector<uint16_t> gsum;
+      group_sums(d, gg, gsum);
+      std::vector<uint32_t> list;
+      list.reserve(gbytes / 4);
+      s->goff.assign((size_t)d->max_levels + 1, 0);
+      s->gxcd.assign((size_t)d->max_levels * 9, 0);
+      const int top = d->nheaps - 1;
+      const u64 C = d->pstride[top] / 256;  // groups per top-digit slice
+      bool cols = top >= 2 && d->pstride[top] % 256 == 0 && C >= 8;
+      u64 tile = 0;  // columns per top-major tile (0: the XCD's whole range)
+      if (const char* e = getenv("GM_GROUP_TILE")) {  // A/B: -1 = address order
+        const long long v = atoll(e);
+        if (v < 0) cols = false;
+        else tile = (u64)v;
+      }
+      const u64 NT = cols ? gg.groups / C : 1, NC = cols ? C : gg.groups;
+      std::vector<u64> live(NC);
+      for (int L = 0; L < d->max_levels; L++) {
+        s->goff[L] = list.size();
+        u64 tot = 0;
+        for (u64 c = 0; c < NC; c++) {
+          u64 n = 0;
+          for (u64 t = 0; t < NT; t++) n += group_live(d, gg, gsum[c + t * NC], L);
+          live[c] = n;
+          tot += n;
+        }
+        // 8 contiguous column ranges of ~equal live count, each walked
+        // top-major in tiles of `tile` columns
+        u64 c0 = 0, acc = 0;
+        for (int x = 0; x < 8; x++) {
+          s->gxcd[(size_t)L * 9 + x] = (uint32_t)(list.size() - s->goff[L]);
+          u64 c1 = c0;
+          const u64 want = tot * (u64)(x + 1) / 8;
+          while (c1 < NC && (acc < want || x == 7)) acc += live[c1++];
+          const u64 tw = tile ? tile : std::max<u64>(1, c1 - c0);
+          for (u64 ta = c0; ta < c1; ta += tw)
+            for (u64 t = 0; t < NT; t++)
+              for (u64 c = ta; c < std::min(c1, ta + tw); c++)
+                if (group_live(d, gg, gsum[c + t * NC], L)) list.push_back((uint32_t)(c + t * NC));
+          c0 = c1;
+        }
+        s->gxcd[(size_t)L * 9 + 8] = (uint32_t)(list.size() - s->goff[L]);
+      }
+      s->goff[d->max_levels] = list.size();
+      uint32_t* dl = (uint32_t*)((char*)buf->scratch + scratch_bytes_for(d->max_levels));
+      e = list.empty() ? hipSuccess : hipMemcpy(dl, list.data(), list.size() * 4, hipMemcpyHostToDevice);
+      if (e != hipSuccess) {
+        gm_solver_destroy(s);
+        return fail(GM_EHIP, "group lists: %s", hipGetErrorString(e));
+      }
+      s->glist = dl;
     }
   }
   *out = s;
