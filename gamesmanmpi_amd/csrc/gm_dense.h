@@ -23,7 +23,28 @@
 // marker; W_REACHED/W_UNREACHED never appear in resolved words.
 
 constexpr uint32_t W_UNREACHED = 0xFFFFFFFFu;
-constexpr uint32_t W_REACHED = 0xFFFFFFFEu;
+
+// Dense tables hold only WIN/LOSS positions (K_SUM: every primitive is a
+// LOSS, four_to_one.py:19-22), stored in an ORDER form y whose unsigned max
+// over a position's children is the whole reduction (reference-canonical
+// _res_red/_remote_red, process.py:187-220):
+//   WIN  remoteness r -> y = r                          (top bit 0)
+//   LOSS remoteness r -> y = 0x80000000 | (0x7FFFFFFF - r)
+// max over children: any LOSS child -> top bit set, low bits = 0x7FFFFFFF -
+// (smallest LOSS remoteness) -> parent WIN, 1 + that; else max WIN
+// remoteness -> parent LOSS, 1 + that.  An absent child reads 0 (a WIN of
+// remoteness 0, which no position holds): neutral.  Converted to the
+// value | remoteness << 2 word only where words leave the table (root,
+// query).  W_UNREACHED marks reached-bit-clear slots (never read as
+// children; readers check the reach bit first).
+__host__ __device__ __forceinline__ uint32_t dense_word(uint32_t y) {
+  return (y & 0x80000000u) ? make_word(LOSS, 0x7FFFFFFFu - (y & 0x7FFFFFFFu)) : make_word(WIN, y);
+}
+// parent order form from the max m over its children's order forms
+__device__ __forceinline__ uint32_t dense_parent(uint32_t m) {
+  return (m & 0x80000000u) ? (0x7FFFFFFFu - (m & 0x7FFFFFFFu)) + 1u : 0x80000000u | (0x7FFFFFFFu - (m + 1u));
+}
+constexpr uint32_t DENSE_PRIMITIVE = 0xFFFFFFFFu;  // LOSS, remoteness 0 (all heaps empty)
 
 // digit i (i >= 1) of a prefix
 __device__ __forceinline__ uint32_t pdigit(const Desc& d, u64 p, int i) {
@@ -369,7 +390,6 @@ __global__ __launch_bounds__(256) void k_dense_resolve(Desc d, DenseView v, uint
   n1.init(words + (L + 1) * v.Wl, S >= 1 ? v.Wl : 0);
   n2.init(words + (L + 2) * v.Wl, S >= 2 ? v.Wl : 0);
   u64 npos = 0, edges = 0, prims = 0;
-  uint32_t err = 0;
   WaveDigits<MAXH, POW2> wd;
   wd.init(d);
   const XcdRange r = xcd_range(v.p_hi - v.p_lo);
@@ -424,22 +444,12 @@ __global__ __launch_bounds__(256) void k_dense_resolve(Desc d, DenseView v, uint
 #pragma unroll
     for (int u = 0; u < U; u++) {
       if (!ok[u]) continue;
-      // x = rotr(w ^ 1, 2): value code on top, remapped so LOSS < WIN <
-      // DRAW < TIE (LOSS 00, WIN 01, DRAW 10, TIE 11); an absent child
-      // (w = 0) is a WIN of remoteness 0 and changes no term below
-      uint32_t mn = 0xFFFFFFFFu, mxx = 0, mxw = 0;
+      // order forms: the max over the children is the reduction (absent
+      // children read 0, neutral)
+      uint32_t m = 0;
 #pragma unroll
-      for (int j = 0; j < 2 * MAXH; j++) {
-        const uint32_t w = c[u][j];
-        const uint32_t x = __builtin_amdgcn_alignbit(w ^ 1u, w ^ 1u, 2);
-        mn = min(mn, x);
-        mxx = max(mxx, x);
-        mxw = max(mxw, w);
-      }
-      uint32_t word;
-      if (S == 0) word = make_word(LOSS, 0);  // all heaps empty: four_to_one.py:19-22
-      else if (mn < 0x40000000u) word = make_word(WIN, (mn & 0x3FFFFFFFu) + 1);  // a LOSS child
-      else word = make_word(mxx >= 0xC0000000u ? TIE : mxx >= 0x80000000u ? DRAW : LOSS, (mxw >> 2) + 1);
+      for (int j = 0; j < 2 * MAXH; j++) m = max(m, c[u][j]);
+      const uint32_t word = S == 0 ? DENSE_PRIMITIVE : dense_parent(m);
       // Every non-hole slot is written (the word is consumed unconditionally,
       // so the child loads issue together with the reach word); unreached
       // slots get W_UNREACHED and are never read as children.
@@ -450,11 +460,9 @@ __global__ __launch_bounds__(256) void k_dense_resolve(Desc d, DenseView v, uint
         npos++;
         edges += (u64)nch[u];
         prims += S == 0;
-        if (S != 0 && mxw >= W_REACHED) err |= ERR_CHILD_UNRESOLVED;
       }
     }
   }
-  if (err) atomicOr(&st->err, err);
   block_add(&st->cursor_front, npos);  // positions resolved
   block_add(&st->edges, edges);
   block_add(&st->prims, prims);
@@ -506,8 +514,7 @@ __global__ __launch_bounds__(256) void k_dense_resolve4(Desc d, DenseView v, uin
   WordRow4 n1, n2;  // levels L+1, L+2 (empty rows past the last level)
   n1.init(words + (L + 1) * v.Wl, S >= 1 ? v.Wl : 0);
   n2.init(words + (L + 2) * v.Wl, S >= 2 ? v.Wl : 0);
-  u64 npos = 0, edges = 0, prims = 0;
-  uint32_t err = 0;
+  uint32_t npos = 0, edges = 0;  // per thread: far below 2^32
   // digits of the lane's first prefix offset 4 * lane (pow2 digit split)
   const uint32_t lane = __lane_id();
   uint32_t hl[MAXH], sl = 0;
@@ -580,40 +587,18 @@ __global__ __launch_bounds__(256) void k_dense_resolve4(Desc d, DenseView v, uin
     for (int e = 0; e < 4; e++) {
       const uint32_t h0 = S - (s + e), h1 = h[1] + e;
       // heap 0: same prefix; heap 1: one / two prefixes down
-      const uint32_t c[4] = {h0 >= 1 ? A1[e] : 0u, h0 >= 2 ? A2[e] : 0u,
-                             h1 >= 1 ? (e >= 1 ? A1[e - 1] : P1[3]) : 0u,
-                             h1 >= 2 ? (e >= 2 ? A2[e - 2] : P2[2 + e]) : 0u};
-      uint32_t mn = 0xFFFFFFFFu, mxx = 0, mxw = 0;
+      // order forms (see dense_word): the max over the children is the
+      // reduction; heap-0/1 quads may hold hole words (masked to 0)
+      uint32_t m = max(h0 >= 1 ? A1[e] : 0u, h0 >= 2 ? A2[e] : 0u);
+      m = max(m, max(h1 >= 1 ? (e >= 1 ? A1[e - 1] : P1[3]) : 0u, h1 >= 2 ? (e >= 2 ? A2[e - 2] : P2[2 + e]) : 0u));
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const uint32_t w = c[j];
-        const uint32_t x = __builtin_amdgcn_alignbit(w ^ 1u, w ^ 1u, 2);
-        mn = min(mn, x);
-        mxx = max(mxx, x);
-        mxw = max(mxw, w);
-      }
-#pragma unroll
-      for (int i = 2; i < MAXH; i++) {
-#pragma unroll
-        for (int k = 0; k < 2; k++) {
-          const uint32_t w = k ? C2[i][e] : C1[i][e];
-          const uint32_t x = __builtin_amdgcn_alignbit(w ^ 1u, w ^ 1u, 2);
-          mn = min(mn, x);
-          mxx = max(mxx, x);
-          mxw = max(mxw, w);
-        }
-      }
-      uint32_t word;
-      if (S == 0) word = make_word(LOSS, 0);  // all heaps empty: four_to_one.py:19-22
-      else if (mn < 0x40000000u) word = make_word(WIN, (mn & 0x3FFFFFFFu) + 1);
-      else word = make_word(mxx >= 0xC0000000u ? TIE : mxx >= 0x80000000u ? DRAW : LOSS, (mxw >> 2) + 1);
+      for (int i = 2; i < MAXH; i++) m = max(m, max(C1[i][e], C2[i][e]));
+      const uint32_t word = S == 0 ? DENSE_PRIMITIVE : dense_parent(m);
       const bool reached = (rbits >> e) & 1u;
       out[e] = reached ? word : W_UNREACHED;
       if (reached && ((valid >> e) & 1u)) {
         npos++;
-        edges += (u64)(min(h0, 2u) + min(h1, 2u) + nch_hi);
-        prims += S == 0;
-        if (S != 0 && mxw >= W_REACHED) err |= ERR_CHILD_UNRESOLVED;
+        edges += min(h0, 2u) + min(h1, 2u) + nch_hi;
       }
     }
     if (valid == 15u) {
@@ -625,10 +610,9 @@ __global__ __launch_bounds__(256) void k_dense_resolve4(Desc d, DenseView v, uin
         if ((valid >> e) & 1u) mine[q + e] = out[e];
     }
   }
-  if (err) atomicOr(&st->err, err);
-  block_add(&st->cursor_front, npos);  // positions resolved
-  block_add(&st->edges, edges);
-  block_add(&st->prims, prims);
+  block_add(&st->cursor_front, (u64)npos);  // positions resolved
+  block_add(&st->edges, (u64)edges);
+  block_add(&st->prims, S == 0 ? (u64)npos : 0ull);
 }
 
 // root word (on the shard that owns the root, root_q = its local prefix;
@@ -636,7 +620,7 @@ __global__ __launch_bounds__(256) void k_dense_resolve4(Desc d, DenseView v, uin
 __global__ void k_dense_root(DenseView v, const uint32_t* words, const u64* bits, u64 root_q, DevState* st) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     uint32_t w = NO_WORD;
-    if (root_q != ~0ull && reach_bit(bits, root_q)) w = words[root_q];  // level 0
+    if (root_q != ~0ull && reach_bit(bits, root_q)) w = dense_word(words[root_q]);  // level 0
     st->root_word = w;
   }
 }
@@ -650,7 +634,7 @@ __global__ void k_dense_query(Desc d, DenseView v, const uint32_t* words, const 
     if (dense_slot_of(d, keys[i], &slot)) {
       slot_split(d, slot, &L, &p);
       uint64_t q;
-      if (dense_local(v, p, &q) && reach_bit(bits, L * v.Wbl + q)) w = words[L * v.Wl + q];
+      if (dense_local(v, p, &q) && reach_bit(bits, L * v.Wbl + q)) w = dense_word(words[L * v.Wl + q]);
     }
     out[i] = w;
   }

@@ -237,6 +237,7 @@ static int dense_geom(const Desc* d, int rank, int world, DenseGeom* g) {
     g->v.p_lo = 0;
     g->v.p_hi = d->W;
     g->v.Wl = d->W;
+    if (const char* e = getenv("GM_ROW_PAD")) g->v.Wl += (u64)atoll(e) & ~3ull;  // A/B: row stride padding (words)
     g->v.Wbl = (d->W + 63) & ~63ull;
     g->v.world = 1;
     g->v.zshift = -1;

@@ -47,6 +47,25 @@ __global__ void write_b32(uint32_t* __restrict__ p, size_t n) {
     p[i] = (uint32_t)i;
 }
 
+// 64 B of every 128-B line (16 lanes x 4 B, lines 128 B apart): does a
+// partial-line read fetch 64 or 128 B?  n = lines
+__global__ void read_half_lines(const uint32_t* __restrict__ p, size_t n, uint32_t* out) {
+  uint32_t acc = 0;
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (size_t i = t; i < n * 16; i += (size_t)gridDim.x * blockDim.x) acc ^= p[(i >> 4) * 32 + (i & 15)];
+  if (acc == 0x12345678u) out[0] = acc;
+}
+// resolve-shaped stream: two 16-B-per-lane reads and one 16-B-per-lane
+// write per element (achievable rate of the dense resolve's compulsory
+// traffic); n = elements of 16 B per stream
+__global__ void triad_b128(const uint4* __restrict__ a, const uint4* __restrict__ b, uint4* __restrict__ c,
+                           size_t n) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    uint4 x = a[i], y = b[i];
+    c[i] = make_uint4(max(x.x, y.x), max(x.y, y.y), max(x.z, y.z), max(x.w, y.w));
+  }
+}
+
 int main() {
   const size_t bytes = (size_t)1 << 30;
   void* buf = nullptr;
@@ -62,7 +81,28 @@ int main() {
     hipLaunchKernelGGL(write_b32, dim3(grid), dim3(block), 0, 0, (uint32_t*)buf, bytes / 4);
   }
   CHK(hipDeviceSynchronize());
-  printf("{\"bytes_per_kernel\": %zu}\n", bytes);
+  // timed: half-line reads and the resolve-shaped triad over 3 x 1/3 GiB
+  hipEvent_t e0, e1;
+  CHK(hipEventCreate(&e0));
+  CHK(hipEventCreate(&e1));
+  float ms_half = 0, ms_triad = 0;
+  for (int rep = 0; rep < 3; rep++) {
+    CHK(hipEventRecord(e0, 0));
+    hipLaunchKernelGGL(read_half_lines, dim3(grid), dim3(block), 0, 0, (const uint32_t*)buf, bytes / 128, out);
+    CHK(hipEventRecord(e1, 0));
+    CHK(hipEventSynchronize(e1));
+    CHK(hipEventElapsedTime(&ms_half, e0, e1));
+    const size_t third = bytes / 3 / 16;
+    const uint4* a = (const uint4*)buf;
+    CHK(hipEventRecord(e0, 0));
+    hipLaunchKernelGGL(triad_b128, dim3(grid), dim3(block), 0, 0, a, a + third, (uint4*)(a + 2 * third), third);
+    CHK(hipEventRecord(e1, 0));
+    CHK(hipEventSynchronize(e1));
+    CHK(hipEventElapsedTime(&ms_triad, e0, e1));
+  }
+  printf("{\"bytes_per_kernel\": %zu, \"half_lines_ms\": %.4f, \"half_lines_requested_GBps\": %.1f, "
+         "\"triad_ms\": %.4f, \"triad_GBps\": %.1f}\n",
+         bytes, ms_half, bytes / 2 / ms_half / 1e6, ms_triad, (double)(bytes / 3 / 16 * 16 * 3) / ms_triad / 1e6);
   CHK(hipFree(buf));
   CHK(hipFree(out));
   return 0;
