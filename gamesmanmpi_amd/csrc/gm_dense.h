@@ -504,25 +504,118 @@ struct WordRow4 {
   }
 };
 
-template <int MAXH, bool BLK>
-__global__ __launch_bounds__(256) void k_dense_resolve4(Desc d, DenseView v, uint32_t* words, const u64* bits, u64 L,
-                                                        DevState* st, const uint32_t* __restrict__ glist,
-                                                        XcdShares xs) {
-  const uint32_t S = d.root_sum - (uint32_t)L;
-  const uint32_t H0 = d.heap[0];
-  uint32_t* mine = words + L * v.Wl;
+// Body shared by the quad kernels: one lane, four prefixes.  q = local
+// prefix of element 0 (4-aligned), pw = global prefix of the wave's element
+// 0 (256-aligned), qi/qlo/qhi = sweep index of element 0 and the launch's
+// sweep range (elements outside are skipped).
+struct Quad4 {
   WordRow4 n1, n2;  // levels L+1, L+2 (empty rows past the last level)
-  n1.init(words + (L + 1) * v.Wl, S >= 1 ? v.Wl : 0);
-  n2.init(words + (L + 2) * v.Wl, S >= 2 ? v.Wl : 0);
+  uint32_t* mine;
+  const u64* bits;
+  u64 Lb;  // L * Wbl
+  uint32_t S, H0;
   uint32_t npos = 0, edges = 0;  // per thread: far below 2^32
-  // digits of the lane's first prefix offset 4 * lane (pow2 digit split)
+};
+template <int MAXH>
+__device__ __forceinline__ void lane_digits4(const Desc& d, uint32_t (&hl)[MAXH], uint32_t& sl) {
   const uint32_t lane = __lane_id();
-  uint32_t hl[MAXH], sl = 0;
+  sl = 0;
 #pragma unroll
   for (int i = 1; i < MAXH; i++) {
     hl[i] = ((MAXH <= 8) || i < d.nheaps) ? (((4u * lane) >> d.pshift[i]) & (d.base[i] - 1)) : 0u;
     sl += hl[i];
   }
+}
+template <int MAXH>
+__device__ __forceinline__ void resolve_quad(const Desc& d, Quad4& Q, const uint32_t (&hl)[MAXH], uint32_t sl, u64 q,
+                                             u64 pw, u64 qi, u64 qlo, u64 qhi) {
+  const uint32_t S = Q.S;
+  uint32_t h[MAXH];
+  uint32_t s = sl;
+#pragma unroll
+  for (int i = 1; i < MAXH; i++) {
+    const uint32_t hb = ((MAXH <= 8) || i < d.nheaps) ? (uint32_t)((pw >> d.pshift[i]) & (d.base[i] - 1)) : 0u;
+    h[i] = hb + hl[i];
+    s += hb;
+  }
+  // element e: digit sum s + e, heap 0 = S - s - e
+  uint32_t valid = 0;
+#pragma unroll
+  for (int e = 0; e < 4; e++) {
+    const uint32_t se = s + e;
+    const bool ok = qi + e >= qlo && qi + e < qhi && se <= S && S - se <= Q.H0;
+    valid |= (uint32_t)ok << e;
+  }
+  if (!__ballot(valid != 0)) return;  // a wave of holes
+  if (!valid) return;
+  const u64 bw = (Q.Lb + q) >> 6;
+  const uint32_t rbits = (uint32_t)(Q.bits[bw] >> ((Q.Lb + q) & 63)) & 15u;
+  u32x4 A1 = Q.n1.at(q, true), A2 = Q.n2.at(q, true);
+  u32x4 P1 = Q.n1.at(q - 4, q >= 4), P2 = Q.n2.at(q - 4, q >= 4);
+  u32x4 C1[MAXH], C2[MAXH];
+#pragma unroll
+  for (int i = 2; i < MAXH; i++) {
+    const bool live = (MAXH <= 8) || i < d.nheaps;
+    C1[i] = Q.n1.at(q - d.pstride[i], live && h[i] >= 1);
+    C2[i] = Q.n2.at(q - 2 * d.pstride[i], live && h[i] >= 2);
+  }
+  uint32_t nch_hi = 0;  // children through heaps >= 2 (same for the four)
+#pragma unroll
+  for (int i = 2; i < MAXH; i++) nch_hi += ((MAXH <= 8) || i < d.nheaps) ? min(h[i], 2u) : 0u;
+  uint32_t out[4];
+#pragma unroll
+  for (int e = 0; e < 4; e++) {
+    const uint32_t h0 = S - (s + e), h1 = h[1] + e;
+    // heap 0: same prefix; heap 1: one / two prefixes down.  Order forms
+    // (see dense_word): the max over the children is the reduction;
+    // heap-0/1 quads may hold hole words (masked to 0)
+    uint32_t m = max(h0 >= 1 ? A1[e] : 0u, h0 >= 2 ? A2[e] : 0u);
+    m = max(m, max(h1 >= 1 ? (e >= 1 ? A1[e - 1] : P1[3]) : 0u, h1 >= 2 ? (e >= 2 ? A2[e - 2] : P2[2 + e]) : 0u));
+#pragma unroll
+    for (int i = 2; i < MAXH; i++) m = max(m, max(C1[i][e], C2[i][e]));
+    const uint32_t word = S == 0 ? DENSE_PRIMITIVE : dense_parent(m);
+    const bool reached = (rbits >> e) & 1u;
+    out[e] = reached ? word : W_UNREACHED;
+    if (reached && ((valid >> e) & 1u)) {
+      Q.npos++;
+      Q.edges += min(h0, 2u) + min(h1, 2u) + nch_hi;
+    }
+  }
+  if (valid == 15u) {
+    u32x4 o4 = {out[0], out[1], out[2], out[3]};
+    *(u32x4*)(Q.mine + q) = o4;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; e++)
+      if ((valid >> e) & 1u) Q.mine[q + e] = out[e];
+  }
+}
+__device__ __forceinline__ void quad_init(Quad4& Q, const Desc& d, uint32_t* words, const u64* bits, u64 L, u64 Wl,
+                                          u64 Wbl) {
+  Q.S = d.root_sum - (uint32_t)L;
+  Q.H0 = d.heap[0];
+  Q.mine = words + L * Wl;
+  Q.n1.init(words + (L + 1) * Wl, Q.S >= 1 ? Wl : 0);
+  Q.n2.init(words + (L + 2) * Wl, Q.S >= 2 ? Wl : 0);
+  Q.bits = bits;
+  Q.Lb = L * Wbl;
+}
+__device__ __forceinline__ void quad_done(const Quad4& Q, DevState* st) {
+  block_add(&st->cursor_front, (u64)Q.npos);  // positions resolved
+  block_add(&st->edges, (u64)Q.edges);
+  block_add(&st->prims, Q.S == 0 ? (u64)Q.npos : 0ull);
+}
+
+// Sweep forms: the level's band (world 1), the level's live-group list
+// (world 1, XCD shares), or a shard's listed slices (BLK).
+template <int MAXH, bool BLK>
+__global__ __launch_bounds__(256) void k_dense_resolve4(Desc d, DenseView v, uint32_t* words, const u64* bits, u64 L,
+                                                        DevState* st, const uint32_t* __restrict__ glist,
+                                                        XcdShares xs) {
+  Quad4 Q;
+  quad_init(Q, d, words, bits, L, v.Wl, v.Wbl);
+  uint32_t hl[MAXH], sl;
+  lane_digits4<MAXH>(d, hl, sl);
   // units of four prefixes over [p_lo rounded down to 256, p_hi), or over
   // the level's live 256-prefix groups (glist, 64 units each)
   const u64 lo = v.p_lo & ~255ull;
@@ -549,70 +642,53 @@ __global__ __launch_bounds__(256) void k_dense_resolve4(Desc d, DenseView v, uin
       qw = lq;
     }
     if (!run) continue;  // wave-uniform: another launch's slice, or a halo
-    const u64 q = qw + (qi - qiw);
-    uint32_t h[MAXH];
-    uint32_t s = sl;
-#pragma unroll
-    for (int i = 1; i < MAXH; i++) {
-      const uint32_t hb = ((MAXH <= 8) || i < d.nheaps) ? (uint32_t)((pw >> d.pshift[i]) & (d.base[i] - 1)) : 0u;
-      h[i] = hb + hl[i];
-      s += hb;
-    }
-    // element e: digit sum s + e, heap 0 = S - s - e
-    uint32_t valid = 0;
-#pragma unroll
-    for (int e = 0; e < 4; e++) {
-      const uint32_t se = s + e;
-      const bool ok = qi + e >= v.p_lo && qi + e < v.p_hi && se <= S && S - se <= H0;
-      valid |= (uint32_t)ok << e;
-    }
-    if (!__ballot(valid != 0)) continue;  // a wave of holes
-    if (!valid) continue;
-    const u64 bw = (L * v.Wbl + q) >> 6;
-    const uint32_t rbits = (uint32_t)(bits[bw] >> ((L * v.Wbl + q) & 63)) & 15u;
-    u32x4 A1 = n1.at(q, true), A2 = n2.at(q, true);
-    u32x4 P1 = n1.at(q - 4, q >= 4), P2 = n2.at(q - 4, q >= 4);
-    u32x4 C1[MAXH], C2[MAXH];
-#pragma unroll
-    for (int i = 2; i < MAXH; i++) {
-      const bool live = (MAXH <= 8) || i < d.nheaps;
-      C1[i] = n1.at(q - d.pstride[i], live && h[i] >= 1);
-      C2[i] = n2.at(q - 2 * d.pstride[i], live && h[i] >= 2);
-    }
-    uint32_t nch_hi = 0;  // children through heaps >= 2 (same for the four)
-#pragma unroll
-    for (int i = 2; i < MAXH; i++) nch_hi += ((MAXH <= 8) || i < d.nheaps) ? min(h[i], 2u) : 0u;
-    uint32_t out[4];
-#pragma unroll
-    for (int e = 0; e < 4; e++) {
-      const uint32_t h0 = S - (s + e), h1 = h[1] + e;
-      // heap 0: same prefix; heap 1: one / two prefixes down
-      // order forms (see dense_word): the max over the children is the
-      // reduction; heap-0/1 quads may hold hole words (masked to 0)
-      uint32_t m = max(h0 >= 1 ? A1[e] : 0u, h0 >= 2 ? A2[e] : 0u);
-      m = max(m, max(h1 >= 1 ? (e >= 1 ? A1[e - 1] : P1[3]) : 0u, h1 >= 2 ? (e >= 2 ? A2[e - 2] : P2[2 + e]) : 0u));
-#pragma unroll
-      for (int i = 2; i < MAXH; i++) m = max(m, max(C1[i][e], C2[i][e]));
-      const uint32_t word = S == 0 ? DENSE_PRIMITIVE : dense_parent(m);
-      const bool reached = (rbits >> e) & 1u;
-      out[e] = reached ? word : W_UNREACHED;
-      if (reached && ((valid >> e) & 1u)) {
-        npos++;
-        edges += min(h0, 2u) + min(h1, 2u) + nch_hi;
-      }
-    }
-    if (valid == 15u) {
-      u32x4 o4 = {out[0], out[1], out[2], out[3]};
-      *(u32x4*)(mine + q) = o4;
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; e++)
-        if ((valid >> e) & 1u) mine[q + e] = out[e];
-    }
+    resolve_quad<MAXH>(d, Q, hl, sl, qw + (qi - qiw), pw, qi, v.p_lo, v.p_hi);
   }
-  block_add(&st->cursor_front, (u64)npos);  // positions resolved
-  block_add(&st->edges, (u64)edges);
-  block_add(&st->prims, S == 0 ? (u64)npos : 0ull);
+  quad_done(Q, st);
+}
+
+// Column jobs (shards, and any table whose top digit sits above 256-prefix
+// groups): within a top-digit slice, group k (a "column") holds digit sums
+// gsc[k] + t + [0, mj] at top value t, so the live columns of slice t at
+// level L are those with gsc in [S - t - heap0 - mj, S - t] -- ONE range of
+// the columns sorted by gsc (colperm, built once).  A launch lists its
+// slices with their colperm ranges; wave w of the concatenation finds its
+// slice by a scalar binary search over the prefix counts (kernel
+// arguments).  No per-level tables, no hole groups.
+constexpr int kMaxColJobs = 96;
+struct ColJobs {
+  uint32_t n;                     // slices
+  uint32_t cum[kMaxColJobs + 1];  // groups before slice i (cum[n] = total)
+  uint32_t lo[kMaxColJobs];       // first colperm entry of slice i
+  uint32_t u[kMaxColJobs];        // local slice
+  uint32_t t[kMaxColJobs];        // global top value
+};
+struct RowGeom {
+  u64 Wl, Wbl, Z;
+};
+template <int MAXH>
+__global__ __launch_bounds__(256) void k_dense_resolve4c(Desc d, RowGeom g, uint32_t* words, const u64* bits, u64 L,
+                                                         DevState* st, const uint32_t* __restrict__ colperm,
+                                                         ColJobs J) {
+  Quad4 Q;
+  quad_init(Q, d, words, bits, L, g.Wl, g.Wbl);
+  uint32_t hl[MAXH], sl;
+  lane_digits4<MAXH>(d, hl, sl);
+  const XcdRange r = xcd_range((u64)J.cum[J.n] * 64);
+  for (u64 iu = r.first; iu < r.end; iu += r.stride) {
+    const uint32_t w = __builtin_amdgcn_readfirstlane((uint32_t)(iu >> 6));  // group of the concatenation
+    uint32_t a = 0, b = J.n;  // slice i: cum[i] <= w < cum[i + 1]
+    while (b - a > 1) {
+      const uint32_t m = (a + b) >> 1;
+      if (J.cum[m] <= w) a = m;
+      else b = m;
+    }
+    const u64 k = colperm[J.lo[a] + (w - J.cum[a])];
+    const u64 qw = (u64)J.u[a] * g.Z + k * 256, pw = (u64)J.t[a] * g.Z + k * 256;
+    const u64 off = 4 * (iu & 63);
+    resolve_quad<MAXH>(d, Q, hl, sl, qw + off, pw, off, 0, 256);
+  }
+  quad_done(Q, st);
 }
 
 // root word (on the shard that owns the root, root_q = its local prefix;

@@ -412,6 +412,47 @@ static size_t group_bytes(const Desc* d, int world) {
   return g.on ? (group_entries(d, g) * 4 + 255) / 256 * 256 : 0;
 }
 
+// Column permutation (k_dense_resolve4c): the Z / 256 groups ("columns") of
+// a top-digit slice sorted by their digit sum over the digits below the
+// top; cstart[x] = first position with sum >= x.  Any world.
+struct ColGeom {
+  bool on = false;
+  int top = 0, mj = 0, maxgs = 0;
+  u64 C = 0;
+};
+static ColGeom col_geom(const Desc* d) {
+  ColGeom c;
+  if (!d->pow2 || d->nheaps < 3 || d->base[1] < 4) return c;
+  c.top = d->nheaps - 1;
+  const u64 Z = d->pstride[c.top];
+  if (Z % 256 || Z * 4 > 0xFFFFFFF0ull) return c;
+  c.C = Z / 256;
+  for (int i = 1; i < c.top; i++) {
+    c.mj += (int)((255u >> d->pshift[i]) & (d->base[i] - 1));
+    c.maxgs += (int)d->heap[i];
+  }
+  c.on = true;
+  return c;
+}
+static size_t col_bytes(const Desc* d) {
+  const ColGeom c = col_geom(d);
+  return c.on ? (c.C * 4 + 255) / 256 * 256 : 0;
+}
+static void build_colperm(const Desc* d, const ColGeom& c, std::vector<uint32_t>& perm, std::vector<uint32_t>& cstart) {
+  std::vector<int> gs(c.C);
+  for (u64 k = 0; k < c.C; k++) {
+    int x = 0;
+    for (int i = 1; i < c.top; i++) x += (int)(((k * 256) >> d->pshift[i]) & (d->base[i] - 1));
+    gs[k] = x;
+  }
+  cstart.assign((size_t)c.maxgs + 2, 0);
+  for (u64 k = 0; k < c.C; k++) cstart[(size_t)gs[k] + 1]++;
+  for (size_t x = 1; x < cstart.size(); x++) cstart[x] += cstart[x - 1];
+  perm.assign(c.C, 0);
+  std::vector<uint32_t> at(cstart.begin(), cstart.end() - 1);
+  for (u64 k = 0; k < c.C; k++) perm[at[gs[k]]++] = (uint32_t)k;  // stable: address order within a sum
+}
+
 __device__ __forceinline__ u64 mix64(u64 x) {  // splitmix64 finaliser
   x ^= x >> 31;
   x *= 0x7fb5d329728ea185ull;
@@ -728,6 +769,10 @@ struct gm_solver {
   const uint32_t* glist = nullptr;
   std::vector<u64> goff;
   std::vector<uint32_t> gxcd;  // [L * 9 + x]: share x of level L starts at entry gxcd (relative to goff[L])
+  // column permutation (ColGeom): device perm, host cstart
+  const uint32_t* colperm = nullptr;
+  ColGeom cg;
+  std::vector<uint32_t> cstart;
   hipStream_t stream;
   bool own_stream;
   uint32_t flags;
@@ -798,6 +843,17 @@ static bool dense_scalar_resolve() {
   return v == 1;
 }
 
+// world-1 quad resolve sweep: the level's live-group list (default) or
+// column jobs (GM_DENSE_SWEEP=cols, A/B)
+static bool dense_sweep_cols() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("GM_DENSE_SWEEP");
+    v = (e && !strcmp(e, "cols")) ? 1 : 0;
+  }
+  return v == 1;
+}
+
 template <int MAXH, bool POW2>
 static void dense_launch_pull_t(gm_solver* s, const DenseView& v, int grid, u64 L, u64 root_p) {
   if (POW2 && !dense_per_lane_pull()) {  // word-parallel form: one thread per 64-prefix group
@@ -825,7 +881,7 @@ static void dense_launch_resolve_t(gm_solver* s, const DenseView& v, int grid, u
       !dense_scalar_resolve()) {
     const uint32_t* gl = nullptr;
     u64 units = (v.p_hi - (v.p_lo & ~255ull) + 3) / 4;
-    if (s->glist && !v.blk) {  // live groups of level L, 64 units each
+    if (s->glist && !v.blk && !dense_sweep_cols()) {  // live groups of level L, 64 units each
       gl = s->glist + s->goff[L];
       units = (s->goff[L + 1] - s->goff[L]) * 64;
       if (!units) return;
@@ -844,6 +900,39 @@ static void dense_launch_resolve_t(gm_solver* s, const DenseView& v, int grid, u
       if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
         cus = 256;
       resident = std::max(8, (per_cu * cus) & ~7);
+    }
+    // column jobs: a shard's listed slices (or, with GM_DENSE_SWEEP=cols,
+    // every top value of a single table), each with its live columns
+    if constexpr (MAXH >= 3) {
+      const bool cols = s->colperm && (v.blk ? (v.nsl > 0 && v.nsl <= (uint32_t)kMaxColJobs)
+                                             : (dense_sweep_cols() && s->d.base[s->cg.top] <= (uint32_t)kMaxColJobs));
+      if (cols) {
+        ColJobs J;
+        J.n = 0;
+        J.cum[0] = 0;
+        const int64_t S = (int64_t)s->d.root_sum - (int64_t)L;
+        const uint32_t nsl = v.blk ? v.nsl : s->d.base[s->cg.top];
+        for (uint32_t i = 0; i < nsl; i++) {
+          const int64_t t = v.blk ? (int64_t)v.st[i] : (int64_t)i;
+          const int64_t hi = std::min<int64_t>(S - t, s->cg.maxgs);
+          const int64_t lo = std::max<int64_t>(S - t - (int64_t)s->d.heap[0] - s->cg.mj, 0);
+          if (hi < lo) continue;
+          const uint32_t a = s->cstart[(size_t)lo], b = s->cstart[(size_t)hi + 1];
+          if (a == b) continue;
+          J.lo[J.n] = a;
+          J.u[J.n] = v.blk ? (uint32_t)v.sl[i] : i;
+          J.t[J.n] = (uint32_t)t;
+          J.cum[J.n + 1] = J.cum[J.n] + (b - a);
+          J.n++;
+        }
+        if (!J.n) return;
+        const u64 cu = (u64)J.cum[J.n] * 64;
+        const int gc = (int)std::min<u64>(((cu + kBlock - 1) / kBlock + 7) & ~7ull, (u64)resident);
+        const RowGeom rg{v.Wl, v.Wbl, v.blk ? v.Z : s->d.pstride[s->cg.top]};
+        hipLaunchKernelGGL((k_dense_resolve4c<MAXH>), dim3(gc), dim3(kBlock), 0, s->stream, s->d, rg, s->words,
+                           s->bits, L, s->st, s->colperm, J);
+        return;
+      }
     }
     const int g = (int)std::min<u64>(((units + kBlock - 1) / kBlock + 7) & ~7ull, (u64)resident);
     if (gl) {
@@ -1142,7 +1231,7 @@ int gm_plan_shard(int game, int rank, int world, uint32_t flags, uint64_t max_ta
   DenseGeom g;
   int grc = dense_geom(d, rank, world, &g);
   if (grc) return grc;
-  out->scratch_bytes += halo_bytes(halo_geom(d, world, g.nb));
+  out->scratch_bytes += halo_bytes(halo_geom(d, world, g.nb)) + col_bytes(d);
   bool fits = false;
   int rc = plan_dense(d, rank, world, max_table_bytes, out, &fits);
   if (rc) return rc;
@@ -1160,7 +1249,7 @@ int gm_plan(int game, uint64_t positions, uint32_t flags, uint64_t max_table_byt
     bool fits = false;
     int rc = plan_dense(d, 0, 1, max_table_bytes, out, &fits);
     if (rc) return rc;
-    out->scratch_bytes += group_bytes(d, 1);
+    out->scratch_bytes += col_bytes(d) + group_bytes(d, 1);
     if (fits) return 0;
     memset(out, 0, sizeof *out);
     out->max_levels = (uint32_t)d->max_levels;
@@ -1312,9 +1401,25 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
     } else {
       s->hg.on = false;  // scratch from an older plan: whole-slice halos
     }
+    // scratch after the halo region: [column permutation | group lists]
+    size_t off = scratch_bytes_for(d->max_levels) + (s->hg.on ? halo_bytes(s->hg) : 0);
+    const ColGeom cg = col_geom(d);
+    if (cg.on && buf->scratch_bytes >= off + col_bytes(d)) {
+      std::vector<uint32_t> perm;
+      build_colperm(d, cg, perm, s->cstart);
+      uint32_t* dp = (uint32_t*)((char*)buf->scratch + off);
+      e = hipMemcpy(dp, perm.data(), perm.size() * 4, hipMemcpyHostToDevice);
+      if (e != hipSuccess) {
+        gm_solver_destroy(s);
+        return fail(GM_EHIP, "column permutation: %s", hipGetErrorString(e));
+      }
+      s->colperm = dp;
+      s->cg = cg;
+      off += col_bytes(d);
+    }
     const GroupGeom gg = group_geom(d, world);
     const size_t gbytes = gg.on ? (group_entries(d, gg) * 4 + 255) / 256 * 256 : 0;
-    if (gg.on && !s->view.blk && buf->scratch_bytes >= scratch_bytes_for(d->max_levels) + gbytes) {
+    if (gg.on && !s->view.blk && buf->scratch_bytes >= off + gbytes) {
       std::vector<uint16_t> gsum;
       group_sums(d, gg, gsum);
       std::vector<uint32_t> list;
@@ -1359,7 +1464,7 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
         s->gxcd[(size_t)L * 9 + 8] = (uint32_t)(list.size() - s->goff[L]);
       }
       s->goff[d->max_levels] = list.size();
-      uint32_t* dl = (uint32_t*)((char*)buf->scratch + scratch_bytes_for(d->max_levels));
+      uint32_t* dl = (uint32_t*)((char*)buf->scratch + off);
       e = list.empty() ? hipSuccess : hipMemcpy(dl, list.data(), list.size() * 4, hipMemcpyHostToDevice);
       if (e != hipSuccess) {
         gm_solver_destroy(s);
