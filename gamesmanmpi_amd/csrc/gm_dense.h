@@ -274,52 +274,6 @@ __global__ __launch_bounds__(256) void k_dense_pull_words(Desc d, DenseView v, u
 }
 #undef TD
 
-// Packed word halo (sharded power-of-two tables, gm_solver.hip
-// exchange_words): the non-hole words of slice pairs of one level move
-// between the table and a dense buffer, one job per pair (a rank's blocks
-// in one launch).  One wave per 64-slot group; the group's non-hole mask
-// vmask[x][g] and packed offset off[x][g] (x = S - t) come from host-built
-// tables, so both ends of a halo use the same order.  pack = 1: table -> buf.
-constexpr int kMaxHaloJobs = 32;
-struct HaloJobs {
-  uint32_t n;
-  uint32_t u0[kMaxHaloJobs];    // local slice of the pair's first slice
-  int32_t x0[kMaxHaloJobs];     // S - t of the first slice
-  uint32_t base[kMaxHaloJobs];  // buffer offset of the pair's first word
-  uint32_t tot0[kMaxHaloJobs];  // non-hole words of the first slice
-};
-__global__ __launch_bounds__(256) void k_halo_move(const u64* __restrict__ vmask, const uint32_t* __restrict__ off,
-                                                   u64 G, int XN, uint32_t* level_words, u64 Z, HaloJobs jobs,
-                                                   uint32_t* buf, int pack) {
-  const uint32_t lane = __lane_id();
-  const u64 nwaves = (u64)gridDim.x * (blockDim.x >> 6);
-  const u64 w0 = __builtin_amdgcn_readfirstlane((uint32_t)((u64)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
-  // four groups per round: their mask/offset loads and word moves overlap
-  for (u64 wb = w0 * 4; wb < (u64)jobs.n * 2 * G; wb += nwaves * 4) {
-    u64 V[4], idx[4], slot[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      V[k] = 0;
-      const u64 w = wb + k;
-      if (w >= (u64)jobs.n * 2 * G) continue;
-      const u64 job = w / (2 * G), rem = w - job * 2 * G;
-      const u64 slice = rem / G, g = rem - slice * G;
-      const int64_t x = (int64_t)jobs.x0[job] - (int64_t)slice;
-      if (x < 0 || x >= XN) continue;
-      V[k] = vmask[(u64)x * G + g];
-      idx[k] = jobs.base[job] + (slice ? jobs.tot0[job] : 0) + off[(u64)x * G + g];
-      slot[k] = ((u64)jobs.u0[job] + slice) * Z + g * 64 + lane;
-    }
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      if (!((V[k] >> lane) & 1ull)) continue;
-      const u64 i = idx[k] + (u64)__popcll(V[k] & ((1ull << lane) - 1ull));
-      if (pack) buf[i] = level_words[slot[k]];
-      else level_words[slot[k]] = buf[i];
-    }
-  }
-}
-
 // XCD-aware split of [0, n) (MI355X dispatches workgroup b to XCD b % 8):
 // the blocks of one XCD grid-stride over one contiguous, 64-aligned chunk,
 // so the child words that neighbouring prefixes share are fetched into ONE
@@ -689,6 +643,100 @@ __global__ __launch_bounds__(256) void k_dense_resolve4c(Desc d, RowGeom g, uint
     resolve_quad<MAXH>(d, Q, hl, sl, qw + off, pw, off, 0, 256);
   }
   quad_done(Q, st);
+}
+
+// Packed word halos (shards, gm_solver.hip exchange_words): the non-hole
+// words of a halo slice at level L move between the table and a dense
+// buffer in COLUMN order -- live columns in colperm order (digit sum gs
+// ascending), slots ascending inside a column.  With x = S - t and y = x -
+// gs, column position i of slice x starts at
+//   PB[x][gs] + (i - CS[gs]) * NY[y]
+// (PB[x][g] = non-holes of all columns with smaller sum, NY[y] = non-holes
+// of a column at y, CS = colperm's sum starts; host tables built once), and
+// a slot's rank inside its column comes from four ballots.  Both ends
+// derive the same order from (L, t) alone.  W16: words travel as 16 bits
+// (order form: top bit + 15 low bits; exact while every remoteness is below
+// 2^15, which K_SUM's remoteness <= root_sum guarantees when root_sum is).
+constexpr int kMaxHaloColJobs = 64;
+struct HaloColJobs {
+  uint32_t n;
+  uint32_t cum[kMaxHaloColJobs + 1];  // columns before job i
+  uint32_t lo[kMaxHaloColJobs];       // first colperm entry
+  uint32_t u[kMaxHaloColJobs];        // local slice
+  int32_t x[kMaxHaloColJobs];         // S - t
+  uint32_t base[kMaxHaloColJobs];     // buffer offset of the slice's first word
+};
+struct HaloTabs {
+  const uint32_t* PB;  // [XN][NG]
+  const uint32_t* NY;  // [NYn]
+  const uint32_t* CS;  // [NG]
+  int NG, NYn, top;
+};
+__device__ __forceinline__ uint32_t halo16(uint32_t y) { return ((y >> 16) & 0x8000u) | (y & 0x7FFFu); }
+__device__ __forceinline__ uint32_t unhalo16(uint32_t h) { return (h & 0x8000u) ? (0xFFFF8000u | h) : h; }
+
+template <bool PACK, bool W16>
+__global__ __launch_bounds__(256) void k_halo_cols(Desc d, HaloColJobs J, u64 Z, const uint32_t* __restrict__ colperm,
+                                                   HaloTabs T, uint32_t* level_words, void* buf) {
+  const uint32_t lane = __lane_id();
+  uint32_t sl = 0;  // digit sum of the lane's first slot offset 4 * lane (below the top digit)
+  for (int i = 1; i < T.top; i++) sl += ((4u * lane) >> d.pshift[i]) & (d.base[i] - 1);
+  const int H0 = (int)d.heap[0];
+  const u64 ltmask = (1ull << lane) - 1ull;
+  const XcdRange r = xcd_range((u64)J.cum[J.n] * 64);
+  for (u64 iu = r.first; iu < r.end; iu += r.stride) {
+    const uint32_t w = __builtin_amdgcn_readfirstlane((uint32_t)(iu >> 6));
+    uint32_t a = 0, b = J.n;
+    while (b - a > 1) {
+      const uint32_t m = (a + b) >> 1;
+      if (J.cum[m] <= w) a = m;
+      else b = m;
+    }
+    const uint32_t i = J.lo[a] + (w - J.cum[a]);
+    const uint32_t k = colperm[i];
+    int gs = 0;
+    for (int h = 1; h < T.top; h++) gs += (int)(((u64)k * 256 >> d.pshift[h]) & (d.base[h] - 1));
+    const int x = J.x[a], y = x - gs;
+    const uint32_t ny = (y >= 0 && y < T.NYn) ? T.NY[y] : 0u;
+    const u64 base = (u64)J.base[a] + T.PB[(u64)x * T.NG + gs] + (u64)(i - T.CS[gs]) * ny;
+    // element e of the lane: slot 4 lane + e, digit sum sl + e
+    uint32_t valid = 0;
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const int ds = (int)sl + e;
+      valid |= (uint32_t)(ds <= y && ds >= y - H0) << e;
+    }
+    u64 bl[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++) bl[e] = __ballot((valid >> e) & 1u);
+    uint32_t before = 0;  // valid slots in lower lanes
+#pragma unroll
+    for (int e = 0; e < 4; e++) before += (uint32_t)__popcll(bl[e] & ltmask);
+    const u64 q = (u64)J.u[a] * Z + (u64)k * 256 + 4 * lane;
+    if (PACK) {
+      if (!valid) continue;
+      const u32x4 v4 = *(const u32x4*)(level_words + q);
+      uint32_t rk = before;
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        if (!((valid >> e) & 1u)) continue;
+        if (W16) ((uint16_t*)buf)[base + rk] = (uint16_t)halo16(v4[e]);
+        else ((uint32_t*)buf)[base + rk] = v4[e];
+        rk++;
+      }
+    } else {
+      if (!valid) continue;
+      u32x4 v4 = {0u, 0u, 0u, 0u};
+      uint32_t rk = before;
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        if (!((valid >> e) & 1u)) continue;
+        v4[e] = W16 ? unhalo16(((const uint16_t*)buf)[base + rk]) : ((const uint32_t*)buf)[base + rk];
+        rk++;
+      }
+      *(u32x4*)(level_words + q) = v4;  // holes of a live lane get 0 (never read unmasked)
+    }
+  }
 }
 
 // root word (on the shard that owns the root, root_q = its local prefix;

@@ -322,28 +322,34 @@ static size_t scratch_bytes_for(int max_levels) {
 // groups of a slice, XN = values of x = S - t that leave any slot valid),
 // then a send and a receive buffer of 2 slices of words each.
 struct HaloGeom {
-  u64 G = 0, Z = 0, nb = 0;
-  int XN = 0;
+  u64 Z = 0, nb = 0;
+  int XN = 0, NG = 0, NYn = 0, mj = 0, top = 0;
   bool on = false;
 };
 static HaloGeom halo_geom(const Desc* d, int world, u64 nb) {
   HaloGeom h;
-  if (world <= 1 || !d->pow2 || d->nheaps < 2) return h;
+  if (world <= 1 || !d->pow2 || d->nheaps < 3 || d->base[1] < 4) return h;
   const int k = d->nheaps - 1;
   h.Z = d->pstride[k];
-  if (h.Z % 64) return h;
-  h.G = h.Z / 64;
+  if (h.Z % 256) return h;
   h.nb = nb;
+  h.top = k;
   int slow = 0;
-  for (int i = 1; i < k; i++) slow += (int)d->heap[i];
-  h.XN = slow + (int)d->heap[0] + 1;
+  for (int i = 1; i < k; i++) {
+    slow += (int)d->heap[i];
+    h.mj += (int)((255u >> d->pshift[i]) & (d->base[i] - 1));
+  }
+  h.XN = slow + (int)d->heap[0] + 1;  // x = S - t with any non-hole
+  h.NG = slow + 2;                    // column digit sums 0..slow, plus the total
+  h.NYn = h.mj + (int)d->heap[0] + 1;
   h.on = true;
   return h;
 }
-// mask table (u64) + offset table (u32) + send and receive buffers of 2
-// slices per local block
+// column tables PB[XN][NG], NY[NYn], CS[NG] (u32) + send and receive
+// buffers of 2 slices per local block
 static size_t halo_tab_bytes(const HaloGeom& h) {
-  return ((size_t)h.XN * h.G * 8 + 255) / 256 * 256 + ((size_t)h.XN * h.G * 4 + 255) / 256 * 256;
+  auto r = [](size_t b) { return (b + 255) / 256 * 256; };
+  return r((size_t)h.XN * h.NG * 4) + r((size_t)h.NYn * 4) + r((size_t)h.NG * 4);
 }
 static size_t halo_bytes(const HaloGeom& h) {
   if (!h.on) return 0;
@@ -759,8 +765,8 @@ struct gm_solver {
   std::vector<hipEvent_t> pev;
   // packed word halos (HaloGeom): device offset table, buffers, host totals
   HaloGeom hg;
-  const u64* halo_vmask = nullptr;
-  const uint32_t* halo_off = nullptr;
+  HaloTabs ht{};
+  bool halo16 = false;  // words travel as 16 bits (k_halo_cols)
   uint32_t* halo_send = nullptr;
   uint32_t* halo_recv = nullptr;
   std::vector<uint32_t> halo_tot;
@@ -1289,34 +1295,37 @@ static void build_mask_tables(const Desc& d, u64* M) {
   }
 }
 
-// Slot r of a top-value slice is a non-hole at level L iff the digit sum
-// of r (all prefix digits below the top) lies in [x - heap0, x], x = S - t.
-// For every x and every 64-slot group g of a slice: the packed offset of the
-// group's first non-hole (exclusive prefix over groups in slot order) and,
-// per x, the slice's non-hole total.  Sender and receiver of a halo compute
-// the same order, so packed slots need no index.
-static u64 host_mask_le(const u64* T, int t) { return t < 0 ? 0ull : (t >= 63 ? ~0ull : T[t]); }
-static void build_halo_offsets(const Desc& d, const u64* M, const HaloGeom& h, std::vector<uint32_t>& off,
-                               std::vector<u64>& vm, std::vector<uint32_t>& tot) {
-  off.assign((size_t)h.XN * h.G, 0);
-  vm.assign((size_t)h.XN * h.G, 0);
-  tot.assign((size_t)h.XN, 0);
-  std::vector<int> sg(h.G);
-  for (u64 g = 0; g < h.G; g++) {
-    int sum = 0;
-    for (int i = 1; i < d.nheaps; i++) sum += (int)(((g * 64) >> d.pshift[i]) & (d.base[i] - 1));
-    sg[g] = sum;
-  }
+// Column tables of the packed halos (k_halo_cols).  Slot j of a column
+// (j < 256, digit sum ds(j) over the digits below the top) is a non-hole of
+// slice x iff ds(j) in [y - heap0, y], y = x - gs: NY[y] counts them,
+// PB[x][g] sums NY over the columns of smaller sum, and tot[x] = PB[x][NG-1]
+// is the slice's non-hole total.
+static void build_halo_cols(const Desc& d, const HaloGeom& h, const std::vector<uint32_t>& cstart,
+                            std::vector<uint32_t>& PB, std::vector<uint32_t>& NY, std::vector<uint32_t>& CS,
+                            std::vector<uint32_t>& tot) {
   const int H0 = (int)d.heap[0];
+  NY.assign((size_t)h.NYn, 0);
+  for (int j = 0; j < 256; j++) {
+    int ds = 0;
+    for (int i = 1; i < h.top; i++) ds += (int)(((uint32_t)j >> d.pshift[i]) & (d.base[i] - 1));
+    for (int y = ds; y <= ds + H0 && y < h.NYn; y++) NY[(size_t)y]++;
+  }
+  CS.assign((size_t)h.NG, 0);
+  std::vector<uint32_t> cnt((size_t)h.NG, 0);
+  for (int g = 0; g < h.NG; g++) {
+    CS[(size_t)g] = g + 1 < (int)cstart.size() ? cstart[(size_t)g] : cstart.back();
+    if (g + 1 < (int)cstart.size()) cnt[(size_t)g] = cstart[(size_t)g + 1] - cstart[(size_t)g];
+  }
+  PB.assign((size_t)h.XN * h.NG, 0);
+  tot.assign((size_t)h.XN, 0);
   for (int x = 0; x < h.XN; x++) {
     uint32_t run = 0;
-    for (u64 g = 0; g < h.G; g++) {
-      off[(size_t)x * h.G + g] = run;
-      const u64 V = host_mask_le(M, x - sg[g]) & ~host_mask_le(M, x - H0 - 1 - sg[g]);
-      vm[(size_t)x * h.G + g] = V;
-      run += (uint32_t)__builtin_popcountll(V);
+    for (int g = 0; g < h.NG; g++) {
+      PB[(size_t)x * h.NG + g] = run;
+      const int y = x - g;
+      if (y >= 0 && y < h.NYn) run += cnt[(size_t)g] * NY[(size_t)y];
     }
-    tot[x] = run;
+    tot[(size_t)x] = run;
   }
 }
 
@@ -1380,34 +1389,15 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
       gm_solver_destroy(s);
       return fail(GM_EHIP, "mask tables: %s", hipGetErrorString(e));
     }
-    s->hg = halo_geom(d, world, (u64)(s->view.blk ? s->view.Wl / ((s->view.B + 4) * s->view.Z) : 1));
-    if (s->hg.on && buf->scratch_bytes >= scratch_bytes_for(d->max_levels) + halo_bytes(s->hg)) {
-      char* base = (char*)buf->scratch + scratch_bytes_for(d->max_levels);
-      const size_t vbytes = ((size_t)s->hg.XN * s->hg.G * 8 + 255) / 256 * 256;
-      s->halo_vmask = (const u64*)base;
-      s->halo_off = (const uint32_t*)(base + vbytes);
-      s->halo_send = (uint32_t*)(base + halo_tab_bytes(s->hg));
-      s->halo_recv = s->halo_send + s->hg.nb * 2 * s->hg.Z;
-      std::vector<uint32_t> off;
-      std::vector<u64> vm;
-      build_halo_offsets(*d, m.data(), s->hg, off, vm, s->halo_tot);
-      e = hipMemcpy((void*)s->halo_vmask, vm.data(), vm.size() * sizeof(u64), hipMemcpyHostToDevice);
-      if (e == hipSuccess)
-        e = hipMemcpy((void*)s->halo_off, off.data(), off.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
-      if (e != hipSuccess) {
-        gm_solver_destroy(s);
-        return fail(GM_EHIP, "halo offsets: %s", hipGetErrorString(e));
-      }
-    } else {
-      s->hg.on = false;  // scratch from an older plan: whole-slice halos
-    }
-    // scratch after the halo region: [column permutation | group lists]
-    size_t off = scratch_bytes_for(d->max_levels) + (s->hg.on ? halo_bytes(s->hg) : 0);
     const ColGeom cg = col_geom(d);
-    if (cg.on && buf->scratch_bytes >= off + col_bytes(d)) {
-      std::vector<uint32_t> perm;
-      build_colperm(d, cg, perm, s->cstart);
-      uint32_t* dp = (uint32_t*)((char*)buf->scratch + off);
+    std::vector<uint32_t> perm;
+    if (cg.on) build_colperm(d, cg, perm, s->cstart);
+    s->hg = halo_geom(d, world, (u64)(s->view.blk ? s->view.Wl / ((s->view.B + 4) * s->view.Z) : 1));
+    size_t off = scratch_bytes_for(d->max_levels);
+    const size_t hbytes = s->hg.on ? halo_bytes(s->hg) : 0;
+    // scratch: [halo tables + buffers | column permutation | group lists]
+    if (cg.on && buf->scratch_bytes >= off + hbytes + col_bytes(d)) {
+      uint32_t* dp = (uint32_t*)((char*)buf->scratch + off + hbytes);
       e = hipMemcpy(dp, perm.data(), perm.size() * 4, hipMemcpyHostToDevice);
       if (e != hipSuccess) {
         gm_solver_destroy(s);
@@ -1415,8 +1405,30 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
       }
       s->colperm = dp;
       s->cg = cg;
-      off += col_bytes(d);
     }
+    if (s->hg.on && s->colperm) {
+      char* base = (char*)buf->scratch + off;
+      auto r = [](size_t b) { return (b + 255) / 256 * 256; };
+      std::vector<uint32_t> PB, NY, CS;
+      build_halo_cols(*d, s->hg, s->cstart, PB, NY, CS, s->halo_tot);
+      uint32_t* pb = (uint32_t*)base;
+      uint32_t* ny = (uint32_t*)(base + r(PB.size() * 4));
+      uint32_t* cs = (uint32_t*)(base + r(PB.size() * 4) + r(NY.size() * 4));
+      e = hipMemcpy(pb, PB.data(), PB.size() * 4, hipMemcpyHostToDevice);
+      if (e == hipSuccess) e = hipMemcpy(ny, NY.data(), NY.size() * 4, hipMemcpyHostToDevice);
+      if (e == hipSuccess) e = hipMemcpy(cs, CS.data(), CS.size() * 4, hipMemcpyHostToDevice);
+      if (e != hipSuccess) {
+        gm_solver_destroy(s);
+        return fail(GM_EHIP, "halo tables: %s", hipGetErrorString(e));
+      }
+      s->ht = HaloTabs{pb, ny, cs, s->hg.NG, s->hg.NYn, s->hg.top};
+      s->halo_send = (uint32_t*)(base + halo_tab_bytes(s->hg));
+      s->halo_recv = s->halo_send + s->hg.nb * 2 * s->hg.Z;
+      s->halo16 = d->kind == K_SUM && d->root_sum < 32768 && !getenv("GM_HALO32");
+    } else {
+      s->hg.on = false;  // scratch from an older plan: whole-slice halos
+    }
+    off += hbytes + (s->colperm ? col_bytes(d) : 0);
     const GroupGeom gg = group_geom(d, world);
     const size_t gbytes = gg.on ? (group_entries(d, gg) * 4 + 255) / 256 * 256 : 0;
     if (gg.on && !s->view.blk && buf->scratch_bytes >= off + gbytes) {
@@ -1758,31 +1770,50 @@ static uint32_t halo_count(const gm_solver* s, u64 L, int64_t t0) {
 static u64 halo_move_all(gm_solver* s, u64 L, int pack, uint32_t* buf, hipStream_t cs) {
   const u64 nb = blk_count(s), B = s->view.B;
   const int64_t S = (int64_t)s->d.root_sum - (int64_t)L;
-  HaloJobs jobs;
-  memset(&jobs, 0, sizeof jobs);
+  const int H0 = (int)s->d.heap[0];
+  HaloColJobs J;
+  J.n = 0;
+  J.cum[0] = 0;
   u64 at = 0;
   auto flush = [&]() {
-    if (!jobs.n) return;
-    const u64 waves = ((u64)jobs.n * 2 * s->hg.G + 3) / 4;  // four groups per wave round
-    const int grid = (int)std::max<u64>(1, std::min<u64>((waves + 3) / 4, (u64)s->grid));
-    hipLaunchKernelGGL(k_halo_move, dim3(grid), dim3(kBlock), 0, cs, s->halo_vmask, s->halo_off, s->hg.G,
-                       s->hg.XN, s->words + L * s->view.Wl, s->view.Z, jobs, buf, pack);
-    jobs.n = 0;
+    if (!J.n) return;
+    const u64 units = (u64)J.cum[J.n] * 64;
+    const int grid = (int)std::min<u64>(((units + kBlock - 1) / kBlock + 7) & ~7ull, (u64)s->grid);
+    uint32_t* lw = s->words + L * s->view.Wl;
+    if (pack && s->halo16)
+      hipLaunchKernelGGL((k_halo_cols<true, true>), dim3(grid), dim3(kBlock), 0, cs, s->d, J, s->view.Z, s->colperm,
+                         s->ht, lw, (void*)buf);
+    else if (pack)
+      hipLaunchKernelGGL((k_halo_cols<true, false>), dim3(grid), dim3(kBlock), 0, cs, s->d, J, s->view.Z, s->colperm,
+                         s->ht, lw, (void*)buf);
+    else if (s->halo16)
+      hipLaunchKernelGGL((k_halo_cols<false, true>), dim3(grid), dim3(kBlock), 0, cs, s->d, J, s->view.Z, s->colperm,
+                         s->ht, lw, (void*)buf);
+    else
+      hipLaunchKernelGGL((k_halo_cols<false, false>), dim3(grid), dim3(kBlock), 0, cs, s->d, J, s->view.Z,
+                         s->colperm, s->ht, lw, (void*)buf);
+    J.n = 0;
   };
   for (u64 j = 0; j < nb; j++) {
     const u64 k = blk_global(s, j);
     if (pack ? k + 1 >= s->nblocks : k < 1) continue;
     const u64 o = pack ? B : 0;
-    const int64_t t0 = blk_top(s, j, o), x0 = S - t0;
-    const uint32_t n = halo_count(s, L, t0);
-    if (!n) continue;
-    jobs.u0[jobs.n] = (uint32_t)blk_slice(s, j, o);
-    jobs.x0[jobs.n] = (int32_t)x0;
-    jobs.base[jobs.n] = (uint32_t)at;
-    jobs.tot0[jobs.n] = halo_total(s, x0);
-    jobs.n++;
-    at += n;
-    if (jobs.n == kMaxHaloJobs) flush();
+    for (u64 m = 0; m < 2; m++) {
+      const int64_t t = blk_top(s, j, o + m), x = S - t;
+      const uint32_t n = halo_total(s, x);
+      if (!n) continue;
+      // live columns of slice x: sums gs in [x - heap0 - mj, x]
+      const int64_t glo = std::max<int64_t>(0, x - H0 - s->hg.mj), ghi = std::min<int64_t>(x, s->hg.NG - 2);
+      const uint32_t ca = s->cstart[(size_t)glo], cb = s->cstart[(size_t)ghi + 1];
+      if (J.n == (uint32_t)kMaxHaloColJobs) flush();
+      J.lo[J.n] = ca;
+      J.u[J.n] = (uint32_t)blk_slice(s, j, o + m);
+      J.x[J.n] = (int32_t)x;
+      J.base[J.n] = (uint32_t)at;
+      J.cum[J.n + 1] = J.cum[J.n] + (cb - ca);
+      J.n++;
+      at += n;
+    }
   }
   flush();
   return at;
@@ -1811,8 +1842,9 @@ static int exchange_words(std::vector<gm_solver*>& ss, u64 L, int mode, hipStrea
       const u64 nsend = halo_move_all(s, L, 1, s->halo_send, cs);
       const u64 nrecv = halo_recv_count(s, L);
       ncclGroupStart();
-      if (nsend) ncclSend(s->halo_send, nsend * 4, ncclUint8, up, s->comm, cs);
-      if (nrecv) ncclRecv(s->halo_recv, nrecv * 4, ncclUint8, down, s->comm, cs);
+      const u64 wb = s->halo16 ? 2 : 4;  // bytes per packed word
+      if (nsend) ncclSend(s->halo_send, nsend * wb, ncclUint8, up, s->comm, cs);
+      if (nrecv) ncclRecv(s->halo_recv, nrecv * wb, ncclUint8, down, s->comm, cs);
       ncclResult_t r = ncclGroupEnd();
       if (r != ncclSuccess) return fail(GM_EHIP, "RCCL words halo: %s", ncclGetErrorString(r));
       if (nrecv) halo_move_all(s, L, 0, s->halo_recv, cs);
