@@ -9,7 +9,9 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIBPATH = os.path.join(HERE, "libgamesman_hip.so")
+# GM_LIBPATH: an alternative in-tree build of the same ABI (A/B runs of
+# kernel variants, tools/diag_streams.sh)
+LIBPATH = os.environ.get("GM_LIBPATH") or os.path.join(HERE, "libgamesman_hip.so")
 
 GM_EINVAL, GM_EHIP, GM_EFULL, GM_ECORRUPT, GM_ENOGPU = -1, -2, -3, -4, -5
 GM_F_KERNEL_TIMING = 1

@@ -480,9 +480,16 @@ __device__ __forceinline__ void lane_digits4(const Desc& d, uint32_t (&hl)[MAXH]
     sl += hl[i];
   }
 }
-template <int MAXH>
+// WALK (a wave walks one column up the top digit, k_dense_resolve4w): the
+// top-digit children come from the previous steps' own-prefix quads, kept
+// in registers -- H1 = row L+1 at top - 1, H2b = row L+2 at top - 2 (H2a =
+// row L+2 at top - 1 shifts into it) -- instead of two loads 4-8 MB away.
+struct WalkHist {
+  u32x4 H1, H2a, H2b;
+};
+template <int MAXH, bool WALK = false>
 __device__ __forceinline__ void resolve_quad(const Desc& d, Quad4& Q, const uint32_t (&hl)[MAXH], uint32_t sl, u64 q,
-                                             u64 pw, u64 qi, u64 qlo, u64 qhi) {
+                                             u64 pw, u64 qi, u64 qlo, u64 qhi, WalkHist* wh = nullptr) {
   const uint32_t S = Q.S;
   uint32_t h[MAXH];
   uint32_t s = sl;
@@ -500,18 +507,52 @@ __device__ __forceinline__ void resolve_quad(const Desc& d, Quad4& Q, const uint
     const bool ok = qi + e >= qlo && qi + e < qhi && se <= S && S - se <= Q.H0;
     valid |= (uint32_t)ok << e;
   }
-  if (!__ballot(valid != 0)) return;  // a wave of holes
-  if (!valid) return;
+  u32x4 A1, A2;
+  if (WALK) {  // the history needs this step's quads even when nothing here resolves
+    A1 = Q.n1.at(q, true);
+    A2 = Q.n2.at(q, true);
+  }
+  auto shift = [&]() {
+    if (WALK) {
+      wh->H2b = wh->H2a;
+      wh->H2a = A2;
+      wh->H1 = A1;
+    }
+  };
+  if (!__ballot(valid != 0)) {  // a wave of holes
+    shift();
+    return;
+  }
+  if (!valid) {
+    shift();
+    return;
+  }
   const u64 bw = (Q.Lb + q) >> 6;
   const uint32_t rbits = (uint32_t)(Q.bits[bw] >> ((Q.Lb + q) & 63)) & 15u;
-  u32x4 A1 = Q.n1.at(q, true), A2 = Q.n2.at(q, true);
-  u32x4 P1 = Q.n1.at(q - 4, q >= 4), P2 = Q.n2.at(q - 4, q >= 4);
+  if (!WALK) {
+    A1 = Q.n1.at(q, true);
+    A2 = Q.n2.at(q, true);
+  }
+#ifdef GM_DIAG_SKIP
+  constexpr uint32_t kDiag = GM_DIAG_SKIP;
+#else
+  constexpr uint32_t kDiag = 0;
+#endif
+  u32x4 P1 = Q.n1.at(q - 4, !(kDiag & 64) && q >= 4), P2 = Q.n2.at(q - 4, !(kDiag & 64) && q >= 4);
   u32x4 C1[MAXH], C2[MAXH];
+  constexpr int TOPI = MAXH - 1;  // WALK: exact heap count (MAXH <= 8)
 #pragma unroll
   for (int i = 2; i < MAXH; i++) {
     const bool live = (MAXH <= 8) || i < d.nheaps;
-    C1[i] = Q.n1.at(q - d.pstride[i], live && h[i] >= 1);
-    C2[i] = Q.n2.at(q - 2 * d.pstride[i], live && h[i] >= 2);
+    if (WALK && i == TOPI) {
+      const u32x4 z = {0u, 0u, 0u, 0u};
+      C1[i] = h[i] >= 1 ? wh->H1 : z;
+      C2[i] = h[i] >= 2 ? wh->H2b : z;
+      continue;
+    }
+    const bool on = !((kDiag >> i) & 1u);
+    C1[i] = Q.n1.at(q - d.pstride[i], on && live && h[i] >= 1);
+    C2[i] = Q.n2.at(q - 2 * d.pstride[i], on && live && h[i] >= 2);
   }
   uint32_t nch_hi = 0;  // children through heaps >= 2 (same for the four)
 #pragma unroll
@@ -535,7 +576,8 @@ __device__ __forceinline__ void resolve_quad(const Desc& d, Quad4& Q, const uint
       Q.edges += min(h0, 2u) + min(h1, 2u) + nch_hi;
     }
   }
-  if (valid == 15u) {
+  if (kDiag & 128) {
+  } else if (valid == 15u) {
     u32x4 o4 = {out[0], out[1], out[2], out[3]};
     *(u32x4*)(Q.mine + q) = o4;
   } else {
@@ -543,7 +585,96 @@ __device__ __forceinline__ void resolve_quad(const Desc& d, Quad4& Q, const uint
     for (int e = 0; e < 4; e++)
       if ((valid >> e) & 1u) Q.mine[q + e] = out[e];
   }
+  shift();
 }
+// Software-pipelined form (k_dense_resolve4p): quad_issue computes a
+// lane's digits and issues every load of one group; quad_finish reduces and
+// stores.  A wave issues group k+1's loads before finishing group k, so the
+// wait for group k's data never covers group k-1's store (gfx9 counts
+// loads and stores in one in-order vmcnt: without the pipeline every
+// group's loads also waited for the previous group's store acknowledgement;
+// skipping the stores altogether measured 14.3 -> 10.6 ms per solve).
+template <int MAXH>
+struct QuadLoads {
+  u32x4 A1, A2, P1, P2, C1[MAXH], C2[MAXH];
+  u64 bitsw;
+  u64 q;
+  uint32_t h1, s, valid, nch_hi;
+};
+template <int MAXH>
+__device__ __forceinline__ void quad_issue(const Desc& d, const Quad4& Q, const uint32_t (&hl)[MAXH], uint32_t sl,
+                                           u64 q, u64 pw, bool on, QuadLoads<MAXH>& X) {
+  const uint32_t S = Q.S;
+  uint32_t h[MAXH];
+  uint32_t s = sl;
+#pragma unroll
+  for (int i = 1; i < MAXH; i++) {
+    const uint32_t hb = ((MAXH <= 8) || i < d.nheaps) ? (uint32_t)((pw >> d.pshift[i]) & (d.base[i] - 1)) : 0u;
+    h[i] = hb + hl[i];
+    s += hb;
+  }
+  uint32_t valid = 0;
+#pragma unroll
+  for (int e = 0; e < 4; e++) {
+    const uint32_t se = s + e;
+    valid |= (uint32_t)(on && se <= S && S - se <= Q.H0) << e;
+  }
+  X.q = q;
+  X.h1 = h[1];
+  X.s = s;
+  X.valid = valid;
+  uint32_t nch_hi = 0;
+#pragma unroll
+  for (int i = 2; i < MAXH; i++) nch_hi += ((MAXH <= 8) || i < d.nheaps) ? min(h[i], 2u) : 0u;
+  X.nch_hi = nch_hi;
+  // lanes (and waves) without a non-hole issue nothing: out-of-range
+  // buffer offsets read zeros without a memory access
+  const bool any = valid != 0;
+  X.bitsw = any ? Q.bits[(Q.Lb + q) >> 6] : 0ull;
+  X.A1 = Q.n1.at(q, any);
+  X.A2 = Q.n2.at(q, any);
+  X.P1 = Q.n1.at(q - 4, any && q >= 4);
+  X.P2 = Q.n2.at(q - 4, any && q >= 4);
+#pragma unroll
+  for (int i = 2; i < MAXH; i++) {
+    const bool live = (MAXH <= 8) || i < d.nheaps;
+    X.C1[i] = Q.n1.at(q - d.pstride[i], any && live && h[i] >= 1);
+    X.C2[i] = Q.n2.at(q - 2 * d.pstride[i], any && live && h[i] >= 2);
+  }
+}
+template <int MAXH>
+__device__ __forceinline__ void quad_finish(Quad4& Q, const QuadLoads<MAXH>& X) {
+  const uint32_t valid = X.valid;
+  if (!valid) return;
+  const uint32_t S = Q.S;
+  const uint32_t rbits = (uint32_t)(X.bitsw >> ((Q.Lb + X.q) & 63)) & 15u;
+  uint32_t out[4];
+#pragma unroll
+  for (int e = 0; e < 4; e++) {
+    const uint32_t h0 = S - (X.s + e), h1 = X.h1 + e;
+    uint32_t m = max(h0 >= 1 ? X.A1[e] : 0u, h0 >= 2 ? X.A2[e] : 0u);
+    m = max(m, max(h1 >= 1 ? (e >= 1 ? X.A1[e - 1] : X.P1[3]) : 0u,
+                   h1 >= 2 ? (e >= 2 ? X.A2[e - 2] : X.P2[2 + e]) : 0u));
+#pragma unroll
+    for (int i = 2; i < MAXH; i++) m = max(m, max(X.C1[i][e], X.C2[i][e]));
+    const uint32_t word = S == 0 ? DENSE_PRIMITIVE : dense_parent(m);
+    const bool reached = (rbits >> e) & 1u;
+    out[e] = reached ? word : W_UNREACHED;
+    if (reached && ((valid >> e) & 1u)) {
+      Q.npos++;
+      Q.edges += min(h0, 2u) + min(h1, 2u) + X.nch_hi;
+    }
+  }
+  if (valid == 15u) {
+    u32x4 o4 = {out[0], out[1], out[2], out[3]};
+    *(u32x4*)(Q.mine + X.q) = o4;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; e++)
+      if ((valid >> e) & 1u) Q.mine[X.q + e] = out[e];
+  }
+}
+
 __device__ __forceinline__ void quad_init(Quad4& Q, const Desc& d, uint32_t* words, const u64* bits, u64 L, u64 Wl,
                                           u64 Wbl) {
   Q.S = d.root_sum - (uint32_t)L;
@@ -601,6 +732,40 @@ __global__ __launch_bounds__(256) void k_dense_resolve4(Desc d, DenseView v, uin
   quad_done(Q, st);
 }
 
+// Live-group list sweep (world 1), software-pipelined: see quad_issue.
+template <int MAXH>
+__global__ __launch_bounds__(256) void k_dense_resolve4p(Desc d, DenseView v, uint32_t* words, const u64* bits, u64 L,
+                                                         DevState* st, const uint32_t* __restrict__ glist,
+                                                         XcdShares xs) {
+  Quad4 Q;
+  quad_init(Q, d, words, bits, L, v.Wl, v.Wbl);
+  uint32_t hl[MAXH], sl;
+  lane_digits4<MAXH>(d, hl, sl);
+  const uint32_t x = blockIdx.x % kXcds;
+  const u64 first = (u64)xs.o[x] * 64 + (u64)(blockIdx.x / kXcds) * blockDim.x + threadIdx.x;
+  const u64 end = (u64)xs.o[x + 1] * 64, stride = (u64)(gridDim.x / kXcds) * blockDim.x;
+  auto issue = [&](u64 iu, QuadLoads<MAXH>& X) {
+    const bool on = iu < end;  // wave-uniform (64-unit aligned ranges)
+    const uint32_t gi = __builtin_amdgcn_readfirstlane((uint32_t)((on ? iu : first) >> 6));
+    const u64 pw = (u64)glist[gi] << 8;  // world 1: local = global prefix
+    quad_issue<MAXH>(d, Q, hl, sl, pw + 4 * (iu & 63), pw, on, X);
+  };
+  if (first < end) {
+    // two register sets, statically named (a dynamically indexed pair
+    // would live in scratch)
+    QuadLoads<MAXH> X0, X1;
+    issue(first, X0);
+    for (u64 iu = first; iu < end; iu += 2 * stride) {
+      issue(iu + stride, X1);  // next group's loads before this group's store
+      quad_finish<MAXH>(Q, X0);
+      if (iu + stride >= end) break;
+      issue(iu + 2 * stride, X0);
+      quad_finish<MAXH>(Q, X1);
+    }
+  }
+  quad_done(Q, st);
+}
+
 // Column jobs (shards, and any table whose top digit sits above 256-prefix
 // groups): within a top-digit slice, group k (a "column") holds digit sums
 // gsc[k] + t + [0, mj] at top value t, so the live columns of slice t at
@@ -641,6 +806,62 @@ __global__ __launch_bounds__(256) void k_dense_resolve4c(Desc d, RowGeom g, uint
     const u64 qw = (u64)J.u[a] * g.Z + k * 256, pw = (u64)J.t[a] * g.Z + k * 256;
     const u64 off = 4 * (iu & 63);
     resolve_quad<MAXH>(d, Q, hl, sl, qw + off, pw, off, 0, 256);
+  }
+  quad_done(Q, st);
+}
+
+// Column walks (world 1): a wave takes one column k and walks up to
+// kWalkSeg consecutive top values t of it, carrying the top-digit children
+// in registers (WalkHist).  Items are ordered by the column's digit sum g
+// (colperm order): every column of sum g is live for the same top range
+// [tlo(g), thi(g)] at level L and splits into the same number of segments,
+// so item w -> (g, column, segment) is a scalar search over the per-level
+// prefix counts IC (kernel arguments) and two divisions.
+constexpr int kWalkSeg = 8;
+constexpr int kMaxWalkG = 128;
+struct WalkJobs {
+  uint32_t ng;                  // digit sums g0 .. g0 + ng - 1
+  uint32_t g0;
+  uint32_t IC[kMaxWalkG + 1];   // items before sum g0 + i
+  uint32_t CS[kMaxWalkG];       // colperm start of sum g0 + i
+};
+template <int MAXH>
+__global__ __launch_bounds__(256) void k_dense_resolve4w(Desc d, RowGeom g, uint32_t* words, const u64* bits, u64 L,
+                                                         DevState* st, const uint32_t* __restrict__ colperm,
+                                                         WalkJobs J) {
+  Quad4 Q;
+  quad_init(Q, d, words, bits, L, g.Wl, g.Wbl);
+  uint32_t hl[MAXH], sl;
+  lane_digits4<MAXH>(d, hl, sl);
+  constexpr int TOPI = MAXH - 1;
+  const int64_t S = (int64_t)Q.S, H0 = (int64_t)d.heap[0], E1 = (int64_t)d.heap[TOPI];
+  int mj = 0;
+  for (int i = 1; i < TOPI; i++) mj += (int)((255u >> d.pshift[i]) & (d.base[i] - 1));
+  const u64 lane_off = 4ull * __lane_id();
+  const XcdRange r = xcd_range((u64)J.IC[J.ng] * 64);
+  for (u64 iu = r.first; iu < r.end; iu += r.stride) {
+    const uint32_t w = __builtin_amdgcn_readfirstlane((uint32_t)(iu >> 6));
+    uint32_t a = 0, b = J.ng;
+    while (b - a > 1) {
+      const uint32_t m = (a + b) >> 1;
+      if (J.IC[m] <= w) a = m;
+      else b = m;
+    }
+    const int64_t gs = (int64_t)J.g0 + a;
+    const int64_t tlo = max((int64_t)0, S - H0 - mj - gs), thi = min(E1, S - gs);
+    const uint32_t ns = (uint32_t)((thi - tlo + kWalkSeg) / kWalkSeg);
+    const uint32_t rr = w - J.IC[a], ci = rr / ns, seg = rr - ci * ns;
+    const u64 k = colperm[J.CS[a] + ci];
+    const int64_t t0 = tlo + (int64_t)seg * kWalkSeg, t1 = min(t0 + kWalkSeg, thi + 1);
+    const u64 qk = k * 256 + lane_off;
+    WalkHist wh;
+    wh.H1 = Q.n1.at((u64)(t0 - 1) * g.Z + qk, t0 >= 1);
+    wh.H2a = Q.n2.at((u64)(t0 - 1) * g.Z + qk, t0 >= 1);
+    wh.H2b = Q.n2.at((u64)(t0 - 2) * g.Z + qk, t0 >= 2);
+    for (int64_t t = t0; t < t1; t++) {
+      const u64 gb = (u64)t * g.Z + k * 256;
+      resolve_quad<MAXH, true>(d, Q, hl, sl, gb + lane_off, gb, lane_off, 0, 256, &wh);
+    }
   }
   quad_done(Q, st);
 }

@@ -849,13 +849,24 @@ static bool dense_scalar_resolve() {
   return v == 1;
 }
 
-// world-1 quad resolve sweep: the level's live-group list (default) or
-// column jobs (GM_DENSE_SWEEP=cols, A/B)
-static bool dense_sweep_cols() {
+// world-1 quad resolve sweep: the level's live-group list (0, default),
+// column jobs (1, GM_DENSE_SWEEP=cols) or column walks (2, =walk)
+static int dense_sweep_mode() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("GM_DENSE_SWEEP");
-    v = (e && !strcmp(e, "cols")) ? 1 : 0;
+    v = !e ? 0 : !strcmp(e, "cols") ? 1 : !strcmp(e, "walk") ? 2 : 0;
+  }
+  return v;
+}
+static bool dense_sweep_cols() { return dense_sweep_mode() == 1; }
+// list sweep: software-pipelined kernel (default) or the plain one
+// (GM_DENSE_PIPE=0, A/B)
+static bool dense_pipelined() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("GM_DENSE_PIPE");
+    v = (e && !strcmp(e, "0")) ? 0 : 1;
   }
   return v == 1;
 }
@@ -887,7 +898,7 @@ static void dense_launch_resolve_t(gm_solver* s, const DenseView& v, int grid, u
       !dense_scalar_resolve()) {
     const uint32_t* gl = nullptr;
     u64 units = (v.p_hi - (v.p_lo & ~255ull) + 3) / 4;
-    if (s->glist && !v.blk && !dense_sweep_cols()) {  // live groups of level L, 64 units each
+    if (s->glist && !v.blk && dense_sweep_mode() == 0) {  // live groups of level L, 64 units each
       gl = s->glist + s->goff[L];
       units = (s->goff[L + 1] - s->goff[L]) * 64;
       if (!units) return;
@@ -906,6 +917,32 @@ static void dense_launch_resolve_t(gm_solver* s, const DenseView& v, int grid, u
       if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
         cus = 256;
       resident = std::max(8, (per_cu * cus) & ~7);
+    }
+    // column walks (world 1, GM_DENSE_SWEEP=walk)
+    if constexpr (MAXH >= 3 && MAXH <= 8) {
+      if (s->colperm && !v.blk && dense_sweep_mode() == 2 && s->cg.maxgs + 1 <= kMaxWalkG) {
+        WalkJobs J;
+        J.g0 = 0;
+        J.ng = (uint32_t)s->cg.maxgs + 1;
+        J.IC[0] = 0;
+        const int64_t S = (int64_t)s->d.root_sum - (int64_t)L, H0 = s->d.heap[0];
+        const int64_t E1 = s->d.heap[s->cg.top];
+        for (uint32_t i = 0; i < J.ng; i++) {
+          const int64_t gs = i;
+          const int64_t tlo = std::max<int64_t>(0, S - H0 - s->cg.mj - gs), thi = std::min<int64_t>(E1, S - gs);
+          const u64 cnt = s->cstart[i + 1] - s->cstart[i];
+          const u64 ns = thi >= tlo ? (u64)((thi - tlo + kWalkSeg) / kWalkSeg) : 0;
+          J.IC[i + 1] = J.IC[i] + (uint32_t)(cnt * ns);
+          J.CS[i] = s->cstart[i];
+        }
+        if (!J.IC[J.ng]) return;
+        const u64 cu = (u64)J.IC[J.ng] * 64;
+        const int gc = (int)std::min<u64>(((cu + kBlock - 1) / kBlock + 7) & ~7ull, (u64)resident);
+        const RowGeom rg{v.Wl, v.Wbl, s->d.pstride[s->cg.top]};
+        hipLaunchKernelGGL((k_dense_resolve4w<MAXH>), dim3(gc), dim3(kBlock), 0, s->stream, s->d, rg, s->words,
+                           s->bits, L, s->st, s->colperm, J);
+        return;
+      }
     }
     // column jobs: a shard's listed slices (or, with GM_DENSE_SWEEP=cols,
     // every top value of a single table), each with its live columns
@@ -944,8 +981,26 @@ static void dense_launch_resolve_t(gm_solver* s, const DenseView& v, int grid, u
     if (gl) {
       XcdShares xs;
       for (int x = 0; x < 9; x++) xs.o[x] = s->gxcd[(size_t)L * 9 + x];
-      hipLaunchKernelGGL((k_dense_resolve4<MAXH, false>), dim3(g), dim3(kBlock), 0, s->stream, s->d, v, s->words,
-                         s->bits, L, s->st, gl, xs);
+      if (dense_pipelined()) {
+        static int rp = 0;  // resident blocks of the pipelined kernel
+        if (!rp) {
+          int per_cu = 0, dev = 0, cus = 0;
+          if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_dense_resolve4p<MAXH>, kBlock, 0) !=
+                  hipSuccess ||
+              per_cu < 1)
+            per_cu = 2;
+          (void)hipGetDevice(&dev);
+          if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+            cus = 256;
+          rp = std::max(8, (per_cu * cus) & ~7);
+        }
+        const int gp = (int)std::min<u64>(((units + kBlock - 1) / kBlock + 7) & ~7ull, (u64)rp);
+        hipLaunchKernelGGL((k_dense_resolve4p<MAXH>), dim3(gp), dim3(kBlock), 0, s->stream, s->d, v, s->words,
+                           s->bits, L, s->st, gl, xs);
+      } else {
+        hipLaunchKernelGGL((k_dense_resolve4<MAXH, false>), dim3(g), dim3(kBlock), 0, s->stream, s->d, v, s->words,
+                           s->bits, L, s->st, gl, xs);
+      }
     }
     else if (v.blk)
       hipLaunchKernelGGL((k_dense_resolve4<MAXH, true>), dim3(g), dim3(kBlock), 0, s->stream, s->d, v, s->words,
