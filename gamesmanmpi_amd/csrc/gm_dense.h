@@ -216,7 +216,8 @@ __device__ __forceinline__ u64 bits64_at(const u64* bits, u64 pos) {
 
 template <int MAXH>
 __global__ __launch_bounds__(256) void k_dense_pull_words(Desc d, DenseView v, u64* bits, u64 L, u64 root_p,
-                                                          const u64* __restrict__ masks) {
+                                                          const u64* __restrict__ masks,
+                                                          const uint32_t* __restrict__ glist, u64 gwords) {
   // mask tables (built once on the host at solver creation, gm_solver.hip
   // build_mask_tables): M[0..63] = TS, M[64 (i + 1) + t] = TD[i][t]
   __shared__ u64 M[64 * (MAXH + 1)];
@@ -226,10 +227,14 @@ __global__ __launch_bounds__(256) void k_dense_pull_words(Desc d, DenseView v, u
 #define TD(i) (M + 64 * ((i) + 1))
   const int S = (int)(d.root_sum - (uint32_t)L);
   const int H0 = (int)d.heap[0];
-  const u64 ngroups = (v.p_hi - v.p_lo + 63) >> 6;
+  // one thread per 64-prefix bitmap word of the band, or of the level's
+  // live 256-prefix groups (glist, world 1: words of groups without a
+  // non-hole are never read unmasked, so they are not written)
+  const u64 ngroups = glist ? gwords : (v.p_hi - v.p_lo + 63) >> 6;
   const u64 stride = (u64)gridDim.x * blockDim.x;
   for (u64 gi = (u64)blockIdx.x * blockDim.x + threadIdx.x; gi < ngroups; gi += stride) {
-    const u64 qi = v.p_lo + (gi << 6);  // sweep index of lane-bit 0
+    const u64 qi = glist ? ((u64)glist[gi >> 2] << 8) + ((gi & 3) << 6)
+                         : v.p_lo + (gi << 6);  // sweep index of lane-bit 0
     uint64_t q;  // local prefix of lane-bit 0 (multiple of 64)
     bool run;
     const u64 pg = dense_sweep(v, qi, &q, &run);  // global prefix of lane-bit 0
@@ -794,8 +799,10 @@ __global__ __launch_bounds__(256) void k_dense_resolve4c(Desc d, RowGeom g, uint
   uint32_t hl[MAXH], sl;
   lane_digits4<MAXH>(d, hl, sl);
   const XcdRange r = xcd_range((u64)J.cum[J.n] * 64);
-  for (u64 iu = r.first; iu < r.end; iu += r.stride) {
-    const uint32_t w = __builtin_amdgcn_readfirstlane((uint32_t)(iu >> 6));  // group of the concatenation
+  // software-pipelined like k_dense_resolve4p
+  auto issue = [&](u64 iu, QuadLoads<MAXH>& X) {
+    const bool on = iu < r.end;
+    const uint32_t w = __builtin_amdgcn_readfirstlane((uint32_t)((on ? iu : r.first) >> 6));
     uint32_t a = 0, b = J.n;  // slice i: cum[i] <= w < cum[i + 1]
     while (b - a > 1) {
       const uint32_t m = (a + b) >> 1;
@@ -804,8 +811,18 @@ __global__ __launch_bounds__(256) void k_dense_resolve4c(Desc d, RowGeom g, uint
     }
     const u64 k = colperm[J.lo[a] + (w - J.cum[a])];
     const u64 qw = (u64)J.u[a] * g.Z + k * 256, pw = (u64)J.t[a] * g.Z + k * 256;
-    const u64 off = 4 * (iu & 63);
-    resolve_quad<MAXH>(d, Q, hl, sl, qw + off, pw, off, 0, 256);
+    quad_issue<MAXH>(d, Q, hl, sl, qw + 4 * (iu & 63), pw, on, X);
+  };
+  if (r.first < r.end) {
+    QuadLoads<MAXH> X0, X1;
+    issue(r.first, X0);
+    for (u64 iu = r.first; iu < r.end; iu += 2 * r.stride) {
+      issue(iu + r.stride, X1);
+      quad_finish<MAXH>(Q, X0);
+      if (iu + r.stride >= r.end) break;
+      issue(iu + 2 * r.stride, X0);
+      quad_finish<MAXH>(Q, X1);
+    }
   }
   quad_done(Q, st);
 }

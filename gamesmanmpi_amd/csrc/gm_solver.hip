@@ -42,6 +42,8 @@
 #include <mutex>
 #include <string>
 #include <vector>
+#include <map>
+#include <mutex>
 
 #include "../../include/gamesman.h"
 #include "gm_codec.h"
@@ -849,6 +851,25 @@ static bool dense_scalar_resolve() {
   return v == 1;
 }
 
+// Blocks of 256 threads of `kernel` that fit on the device at once (a
+// multiple of 8, one share per XCD): list sweeps launch exactly that many,
+// since blocks that start late would sweep their grid-stride items out of
+// order.  Cached per kernel.
+static int resident_blocks(const void* kernel) {
+  static std::mutex mu;
+  static std::map<const void*, int> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(kernel);
+  if (it != cache.end()) return it->second;
+  int per_cu = 0, dev = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0) != hipSuccess || per_cu < 1) per_cu = 2;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+  const int r = std::max(8, (per_cu * cus) & ~7);
+  cache[kernel] = r;
+  return r;
+}
+
 // world-1 quad resolve sweep: the level's live-group list (0, default),
 // column jobs (1, GM_DENSE_SWEEP=cols) or column walks (2, =walk)
 static int dense_sweep_mode() {
@@ -874,10 +895,16 @@ static bool dense_pipelined() {
 template <int MAXH, bool POW2>
 static void dense_launch_pull_t(gm_solver* s, const DenseView& v, int grid, u64 L, u64 root_p) {
   if (POW2 && !dense_per_lane_pull()) {  // word-parallel form: one thread per 64-prefix group
-    const u64 groups = (v.p_hi - v.p_lo + 63) / 64;
+    const uint32_t* gl = nullptr;
+    u64 groups = (v.p_hi - v.p_lo + 63) / 64;
+    if (s->glist && !v.blk && !getenv("GM_PULL_BAND")) {  // the level's live 256-prefix groups
+      gl = s->glist + s->goff[L];
+      groups = (s->goff[L + 1] - s->goff[L]) * 4;
+      if (!groups) return;
+    }
     const int g = (int)std::min<u64>((groups + kBlock - 1) / kBlock, (u64)s->grid);
     hipLaunchKernelGGL((k_dense_pull_words<MAXH>), dim3(g), dim3(kBlock), 0, s->stream, s->d, v, s->bits, L,
-                       root_p, s->masks);
+                       root_p, s->masks, gl, groups);
     return;
   }
   hipLaunchKernelGGL((k_dense_pull<MAXH, POW2>), dim3(grid), dim3(kBlock), 0, s->stream, s->d, v, s->bits, L,
@@ -906,18 +933,7 @@ static void dense_launch_resolve_t(gm_solver* s, const DenseView& v, int grid, u
     // a grid of exactly the blocks that fit at once (a multiple of 8):
     // blocks that start late would sweep their grid-stride items out of the
     // list order the L2 reuse relies on
-    static int resident = 0;
-    if (!resident) {
-      int per_cu = 0, dev = 0, cus = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_dense_resolve4<MAXH, false>, kBlock,
-                                                       0) != hipSuccess ||
-          per_cu < 1)
-        per_cu = 4;
-      (void)hipGetDevice(&dev);
-      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-        cus = 256;
-      resident = std::max(8, (per_cu * cus) & ~7);
-    }
+    const int resident = resident_blocks((const void*)k_dense_resolve4<MAXH, false>);
     // column walks (world 1, GM_DENSE_SWEEP=walk)
     if constexpr (MAXH >= 3 && MAXH <= 8) {
       if (s->colperm && !v.blk && dense_sweep_mode() == 2 && s->cg.maxgs + 1 <= kMaxWalkG) {
@@ -970,7 +986,8 @@ static void dense_launch_resolve_t(gm_solver* s, const DenseView& v, int grid, u
         }
         if (!J.n) return;
         const u64 cu = (u64)J.cum[J.n] * 64;
-        const int gc = (int)std::min<u64>(((cu + kBlock - 1) / kBlock + 7) & ~7ull, (u64)resident);
+        const int gc = (int)std::min<u64>(((cu + kBlock - 1) / kBlock + 7) & ~7ull,
+                                          (u64)resident_blocks((const void*)k_dense_resolve4c<MAXH>));
         const RowGeom rg{v.Wl, v.Wbl, v.blk ? v.Z : s->d.pstride[s->cg.top]};
         hipLaunchKernelGGL((k_dense_resolve4c<MAXH>), dim3(gc), dim3(kBlock), 0, s->stream, s->d, rg, s->words,
                            s->bits, L, s->st, s->colperm, J);
@@ -982,18 +999,7 @@ static void dense_launch_resolve_t(gm_solver* s, const DenseView& v, int grid, u
       XcdShares xs;
       for (int x = 0; x < 9; x++) xs.o[x] = s->gxcd[(size_t)L * 9 + x];
       if (dense_pipelined()) {
-        static int rp = 0;  // resident blocks of the pipelined kernel
-        if (!rp) {
-          int per_cu = 0, dev = 0, cus = 0;
-          if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_dense_resolve4p<MAXH>, kBlock, 0) !=
-                  hipSuccess ||
-              per_cu < 1)
-            per_cu = 2;
-          (void)hipGetDevice(&dev);
-          if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-            cus = 256;
-          rp = std::max(8, (per_cu * cus) & ~7);
-        }
+        const int rp = resident_blocks((const void*)k_dense_resolve4p<MAXH>);
         const int gp = (int)std::min<u64>(((units + kBlock - 1) / kBlock + 7) & ~7ull, (u64)rp);
         hipLaunchKernelGGL((k_dense_resolve4p<MAXH>), dim3(gp), dim3(kBlock), 0, s->stream, s->d, v, s->words,
                            s->bits, L, s->st, gl, xs);
