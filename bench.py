@@ -91,11 +91,19 @@ def pmc_traffic(kernel, workload):
 
 def dense_resolve_kernel():
     """Name of the dense resolve kernel the library launches for the bench
-    shape (power-of-two heaps, base >= 4): the four-prefixes-per-lane form
-    unless GM_DENSE_RESOLVE=scalar selects the one-prefix form (A/B)."""
+    shape (power-of-two heaps, base >= 4): the software-pipelined
+    four-prefixes-per-lane form over the live-group lists, unless the A/B
+    knobs (GM_DENSE_RESOLVE / GM_DENSE_SWEEP / GM_DENSE_PIPE) select another."""
     if os.environ.get("GM_DENSE_RESOLVE") == "scalar":
         return "k_dense_resolve"
-    return "k_dense_resolve4"
+    sweep = os.environ.get("GM_DENSE_SWEEP", "list")
+    if sweep == "cols":
+        return "k_dense_resolve4c"
+    if sweep == "walk":
+        return "k_dense_resolve4w"
+    if os.environ.get("GM_DENSE_PIPE") == "0":
+        return "k_dense_resolve4"
+    return "k_dense_resolve4p"
 
 
 def model_8d_bytes(positions, edges):

@@ -1,2 +1,4 @@
 set -o pipefail
-bash tools/gpu_session.sh r01s4 && bash tools/pmc_passes.sh gpurun_out/pmc_r01s4
+# PMC passes first (they feed profiles/pmc_traffic.json), then the session
+bash tools/pmc_passes.sh gpurun_out/pmc_art || exit 1
+bash tools/gpu_session.sh art || exit 1

@@ -66,6 +66,22 @@ __global__ void triad_b128(const uint4* __restrict__ a, const uint4* __restrict_
   }
 }
 
+// Reuse at large strides (the dense resolve's top-digit children): a sweep
+// reads every quad at i, i - o1, i - o2, so each line is requested three
+// times, o1 / o2 quads apart in time.  With L2 reuse the misses stay near one
+// per line.  Power-of-two strides against padded ones tests channel / set
+// aliasing.  n = quads swept.
+__global__ void reuse3(const uint4* __restrict__ a, size_t n, size_t o1, size_t o2, uint32_t* out) {
+  uint32_t acc = 0;
+  const size_t G = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += G) {
+    const size_t j = i + o2;
+    const uint4 x = a[j], y = a[j - o1], z = a[j - o2];
+    acc ^= x.x ^ y.y ^ z.z;
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
 int main() {
   const size_t bytes = (size_t)1 << 30;
   void* buf = nullptr;
@@ -100,6 +116,26 @@ int main() {
     CHK(hipEventSynchronize(e1));
     CHK(hipEventElapsedTime(&ms_triad, e0, e1));
   }
+  // reuse3: pow2 vs padded strides (quads; 2^18 quads = 4 MB)
+  float ms_pow2 = 0, ms_pad = 0;
+  {
+    const size_t n = ((size_t)1 << 30) / 16 - ((size_t)1 << 20);
+    for (int rep = 0; rep < 3; rep++) {
+      CHK(hipEventRecord(e0, 0));
+      hipLaunchKernelGGL(reuse3, dim3(grid), dim3(block), 0, 0, (const uint4*)buf, n, (size_t)1 << 18,
+                         (size_t)1 << 19, out);
+      CHK(hipEventRecord(e1, 0));
+      CHK(hipEventSynchronize(e1));
+      CHK(hipEventElapsedTime(&ms_pow2, e0, e1));
+      CHK(hipEventRecord(e0, 0));
+      hipLaunchKernelGGL(reuse3, dim3(grid), dim3(block), 0, 0, (const uint4*)buf, n, ((size_t)1 << 18) + 40,
+                         ((size_t)1 << 19) + 88, out);
+      CHK(hipEventRecord(e1, 0));
+      CHK(hipEventSynchronize(e1));
+      CHK(hipEventElapsedTime(&ms_pad, e0, e1));
+    }
+  }
+  printf("{\"reuse3_pow2_ms\": %.4f, \"reuse3_pad_ms\": %.4f}\n", ms_pow2, ms_pad);
   printf("{\"bytes_per_kernel\": %zu, \"half_lines_ms\": %.4f, \"half_lines_requested_GBps\": %.1f, "
          "\"triad_ms\": %.4f, \"triad_GBps\": %.1f}\n",
          bytes, ms_half, bytes / 2 / ms_half / 1e6, ms_triad, (double)(bytes / 3 / 16 * 16 * 3) / ms_triad / 1e6);
