@@ -843,12 +843,8 @@ static bool dense_per_lane_pull() {
 // resolve: four prefixes per lane (k_dense_resolve4) unless
 // GM_DENSE_RESOLVE=scalar (A/B runs)
 static bool dense_scalar_resolve() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("GM_DENSE_RESOLVE");
-    v = (e && !strcmp(e, "scalar")) ? 1 : 0;
-  }
-  return v == 1;
+  const char* e = getenv("GM_DENSE_RESOLVE");  // read per launch: tests switch it in-process
+  return e && !strcmp(e, "scalar");
 }
 
 // Blocks of 256 threads of `kernel` that fit on the device at once (a
@@ -873,23 +869,15 @@ static int resident_blocks(const void* kernel) {
 // world-1 quad resolve sweep: the level's live-group list (0, default),
 // column jobs (1, GM_DENSE_SWEEP=cols) or column walks (2, =walk)
 static int dense_sweep_mode() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("GM_DENSE_SWEEP");
-    v = !e ? 0 : !strcmp(e, "cols") ? 1 : !strcmp(e, "walk") ? 2 : 0;
-  }
-  return v;
+  const char* e = getenv("GM_DENSE_SWEEP");
+  return !e ? 0 : !strcmp(e, "cols") ? 1 : !strcmp(e, "walk") ? 2 : 0;
 }
 static bool dense_sweep_cols() { return dense_sweep_mode() == 1; }
 // list sweep: software-pipelined kernel (default) or the plain one
 // (GM_DENSE_PIPE=0, A/B)
 static bool dense_pipelined() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("GM_DENSE_PIPE");
-    v = (e && !strcmp(e, "0")) ? 0 : 1;
-  }
-  return v == 1;
+  const char* e = getenv("GM_DENSE_PIPE");
+  return !(e && !strcmp(e, "0"));
 }
 
 template <int MAXH, bool POW2>

@@ -1,0 +1,95 @@
+"""GPU parity of every dense resolve variant: the A/B knobs
+select other kernels / sweep orders for the same solve, and each must give
+the same words as the default path, the closed-form counts and the
+Sprague-Grundy values.  Shapes exercise the quad kernels' paths: live-group
+lists with top-major XCD shares (C >= 8 columns), column jobs, column walks,
+the unpipelined and the one-prefix kernels, and shard halos in 16 and 32
+bits."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+WORLD1 = [
+    {},
+    {"GM_DENSE_PIPE": "0"},
+    {"GM_DENSE_SWEEP": "cols"},
+    {"GM_DENSE_SWEEP": "walk"},
+    {"GM_DENSE_RESOLVE": "scalar"},
+    {"GM_PULL_BAND": "1"},
+    {"GM_GROUP_TILE": "-1"},
+    {"GM_GROUP_TILE": "4"},
+]
+
+
+def _expected(heaps):
+    P = 1
+    for h in heaps:
+        P *= h + 1
+    E = sum(P * (2 * h - 1) // (h + 1) for h in heaps if h >= 1)
+    g = 0
+    for h in heaps:
+        g ^= h % 3
+    return P, E, "LOSS" if g == 0 else "WIN"
+
+
+def _solve(params, monkeypatch, env):
+    from gamesmanmpi_amd.games import GameSpec
+    from gamesmanmpi_amd.solver import Solver
+    for k in ("GM_DENSE_PIPE", "GM_DENSE_SWEEP", "GM_DENSE_RESOLVE", "GM_PULL_BAND", "GM_GROUP_TILE"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    s = Solver(GameSpec("sum_four_to_one", params), layout="dense")
+    r = s.solve()
+    keys, val, rem = s.dump()
+    order = np.argsort(keys)
+    return r, keys[order], val[order], rem[order]
+
+
+@pytest.mark.parametrize("params", ["heaps=15:15:15:15:7", "heaps=31:7:31:15"])
+def test_world1_variants_agree(params, monkeypatch):
+    heaps = [int(h) for h in params.split("=")[1].split(":")]
+    P, E, root = _expected(heaps)
+    base = None
+    for env in WORLD1:
+        r, keys, val, rem = _solve(params, monkeypatch, env)
+        assert (r.positions, r.edges, r.root_line.split()[0]) == (P, E, root), env
+        if base is None:
+            base = (keys, val, rem)
+            # Sprague-Grundy: LOSS iff the XOR of (heap mod 3) is 0
+            k = keys.astype(np.int64)
+            g = np.zeros(len(k), np.int64)
+            for h in heaps:
+                g ^= (k % (h + 1)) % 3
+                k //= h + 1
+            np.testing.assert_array_equal(val == 1, g == 0)
+            continue
+        np.testing.assert_array_equal(keys, base[0], err_msg=str(env))
+        np.testing.assert_array_equal(val, base[1], err_msg=str(env))
+        np.testing.assert_array_equal(rem, base[2], err_msg=str(env))
+
+
+@pytest.mark.parametrize("halo32", [False, True])
+def test_shard_halo_word_widths(halo32, monkeypatch):
+    """Column-order halos (Z % 256 == 0) in 16- and 32-bit words."""
+    from gamesmanmpi_amd.dist import group_solve
+    from gamesmanmpi_amd.games import GameSpec
+    from gamesmanmpi_amd.solver import Solver
+    params = "heaps=15:15:15:15:31"  # Z = 16^3 = 4096 prefixes (16 columns) per slice
+    if halo32:
+        monkeypatch.setenv("GM_HALO32", "1")
+    else:
+        monkeypatch.delenv("GM_HALO32", raising=False)
+    s1 = Solver(GameSpec("sum_four_to_one", params), layout="dense")
+    r1 = s1.solve()
+    rg, shards = group_solve(GameSpec("sum_four_to_one", params), 2)
+    assert (rg.positions, rg.edges, rg.root_line) == (r1.positions, r1.edges, r1.root_line)
+    keys, val, rem = s1.dump()
+    out = np.full(len(keys), 0xFFFFFFFF, np.uint32)
+    for s in shards:
+        w = s.query(keys)
+        own = w != 0xFFFFFFFF
+        out[own] = w[own]
+    np.testing.assert_array_equal(out & 3, val)
+    np.testing.assert_array_equal(out >> 2, rem)
