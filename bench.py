@@ -59,17 +59,20 @@ def expected(heaps):
     return P, E, ("LOSS" if g == 0 else "WIN")
 
 
-def algorithmic_bytes(positions, edges, layout):
+def algorithmic_bytes(positions, edges, layout, word_bytes=4):
     """Bytes each kernel family must move, per DESIGN.md §Roofline.
     hashed (SURVEY §8d keyed model): expand 24 B/position + 8 B/edge,
       resolve 12 B/position + 12 B/edge (8-B keys, 4-B value words).
     dense (level-major perfect hash, key implicit in the slot):
       pull: one reach bit per parent link + one written bit per position
             = (edges + positions) / 8 B (parent links = edges);
-      resolve: own reach bit + 4-B word written per position, one 4-B child
-            word per edge = 4.125 B/position + 4 B/edge."""
+      resolve: own reach bit + one word written per position, one child
+            word per edge = 4.125 B/position + 4 B/edge with 32-bit words,
+            2.125 B/position + 2 B/edge with the 16-bit table (word_bytes 2,
+            DESIGN.md §3: K_SUM remoteness < 2^15)."""
     if layout == "dense":
-        return (edges + positions) / 8.0, 4.125 * positions + 4 * edges
+        return ((edges + positions) / 8.0,
+                (word_bytes + 0.125) * positions + word_bytes * edges)
     return 24 * positions + 8 * edges, 12 * positions + 12 * edges
 
 
@@ -89,11 +92,15 @@ def pmc_traffic(kernel, workload):
     return row["bytes_per_launch"], "profiles/pmc_traffic.json (%s)" % row.get("source", "?")
 
 
-def dense_resolve_kernel():
+def dense_resolve_kernel(word_bits):
     """Name of the dense resolve kernel the library launches for the bench
-    shape (power-of-two heaps, base >= 4): the software-pipelined
-    four-prefixes-per-lane form over the live-group lists, unless the A/B
-    knobs (GM_DENSE_RESOLVE / GM_DENSE_SWEEP / GM_DENSE_PIPE) select another."""
+    shape (power-of-two heaps, base >= 8): over the live-group lists, the
+    software-pipelined eight-prefixes-per-lane form on the 16-bit table (the
+    solve reports word_bits 16), else the four-prefixes-per-lane form, unless
+    the A/B knobs (GM_DENSE_RESOLVE / GM_DENSE_SWEEP / GM_DENSE_PIPE) select
+    another."""
+    if word_bits == 16:
+        return "k_dense_resolve8p"
     if os.environ.get("GM_DENSE_RESOLVE") == "scalar":
         return "k_dense_resolve"
     sweep = os.environ.get("GM_DENSE_SWEEP", "list")
@@ -198,9 +205,10 @@ def main():
         tr_pos, tr_edges = tr.positions // world, tr.edges // world  # per GPU
     else:
         tr_pos, tr_edges = tr.positions, tr.edges
-    fwd_b, bwd_b = algorithmic_bytes(tr_pos, tr_edges, layout)
+    word_bits = tr.extra.get("word_bits", 32) or 32
+    fwd_b, bwd_b = algorithmic_bytes(tr_pos, tr_edges, layout, word_bits // 8)
     if tr.ms_resolve_kernels >= tr.ms_expand_kernels:
-        kname, kb, kms, kn = (dense_resolve_kernel() if layout == "dense"
+        kname, kb, kms, kn = (dense_resolve_kernel(word_bits) if layout == "dense"
                               else "k_resolve", bwd_b, tr.ms_resolve_kernels,
                               tr.n_resolve_launches)
     else:
@@ -221,7 +229,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u64 keys / u32 words (integer)",
+        "dtype": "u64 keys / u%d words (integer)" % word_bits,
         "data": "synthetic: sum of Four-To-One heaps, fully determined state space",
         "config": {"workload": workload,
                    "positions_per_gpu": r.positions // world, "edges_per_gpu": r.edges // world,
@@ -235,7 +243,8 @@ def main():
                      "traffic_unit": "HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE)",
                      "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": kb / kn,
-                     "model": ("dense: resolve 4.125 B/position + 4 B/edge, pull (edges + positions)/8 B"
+                     "model": ("dense: resolve %.3f B/position + %d B/edge (%d-bit words), pull (edges + positions)/8 B"
+                               % (word_bits / 8 + 0.125, word_bits // 8, word_bits)
                                if layout == "dense" else
                                "SURVEY 8d keyed: expand 24 B/position + 8 B/edge, resolve 12 B/position + 12 B/edge"),
                      "launches": kn, "ms_kernel_total": kms,

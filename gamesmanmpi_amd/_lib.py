@@ -68,7 +68,9 @@ class gm_result(ctypes.Structure):
                 ("ms_expand_kernels", ctypes.c_double),
                 ("ms_resolve_kernels", ctypes.c_double),
                 ("n_expand_launches", ctypes.c_uint64),
-                ("n_resolve_launches", ctypes.c_uint64)]
+                ("n_resolve_launches", ctypes.c_uint64),
+                ("word_bits", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
 
 
 # every symbol include/gamesman.h declares (tests check the exports)

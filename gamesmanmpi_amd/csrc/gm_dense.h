@@ -771,6 +771,171 @@ __global__ __launch_bounds__(256) void k_dense_resolve4p(Desc d, DenseView v, ui
   quad_done(Q, st);
 }
 
+// ---------------------------------------------------------------------------
+// 16-bit tables (world 1, k_dense_resolve8p).  K_SUM remoteness never exceeds
+// root_sum, so below 2^15 the order form fits 16 bits: WIN r -> r, LOSS r ->
+// 0x8000 | (0x7FFF - r) -- the same ordering, so the unsigned max over the
+// children is still the whole reduction, and an absent child (0) is still
+// neutral.  Half the bytes per child stream, and a 16-B load now carries
+// EIGHT consecutive prefixes: a lane owns an octet (the eight share every
+// digit but the lowest, base[1] >= 8), a wave two 256-prefix groups of the
+// level's live-group list, so each group costs half the memory instructions
+// of the quad form.  Converted to value | remoteness << 2 at the root and in
+// queries (dense_word16).  Octet stores are whole 16-B stores: the hole
+// slots they overwrite are never read unmasked (heap-0/1 children of a
+// valid parent are masked when they would be holes; heap >= 2 children of a
+// valid parent are never holes).
+// ---------------------------------------------------------------------------
+typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
+constexpr uint32_t W16_UNREACHED = 0xFFFFu;
+constexpr uint32_t DENSE_PRIMITIVE16 = 0xFFFFu;  // LOSS, remoteness 0
+__device__ __forceinline__ uint32_t dense_parent16(uint32_t m) {
+  return (m & 0x8000u) ? (0x7FFFu - (m & 0x7FFFu)) + 1u : 0x8000u | (0x7FFFu - (m + 1u));
+}
+__host__ __device__ __forceinline__ uint32_t dense_word16(uint32_t h) {
+  return dense_word((h & 0x8000u) ? (0xFFFF8000u | h) : h);
+}
+struct WordRow8 {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ __forceinline__ void init(const uint16_t* base, u64 nwords) {
+    r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(uint32_t)(nwords * 2u), 0x00020000);
+  }
+  // words [idx, idx + 8), idx 8-aligned; !ok reads zeros with no memory access
+  __device__ __forceinline__ u16x8 at(u64 idx, bool ok) const {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, ok ? (uint32_t)idx * 2u : 0xFFFFFFF0u, 0, 0);
+    return __builtin_bit_cast(u16x8, v);
+  }
+};
+struct Oct8 {
+  WordRow8 n1, n2;  // levels L+1, L+2 (empty rows past the last level)
+  uint16_t* mine;
+  const u64* bits;
+  u64 Lb;  // L * Wbl
+  uint32_t S, H0;
+  uint32_t npos = 0, edges = 0;
+};
+template <int MAXH>
+struct OctLoads {
+  u16x8 A1, A2, P1, P2, C1[MAXH], C2[MAXH];
+  u64 bitsw;
+  u64 q;
+  uint32_t h1, s, valid, nch_hi;
+};
+__device__ __forceinline__ void oct_init(Oct8& Q, const Desc& d, uint16_t* words, const u64* bits, u64 L, u64 Wl,
+                                         u64 Wbl) {
+  Q.S = d.root_sum - (uint32_t)L;
+  Q.H0 = d.heap[0];
+  Q.mine = words + L * Wl;
+  Q.n1.init(words + (L + 1) * Wl, Q.S >= 1 ? Wl : 0);
+  Q.n2.init(words + (L + 2) * Wl, Q.S >= 2 ? Wl : 0);
+  Q.bits = bits;
+  Q.Lb = L * Wbl;
+}
+// digits of the lane's prefix q (8-aligned; world 1: local = global) and
+// every load of its octet
+template <int MAXH>
+__device__ __forceinline__ void oct_issue(const Desc& d, const Oct8& Q, u64 q, bool on, OctLoads<MAXH>& X) {
+  const uint32_t S = Q.S;
+  uint32_t h[MAXH];
+  uint32_t s = 0;
+#pragma unroll
+  for (int i = 1; i < MAXH; i++) {
+    h[i] = ((MAXH <= 8) || i < d.nheaps) ? (uint32_t)((q >> d.pshift[i]) & (d.base[i] - 1)) : 0u;
+    s += h[i];
+  }
+  uint32_t valid = 0;
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const uint32_t se = s + e;
+    valid |= (uint32_t)(on && se <= S && S - se <= Q.H0) << e;
+  }
+  X.q = q;
+  X.h1 = h[1];
+  X.s = s;
+  X.valid = valid;
+  uint32_t nch_hi = 0;
+#pragma unroll
+  for (int i = 2; i < MAXH; i++) nch_hi += ((MAXH <= 8) || i < d.nheaps) ? min(h[i], 2u) : 0u;
+  X.nch_hi = nch_hi;
+  const bool any = valid != 0;
+  X.bitsw = any ? Q.bits[(Q.Lb + q) >> 6] : 0ull;
+  X.A1 = Q.n1.at(q, any);
+  X.A2 = Q.n2.at(q, any);
+  X.P1 = Q.n1.at(q - 8, any && q >= 8);
+  X.P2 = Q.n2.at(q - 8, any && q >= 8);
+#pragma unroll
+  for (int i = 2; i < MAXH; i++) {
+    const bool live = (MAXH <= 8) || i < d.nheaps;
+    X.C1[i] = Q.n1.at(q - d.pstride[i], any && live && h[i] >= 1);
+    X.C2[i] = Q.n2.at(q - 2 * d.pstride[i], any && live && h[i] >= 2);
+  }
+}
+template <int MAXH>
+__device__ __forceinline__ void oct_finish(Oct8& Q, const OctLoads<MAXH>& X) {
+  const uint32_t valid = X.valid;
+  if (!valid) return;
+  const uint32_t S = Q.S;
+  const uint32_t rbits = (uint32_t)(X.bitsw >> ((Q.Lb + X.q) & 63)) & 0xFFu;
+  u16x8 mc = {0, 0, 0, 0, 0, 0, 0, 0};  // heaps >= 2: never holes under a valid parent
+#pragma unroll
+  for (int i = 2; i < MAXH; i++) mc = __builtin_elementwise_max(mc, __builtin_elementwise_max(X.C1[i], X.C2[i]));
+  u16x8 o;
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const uint32_t h0 = S - (X.s + e), h1 = X.h1 + e;
+    uint32_t m = max(h0 >= 1 ? (uint32_t)X.A1[e] : 0u, h0 >= 2 ? (uint32_t)X.A2[e] : 0u);
+    m = max(m, max(h1 >= 1 ? (uint32_t)(e >= 1 ? X.A1[e - 1] : X.P1[7]) : 0u,
+                   h1 >= 2 ? (uint32_t)(e >= 2 ? X.A2[e - 2] : X.P2[6 + e]) : 0u));
+    m = max(m, (uint32_t)mc[e]);
+    const uint32_t word = S == 0 ? DENSE_PRIMITIVE16 : dense_parent16(m);
+    const bool reached = (rbits >> e) & 1u;
+    o[e] = (uint16_t)(reached ? word : W16_UNREACHED);
+    if (reached && ((valid >> e) & 1u)) {
+      Q.npos++;
+      Q.edges += min(h0, 2u) + min(h1, 2u) + X.nch_hi;
+    }
+  }
+  *(u16x8*)(Q.mine + X.q) = o;
+}
+// Live-group list sweep over a 16-bit table, software-pipelined like
+// k_dense_resolve4p.  Units of 8 prefixes, 32 per group; the host starts
+// every XCD share at an even list entry, so a wave's 64 units are two whole
+// groups (lanes 0-31 / 32-63), read with two scalar loads.
+template <int MAXH>
+__global__ __launch_bounds__(256) void k_dense_resolve8p(Desc d, DenseView v, uint16_t* words, const u64* bits, u64 L,
+                                                         DevState* st, const uint32_t* __restrict__ glist,
+                                                         XcdShares xs) {
+  Oct8 Q;
+  oct_init(Q, d, words, bits, L, v.Wl, v.Wbl);
+  const uint32_t lane = __lane_id();
+  const uint32_t x = blockIdx.x % kXcds;
+  const u64 first = (u64)xs.o[x] * 32 + (u64)(blockIdx.x / kXcds) * blockDim.x + threadIdx.x;
+  const u64 end = (u64)xs.o[x + 1] * 32, stride = (u64)(gridDim.x / kXcds) * blockDim.x;
+  const uint32_t last = xs.o[8] - 1;  // last entry of the level's list (the host launches only non-empty lists)
+  auto issue = [&](u64 iu, OctLoads<MAXH>& X) {
+    const bool on = iu < end;
+    const uint32_t g0 = min(__builtin_amdgcn_readfirstlane((uint32_t)((iu - lane) >> 5)), last);
+    const uint32_t g1 = min(g0 + 1, last);
+    const uint32_t e0 = glist[g0], e1 = glist[g1];
+    const u64 pg = (u64)(lane < 32 ? e0 : e1) << 8;
+    oct_issue<MAXH>(d, Q, pg + 8 * (lane & 31), on, X);
+  };
+  if (first < end) {
+    OctLoads<MAXH> X0, X1;
+    issue(first, X0);
+    for (u64 iu = first; iu < end; iu += 2 * stride) {
+      issue(iu + stride, X1);
+      oct_finish<MAXH>(Q, X0);
+      if (iu + stride >= end) break;
+      issue(iu + 2 * stride, X0);
+      oct_finish<MAXH>(Q, X1);
+    }
+  }
+  block_add(&st->cursor_front, (u64)Q.npos);
+  block_add(&st->edges, (u64)Q.edges);
+  block_add(&st->prims, Q.S == 0 ? (u64)Q.npos : 0ull);
+}
+
 // Column jobs (shards, and any table whose top digit sits above 256-prefix
 // groups): within a top-digit slice, group k (a "column") holds digit sums
 // gsc[k] + t + [0, mj] at top value t, so the live columns of slice t at
@@ -979,24 +1144,26 @@ __global__ __launch_bounds__(256) void k_halo_cols(Desc d, HaloColJobs J, u64 Z,
 
 // root word (on the shard that owns the root, root_q = its local prefix;
 // others pass ~0 and report NO_WORD)
-__global__ void k_dense_root(DenseView v, const uint32_t* words, const u64* bits, u64 root_q, DevState* st) {
+__global__ void k_dense_root(DenseView v, const uint32_t* words, const u64* bits, u64 root_q, DevState* st, bool w16) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     uint32_t w = NO_WORD;
-    if (root_q != ~0ull && reach_bit(bits, root_q)) w = dense_word(words[root_q]);  // level 0
+    if (root_q != ~0ull && reach_bit(bits, root_q))  // level 0
+      w = w16 ? dense_word16(((const uint16_t*)words)[root_q]) : dense_word(words[root_q]);
     st->root_word = w;
   }
 }
 
 // word of each key this table owns (NO_WORD for unreachable / not owned)
 __global__ void k_dense_query(Desc d, DenseView v, const uint32_t* words, const u64* bits, const u64* keys, u64 n,
-                              uint32_t* out) {
+                              uint32_t* out, bool w16) {
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
     u64 slot, L, p;
     uint32_t w = NO_WORD;
     if (dense_slot_of(d, keys[i], &slot)) {
       slot_split(d, slot, &L, &p);
       uint64_t q;
-      if (dense_local(v, p, &q) && reach_bit(bits, L * v.Wbl + q)) w = dense_word(words[L * v.Wl + q]);
+      if (dense_local(v, p, &q) && reach_bit(bits, L * v.Wbl + q))
+        w = w16 ? dense_word16(((const uint16_t*)words)[L * v.Wl + q]) : dense_word(words[L * v.Wl + q]);
     }
     out[i] = w;
   }

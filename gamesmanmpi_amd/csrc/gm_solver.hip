@@ -769,6 +769,7 @@ struct gm_solver {
   HaloGeom hg;
   HaloTabs ht{};
   bool halo16 = false;  // words travel as 16 bits (k_halo_cols)
+  bool w16 = false;     // this solve's table holds 16-bit order-form words (k_dense_resolve8p)
   uint32_t* halo_send = nullptr;
   uint32_t* halo_recv = nullptr;
   std::vector<uint32_t> halo_tot;
@@ -879,6 +880,8 @@ static bool dense_pipelined() {
   const char* e = getenv("GM_DENSE_PIPE");
   return !(e && !strcmp(e, "0"));
 }
+// any A/B knob that selects a non-default (32-bit word) resolve kernel
+static bool dense_resolve_knob_set() { return dense_scalar_resolve() || dense_sweep_mode() != 0 || !dense_pipelined(); }
 
 template <int MAXH, bool POW2>
 static void dense_launch_pull_t(gm_solver* s, const DenseView& v, int grid, u64 L, u64 root_p) {
@@ -981,6 +984,17 @@ static void dense_launch_resolve_t(gm_solver* s, const DenseView& v, int grid, u
                            s->bits, L, s->st, s->colperm, J);
         return;
       }
+    }
+    if (s->w16) {  // 16-bit table: octets over the live-group list (run_dense chose it for this solve)
+      XcdShares xs;
+      for (int x = 0; x < 9; x++) xs.o[x] = s->gxcd[(size_t)L * 9 + x];
+      for (int x = 1; x < 8; x++) xs.o[x] &= ~1u;  // shares start at even entries: a wave = two whole groups
+      const u64 u8 = (u64)xs.o[8] * 32;
+      const int rp = resident_blocks((const void*)k_dense_resolve8p<MAXH>);
+      const int gp = (int)std::min<u64>(((u8 + kBlock - 1) / kBlock + 7) & ~7ull, (u64)rp);
+      hipLaunchKernelGGL((k_dense_resolve8p<MAXH>), dim3(gp), dim3(kBlock), 0, s->stream, s->d, v,
+                         (uint16_t*)s->words, s->bits, L, s->st, gl, xs);
+      return;
     }
     const int g = (int)std::min<u64>(((units + kBlock - 1) / kBlock + 7) & ~7ull, (u64)resident);
     if (gl) {
@@ -1962,6 +1976,15 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
   }
   const bool timing = s0->flags & GM_F_KERNEL_TIMING;
   hipStream_t st = s0->stream;
+  // 16-bit words (k_dense_resolve8p) for the default world-1 sweep: K_SUM
+  // remoteness <= root_sum < 2^15, octets need base[1] >= 8.  GM_WORDS32=1
+  // keeps 32-bit words (A/B); any other resolve knob selects a 32-bit kernel.
+  for (gm_solver* s : ss) {
+    const char* w32 = getenv("GM_WORDS32");
+    s->w16 = mode == 0 && s->glist && !s->view.blk && d.pow2 && d.kind == K_SUM && d.nheaps >= 2 &&
+             d.nheaps <= 8 && d.base[1] >= 8 && d.root_sum < 0x7FFF && s->view.Wl * 2 <= 0xFFFFFFF0ull &&
+             !dense_resolve_knob_set() && !(w32 && atoi(w32));
+  }
   std::vector<hipEvent_t> ev;
   auto new_event = [&](hipEvent_t* e) -> int {
     HIPCHK(hipEventCreate(e));
@@ -2121,7 +2144,7 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
   for (gm_solver* s : ss) {
     uint64_t root_q = ~0ull;
     if (!dense_local(s->view, root_p, &root_q)) root_q = ~0ull;
-    hipLaunchKernelGGL(k_dense_root, dim3(1), dim3(64), 0, st, s->view, s->words, s->bits, root_q, s->st);
+    hipLaunchKernelGGL(k_dense_root, dim3(1), dim3(64), 0, st, s->view, s->words, s->bits, root_q, s->st, s->w16);
     hipLaunchKernelGGL(k_fill_red, dim3(1), dim3(64), 0, st, s->st);
   }
   if (mode == 1) {
@@ -2163,6 +2186,7 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
   out->primitives = red[2];
   out->levels = (uint32_t)T;
   out->max_level_width = 0;
+  out->word_bits = s0->w16 ? 16u : 32u;
   const uint32_t word = red[3] ? (uint32_t)(red[3] - 1) : NO_WORD;
   out->root_word = word;
   if (red[4]) return fail(GM_ECORRUPT, "solve failed:%s", err_text((uint32_t)red[4]).c_str());
@@ -2189,7 +2213,7 @@ int gm_solver_query(gm_solver* s, const uint64_t* keys_dev, uint64_t n, uint32_t
   int grid = (int)std::min<u64>((n + kBlock - 1) / kBlock, (u64)s->grid);
   if (s->mode == GM_MODE_DENSE)
     hipLaunchKernelGGL(k_dense_query, dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->view, s->words, s->bits,
-                       (const u64*)keys_dev, n, words_dev);
+                       (const u64*)keys_dev, n, words_dev, s->w16);
   else
     hipLaunchKernelGGL(k_query, dim3(grid), dim3(kBlock), 0, s->stream, s->tab, s->mask, (const u64*)keys_dev, n,
                        words_dev);

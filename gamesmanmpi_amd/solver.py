@@ -170,6 +170,7 @@ class Solver:
             n_resolve_launches=r.n_resolve_launches,
             extra={"layout": "dense" if self.plan.mode == _lib.GM_MODE_DENSE
                    else "hashed",
+                   "word_bits": r.word_bits,
                    "table_bytes": self.plan.table_bytes})
 
     # -- reading the table -------------------------------------------------

@@ -12,6 +12,7 @@ pytestmark = pytest.mark.gpu
 
 WORLD1 = [
     {},
+    {"GM_WORDS32": "1"},
     {"GM_DENSE_PIPE": "0"},
     {"GM_DENSE_SWEEP": "cols"},
     {"GM_DENSE_SWEEP": "walk"},
@@ -36,7 +37,8 @@ def _expected(heaps):
 def _solve(params, monkeypatch, env):
     from gamesmanmpi_amd.games import GameSpec
     from gamesmanmpi_amd.solver import Solver
-    for k in ("GM_DENSE_PIPE", "GM_DENSE_SWEEP", "GM_DENSE_RESOLVE", "GM_PULL_BAND", "GM_GROUP_TILE"):
+    for k in ("GM_DENSE_PIPE", "GM_DENSE_SWEEP", "GM_DENSE_RESOLVE", "GM_PULL_BAND", "GM_GROUP_TILE",
+              "GM_WORDS32"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
