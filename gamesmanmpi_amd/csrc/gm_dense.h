@@ -831,16 +831,16 @@ __device__ __forceinline__ void oct_init(Oct8& Q, const Desc& d, uint16_t* words
   Q.bits = bits;
   Q.Lb = L * Wbl;
 }
-// digits of the lane's prefix q (8-aligned; world 1: local = global) and
-// every load of its octet
+// digits of the lane's global prefix pg and every load of its octet at local
+// prefix q (both 8-aligned; world 1: q = pg)
 template <int MAXH>
-__device__ __forceinline__ void oct_issue(const Desc& d, const Oct8& Q, u64 q, bool on, OctLoads<MAXH>& X) {
+__device__ __forceinline__ void oct_issue(const Desc& d, const Oct8& Q, u64 q, u64 pg, bool on, OctLoads<MAXH>& X) {
   const uint32_t S = Q.S;
   uint32_t h[MAXH];
   uint32_t s = 0;
 #pragma unroll
   for (int i = 1; i < MAXH; i++) {
-    h[i] = ((MAXH <= 8) || i < d.nheaps) ? (uint32_t)((q >> d.pshift[i]) & (d.base[i] - 1)) : 0u;
+    h[i] = ((MAXH <= 8) || i < d.nheaps) ? (uint32_t)((pg >> d.pshift[i]) & (d.base[i] - 1)) : 0u;
     s += h[i];
   }
   uint32_t valid = 0;
@@ -917,8 +917,8 @@ __global__ __launch_bounds__(256) void k_dense_resolve8p(Desc d, DenseView v, ui
     const uint32_t g0 = min(__builtin_amdgcn_readfirstlane((uint32_t)((iu - lane) >> 5)), last);
     const uint32_t g1 = min(g0 + 1, last);
     const uint32_t e0 = glist[g0], e1 = glist[g1];
-    const u64 pg = (u64)(lane < 32 ? e0 : e1) << 8;
-    oct_issue<MAXH>(d, Q, pg + 8 * (lane & 31), on, X);
+    const u64 pg = ((u64)(lane < 32 ? e0 : e1) << 8) + 8 * (lane & 31);
+    oct_issue<MAXH>(d, Q, pg, pg, on, X);
   };
   if (first < end) {
     OctLoads<MAXH> X0, X1;
@@ -990,6 +990,56 @@ __global__ __launch_bounds__(256) void k_dense_resolve4c(Desc d, RowGeom g, uint
     }
   }
   quad_done(Q, st);
+}
+
+// Column jobs over a 16-bit table (shards): the octet body of
+// k_dense_resolve8p, a wave = two consecutive columns of the jobs'
+// concatenation (lanes 0-31 / 32-63; each half finds its slice by a scalar
+// search), software-pipelined.
+template <int MAXH>
+__global__ __launch_bounds__(256) void k_dense_resolve8c(Desc d, RowGeom g, uint16_t* words, const u64* bits, u64 L,
+                                                         DevState* st, const uint32_t* __restrict__ colperm,
+                                                         ColJobs J) {
+  Oct8 Q;
+  oct_init(Q, d, words, bits, L, g.Wl, g.Wbl);
+  const uint32_t lane = __lane_id();
+  const uint32_t total = J.cum[J.n];  // columns (host: > 0)
+  const XcdRange r = xcd_range((u64)((total + 1) / 2) * 64);
+  auto find = [&](uint32_t w, u64* q, u64* pg) {  // column w of the concatenation (scalar)
+    uint32_t a = 0, b = J.n;  // slice i: cum[i] <= w < cum[i + 1]
+    while (b - a > 1) {
+      const uint32_t m = (a + b) >> 1;
+      if (J.cum[m] <= w) a = m;
+      else b = m;
+    }
+    const u64 k = colperm[J.lo[a] + (w - J.cum[a])];
+    *q = (u64)J.u[a] * g.Z + k * 256;
+    *pg = (u64)J.t[a] * g.Z + k * 256;
+  };
+  auto issue = [&](u64 iu, OctLoads<MAXH>& X) {
+    const uint32_t c0 = min(__builtin_amdgcn_readfirstlane((uint32_t)((iu - lane) >> 6)) * 2, total - 1);
+    const uint32_t c1 = min(c0 + 1, total - 1);
+    const bool on = iu < r.end && (lane < 32 || c0 + 1 < total);
+    u64 q0, p0, q1, p1;
+    find(c0, &q0, &p0);
+    find(c1, &q1, &p1);
+    const u64 o = 8 * (lane & 31);
+    oct_issue<MAXH>(d, Q, (lane < 32 ? q0 : q1) + o, (lane < 32 ? p0 : p1) + o, on, X);
+  };
+  if (r.first < r.end) {
+    OctLoads<MAXH> X0, X1;
+    issue(r.first, X0);
+    for (u64 iu = r.first; iu < r.end; iu += 2 * r.stride) {
+      issue(iu + r.stride, X1);
+      oct_finish<MAXH>(Q, X0);
+      if (iu + r.stride >= r.end) break;
+      issue(iu + 2 * r.stride, X0);
+      oct_finish<MAXH>(Q, X1);
+    }
+  }
+  block_add(&st->cursor_front, (u64)Q.npos);
+  block_add(&st->edges, (u64)Q.edges);
+  block_add(&st->prims, Q.S == 0 ? (u64)Q.npos : 0ull);
 }
 
 // Column walks (world 1): a wave takes one column k and walks up to
@@ -1078,9 +1128,15 @@ struct HaloTabs {
 __device__ __forceinline__ uint32_t halo16(uint32_t y) { return ((y >> 16) & 0x8000u) | (y & 0x7FFFu); }
 __device__ __forceinline__ uint32_t unhalo16(uint32_t h) { return (h & 0x8000u) ? (0xFFFF8000u | h) : h; }
 
-template <bool PACK, bool W16>
+// T16: the table itself holds 16-bit order forms (k_dense_resolve8c; implies
+// W16), which are already the halo's 16-bit form.
+template <bool PACK, bool W16, bool T16 = false>
 __global__ __launch_bounds__(256) void k_halo_cols(Desc d, HaloColJobs J, u64 Z, const uint32_t* __restrict__ colperm,
-                                                   HaloTabs T, uint32_t* level_words, void* buf) {
+                                                   HaloTabs T, void* level_words_v, void* buf) {
+  static_assert(!T16 || W16, "a 16-bit table travels as 16-bit words");
+  uint32_t* level_words = (uint32_t*)level_words_v;
+  uint16_t* level_words16 = (uint16_t*)level_words_v;
+  typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
   const uint32_t lane = __lane_id();
   uint32_t sl = 0;  // digit sum of the lane's first slot offset 4 * lane (below the top digit)
   for (int i = 1; i < T.top; i++) sl += ((4u * lane) >> d.pshift[i]) & (d.base[i] - 1);
@@ -1116,6 +1172,29 @@ __global__ __launch_bounds__(256) void k_halo_cols(Desc d, HaloColJobs J, u64 Z,
 #pragma unroll
     for (int e = 0; e < 4; e++) before += (uint32_t)__popcll(bl[e] & ltmask);
     const u64 q = (u64)J.u[a] * Z + (u64)k * 256 + 4 * lane;
+    if (T16) {
+      if (!valid) continue;
+      uint32_t rk = before;
+      if (PACK) {
+        const u16x4 v4 = *(const u16x4*)(level_words16 + q);
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          if (!((valid >> e) & 1u)) continue;
+          ((uint16_t*)buf)[base + rk] = v4[e];
+          rk++;
+        }
+      } else {
+        u16x4 v4 = {0, 0, 0, 0};
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          if (!((valid >> e) & 1u)) continue;
+          v4[e] = ((const uint16_t*)buf)[base + rk];
+          rk++;
+        }
+        *(u16x4*)(level_words16 + q) = v4;  // holes of a live lane get 0 (never read unmasked)
+      }
+      continue;
+    }
     if (PACK) {
       if (!valid) continue;
       const u32x4 v4 = *(const u32x4*)(level_words + q);

@@ -976,10 +976,18 @@ static void dense_launch_resolve_t(gm_solver* s, const DenseView& v, int grid, u
           J.n++;
         }
         if (!J.n) return;
+        const RowGeom rg{v.Wl, v.Wbl, v.blk ? v.Z : s->d.pstride[s->cg.top]};
+        if (s->w16) {  // 16-bit shard table: octets, two columns per wave
+          const u64 cu8 = (u64)((J.cum[J.n] + 1) / 2) * 64;
+          const int g8 = (int)std::min<u64>(((cu8 + kBlock - 1) / kBlock + 7) & ~7ull,
+                                            (u64)resident_blocks((const void*)k_dense_resolve8c<MAXH>));
+          hipLaunchKernelGGL((k_dense_resolve8c<MAXH>), dim3(g8), dim3(kBlock), 0, s->stream, s->d, rg,
+                             (uint16_t*)s->words, s->bits, L, s->st, s->colperm, J);
+          return;
+        }
         const u64 cu = (u64)J.cum[J.n] * 64;
         const int gc = (int)std::min<u64>(((cu + kBlock - 1) / kBlock + 7) & ~7ull,
                                           (u64)resident_blocks((const void*)k_dense_resolve4c<MAXH>));
-        const RowGeom rg{v.Wl, v.Wbl, v.blk ? v.Z : s->d.pstride[s->cg.top]};
         hipLaunchKernelGGL((k_dense_resolve4c<MAXH>), dim3(gc), dim3(kBlock), 0, s->stream, s->d, rg, s->words,
                            s->bits, L, s->st, s->colperm, J);
         return;
@@ -1843,7 +1851,14 @@ static u64 halo_move_all(gm_solver* s, u64 L, int pack, uint32_t* buf, hipStream
     const u64 units = (u64)J.cum[J.n] * 64;
     const int grid = (int)std::min<u64>(((units + kBlock - 1) / kBlock + 7) & ~7ull, (u64)s->grid);
     uint32_t* lw = s->words + L * s->view.Wl;
-    if (pack && s->halo16)
+    void* lw16 = (uint16_t*)s->words + L * s->view.Wl;
+    if (s->w16 && pack)
+      hipLaunchKernelGGL((k_halo_cols<true, true, true>), dim3(grid), dim3(kBlock), 0, cs, s->d, J, s->view.Z,
+                         s->colperm, s->ht, lw16, (void*)buf);
+    else if (s->w16)
+      hipLaunchKernelGGL((k_halo_cols<false, true, true>), dim3(grid), dim3(kBlock), 0, cs, s->d, J, s->view.Z,
+                         s->colperm, s->ht, lw16, (void*)buf);
+    else if (pack && s->halo16)
       hipLaunchKernelGGL((k_halo_cols<true, true>), dim3(grid), dim3(kBlock), 0, cs, s->d, J, s->view.Z, s->colperm,
                          s->ht, lw, (void*)buf);
     else if (pack)
@@ -1979,11 +1994,18 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
   // 16-bit words (k_dense_resolve8p) for the default world-1 sweep: K_SUM
   // remoteness <= root_sum < 2^15, octets need base[1] >= 8.  GM_WORDS32=1
   // keeps 32-bit words (A/B); any other resolve knob selects a 32-bit kernel.
+  // Shards (column jobs, k_dense_resolve8c) additionally need the packed
+  // 16-bit halos and every level's slice list to fit one ColJobs.
   for (gm_solver* s : ss) {
     const char* w32 = getenv("GM_WORDS32");
-    s->w16 = mode == 0 && s->glist && !s->view.blk && d.pow2 && d.kind == K_SUM && d.nheaps >= 2 &&
-             d.nheaps <= 8 && d.base[1] >= 8 && d.root_sum < 0x7FFF && s->view.Wl * 2 <= 0xFFFFFFF0ull &&
-             !dense_resolve_knob_set() && !(w32 && atoi(w32));
+    const bool base_ok = d.pow2 && d.kind == K_SUM && d.nheaps >= 2 && d.nheaps <= 8 && d.base[1] >= 8 &&
+                         d.root_sum < 0x7FFF && s->view.Wl * 2 <= 0xFFFFFFF0ull && !(w32 && atoi(w32));
+    if (mode == 0)
+      s->w16 = base_ok && s->glist && !s->view.blk && !dense_resolve_knob_set();
+    else
+      s->w16 = base_ok && d.nheaps >= 3 && s->view.blk && s->colperm && s->hg.on && s->halo16 &&
+               s->view.Z % 256 == 0 && s->view.E <= 0xFFFF &&
+               blk_count(s) * (s->view.B + 4) <= (u64)kMaxColJobs && !dense_scalar_resolve();
   }
   std::vector<hipEvent_t> ev;
   auto new_event = [&](hipEvent_t* e) -> int {

@@ -72,21 +72,25 @@ def test_world1_variants_agree(params, monkeypatch):
         np.testing.assert_array_equal(rem, base[2], err_msg=str(env))
 
 
-@pytest.mark.parametrize("halo32", [False, True])
-def test_shard_halo_word_widths(halo32, monkeypatch):
-    """Column-order halos (Z % 256 == 0) in 16- and 32-bit words."""
+@pytest.mark.parametrize("env", [{}, {"GM_WORDS32": "1"}, {"GM_HALO32": "1"}])
+@pytest.mark.parametrize("world", [2, 3])
+def test_shard_halo_word_widths(env, world, monkeypatch):
+    """Column-order halos (Z % 256 == 0): 16-bit shard tables with 16-bit
+    halos (default, k_dense_resolve8c), 32-bit tables with 16-bit halos,
+    32-bit tables and halos -- each against the single-table solve."""
     from gamesmanmpi_amd.dist import group_solve
     from gamesmanmpi_amd.games import GameSpec
     from gamesmanmpi_amd.solver import Solver
     params = "heaps=15:15:15:15:31"  # Z = 16^3 = 4096 prefixes (16 columns) per slice
-    if halo32:
-        monkeypatch.setenv("GM_HALO32", "1")
-    else:
-        monkeypatch.delenv("GM_HALO32", raising=False)
+    for k in ("GM_HALO32", "GM_WORDS32"):
+        monkeypatch.delenv(k, raising=False)
     s1 = Solver(GameSpec("sum_four_to_one", params), layout="dense")
     r1 = s1.solve()
-    rg, shards = group_solve(GameSpec("sum_four_to_one", params), 2)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    rg, shards = group_solve(GameSpec("sum_four_to_one", params), world)
     assert (rg.positions, rg.edges, rg.root_line) == (r1.positions, r1.edges, r1.root_line)
+    assert rg.extra["word_bits"] == (16 if not env else 32), rg.extra
     keys, val, rem = s1.dump()
     out = np.full(len(keys), 0xFFFFFFFF, np.uint32)
     for s in shards:
