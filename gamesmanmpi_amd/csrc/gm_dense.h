@@ -904,7 +904,7 @@ __device__ __forceinline__ void oct_finish(Oct8& Q, const OctLoads<MAXH>& X) {
 template <int MAXH>
 __global__ __launch_bounds__(256) void k_dense_resolve8p(Desc d, DenseView v, uint16_t* words, const u64* bits, u64 L,
                                                          DevState* st, const uint32_t* __restrict__ glist,
-                                                         XcdShares xs) {
+                                                         XcdShares xs, BlockCount* bc) {
   Oct8 Q;
   oct_init(Q, d, words, bits, L, v.Wl, v.Wbl);
   const uint32_t lane = __lane_id();
@@ -931,9 +931,8 @@ __global__ __launch_bounds__(256) void k_dense_resolve8p(Desc d, DenseView v, ui
       oct_finish<MAXH>(Q, X1);
     }
   }
-  block_add(&st->cursor_front, (u64)Q.npos);
-  block_add(&st->edges, (u64)Q.edges);
-  block_add(&st->prims, Q.S == 0 ? (u64)Q.npos : 0ull);
+  block_count(bc, (u64)Q.npos, (u64)Q.edges);
+  if (Q.S == 0) block_add(&st->prims, (u64)Q.npos);  // one launch per solve
 }
 
 // Column jobs (shards, and any table whose top digit sits above 256-prefix
@@ -999,7 +998,7 @@ __global__ __launch_bounds__(256) void k_dense_resolve4c(Desc d, RowGeom g, uint
 template <int MAXH>
 __global__ __launch_bounds__(256) void k_dense_resolve8c(Desc d, RowGeom g, uint16_t* words, const u64* bits, u64 L,
                                                          DevState* st, const uint32_t* __restrict__ colperm,
-                                                         ColJobs J) {
+                                                         ColJobs J, BlockCount* bc) {
   Oct8 Q;
   oct_init(Q, d, words, bits, L, g.Wl, g.Wbl);
   const uint32_t lane = __lane_id();
@@ -1037,9 +1036,8 @@ __global__ __launch_bounds__(256) void k_dense_resolve8c(Desc d, RowGeom g, uint
       oct_finish<MAXH>(Q, X1);
     }
   }
-  block_add(&st->cursor_front, (u64)Q.npos);
-  block_add(&st->edges, (u64)Q.edges);
-  block_add(&st->prims, Q.S == 0 ? (u64)Q.npos : 0ull);
+  block_count(bc, (u64)Q.npos, (u64)Q.edges);
+  if (Q.S == 0) block_add(&st->prims, (u64)Q.npos);  // one launch per solve
 }
 
 // Column walks (world 1): a wave takes one column k and walks up to

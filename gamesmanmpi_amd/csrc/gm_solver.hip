@@ -316,8 +316,18 @@ static size_t devstate_bytes(int max_levels) {
 // once at solver creation): TS[64] then TD[16][64], u64 each.
 constexpr size_t kMaskTableWords = 64 * 17;
 static size_t mask_tables_offset(int max_levels) { return (devstate_bytes(max_levels) + 255) / 256 * 256; }
+// then per-block position/edge counts of the octet resolves (block_count):
+// one plain read-modify-write per block and launch instead of device-scope
+// atomics on one line, which serialise at ~12 ns each (MI355X_MICROARCH.md
+// "fanin"): 768 resident blocks x 2 counters cost ~18 us at the end of every
+// launch.  Cleared per solve, summed by k_fill_red.
+struct BlockCount {
+  u64 npos, edges;
+};
+constexpr int kCountSlots = 4096;  // >= any octet-resolve grid (host clamps)
+static size_t count_slots_offset(int max_levels) { return mask_tables_offset(max_levels) + kMaskTableWords * sizeof(u64); }
 static size_t scratch_bytes_for(int max_levels) {
-  return mask_tables_offset(max_levels) + kMaskTableWords * sizeof(u64);
+  return count_slots_offset(max_levels) + kCountSlots * sizeof(BlockCount);
 }
 // Packed word halos of sharded power-of-two dense tables (exchange_words):
 // after the mask tables, the group offset table off[XN][G] (u32; G = Z/64
@@ -520,6 +530,33 @@ __device__ __forceinline__ u64 level_key(const u64* lv, u64 lcap, const LevelSeg
 }
 
 // block-wide sum then one atomic per block
+// per-block counts into this block's own slot (no atomics; launches on one
+// stream run in order, so slot b has one writer at a time)
+__device__ __forceinline__ void block_count(BlockCount* bc, u64 npos, u64 edges) {
+  __shared__ u64 rn[16], re[16];
+  for (int o = 32; o > 0; o >>= 1) {
+    npos += __shfl_xor(npos, o);
+    edges += __shfl_xor(edges, o);
+  }
+  const int w = threadIdx.x >> 6;
+  if (__lane_id() == 0) {
+    rn[w] = npos;
+    re[w] = edges;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u64 sn = 0, se = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); i++) {
+      sn += rn[i];
+      se += re[i];
+    }
+    if (sn | se) {
+      bc[blockIdx.x].npos += sn;
+      bc[blockIdx.x].edges += se;
+    }
+  }
+  __syncthreads();
+}
 __device__ __forceinline__ void block_add(u64* dst, u64 v) {
   __shared__ u64 red[16];
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -770,6 +807,7 @@ struct gm_solver {
   HaloTabs ht{};
   bool halo16 = false;  // words travel as 16 bits (k_halo_cols)
   bool w16 = false;     // this solve's table holds 16-bit order-form words (k_dense_resolve8p)
+  BlockCount* bcount = nullptr;  // per-block counts in scratch (block_count)
   uint32_t* halo_send = nullptr;
   uint32_t* halo_recv = nullptr;
   std::vector<uint32_t> halo_tot;
@@ -979,10 +1017,12 @@ static void dense_launch_resolve_t(gm_solver* s, const DenseView& v, int grid, u
         const RowGeom rg{v.Wl, v.Wbl, v.blk ? v.Z : s->d.pstride[s->cg.top]};
         if (s->w16) {  // 16-bit shard table: octets, two columns per wave
           const u64 cu8 = (u64)((J.cum[J.n] + 1) / 2) * 64;
-          const int g8 = (int)std::min<u64>(((cu8 + kBlock - 1) / kBlock + 7) & ~7ull,
-                                            (u64)resident_blocks((const void*)k_dense_resolve8c<MAXH>));
+          const int g8 = (int)std::min<u64>(
+              std::min<u64>(((cu8 + kBlock - 1) / kBlock + 7) & ~7ull,
+                            (u64)resident_blocks((const void*)k_dense_resolve8c<MAXH>)),
+              (u64)kCountSlots);
           hipLaunchKernelGGL((k_dense_resolve8c<MAXH>), dim3(g8), dim3(kBlock), 0, s->stream, s->d, rg,
-                             (uint16_t*)s->words, s->bits, L, s->st, s->colperm, J);
+                             (uint16_t*)s->words, s->bits, L, s->st, s->colperm, J, s->bcount);
           return;
         }
         const u64 cu = (u64)J.cum[J.n] * 64;
@@ -999,9 +1039,10 @@ static void dense_launch_resolve_t(gm_solver* s, const DenseView& v, int grid, u
       for (int x = 1; x < 8; x++) xs.o[x] &= ~1u;  // shares start at even entries: a wave = two whole groups
       const u64 u8 = (u64)xs.o[8] * 32;
       const int rp = resident_blocks((const void*)k_dense_resolve8p<MAXH>);
-      const int gp = (int)std::min<u64>(((u8 + kBlock - 1) / kBlock + 7) & ~7ull, (u64)rp);
+      const int gp = (int)std::min<u64>(std::min<u64>(((u8 + kBlock - 1) / kBlock + 7) & ~7ull, (u64)rp),
+                                        (u64)kCountSlots);
       hipLaunchKernelGGL((k_dense_resolve8p<MAXH>), dim3(gp), dim3(kBlock), 0, s->stream, s->d, v,
-                         (uint16_t*)s->words, s->bits, L, s->st, gl, xs);
+                         (uint16_t*)s->words, s->bits, L, s->st, gl, xs, s->bcount);
       return;
     }
     const int g = (int)std::min<u64>(((units + kBlock - 1) / kBlock + 7) & ~7ull, (u64)resident);
@@ -1439,6 +1480,7 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
   s->lcap = buf->level_capacity;
   s->st = (DevState*)buf->scratch;
   s->masks = (const u64*)((char*)buf->scratch + mask_tables_offset(d->max_levels));
+  s->bcount = (BlockCount*)((char*)buf->scratch + count_slots_offset(d->max_levels));
   s->flags = buf->flags;
   s->grid = launch_grid();
   if (buf->stream) {
@@ -1700,8 +1742,19 @@ int gm_solver_solve(gm_solver* s, gm_result* out) {
   return 0;
 }
 
-__global__ void k_fill_red(DevState* st) {
+__global__ void k_fill_red(DevState* st, const BlockCount* bc) {  // one wave
+  u64 sn = 0, se = 0;
+  for (int i = (int)threadIdx.x; i < kCountSlots; i += 64) {
+    sn += bc[i].npos;
+    se += bc[i].edges;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    sn += __shfl_xor(sn, o);
+    se += __shfl_xor(se, o);
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st->cursor_front += sn;  // this table's totals (gm_solver_positions reads them)
+    st->edges += se;
     st->red[0] = st->cursor_front;
     st->red[1] = st->edges;
     st->red[2] = st->prims;
@@ -2033,7 +2086,10 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
   };
   auto t0 = std::chrono::steady_clock::now();
   HIPCHK(hipEventRecord(e0, st));
-  for (gm_solver* s : ss) HIPCHK(hipMemsetAsync(s->st, 0, devstate_bytes(T), st));
+  for (gm_solver* s : ss) {
+    HIPCHK(hipMemsetAsync(s->st, 0, devstate_bytes(T), st));
+    HIPCHK(hipMemsetAsync(s->bcount, 0, kCountSlots * sizeof(BlockCount), st));
+  }
   // Sharded solves overlap each level's halo exchange with compute: a
   // level's launch is split into the part whose parents (pull) / children
   // (resolve) lie inside the shard's own block -- which includes the two
@@ -2167,7 +2223,7 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
     uint64_t root_q = ~0ull;
     if (!dense_local(s->view, root_p, &root_q)) root_q = ~0ull;
     hipLaunchKernelGGL(k_dense_root, dim3(1), dim3(64), 0, st, s->view, s->words, s->bits, root_q, s->st, s->w16);
-    hipLaunchKernelGGL(k_fill_red, dim3(1), dim3(64), 0, st, s->st);
+    hipLaunchKernelGGL(k_fill_red, dim3(1), dim3(64), 0, st, s->st, s->bcount);
   }
   if (mode == 1) {
     ncclResult_t r = ncclAllReduce(s0->st->red, s0->st->red, 5, ncclUint64, ncclSum, s0->comm, st);
