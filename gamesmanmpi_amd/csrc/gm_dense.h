@@ -902,9 +902,9 @@ __device__ __forceinline__ void oct_finish(Oct8& Q, const OctLoads<MAXH>& X) {
 // every XCD share at an even list entry, so a wave's 64 units are two whole
 // groups (lanes 0-31 / 32-63), read with two scalar loads.
 template <int MAXH>
-__global__ __launch_bounds__(256) void k_dense_resolve8p(Desc d, DenseView v, uint16_t* words, const u64* bits, u64 L,
-                                                         DevState* st, const uint32_t* __restrict__ glist,
-                                                         XcdShares xs, BlockCount* bc) {
+__device__ __forceinline__ void resolve8p_body(const Desc& d, const DenseView& v, uint16_t* words, const u64* bits,
+                                               u64 L, DevState* st, const uint32_t* __restrict__ glist,
+                                               const XcdShares& xs, BlockCount* bc) {
   Oct8 Q;
   oct_init(Q, d, words, bits, L, v.Wl, v.Wbl);
   const uint32_t lane = __lane_id();
@@ -990,6 +990,15 @@ __global__ __launch_bounds__(256) void k_dense_resolve4c(Desc d, RowGeom g, uint
   }
   quad_done(Q, st);
 }
+
+template <int MAXH>
+__global__ __launch_bounds__(256) void k_dense_resolve8p(Desc d, DenseView v, uint16_t* words, const u64* bits, u64 L,
+                                                         DevState* st, const uint32_t* __restrict__ glist,
+                                                         XcdShares xs, BlockCount* bc) {
+  resolve8p_body<MAXH>(d, v, words, bits, L, st, glist, xs, bc);
+}
+// (held to 128 VGPRs for 4 waves per SIMD it spills 88 B per lane and runs
+// 1.5x slower: profiles/r01_ab_occupancy.jsonl)
 
 // Column jobs over a 16-bit table (shards): the octet body of
 // k_dense_resolve8p, a wave = two consecutive columns of the jobs'

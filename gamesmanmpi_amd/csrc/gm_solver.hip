@@ -1742,9 +1742,10 @@ int gm_solver_solve(gm_solver* s, gm_result* out) {
   return 0;
 }
 
-__global__ void k_fill_red(DevState* st, const BlockCount* bc) {  // one wave
+__global__ __launch_bounds__(1024) void k_fill_red(DevState* st, const BlockCount* bc) {  // one block of 1024
+  __shared__ u64 rn[16], re[16];
   u64 sn = 0, se = 0;
-  for (int i = (int)threadIdx.x; i < kCountSlots; i += 64) {
+  for (int i = (int)threadIdx.x; i < kCountSlots; i += (int)blockDim.x) {
     sn += bc[i].npos;
     se += bc[i].edges;
   }
@@ -1752,7 +1753,17 @@ __global__ void k_fill_red(DevState* st, const BlockCount* bc) {  // one wave
     sn += __shfl_xor(sn, o);
     se += __shfl_xor(se, o);
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (__lane_id() == 0) {
+    rn[threadIdx.x >> 6] = sn;
+    re[threadIdx.x >> 6] = se;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    sn = se = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); w++) {
+      sn += rn[w];
+      se += re[w];
+    }
     st->cursor_front += sn;  // this table's totals (gm_solver_positions reads them)
     st->edges += se;
     st->red[0] = st->cursor_front;
@@ -2223,7 +2234,7 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
     uint64_t root_q = ~0ull;
     if (!dense_local(s->view, root_p, &root_q)) root_q = ~0ull;
     hipLaunchKernelGGL(k_dense_root, dim3(1), dim3(64), 0, st, s->view, s->words, s->bits, root_q, s->st, s->w16);
-    hipLaunchKernelGGL(k_fill_red, dim3(1), dim3(64), 0, st, s->st, s->bcount);
+    hipLaunchKernelGGL(k_fill_red, dim3(1), dim3(1024), 0, st, s->st, s->bcount);
   }
   if (mode == 1) {
     ncclResult_t r = ncclAllReduce(s0->st->red, s0->st->red, 5, ncclUint64, ncclSum, s0->comm, st);
