@@ -14,6 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIBPATH = os.environ.get("GM_LIBPATH") or os.path.join(HERE, "libgamesman_hip.so")
 
 GM_EINVAL, GM_EHIP, GM_EFULL, GM_ECORRUPT, GM_ENOGPU = -1, -2, -3, -4, -5
+GM_PARTIAL = 1  # gm_solver_solve stopped at the gm_solver_set_steps bound
 GM_F_KERNEL_TIMING = 1
 GM_F_FORCE_HASHED = 2
 GM_MODE_HASHED, GM_MODE_DENSE = 0, 1
@@ -80,7 +81,7 @@ EXPORTS = (
     "gm_solver_solve", "gm_solver_query", "gm_solver_positions",
     "gm_solver_destroy", "gm_solve", "gm_owner", "gm_owner_host",
     "gm_plan_shard", "gm_solver_create_shard", "gm_comm_unique_id",
-    "gm_solver_comm_init", "gm_solve_group", "gm_solver_set_flags",
+    "gm_solver_comm_init", "gm_solve_group", "gm_solver_set_flags", "gm_solver_set_steps",
     "gm_shard_info",
     "gm_ks_begin", "gm_ks_level_size", "gm_ks_expand", "gm_ks_insert",
     "gm_ks_finalize", "gm_ks_counts", "gm_ks_children", "gm_ks_reduce",
@@ -141,6 +142,7 @@ def load():
         "gm_solver_comm_init": [c.c_void_p, c.c_void_p],
         "gm_solve_group": [c.POINTER(c.c_void_p), c.c_int, P(gm_result)],
         "gm_solver_set_flags": [c.c_void_p, c.c_uint32],
+        "gm_solver_set_steps": [c.c_void_p, c.c_uint32, c.c_uint32],
         "gm_shard_info": [c.c_int, c.c_int, c.c_int, P(c.c_uint64)],
         "gm_ks_begin": [c.c_void_p, c.c_int],
         "gm_ks_level_size": [c.c_void_p, c.c_int, P(c.c_uint64)],

@@ -307,6 +307,8 @@ struct DevState {
   uint32_t root_word;
   u64 ks_cursor;    // keyed shards: children emitted by k_ks_expand
   u64 red[5];     // cross-shard reduction: positions, edges, prims, root word + 1, err
+  uint32_t word_bits;  // dense: table word width of the solve in progress (resume reads it back)
+  uint32_t pad_;
   LevelSeg seg[1];  // [max_levels + 2]
 };
 static size_t devstate_bytes(int max_levels) {
@@ -824,6 +826,7 @@ struct gm_solver {
   bool own_stream;
   uint32_t flags;
   int grid;
+  uint32_t step_first = 0, step_stop = 0;  // gm_solver_set_steps (one solve)
 };
 
 static const int kBlock = 256;
@@ -1627,6 +1630,16 @@ int gm_solver_comm_init(gm_solver* s, const void* id) {
   return 0;
 }
 
+int gm_solver_set_steps(gm_solver* s, uint32_t first, uint32_t stop) {
+  if (!s) return fail(GM_EINVAL, "bad argument");
+  const uint32_t n = 2u * (uint32_t)s->d.max_levels;
+  if (s->world > 1) return fail(GM_EINVAL, "stop/resume drives one-GPU solves only");
+  if (first > n || (stop && (stop <= first || stop > n))) return fail(GM_EINVAL, "bad step range [%u, %u) of %u", first, stop, n);
+  s->step_first = first;
+  s->step_stop = stop;
+  return 0;
+}
+
 int gm_solver_set_flags(gm_solver* s, uint32_t flags) {
   if (!s) return fail(GM_EINVAL, "null solver");
   s->flags = flags;
@@ -1650,7 +1663,11 @@ int gm_solver_solve(gm_solver* s, gm_result* out) {
   if (s->mode == GM_MODE_DENSE) return solve_dense(s, out);
   if (s->world > 1) return fail(GM_EINVAL, "keyed-table shard %d/%d: drive it with gm_ks_* (md5 exchange)", s->rank, s->world);
   const int T = s->d.max_levels;
-  const bool timing = s->flags & GM_F_KERNEL_TIMING;
+  // steps [first, stop) of the 2T (gm_solver_set_steps); forward level L is
+  // step L (level T-1 expands nothing), backward level L is step 2T-1-L
+  const int first = (int)s->step_first, stop = s->step_stop ? (int)s->step_stop : 2 * T;
+  s->step_first = s->step_stop = 0;
+  const bool timing = (s->flags & GM_F_KERNEL_TIMING) && first == 0 && stop == 2 * T;
   std::vector<hipEvent_t> ev;
   auto new_event = [&](hipEvent_t* e) -> int {
     HIPCHK(hipEventCreate(e));
@@ -1670,11 +1687,13 @@ int gm_solver_solve(gm_solver* s, gm_result* out) {
   }
   auto t0 = std::chrono::steady_clock::now();
   HIPCHK(hipEventRecord(e0, s->stream));
-  // fresh table: keys EMPTY, words NO_WORD
-  HIPCHK(hipMemsetAsync(s->tab, 0xFF, (s->mask + 1) * sizeof(gm_slot), s->stream));
-  HIPCHK(hipMemsetAsync(s->st, 0, devstate_bytes(T), s->stream));
-  hipLaunchKernelGGL(k_seed, dim3(1), dim3(64), 0, s->stream, s->tab, s->mask, s->lv, s->st, s->d.root);
-  for (int L = 0; L + 1 < T; L++) {
+  if (first == 0) {
+    // fresh table: keys EMPTY, words NO_WORD
+    HIPCHK(hipMemsetAsync(s->tab, 0xFF, (s->mask + 1) * sizeof(gm_slot), s->stream));
+    HIPCHK(hipMemsetAsync(s->st, 0, devstate_bytes(T), s->stream));
+    hipLaunchKernelGGL(k_seed, dim3(1), dim3(64), 0, s->stream, s->tab, s->mask, s->lv, s->st, s->d.root);
+  }
+  for (int L = std::max(first, 0); L + 1 < T && L < stop; L++) {
     if (timing) HIPCHK(hipEventRecord(kx[2 * L], s->stream));
     do_expand(s, L);
     if (timing) HIPCHK(hipEventRecord(kx[2 * L + 1], s->stream));
@@ -1683,12 +1702,21 @@ int gm_solver_solve(gm_solver* s, gm_result* out) {
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(e1, s->stream));
   for (int L = T - 1; L >= 0; L--) {
+    const int k = 2 * T - 1 - L;
+    if (k < first) continue;
+    if (k >= stop) break;
     if (timing) HIPCHK(hipEventRecord(kr[2 * L], s->stream));
     do_resolve(s, L);
     if (timing) HIPCHK(hipEventRecord(kr[2 * L + 1], s->stream));
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(e2, s->stream));
+  if (stop < 2 * T) {  // stopped early: the state stays on the device for a resume
+    HIPCHK(hipStreamSynchronize(s->stream));
+    for (auto e : ev) (void)hipEventDestroy(e);
+    out->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return GM_PARTIAL;
+  }
   hipLaunchKernelGGL(k_root_word, dim3(1), dim3(64), 0, s->stream, s->tab, s->mask, s->d.root, s->st);
   HIPCHK(hipGetLastError());
   std::vector<unsigned char> host(devstate_bytes(T));
@@ -2053,7 +2081,12 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
       if (ss[g]->rank != (int)g || ss[g]->stream != s0->stream || ss[g]->mode != GM_MODE_DENSE)
         return fail(GM_EINVAL, "group shards must be ranks 0..n-1 on one stream");
   }
-  const bool timing = s0->flags & GM_F_KERNEL_TIMING;
+  // steps [first, stop) (gm_solver_set_steps, world 1 only): forward level L
+  // is step L, backward level L is step 2T-1-L
+  const int first = mode == 0 ? (int)s0->step_first : 0;
+  const int stop = mode == 0 && s0->step_stop ? (int)s0->step_stop : 2 * T;
+  s0->step_first = s0->step_stop = 0;
+  const bool timing = (s0->flags & GM_F_KERNEL_TIMING) && first == 0 && stop == 2 * T;
   hipStream_t st = s0->stream;
   // 16-bit words (k_dense_resolve8p) for the default world-1 sweep: K_SUM
   // remoteness <= root_sum < 2^15, octets need base[1] >= 8.  GM_WORDS32=1
@@ -2061,6 +2094,13 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
   // Shards (column jobs, k_dense_resolve8c) additionally need the packed
   // 16-bit halos and every level's slice list to fit one ColJobs.
   for (gm_solver* s : ss) {
+    if (first > 0) {  // resume: the word width the interrupted solve chose
+      uint32_t wb = 0;
+      HIPCHK(hipMemcpy(&wb, &s->st->word_bits, sizeof wb, hipMemcpyDeviceToHost));
+      if (wb != 16 && wb != 32) return fail(GM_EINVAL, "resume: scratch holds no solve in progress");
+      s->w16 = wb == 16;
+      continue;
+    }
     const char* w32 = getenv("GM_WORDS32");
     const bool base_ok = d.pow2 && d.kind == K_SUM && d.nheaps >= 2 && d.nheaps <= 8 && d.base[1] >= 8 &&
                          d.root_sum < 0x7FFF && s->view.Wl * 2 <= 0xFFFFFFF0ull && !(w32 && atoi(w32));
@@ -2097,9 +2137,14 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
   };
   auto t0 = std::chrono::steady_clock::now();
   HIPCHK(hipEventRecord(e0, st));
-  for (gm_solver* s : ss) {
-    HIPCHK(hipMemsetAsync(s->st, 0, devstate_bytes(T), st));
-    HIPCHK(hipMemsetAsync(s->bcount, 0, kCountSlots * sizeof(BlockCount), st));
+  if (first == 0) {
+    static const uint32_t kWordBits[2] = {32u, 16u};
+    for (gm_solver* s : ss) {
+      HIPCHK(hipMemsetAsync(s->st, 0, devstate_bytes(T), st));
+      HIPCHK(hipMemsetAsync(s->bcount, 0, kCountSlots * sizeof(BlockCount), st));
+      HIPCHK(hipMemcpyAsync(&s->st->word_bits, &kWordBits[s->w16 ? 1 : 0], sizeof(uint32_t),
+                            hipMemcpyHostToDevice, st));
+    }
   }
   // Sharded solves overlap each level's halo exchange with compute: a
   // level's launch is split into the part whose parents (pull) / children
@@ -2165,7 +2210,7 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
   // Parents are one or two top values ABOVE: the boundary is the top two
   // slices [b-2, b), whose parents sit in the halo [b, b+2) sent down by the
   // rank above.
-  for (int L = 0; L < T; L++) {
+  for (int L = first; L < T && L < stop; L++) {
     if (timing) HIPCHK(hipEventRecord(kx[2 * L], st));
     for (gm_solver* s : ss) {
       const uint32_t B = s->view.B;  // pull: the top two own slices read the upper halo
@@ -2200,6 +2245,8 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
   // boundary is the bottom two slices [a, a+2), whose children sit in the
   // halo [a-2, a) sent up by the rank below.
   for (int L = T - 1; L >= 0; L--) {
+    if (2 * T - 1 - L < first) continue;
+    if (2 * T - 1 - L >= stop) break;
     if (timing) HIPCHK(hipEventRecord(kr[2 * L], st));
     for (gm_solver* s : ss) {
       const uint32_t B = s->view.B;  // resolve: the bottom two own slices read the lower halo
@@ -2230,6 +2277,13 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
     HIPCHK(hipStreamWaitEvent(st, E[0], 0));
   }
   HIPCHK(hipEventRecord(e2, st));
+  if (stop < 2 * T) {  // stopped early (world 1): the state stays on the device for a resume
+    HIPCHK(hipStreamSynchronize(st));
+    for (auto e : ev) (void)hipEventDestroy(e);
+    out->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    out->word_bits = s0->w16 ? 16u : 32u;
+    return GM_PARTIAL;
+  }
   for (gm_solver* s : ss) {
     uint64_t root_q = ~0ull;
     if (!dense_local(s->view, root_p, &root_q)) root_q = ~0ull;

@@ -157,6 +157,35 @@ class Solver:
                 self._alloc(self.positions_hint)
         return self._result(r)
 
+    # -- stop / resume (checkpoints: gamesmanmpi_amd.checkpoint) ------------
+    @property
+    def steps(self):
+        """Steps of a full solve (gm_solver_set_steps): forward levels
+        0..T-1, then backward levels T-1..0."""
+        return 2 * int(self.plan.max_levels)
+
+    def solve_steps(self, first=0, stop=0):
+        """Run steps [first, stop) of the solve (stop 0 = to the end).
+        Returns the SolveResult when the solve completed, None when it
+        stopped early -- the state then stays in this solver's buffers
+        (save it with checkpoint.save, or continue with first=stop).  No
+        buffer regrowth: a table that fills raises TableFull."""
+        L = _lib.load()
+        _lib.check(L.gm_solver_set_steps(self._h, int(first), int(stop)))
+        r = _lib.gm_result()
+        with self.torch.cuda.device(self.device):
+            rc = L.gm_solver_solve(self._h, ctypes.byref(r))
+        if rc == _lib.GM_PARTIAL:
+            return None
+        _lib.check(rc)
+        return self._result(r)
+
+    @property
+    def buffers(self):
+        """(table, level store, scratch) device tensors (uint8 / int64 /
+        uint8): everything a stopped solve leaves behind."""
+        return self._tensors
+
     def _result(self, r):
         return SolveResult(
             root_value=r.root_value, root_remoteness=r.root_remoteness,

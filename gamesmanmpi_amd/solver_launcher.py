@@ -87,6 +87,13 @@ def build_parser():
     p.add_argument("--verify-samples", type=int, default=200)
     p.add_argument("--json", action="store_true",
                    help="also print a JSON line with counts and timings")
+    p.add_argument("-ck", "--checkpoint", metavar="DIR",
+                   help="one-GPU solves: checkpoint the solver state into DIR "
+                        "every --checkpoint-every levels and resume from DIR "
+                        "when it holds a checkpoint of the same game "
+                        "(gamesmanmpi_amd.checkpoint); removed on completion")
+    p.add_argument("--checkpoint-every", type=int, default=32, metavar="N",
+                   help="levels (steps) between checkpoints")
     return p
 
 
@@ -193,6 +200,23 @@ def main(argv=None):
             result, shard = dist_keyed_solve(spec, device="cuda:%d" % local,
                                              positions=args.positions)
             solver = shard.solver
+    elif args.checkpoint:
+        from gamesmanmpi_amd import checkpoint
+        from gamesmanmpi_amd.solver import Solver
+        first = 0
+        if os.path.isfile(os.path.join(args.checkpoint, "meta.json")):
+            meta = checkpoint.read_meta(args.checkpoint)
+            if (meta["game"], meta["params"]) != (spec.name, spec.params):
+                raise SystemExit("%s holds a checkpoint of %s %s, not %s %s"
+                                 % (args.checkpoint, meta["game"], meta["params"],
+                                    spec.name, spec.params))
+            solver, first = checkpoint.restore(args.checkpoint, device="cuda:%d" % local)
+            logging.debug("resuming %r at step %d of %d", spec, first, solver.steps)
+        else:
+            solver = Solver(spec, positions=args.positions,
+                            device="cuda:%d" % local, layout=args.layout)
+        result = checkpoint.solve_checkpointed(solver, args.checkpoint,
+                                               args.checkpoint_every, first=first)
     else:
         from gamesmanmpi_amd.solver import Solver
         solver = Solver(spec, positions=args.positions,

@@ -1,0 +1,134 @@
+"""Level-granular stop / resume and on-disk checkpoints (include/gamesman.h
+gm_solver_set_steps, gamesmanmpi_amd/checkpoint.py): a solve interrupted
+after any step -- forward or backward, HASHED or DENSE (16- and 32-bit
+words) -- and resumed, in the same solver or in a fresh one restored from
+disk, gives exactly the uninterrupted solve's counts, root and words."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CASES = [
+    ("tic_tac_toe_np", "", "hashed", {}),
+    ("othello_bit_new", "length=4,height=4", "hashed", {}),
+    ("sum_four_to_one", "heaps=15:15:15:15", "dense", {}),
+    ("sum_four_to_one", "heaps=15:15:15:15", "dense", {"GM_WORDS32": "1"}),
+    ("four_to_one", "start=40", "dense", {}),
+]
+
+
+def _full(name, params, layout):
+    from gamesmanmpi_amd.games import GameSpec
+    from gamesmanmpi_amd.solver import Solver
+    s = Solver(GameSpec(name, params), layout=layout)
+    r = s.solve()
+    keys, val, rem = s.dump()
+    o = np.argsort(keys)
+    return r, (keys[o], val[o], rem[o])
+
+
+def _same(r, d, r0, d0):
+    assert (r.positions, r.edges, r.primitives, r.root_line) == (
+        r0.positions, r0.edges, r0.primitives, r0.root_line)
+    for a, b in zip(d, d0):
+        np.testing.assert_array_equal(a, b)
+
+
+def _dump(s):
+    keys, val, rem = s.dump()
+    o = np.argsort(keys)
+    return keys[o], val[o], rem[o]
+
+
+@pytest.mark.parametrize("name,params,layout,env", CASES)
+def test_stop_resume_same_solver(name, params, layout, env, monkeypatch):
+    from gamesmanmpi_amd.games import GameSpec
+    from gamesmanmpi_amd.solver import Solver
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    r0, d0 = _full(name, params, layout)
+    s = Solver(GameSpec(name, params), layout=layout)
+    n = s.steps
+    for cut in sorted({1, n // 4, n // 2, n // 2 + 1, (3 * n) // 4, n - 1}):
+        assert s.solve_steps(0, cut) is None
+        r = s.solve_steps(cut, 0)
+        assert r is not None
+        _same(r, _dump(s), r0, d0)
+        if layout == "dense":
+            assert r.extra["word_bits"] == (32 if env else 16) or name == "four_to_one"
+
+
+@pytest.mark.parametrize("name,params,layout,env", CASES)
+def test_checkpoint_on_disk(name, params, layout, env, monkeypatch, tmp_path):
+    from gamesmanmpi_amd import checkpoint
+    from gamesmanmpi_amd.games import GameSpec
+    from gamesmanmpi_amd.solver import Solver
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    r0, d0 = _full(name, params, layout)
+    s = Solver(GameSpec(name, params), layout=layout)
+    cut = s.steps // 2 + 1  # inside the backward pass
+    assert s.solve_steps(0, cut) is None
+    ck = str(tmp_path / "ck")
+    checkpoint.save(s, ck, cut)
+    del s
+    s2, step = checkpoint.restore(ck)
+    assert step == cut
+    monkeypatch.delenv("GM_WORDS32", raising=False)  # the width travels in the checkpoint
+    r = s2.solve_steps(step, 0)
+    _same(r, _dump(s2), r0, d0)
+
+
+def test_solve_checkpointed_chunks(tmp_path):
+    from gamesmanmpi_amd import checkpoint
+    from gamesmanmpi_amd.games import GameSpec
+    from gamesmanmpi_amd.solver import Solver
+    r0, d0 = _full("sum_four_to_one", "heaps=7:7:7:7:7", "dense")
+    s = Solver(GameSpec("sum_four_to_one", "heaps=7:7:7:7:7"), layout="dense")
+    ck = str(tmp_path / "ck")
+    r = checkpoint.solve_checkpointed(s, ck, every=7)
+    _same(r, _dump(s), r0, d0)
+    assert not os.path.exists(ck)
+
+
+def test_bad_step_ranges_refused():
+    from gamesmanmpi_amd import _lib
+    from gamesmanmpi_amd.games import GameSpec
+    from gamesmanmpi_amd.solver import Solver
+    s = Solver(GameSpec("tic_tac_toe_np"))
+    n = s.steps
+    for first, stop in ((n + 1, 0), (5, 5), (5, 3), (0, n + 1)):
+        with pytest.raises(_lib.GmError):
+            s.solve_steps(first, stop)
+    assert s.solve().root_line == "TIE in 9 moves"
+
+
+def test_launcher_resumes_from_checkpoint(tmp_path):
+    """A launcher run that finds a checkpoint of its game resumes there and
+    prints the uninterrupted root line; the checkpoint is removed after."""
+    from gamesmanmpi_amd import checkpoint
+    from gamesmanmpi_amd.games import GameSpec
+    from gamesmanmpi_amd.solver import Solver
+    params = "heaps=15:15:15:15"
+    r0, _ = _full("sum_four_to_one", params, "dense")
+    src = open(os.path.join(ROOT, "gamesmanmpi_amd", "games", "sum_four_to_one.py")).read()
+    game = tmp_path / "sum_four_to_one.py"
+    game.write_text(src.replace("HEAPS = (31, 31, 31, 31, 31, 31)", "HEAPS = (15, 15, 15, 15)"))
+    s = Solver(GameSpec("sum_four_to_one", params))
+    cut = s.steps // 2 + 3
+    assert s.solve_steps(0, cut) is None
+    ck = str(tmp_path / "ck")
+    checkpoint.save(s, ck, cut)
+    del s
+    out = subprocess.run([sys.executable, "-m", "gamesmanmpi_amd.solver_launcher", str(game),
+                          "-ck", ck, "--checkpoint-every", "4"],
+                         cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.stdout.strip().splitlines()[-1] == r0.root_line
+    assert not os.path.exists(ck)
