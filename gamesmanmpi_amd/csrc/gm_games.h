@@ -77,6 +77,10 @@ struct Desc {
   uint64_t W;      // prefixes per level = prod_{i>=1} base[i]
   uint64_t pstride[16];  // stride of heap digit i inside the prefix (i >= 1)
   uint32_t pshift[16];   // log2(pstride[i]) when pow2
+  // symmetry hooks (params "symmetry=1"): keys are
+  // canonical representatives of their orbit under the game module's
+  // symmetry_functions() (othello_bit_new.py:224-226: player_flip, order 2)
+  int sym;
 };
 
 // Which part of a DENSE table's global prefix space one table holds, and
@@ -329,6 +333,21 @@ GM_HD uint64_t oth_flips(const Desc& d, uint64_t me, uint64_t opp, int x, int y)
     }
   return flips;
 }
+// player_flip (othello_bit_new.py:228-235): every piece changes colour
+// (flip :274-275 maps BLANK to BLANK), incr_turn toggles the side to move,
+// the pass count stays.  Values and remoteness are invariant under it:
+// oth_prim, the move rules and the level only see (mover, opponent) planes.
+GM_HD uint64_t oth_flip(const Desc& d, uint64_t k) {
+  const int A = d.A;
+  const uint64_t w = k & d.full, b = (k >> A) & d.full, hi = ~((1ull << (2 * A)) - 1);
+  return b | (w << A) | ((k ^ (1ull << (2 * A))) & hi);
+}
+// canonical representative: the smaller key of {k, player_flip(k)}
+GM_HD uint64_t oth_canon(const Desc& d, uint64_t k) {
+  if (!d.sym) return k;
+  const uint64_t f = oth_flip(d, k);
+  return f < k ? f : k;
+}
 template <class F>
 GM_HD int oth_children(const Desc& d, uint64_t k, F&& emit) {
   const int A = d.A, L = d.L, H = d.H;
@@ -345,11 +364,11 @@ GM_HD int oth_children(const Desc& d, uint64_t k, F&& emit) {
       uint64_t nme = me | cell | f, nopp = opp & ~f;
       uint64_t nw = black ? nopp : nme, nb = black ? nme : nopp;
       // reset_pass, place + flip, incr_turn (:125-129)
-      emit(nw | (nb << A) | ((uint64_t)(!black) << (2 * A)), 1);
+      emit(oth_canon(d, nw | (nb << A) | ((uint64_t)(!black) << (2 * A))), 1);
       n++;
     }
   if (n == 0) {  // [None]: incr_pass only (:122-124)
-    emit(k + (1ull << (2 * A + 1)), 1);
+    emit(oth_canon(d, k + (1ull << (2 * A + 1))), 1);
     n = 1;
   }
   return n;
@@ -401,6 +420,8 @@ GM_HD int any_children(const Desc& d, uint64_t k, F&& f) {
     default: return oth_children(d, k, f);
   }
 }
+// canonical key of any position (identity without symmetry hooks)
+GM_HD uint64_t any_canon(const Desc& d, uint64_t k) { return d.kind == K_OTHELLO ? oth_canon(d, k) : k; }
 GM_HD int any_level(const Desc& d, uint64_t k) {
   switch (d.kind) {
     case K_SUM: return sum_level(d, k);

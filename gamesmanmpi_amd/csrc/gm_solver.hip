@@ -213,9 +213,13 @@ static int build_desc(const char* name, const char* params, Desc* out) {
     put(hx, hy, 1);
     // two incr_turn calls from 0 -> turn_count 2 (WHITE): bit 2A = 0
     d.max_levels = d.A + 3;
+    d.sym = kv(params, "symmetry", 0) ? 1 : 0;  // player_flip orbits (symmetry_functions, :224-226)
+    d.root = oth_canon(d, d.root);
   } else {
     return fail(GM_EINVAL, "no device descriptor for game '%s'", name);
   }
+  if (kv(params, "symmetry", 0) && d.kind != K_OTHELLO)
+    return fail(GM_EINVAL, "'%s' defines no symmetry_functions() to reduce by", name);
   *out = d;
   return 0;
 }
@@ -748,9 +752,9 @@ __global__ __launch_bounds__(256) void k_resolve(Desc d, gm_slot* tab, u64 mask,
   block_add(&st->prims, prims);
 }
 
-__global__ void k_query(const gm_slot* tab, u64 mask, const u64* keys, u64 n, uint32_t* words) {
+__global__ void k_query(Desc d, const gm_slot* tab, u64 mask, const u64* keys, u64 n, uint32_t* words) {
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
-    u64 h = table_find(tab, mask, keys[i]);
+    u64 h = table_find(tab, mask, any_canon(d, keys[i]));  // symmetry hooks: the orbit's representative
     words[i] = h == ~0ull ? NO_WORD : tab[h].word;
   }
 }
@@ -1301,6 +1305,18 @@ int gm_host_level(int game, const uint64_t* keys, size_t n, int32_t* levels) {
   const Desc* d = get_game(game);
   if (!d || (n && (!keys || !levels))) return fail(GM_EINVAL, "bad argument");
   for (size_t i = 0; i < n; i++) levels[i] = any_level(*d, keys[i]);
+  return 0;
+}
+
+int gm_symmetry(int game, int which, const uint64_t* keys, size_t n, uint64_t* out) {
+  const Desc* d = get_game(game);
+  if (!d || (n && (!keys || !out))) return fail(GM_EINVAL, "bad argument");
+  if (which == -1) {
+    for (size_t i = 0; i < n; i++) out[i] = any_canon(*d, keys[i]);
+    return 0;
+  }
+  if (which != 0 || d->kind != K_OTHELLO) return fail(GM_EINVAL, "no symmetry function %d for this game", which);
+  for (size_t i = 0; i < n; i++) out[i] = oth_flip(*d, keys[i]);
   return 0;
 }
 
@@ -2358,7 +2374,7 @@ int gm_solver_query(gm_solver* s, const uint64_t* keys_dev, uint64_t n, uint32_t
     hipLaunchKernelGGL(k_dense_query, dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->view, s->words, s->bits,
                        (const u64*)keys_dev, n, words_dev, s->w16);
   else
-    hipLaunchKernelGGL(k_query, dim3(grid), dim3(kBlock), 0, s->stream, s->tab, s->mask, (const u64*)keys_dev, n,
+    hipLaunchKernelGGL(k_query, dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->tab, s->mask, (const u64*)keys_dev, n,
                        words_dev);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(s->stream));

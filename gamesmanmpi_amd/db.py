@@ -80,7 +80,13 @@ class SolutionDB:
             return self.lookup_name(str(pos))
         if spec is None:
             raise ValueError("a keyed table needs the game's GameSpec")
-        return self.lookup_key(spec.key_of(pos))
+        key = spec.key_of(pos)
+        if "symmetry=1" in self.meta.get("params", "").split(","):
+            # a symmetric solve stored orbit representatives (gm_symmetry)
+            from .games import GameSpec
+            key = int(GameSpec(spec.name, self.meta["params"]).symmetry(
+                np.array([key], np.uint64))[0])
+        return self.lookup_key(key)
 
 
 def main(argv=None):

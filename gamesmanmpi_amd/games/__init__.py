@@ -47,6 +47,21 @@ class GameSpec:
     def __repr__(self):
         return "GameSpec(%r, %r)" % (self.name, self.params)
 
+    # -- symmetry hooks (params "symmetry=1") ------------------------------
+    @property
+    def symmetric(self):
+        return any(p.strip() == "symmetry=1" for p in self.params.split(","))
+
+    def symmetry(self, keys, which=-1):
+        """which=-1: canonical orbit representatives of `keys` (identity
+        for specs without symmetry); which=i: the module's i-th symmetry
+        function as a key map (include/gamesman.h gm_symmetry)."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        out = np.zeros(len(keys), np.uint64)
+        _lib.check(_lib.load().gm_symmetry(self.id, int(which), keys.ctypes.data,
+                                           len(keys), out.ctypes.data))
+        return out
+
     # -- canonical bytes <-> keys ------------------------------------------
     def encode(self, canon):
         k = _lib.ctypes.c_uint64()
@@ -164,7 +179,10 @@ class GameSpec:
         str(pos).  Raises ValueError on the first disagreement."""
         rng = random.Random(seed)
         root = module.initial_position()
-        if self.key_of(root) != self.root_key:
+        # a symmetric spec stores orbit representatives: compare canonically
+        canon = (lambda ks: [int(x) for x in self.symmetry(np.array(ks, np.uint64))]) \
+            if self.symmetric else (lambda ks: ks)
+        if canon([self.key_of(root)])[0] != self.root_key:
             raise ValueError("initial_position() does not match descriptor "
                              "%r root" % (self,))
         checked = 0
@@ -173,7 +191,7 @@ class GameSpec:
             key = self.key_of(pos)
             if self.str_utf8(key) != str(pos).encode("utf-8"):
                 raise ValueError("str(pos) mismatch at %r" % (pos,))
-            pr, nc, ch = self.host_expand(np.array([key], np.uint64))
+            pr, nc, ch = self.host_expand(np.array(canon([key]), np.uint64))
             p = module.primitive(pos)
             if int(pr[0]) != int(p):
                 raise ValueError("primitive mismatch at %r: module %r, "
@@ -183,10 +201,40 @@ class GameSpec:
                 pos = root
                 continue
             kids = [module.do_move(pos, m) for m in module.gen_moves(pos)]
-            want = [self.key_of(c) for c in kids]
+            want = canon([self.key_of(c) for c in kids])
             got = [int(x) for x in ch[0, :nc[0]]]
+            if self.symmetric:  # the representative's children are an image of pos's
+                want, got = sorted(want), sorted(got)
             if want != got:
                 raise ValueError("children mismatch at %r" % (pos,))
+            pos = kids[rng.randrange(len(kids))]
+        return checked
+
+    def verify_symmetries(self, module, samples=200, seed=0):
+        """The module's symmetry_functions() (othello_bit_new.py:224-226:
+        [(player_flip, 2)]) must be the descriptor's key maps: for positions
+        on random playouts, key(f(pos)) == gm_symmetry(i, key(pos)) and f
+        applied `order` times is the identity."""
+        funcs = list(module.symmetry_functions())
+        rng = random.Random(seed)
+        root = module.initial_position()
+        pos, checked = root, 0
+        while checked < samples:
+            k = np.array([self.key_of(pos)], np.uint64)
+            for i, (f, order) in enumerate(funcs):
+                img = f(pos)
+                if self.key_of(img) != int(self.symmetry(k, i)[0]):
+                    raise ValueError("symmetry %d (%s) disagrees with the descriptor at %r"
+                                     % (i, getattr(f, "__name__", f), pos))
+                for _ in range(int(order) - 1):
+                    img = f(img)
+                if self.key_of(img) != int(k[0]):
+                    raise ValueError("symmetry %d is not of order %d" % (i, order))
+            checked += 1
+            if module.primitive(pos) != 4:
+                pos = root
+                continue
+            kids = [module.do_move(pos, m) for m in module.gen_moves(pos)]
             pos = kids[rng.randrange(len(kids))]
         return checked
 

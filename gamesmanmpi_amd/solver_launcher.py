@@ -87,6 +87,10 @@ def build_parser():
     p.add_argument("--verify-samples", type=int, default=200)
     p.add_argument("--json", action="store_true",
                    help="also print a JSON line with counts and timings")
+    p.add_argument("--symmetries", action="store_true",
+                   help="solve orbit representatives under the game module's "
+                        "symmetry_functions() (othello_bit_new: player_flip); "
+                        "every position keeps its own value and remoteness")
     p.add_argument("-ck", "--checkpoint", metavar="DIR",
                    help="one-GPU solves: checkpoint the solver state into DIR "
                         "every --checkpoint-every levels and resume from DIR "
@@ -180,6 +184,13 @@ def main(argv=None):
         return solve_generic(args, game, rank, world, local)
     if args.layout == "graph":
         return solve_generic(args, game, rank, world, local)
+    if args.symmetries:
+        if not hasattr(game, "symmetry_functions"):
+            raise SystemExit("%s defines no symmetry_functions()" % args.game_file)
+        from gamesmanmpi_amd.games import GameSpec
+        spec = GameSpec(spec.name, (spec.params + ",symmetry=1").lstrip(","))
+        if not args.no_verify:
+            spec.verify_symmetries(game, samples=args.verify_samples)
     if not args.no_verify:
         n = spec.verify(game, samples=args.verify_samples)
         logging.debug("descriptor %r verified on %d positions", spec, n)
