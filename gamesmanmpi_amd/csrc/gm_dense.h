@@ -1228,6 +1228,77 @@ __global__ __launch_bounds__(256) void k_halo_cols(Desc d, HaloColJobs J, u64 Z,
   }
 }
 
+// 16-bit tables (k_dense_resolve8c shards): the same column-order packing,
+// two columns per wave (lanes 0-31 / 32-63) and eight slots per lane (one
+// 16-B access), so a level's halo is one pass of the grid instead of two.
+// Each half finds its column with scalar searches; a slot's rank is the
+// valid slots of lower lanes in its half (eight ballots) plus the lower
+// valid elements of its own lane.  Needs base[1] >= 8 (w16 tables do).
+template <bool PACK>
+__global__ __launch_bounds__(256) void k_halo_cols16(Desc d, HaloColJobs J, u64 Z, const uint32_t* __restrict__ colperm,
+                                                     HaloTabs T, uint16_t* level_words, uint16_t* buf) {
+  const uint32_t lane = __lane_id(), hl = lane & 31;
+  uint32_t sl = 0;  // digit sum of the lane's first slot offset 8 hl (below the top digit)
+  for (int i = 1; i < T.top; i++) sl += ((8u * hl) >> d.pshift[i]) & (d.base[i] - 1);
+  const int H0 = (int)d.heap[0];
+  const u64 below = ((1ull << lane) - 1ull) & (lane < 32 ? 0x00000000FFFFFFFFull : 0xFFFFFFFF00000000ull);
+  const uint32_t total = J.cum[J.n];  // columns (host: > 0)
+  const XcdRange r = xcd_range((u64)((total + 1) / 2) * 64);
+  struct Col {
+    u64 q, base;
+    int y;
+  };
+  auto find = [&](uint32_t c) {  // column c of the concatenation (scalar)
+    uint32_t a = 0, b = J.n;
+    while (b - a > 1) {
+      const uint32_t m = (a + b) >> 1;
+      if (J.cum[m] <= c) a = m;
+      else b = m;
+    }
+    const uint32_t i = J.lo[a] + (c - J.cum[a]);
+    const uint32_t k = colperm[i];
+    int gs = 0;
+    for (int h = 1; h < T.top; h++) gs += (int)(((u64)k * 256 >> d.pshift[h]) & (d.base[h] - 1));
+    const int x = J.x[a], y = x - gs;
+    const uint32_t ny = (y >= 0 && y < T.NYn) ? T.NY[y] : 0u;
+    Col col;
+    col.base = (u64)J.base[a] + T.PB[(u64)x * T.NG + gs] + (u64)(i - T.CS[gs]) * ny;
+    col.q = (u64)J.u[a] * Z + (u64)k * 256;
+    col.y = y;
+    return col;
+  };
+  for (u64 iu = r.first; iu < r.end; iu += r.stride) {
+    const uint32_t c0 = __builtin_amdgcn_readfirstlane((uint32_t)(iu >> 6)) * 2;
+    const Col A = find(c0), B = find(min(c0 + 1, total - 1));
+    const bool on = lane < 32 || c0 + 1 < total;
+    const int y = lane < 32 ? A.y : B.y;
+    const u64 base = lane < 32 ? A.base : B.base;
+    const u64 q = (lane < 32 ? A.q : B.q) + 8 * hl;
+    uint32_t valid = 0;
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      const int ds = (int)sl + e;
+      valid |= (uint32_t)(on && ds <= y && ds >= y - H0) << e;
+    }
+    uint32_t rk = 0;  // valid slots of lower lanes in this half
+#pragma unroll
+    for (int e = 0; e < 8; e++) rk += (uint32_t)__popcll(__ballot((valid >> e) & 1u) & below);
+    if (!valid) continue;
+    if (PACK) {
+      const u16x8 v = *(const u16x8*)(level_words + q);
+#pragma unroll
+      for (int e = 0; e < 8; e++)
+        if ((valid >> e) & 1u) buf[base + rk++] = v[e];
+    } else {
+      u16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};  // holes of a live lane get 0 (never read unmasked)
+#pragma unroll
+      for (int e = 0; e < 8; e++)
+        if ((valid >> e) & 1u) v[e] = buf[base + rk++];
+      *(u16x8*)(level_words + q) = v;
+    }
+  }
+}
+
 // root word (on the shard that owns the root, root_q = its local prefix;
 // others pass ~0 and report NO_WORD)
 __global__ void k_dense_root(DenseView v, const uint32_t* words, const u64* bits, u64 root_q, DevState* st, bool w16) {

@@ -1959,13 +1959,23 @@ static u64 halo_move_all(gm_solver* s, u64 L, int pack, uint32_t* buf, hipStream
     const u64 units = (u64)J.cum[J.n] * 64;
     const int grid = (int)std::min<u64>(((units + kBlock - 1) / kBlock + 7) & ~7ull, (u64)s->grid);
     uint32_t* lw = s->words + L * s->view.Wl;
-    void* lw16 = (uint16_t*)s->words + L * s->view.Wl;
-    if (s->w16 && pack)
+    uint16_t* lw16 = (uint16_t*)s->words + L * s->view.Wl;
+    const char* hc4 = getenv("GM_HALO_COLS4");  // A/B: one column per wave, four slots per lane
+    if (s->w16 && !(hc4 && atoi(hc4))) {  // two columns per wave, eight slots per lane
+      const u64 u2 = (u64)((J.cum[J.n] + 1) / 2) * 64;
+      const int g2 = (int)std::min<u64>(((u2 + kBlock - 1) / kBlock + 7) & ~7ull, (u64)s->grid);
+      if (pack)
+        hipLaunchKernelGGL((k_halo_cols16<true>), dim3(g2), dim3(kBlock), 0, cs, s->d, J, s->view.Z, s->colperm,
+                           s->ht, lw16, (uint16_t*)buf);
+      else
+        hipLaunchKernelGGL((k_halo_cols16<false>), dim3(g2), dim3(kBlock), 0, cs, s->d, J, s->view.Z, s->colperm,
+                           s->ht, lw16, (uint16_t*)buf);
+    } else if (s->w16 && pack)
       hipLaunchKernelGGL((k_halo_cols<true, true, true>), dim3(grid), dim3(kBlock), 0, cs, s->d, J, s->view.Z,
-                         s->colperm, s->ht, lw16, (void*)buf);
+                         s->colperm, s->ht, (void*)lw16, (void*)buf);
     else if (s->w16)
       hipLaunchKernelGGL((k_halo_cols<false, true, true>), dim3(grid), dim3(kBlock), 0, cs, s->d, J, s->view.Z,
-                         s->colperm, s->ht, lw16, (void*)buf);
+                         s->colperm, s->ht, (void*)lw16, (void*)buf);
     else if (pack && s->halo16)
       hipLaunchKernelGGL((k_halo_cols<true, true>), dim3(grid), dim3(kBlock), 0, cs, s->d, J, s->view.Z, s->colperm,
                          s->ht, lw, (void*)buf);

@@ -72,7 +72,7 @@ def test_world1_variants_agree(params, monkeypatch):
         np.testing.assert_array_equal(rem, base[2], err_msg=str(env))
 
 
-@pytest.mark.parametrize("env", [{}, {"GM_WORDS32": "1"}, {"GM_HALO32": "1"}])
+@pytest.mark.parametrize("env", [{}, {"GM_HALO_COLS4": "1"}, {"GM_WORDS32": "1"}, {"GM_HALO32": "1"}])
 @pytest.mark.parametrize("world", [2, 3])
 def test_shard_halo_word_widths(env, world, monkeypatch):
     """Column-order halos (Z % 256 == 0): 16-bit shard tables with 16-bit
@@ -82,7 +82,7 @@ def test_shard_halo_word_widths(env, world, monkeypatch):
     from gamesmanmpi_amd.games import GameSpec
     from gamesmanmpi_amd.solver import Solver
     params = "heaps=15:15:15:15:31"  # Z = 16^3 = 4096 prefixes (16 columns) per slice
-    for k in ("GM_HALO32", "GM_WORDS32"):
+    for k in ("GM_HALO32", "GM_WORDS32", "GM_HALO_COLS4"):
         monkeypatch.delenv(k, raising=False)
     s1 = Solver(GameSpec("sum_four_to_one", params), layout="dense")
     r1 = s1.solve()
@@ -90,7 +90,8 @@ def test_shard_halo_word_widths(env, world, monkeypatch):
         monkeypatch.setenv(k, v)
     rg, shards = group_solve(GameSpec("sum_four_to_one", params), world)
     assert (rg.positions, rg.edges, rg.root_line) == (r1.positions, r1.edges, r1.root_line)
-    assert rg.extra["word_bits"] == (16 if not env else 32), rg.extra
+    wide = "GM_WORDS32" in env or "GM_HALO32" in env
+    assert rg.extra["word_bits"] == (32 if wide else 16), rg.extra
     keys, val, rem = s1.dump()
     out = np.full(len(keys), 0xFFFFFFFF, np.uint32)
     for s in shards:
