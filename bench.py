@@ -92,7 +92,7 @@ def pmc_traffic(kernel, workload):
     return row["bytes_per_launch"], "profiles/pmc_traffic.json (%s)" % row.get("source", "?")
 
 
-def dense_resolve_kernel(word_bits):
+def dense_resolve_kernel(word_bits, world=1):
     """Name of the dense resolve kernel the library launches for the bench
     shape (power-of-two heaps, base >= 8): over the live-group lists, the
     software-pipelined eight-prefixes-per-lane form on the 16-bit table (the
@@ -100,7 +100,7 @@ def dense_resolve_kernel(word_bits):
     the A/B knobs (GM_DENSE_RESOLVE / GM_DENSE_SWEEP / GM_DENSE_PIPE) select
     another."""
     if word_bits == 16:
-        return "k_dense_resolve8p"
+        return "k_dense_resolve8p" if world == 1 else "k_dense_resolve8c"
     if os.environ.get("GM_DENSE_RESOLVE") == "scalar":
         return "k_dense_resolve"
     sweep = os.environ.get("GM_DENSE_SWEEP", "list")
@@ -208,7 +208,7 @@ def main():
     word_bits = tr.extra.get("word_bits", 32) or 32
     fwd_b, bwd_b = algorithmic_bytes(tr_pos, tr_edges, layout, word_bits // 8)
     if tr.ms_resolve_kernels >= tr.ms_expand_kernels:
-        kname, kb, kms, kn = (dense_resolve_kernel(word_bits) if layout == "dense"
+        kname, kb, kms, kn = (dense_resolve_kernel(word_bits, world) if layout == "dense"
                               else "k_resolve", bwd_b, tr.ms_resolve_kernels,
                               tr.n_resolve_launches)
     else:
