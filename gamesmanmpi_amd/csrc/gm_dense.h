@@ -221,19 +221,23 @@ __global__ __launch_bounds__(256) void k_dense_pull_words(Desc d, DenseView v, u
   // mask tables (built once on the host at solver creation, gm_solver.hip
   // build_mask_tables): M[0..63] = TS, M[64 (i + 1) + t] = TD[i][t]
   __shared__ u64 M[64 * (MAXH + 1)];
+  // one thread per 64-prefix bitmap word of the band, or of the level's
+  // live 256-prefix groups (glist, world 1: words of groups without a
+  // non-hole are never read unmasked, so they are not written)
+  const u64 ngroups = glist ? gwords : (v.p_hi - v.p_lo + 63) >> 6;
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  const u64 g_first = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  // the first item's list entry is loaded before the table fill + barrier
+  // (most launches give a thread a single item)
+  const uint32_t e_first = (glist && g_first < ngroups) ? glist[g_first >> 2] : 0u;
   for (int k = threadIdx.x; k < 64 * (MAXH + 1); k += blockDim.x) M[k] = masks[k];
   __syncthreads();
   const u64* TS = M;
 #define TD(i) (M + 64 * ((i) + 1))
   const int S = (int)(d.root_sum - (uint32_t)L);
   const int H0 = (int)d.heap[0];
-  // one thread per 64-prefix bitmap word of the band, or of the level's
-  // live 256-prefix groups (glist, world 1: words of groups without a
-  // non-hole are never read unmasked, so they are not written)
-  const u64 ngroups = glist ? gwords : (v.p_hi - v.p_lo + 63) >> 6;
-  const u64 stride = (u64)gridDim.x * blockDim.x;
-  for (u64 gi = (u64)blockIdx.x * blockDim.x + threadIdx.x; gi < ngroups; gi += stride) {
-    const u64 qi = glist ? ((u64)glist[gi >> 2] << 8) + ((gi & 3) << 6)
+  for (u64 gi = g_first; gi < ngroups; gi += stride) {
+    const u64 qi = glist ? ((u64)(gi == g_first ? e_first : glist[gi >> 2]) << 8) + ((gi & 3) << 6)
                          : v.p_lo + (gi << 6);  // sweep index of lane-bit 0
     uint64_t q;  // local prefix of lane-bit 0 (multiple of 64)
     bool run;
