@@ -67,3 +67,18 @@ def test_duplicate_keys_refused(tmp_path):
                     value=np.array([0], np.uint8), remoteness=np.array([1], np.uint32))
     with pytest.raises(ValueError):
         SolutionDB(str(tmp_path / "sd"))
+
+
+def test_checkpoint_meta_format_is_checked(tmp_path):
+    """checkpoint.read_meta refuses unknown formats (restore would otherwise
+    load buffers laid out by another build)."""
+    import json
+    from gamesmanmpi_amd import checkpoint
+    d = tmp_path / "ck"
+    d.mkdir()
+    (d / "meta.json").write_text(json.dumps({"format": checkpoint.FORMAT + 1}))
+    with pytest.raises(ValueError):
+        checkpoint.read_meta(str(d))
+    (d / "meta.json").write_text(json.dumps({"format": checkpoint.FORMAT, "game": "mttt",
+                                             "params": "", "step": 3}))
+    assert checkpoint.read_meta(str(d))["step"] == 3
