@@ -214,6 +214,67 @@ __device__ __forceinline__ u64 bits64_at(const u64* bits, u64 pos) {
   return sh ? (lo >> sh) | (bits[w + 1] << (64 - sh)) : lo;
 }
 
+// Column-job tables (k_dense_resolve8c / k_dense_resolve4c / k_dense_pull_cols)
+constexpr int kMaxColJobs = 96;
+struct ColJobs {
+  uint32_t n;                     // slices
+  uint32_t cum[kMaxColJobs + 1];  // groups before slice i (cum[n] = total)
+  uint32_t lo[kMaxColJobs];       // first colperm entry of slice i
+  uint32_t u[kMaxColJobs];        // local slice
+  uint32_t t[kMaxColJobs];        // global top value
+};
+struct RowGeom {
+  u64 Wl, Wbl, Z;
+};
+
+// One 64-prefix bitmap word of level L: reach bits = OR of the parents'
+// bits (undo-moves +1/+2 on one heap), masked to the word's non-holes.  q =
+// local prefix of lane-bit 0 (multiple of 64), pg = its global prefix, V0 =
+// extra validity mask (band end), TS/TD = the mask tables in LDS.
+template <int MAXH>
+__device__ __forceinline__ void pull_word(const Desc& d, u64 Wbl, u64* bits, u64 L, u64 root_p, u64 q, u64 pg,
+                                          u64 V0, const u64* TS, const u64* M) {
+#define TD(i) (M + 64 * ((i) + 1))
+  const int S = (int)(d.root_sum - (uint32_t)L);
+  const int H0 = (int)d.heap[0];
+  int dg[MAXH];
+  int sg = 0;
+#pragma unroll
+  for (int i = 1; i < MAXH; i++) {
+    const bool live = (MAXH <= 8) || i < d.nheaps;
+    dg[i] = live ? (int)((pg >> d.pshift[i]) & (d.base[i] - 1)) : 0;
+    sg += dg[i];
+  }
+  // valid: S - H0 <= sg + sj <= S
+  const int lo_s = S - H0 - sg, hi_s = S - sg;
+  const u64 V = mask_le(TS, hi_s) & ~mask_le(TS, lo_s - 1) & V0;
+  u64 reached = 0;
+  if (L == 0) {
+    if (root_p >= pg && root_p < pg + 64) reached = 1ull << (root_p - pg);
+  } else if (V) {
+    const u64 b1 = (L - 1) * Wbl + q, b2 = (L - 2) * Wbl + q;
+    // heap 0 +1 / +2: parent at the same prefix, one / two levels up;
+    // exists iff h0 + d <= H0  <=>  sj >= lo_s + d
+    reached |= bits[b1 >> 6] & ~mask_le(TS, lo_s);
+    if (L >= 2) reached |= bits[b2 >> 6] & ~mask_le(TS, lo_s + 1);
+#pragma unroll
+    for (int i = 1; i < MAXH; i++) {
+      const bool live = (MAXH <= 8) || i < d.nheaps;
+      if (!live) continue;
+      // heap i +1 / +2: exists iff dg + dj <= H_i - d
+      const int Hi = (int)d.heap[i];
+      const u64 m1 = mask_le(TD(i), Hi - 1 - dg[i]);
+      if (m1) reached |= bits64_at(bits, b1 + d.pstride[i]) & m1;
+      if (L >= 2) {
+        const u64 m2 = mask_le(TD(i), Hi - 2 - dg[i]);
+        if (m2) reached |= bits64_at(bits, b2 + 2 * d.pstride[i]) & m2;
+      }
+    }
+  }
+  bits[(L * Wbl + q) >> 6] = reached & V;
+#undef TD
+}
+
 template <int MAXH>
 __global__ __launch_bounds__(256) void k_dense_pull_words(Desc d, DenseView v, u64* bits, u64 L, u64 root_p,
                                                           const u64* __restrict__ masks,
@@ -232,10 +293,6 @@ __global__ __launch_bounds__(256) void k_dense_pull_words(Desc d, DenseView v, u
   const uint32_t e_first = (glist && g_first < ngroups) ? glist[g_first >> 2] : 0u;
   for (int k = threadIdx.x; k < 64 * (MAXH + 1); k += blockDim.x) M[k] = masks[k];
   __syncthreads();
-  const u64* TS = M;
-#define TD(i) (M + 64 * ((i) + 1))
-  const int S = (int)(d.root_sum - (uint32_t)L);
-  const int H0 = (int)d.heap[0];
   for (u64 gi = g_first; gi < ngroups; gi += stride) {
     const u64 qi = glist ? ((u64)(gi == g_first ? e_first : glist[gi >> 2]) << 8) + ((gi & 3) << 6)
                          : v.p_lo + (gi << 6);  // sweep index of lane-bit 0
@@ -243,45 +300,46 @@ __global__ __launch_bounds__(256) void k_dense_pull_words(Desc d, DenseView v, u
     bool run;
     const u64 pg = dense_sweep(v, qi, &q, &run);  // global prefix of lane-bit 0
     if (!run) continue;  // another launch's slice, or a halo
-    int dg[MAXH];
-    int sg = 0;
-#pragma unroll
-    for (int i = 1; i < MAXH; i++) {
-      const bool live = (MAXH <= 8) || i < d.nheaps;
-      dg[i] = live ? (int)((pg >> d.pshift[i]) & (d.base[i] - 1)) : 0;
-      sg += dg[i];
-    }
-    // valid: S - H0 <= sg + sj <= S
-    const int lo_s = S - H0 - sg, hi_s = S - sg;
-    u64 V = mask_le(TS, hi_s) & ~mask_le(TS, lo_s - 1);
-    if (qi + 64 > v.p_hi) V &= (1ull << (v.p_hi - qi)) - 1;
-    u64 reached = 0;
-    if (L == 0) {
-      if (root_p >= pg && root_p < pg + 64) reached = 1ull << (root_p - pg);
-    } else if (V) {
-      const u64 b1 = (L - 1) * v.Wbl + q, b2 = (L - 2) * v.Wbl + q;
-      // heap 0 +1 / +2: parent at the same prefix, one / two levels up;
-      // exists iff h0 + d <= H0  <=>  sj >= lo_s + d
-      reached |= bits[b1 >> 6] & ~mask_le(TS, lo_s);
-      if (L >= 2) reached |= bits[b2 >> 6] & ~mask_le(TS, lo_s + 1);
-#pragma unroll
-      for (int i = 1; i < MAXH; i++) {
-        const bool live = (MAXH <= 8) || i < d.nheaps;
-        if (!live) continue;
-        // heap i +1 / +2: exists iff dg + dj <= H_i - d
-        const int Hi = (int)d.heap[i];
-        const u64 m1 = mask_le(TD(i), Hi - 1 - dg[i]);
-        if (m1) reached |= bits64_at(bits, b1 + d.pstride[i]) & m1;
-        if (L >= 2) {
-          const u64 m2 = mask_le(TD(i), Hi - 2 - dg[i]);
-          if (m2) reached |= bits64_at(bits, b2 + 2 * d.pstride[i]) & m2;
-        }
-      }
-    }
-    bits[(L * v.Wbl + q) >> 6] = reached & V;
+    const u64 V0 = qi + 64 > v.p_hi ? (1ull << (v.p_hi - qi)) - 1 : ~0ull;
+    pull_word<MAXH>(d, v.Wbl, bits, L, root_p, q, pg, V0, M, M);
   }
 }
-#undef TD
+
+// Column jobs (shards): the words of each listed slice's live 256-prefix
+// columns only (ColJobs, as k_dense_resolve8c), instead of every word of
+// the slices' band.  Words of dead columns hold only holes, which readers
+// mask.  The job tables go to LDS with the mask tables; a thread finds its
+// column by a binary search there.
+template <int MAXH>
+__global__ __launch_bounds__(256) void k_dense_pull_cols(Desc d, RowGeom g, u64* bits, u64 L, u64 root_p,
+                                                         const u64* __restrict__ masks,
+                                                         const uint32_t* __restrict__ colperm, ColJobs J) {
+  __shared__ u64 M[64 * (MAXH + 1)];
+  __shared__ uint32_t cum[kMaxColJobs + 1], lo[kMaxColJobs], us[kMaxColJobs], ts[kMaxColJobs];
+  for (int k = threadIdx.x; k < 64 * (MAXH + 1); k += blockDim.x) M[k] = masks[k];
+  for (int k = threadIdx.x; k <= (int)J.n; k += blockDim.x) {
+    cum[k] = J.cum[k];
+    if (k < (int)J.n) {
+      lo[k] = J.lo[k];
+      us[k] = J.u[k];
+      ts[k] = J.t[k];
+    }
+  }
+  __syncthreads();
+  const u64 nwords = (u64)cum[J.n] * 4;
+  for (u64 gi = (u64)blockIdx.x * blockDim.x + threadIdx.x; gi < nwords; gi += (u64)gridDim.x * blockDim.x) {
+    const uint32_t c = (uint32_t)(gi >> 2);
+    uint32_t a = 0, b = J.n;  // slice i: cum[i] <= c < cum[i + 1]
+    while (b - a > 1) {
+      const uint32_t m = (a + b) >> 1;
+      if (cum[m] <= c) a = m;
+      else b = m;
+    }
+    const u64 k = colperm[lo[a] + (c - cum[a])];
+    const u64 off = k * 256 + ((gi & 3) << 6);
+    pull_word<MAXH>(d, g.Wbl, bits, L, root_p, (u64)us[a] * g.Z + off, (u64)ts[a] * g.Z + off, ~0ull, M, M);
+  }
+}
 
 // XCD-aware split of [0, n) (MI355X dispatches workgroup b to XCD b % 8):
 // the blocks of one XCD grid-stride over one contiguous, 64-aligned chunk,
@@ -947,17 +1005,6 @@ __device__ __forceinline__ void resolve8p_body(const Desc& d, const DenseView& v
 // slices with their colperm ranges; wave w of the concatenation finds its
 // slice by a scalar binary search over the prefix counts (kernel
 // arguments).  No per-level tables, no hole groups.
-constexpr int kMaxColJobs = 96;
-struct ColJobs {
-  uint32_t n;                     // slices
-  uint32_t cum[kMaxColJobs + 1];  // groups before slice i (cum[n] = total)
-  uint32_t lo[kMaxColJobs];       // first colperm entry of slice i
-  uint32_t u[kMaxColJobs];        // local slice
-  uint32_t t[kMaxColJobs];        // global top value
-};
-struct RowGeom {
-  u64 Wl, Wbl, Z;
-};
 template <int MAXH>
 __global__ __launch_bounds__(256) void k_dense_resolve4c(Desc d, RowGeom g, uint32_t* words, const u64* bits, u64 L,
                                                          DevState* st, const uint32_t* __restrict__ colperm,

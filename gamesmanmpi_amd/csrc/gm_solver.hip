@@ -928,8 +928,50 @@ static bool dense_pipelined() {
 // any A/B knob that selects a non-default (32-bit word) resolve kernel
 static bool dense_resolve_knob_set() { return dense_scalar_resolve() || dense_sweep_mode() != 0 || !dense_pipelined(); }
 
+// Column jobs of level L over the view's slices (a shard's listed slices,
+// or every top value of a single table): each slice's live columns are one
+// range of the digit-sum-sorted permutation.  False if no column is live.
+static bool build_col_jobs(const gm_solver* s, const DenseView& v, u64 L, ColJobs& J) {
+  J.n = 0;
+  J.cum[0] = 0;
+  const int64_t S = (int64_t)s->d.root_sum - (int64_t)L;
+  const uint32_t nsl = v.blk ? v.nsl : s->d.base[s->cg.top];
+  for (uint32_t i = 0; i < nsl; i++) {
+    const int64_t t = v.blk ? (int64_t)v.st[i] : (int64_t)i;
+    const int64_t hi = std::min<int64_t>(S - t, s->cg.maxgs);
+    const int64_t lo = std::max<int64_t>(S - t - (int64_t)s->d.heap[0] - s->cg.mj, 0);
+    if (hi < lo) continue;
+    const uint32_t a = s->cstart[(size_t)lo], b = s->cstart[(size_t)hi + 1];
+    if (a == b) continue;
+    J.lo[J.n] = a;
+    J.u[J.n] = v.blk ? (uint32_t)v.sl[i] : i;
+    J.t[J.n] = (uint32_t)t;
+    J.cum[J.n + 1] = J.cum[J.n] + (b - a);
+    J.n++;
+  }
+  return J.n > 0;
+}
+
 template <int MAXH, bool POW2>
 static void dense_launch_pull_t(gm_solver* s, const DenseView& v, int grid, u64 L, u64 root_p) {
+  // shards, A/B (GM_PULL_COLS=1): the listed slices' live columns only.
+  // Measured slower than the band sweep (9.6 vs 8.3 us per launch in the
+  // 2-shard group: the per-thread column search and permutation load cost
+  // more than the dead words they skip; profiles/r01_ab_pull_cols.jsonl)
+  if constexpr (POW2 && MAXH >= 3) {
+    const char* pc = getenv("GM_PULL_COLS");
+    if (pc && atoi(pc) && v.blk && s->colperm && v.nsl > 0 && v.nsl <= (uint32_t)kMaxColJobs &&
+        v.Z % 256 == 0 && !dense_per_lane_pull()) {
+      ColJobs J;
+      if (!build_col_jobs(s, v, L, J)) return;
+      const u64 words = (u64)J.cum[J.n] * 4;
+      const int g = (int)std::min<u64>((words + kBlock - 1) / kBlock, (u64)s->grid);
+      const RowGeom rg{v.Wl, v.Wbl, v.Z};
+      hipLaunchKernelGGL((k_dense_pull_cols<MAXH>), dim3(g), dim3(kBlock), 0, s->stream, s->d, rg, s->bits, L,
+                         root_p, s->masks, s->colperm, J);
+      return;
+    }
+  }
   if (POW2 && !dense_per_lane_pull()) {  // word-parallel form: one thread per 64-prefix group
     const uint32_t* gl = nullptr;
     u64 groups = (v.p_hi - v.p_lo + 63) / 64;
@@ -1003,24 +1045,7 @@ static void dense_launch_resolve_t(gm_solver* s, const DenseView& v, int grid, u
                                              : (dense_sweep_cols() && s->d.base[s->cg.top] <= (uint32_t)kMaxColJobs));
       if (cols) {
         ColJobs J;
-        J.n = 0;
-        J.cum[0] = 0;
-        const int64_t S = (int64_t)s->d.root_sum - (int64_t)L;
-        const uint32_t nsl = v.blk ? v.nsl : s->d.base[s->cg.top];
-        for (uint32_t i = 0; i < nsl; i++) {
-          const int64_t t = v.blk ? (int64_t)v.st[i] : (int64_t)i;
-          const int64_t hi = std::min<int64_t>(S - t, s->cg.maxgs);
-          const int64_t lo = std::max<int64_t>(S - t - (int64_t)s->d.heap[0] - s->cg.mj, 0);
-          if (hi < lo) continue;
-          const uint32_t a = s->cstart[(size_t)lo], b = s->cstart[(size_t)hi + 1];
-          if (a == b) continue;
-          J.lo[J.n] = a;
-          J.u[J.n] = v.blk ? (uint32_t)v.sl[i] : i;
-          J.t[J.n] = (uint32_t)t;
-          J.cum[J.n + 1] = J.cum[J.n] + (b - a);
-          J.n++;
-        }
-        if (!J.n) return;
+        if (!build_col_jobs(s, v, L, J)) return;
         const RowGeom rg{v.Wl, v.Wbl, v.blk ? v.Z : s->d.pstride[s->cg.top]};
         if (s->w16) {  // 16-bit shard table: octets, two columns per wave
           const u64 cu8 = (u64)((J.cum[J.n] + 1) / 2) * 64;

@@ -72,7 +72,8 @@ def test_world1_variants_agree(params, monkeypatch):
         np.testing.assert_array_equal(rem, base[2], err_msg=str(env))
 
 
-@pytest.mark.parametrize("env", [{}, {"GM_HALO_COLS4": "1"}, {"GM_WORDS32": "1"}, {"GM_HALO32": "1"}])
+@pytest.mark.parametrize("env", [{}, {"GM_HALO_COLS4": "1"}, {"GM_WORDS32": "1"}, {"GM_HALO32": "1"},
+                                 {"GM_PULL_COLS": "1"}])
 @pytest.mark.parametrize("world", [2, 3])
 def test_shard_halo_word_widths(env, world, monkeypatch):
     """Column-order halos (Z % 256 == 0): 16-bit shard tables with 16-bit
@@ -82,7 +83,7 @@ def test_shard_halo_word_widths(env, world, monkeypatch):
     from gamesmanmpi_amd.games import GameSpec
     from gamesmanmpi_amd.solver import Solver
     params = "heaps=15:15:15:15:31"  # Z = 16^3 = 4096 prefixes (16 columns) per slice
-    for k in ("GM_HALO32", "GM_WORDS32", "GM_HALO_COLS4"):
+    for k in ("GM_HALO32", "GM_WORDS32", "GM_HALO_COLS4", "GM_PULL_COLS"):
         monkeypatch.delenv(k, raising=False)
     s1 = Solver(GameSpec("sum_four_to_one", params), layout="dense")
     r1 = s1.solve()
