@@ -2095,6 +2095,12 @@ static int exchange_words(std::vector<gm_solver*>& ss, u64 L, int mode, hipStrea
     for (int g = 0; g < W; g++) {
       gm_solver* dst = ss[(g + 1) % W];
       const u64 n = halo_move_all(ss[g], L, 1, dst->halo_recv, cs);
+      // the RCCL path posts a receive of halo_recv_count words for the
+      // sender's count: a mismatch would hang it, so the group checks it
+      if (n != halo_recv_count(dst, L))
+        return fail(GM_ECORRUPT, "halo count mismatch at level %llu: shard %d packs %llu, shard %d expects %llu",
+                    (unsigned long long)L, g, (unsigned long long)n, (g + 1) % W,
+                    (unsigned long long)halo_recv_count(dst, L));
       if (n) halo_move_all(dst, L, 0, dst->halo_recv, cs);
     }
     HIPCHK(hipGetLastError());

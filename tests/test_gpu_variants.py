@@ -101,3 +101,32 @@ def test_shard_halo_word_widths(env, world, monkeypatch):
         out[own] = w[own]
     np.testing.assert_array_equal(out & 3, val)
     np.testing.assert_array_equal(out >> 2, rem)
+
+
+@pytest.mark.parametrize("world,params", [(8, "heaps=15:15:15:15:127"), (4, "heaps=15:15:15:15:63"),
+                                          (8, "heaps=15:15:15:15:31")])
+def test_shard_geometries_like_the_bench(world, params):
+    """The bench's N-rank structure at a smaller slice size: round-robin
+    blocks of 8 top values (two per rank at N = 8), 16-bit tables, packed
+    16-bit halos in column order.  The in-process group checks every level's
+    halo word count against what the receiving rank would post (the RCCL
+    path's receive size) and the words against the single-table solve."""
+    from gamesmanmpi_amd.dist import group_solve
+    from gamesmanmpi_amd.games import GameSpec
+    from gamesmanmpi_amd.solver import Solver
+    s1 = Solver(GameSpec("sum_four_to_one", params), layout="dense")
+    r1 = s1.solve()
+    rg, shards = group_solve(GameSpec("sum_four_to_one", params), world)
+    assert (rg.positions, rg.edges, rg.root_line) == (r1.positions, r1.edges, r1.root_line)
+    assert rg.extra["word_bits"] == 16
+    keys, val, rem = s1.dump()
+    out = np.full(len(keys), 0xFFFFFFFF, np.uint32)
+    hits = np.zeros(len(keys), np.int64)
+    for s in shards:
+        w = s.query(keys)
+        own = w != 0xFFFFFFFF
+        out[own] = w[own]
+        hits += own
+    assert (hits == 1).all()
+    np.testing.assert_array_equal(out & 3, val)
+    np.testing.assert_array_equal(out >> 2, rem)
