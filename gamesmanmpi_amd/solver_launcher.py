@@ -195,6 +195,8 @@ def main(argv=None):
         n = spec.verify(game, samples=args.verify_samples)
         logging.debug("descriptor %r verified on %d positions", spec, n)
 
+    if args.checkpoint and world > 1:
+        raise SystemExit("-ck/--checkpoint covers one-GPU solves (a sharded solve's state spans ranks)")
     import torch
     torch.cuda.set_device(local)
     if world > 1:
