@@ -281,8 +281,12 @@ static int dense_geom(const Desc* d, int rank, int world, DenseGeom* g) {
   v.p_hi = v.Wl;
   return 0;
 }
-static u64 dense_words_bytes(const Desc* d, const DenseGeom& g) {
-  return ((u64)d->max_levels * g.v.Wl * 4 + 255) & ~255ull;
+static bool dense_resolve_knob_set();
+static bool dense_plan16(const Desc* d, int world);
+// word area of a dense table: 16-bit order forms when the plan chose them
+// (dense_plan16: one-GPU K_SUM tables the octet kernels handle), else 32-bit
+static u64 dense_words_bytes(const Desc* d, const DenseGeom& g, bool w16) {
+  return ((u64)d->max_levels * g.v.Wl * (w16 ? 2 : 4) + 255) & ~255ull;
 }
 static u64 dense_bits_bytes(const Desc* d, const DenseGeom& g) {
   return (u64)d->max_levels * g.v.Wbl / 8;
@@ -406,6 +410,17 @@ static GroupGeom group_geom(const Desc* d, int world) {
   for (int i = 1; i < d->nheaps; i++) g.mj += (int)((255u >> d->pshift[i]) & (d->base[i] - 1));
   g.on = true;
   return g;
+}
+// Plan-time choice of 16-bit table words (half the HBM of the word area):
+// one-GPU tables whose solves run the octet kernel (run_dense's w16 rule)
+// unless GM_WORDS32 or a 32-bit resolve knob is set when the solver is
+// planned and created.  A solve of such a table refuses 32-bit kernels.
+static bool dense_plan16(const Desc* d, int world) {
+  if (world != 1 || d->kind != K_SUM || !d->pow2 || d->nheaps < 2 || d->nheaps > 8 || d->base[1] < 8 ||
+      d->root_sum >= 0x7FFF || d->W * 2 > 0xFFFFFFF0ull || !group_geom(d, 1).on)
+    return false;
+  const char* w32 = getenv("GM_WORDS32");
+  return !(w32 && atoi(w32)) && !dense_resolve_knob_set();
 }
 static void group_sums(const Desc* d, const GroupGeom& g, std::vector<uint16_t>& gs) {
   gs.resize(g.groups);
@@ -813,6 +828,7 @@ struct gm_solver {
   HaloTabs ht{};
   bool halo16 = false;  // words travel as 16 bits (k_halo_cols)
   bool w16 = false;     // this solve's table holds 16-bit order-form words (k_dense_resolve8p)
+  bool plan16 = false;  // the table was planned with 16-bit words only (dense_plan16)
   BlockCount* bcount = nullptr;  // per-block counts in scratch (block_count)
   uint32_t* halo_send = nullptr;
   uint32_t* halo_recv = nullptr;
@@ -1361,7 +1377,7 @@ static int plan_dense(const Desc* d, int rank, int world, uint64_t max_table_byt
   DenseGeom g;
   int rc = dense_geom(d, rank, world, &g);
   if (rc) return rc;
-  const u64 bytes = dense_words_bytes(d, g) + dense_bits_bytes(d, g);
+  const u64 bytes = dense_words_bytes(d, g, dense_plan16(d, world)) + dense_bits_bytes(d, g);
   *fits = max_table_bytes == 0 || bytes <= max_table_bytes;
   out->mode = GM_MODE_DENSE;
   out->table_slots = (u64)d->max_levels * g.v.Wl;
@@ -1513,7 +1529,8 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
   s->words = (uint32_t*)buf->table;
   s->nslots = buf->table_slots;
   s->view = g.v;
-  s->bits = (u64*)((char*)buf->table + (buf->mode == GM_MODE_DENSE ? dense_words_bytes(d, g) : 0));
+  s->plan16 = buf->mode == GM_MODE_DENSE && dense_plan16(d, world);
+  s->bits = (u64*)((char*)buf->table + (buf->mode == GM_MODE_DENSE ? dense_words_bytes(d, g, s->plan16) : 0));
   s->rank = rank;
   s->world = world;
   s->nblocks = g.nblocks;
@@ -2156,6 +2173,7 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
       HIPCHK(hipMemcpy(&wb, &s->st->word_bits, sizeof wb, hipMemcpyDeviceToHost));
       if (wb != 16 && wb != 32) return fail(GM_EINVAL, "resume: scratch holds no solve in progress");
       s->w16 = wb == 16;
+      if (s->plan16 && !s->w16) return fail(GM_EINVAL, "resume: 32-bit state in a 16-bit table");
       continue;
     }
     const char* w32 = getenv("GM_WORDS32");
@@ -2167,6 +2185,8 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
       s->w16 = base_ok && d.nheaps >= 3 && s->view.blk && s->colperm && s->hg.on && s->halo16 &&
                s->view.Z % 256 == 0 && s->view.E <= 0xFFFF &&
                blk_count(s) * (s->view.B + 4) <= (u64)kMaxColJobs && !dense_scalar_resolve();
+    if (s->plan16 && !s->w16)  // a 16-bit table cannot take a 32-bit kernel
+      return fail(GM_EINVAL, "table planned with 16-bit words: set GM_WORDS32 / resolve knobs before creating the solver");
   }
   std::vector<hipEvent_t> ev;
   auto new_event = [&](hipEvent_t* e) -> int {

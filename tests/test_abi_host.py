@@ -131,7 +131,14 @@ def test_plan_sizes():
     _lib.check(_lib.load().gm_plan(s.id, 0, 0, 0, ctypes.byref(p)))
     assert p.mode == _lib.GM_MODE_DENSE
     assert p.table_slots == 187 * 32 ** 5
-    assert p.table_bytes == 4 * 187 * 32 ** 5 + 187 * 32 ** 5 // 8  # words + reach bitmap
+    # 16-bit order-form words (one-GPU octet kernels) + reach bitmap
+    assert p.table_bytes == 2 * 187 * 32 ** 5 + 187 * 32 ** 5 // 8
+    os.environ["GM_WORDS32"] = "1"  # the A/B knob plans 32-bit words
+    try:
+        _lib.check(_lib.load().gm_plan(s.id, 0, 0, 0, ctypes.byref(p)))
+        assert p.table_bytes == 4 * 187 * 32 ** 5 + 187 * 32 ** 5 // 8
+    finally:
+        del os.environ["GM_WORDS32"]
     # a byte budget below the dense table falls back to the keyed table
     _lib.check(_lib.load().gm_plan(s.id, 0, 0, 1 << 30, ctypes.byref(p)))
     assert p.mode == _lib.GM_MODE_HASHED
