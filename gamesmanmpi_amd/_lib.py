@@ -77,7 +77,7 @@ class gm_result(ctypes.Structure):
 # every symbol include/gamesman.h declares (tests check the exports)
 EXPORTS = (
     "gm_game_lookup", "gm_game_info", "gm_root", "gm_encode", "gm_decode",
-    "gm_encode_batch", "gm_decode_batch", "gm_str_utf8", "gm_host_expand", "gm_host_level", "gm_symmetry", "gm_plan", "gm_solver_create",
+    "gm_encode_batch", "gm_decode_batch", "gm_str_utf8", "gm_host_expand", "gm_host_level", "gm_symmetry", "gm_abi_sizes", "gm_plan", "gm_solver_create",
     "gm_solver_solve", "gm_solver_query", "gm_solver_positions",
     "gm_solver_destroy", "gm_solve", "gm_owner", "gm_owner_host",
     "gm_plan_shard", "gm_solver_create_shard", "gm_comm_unique_id",
@@ -122,6 +122,7 @@ def load():
                            c.c_void_p, c.c_void_p],
         "gm_host_level": [c.c_int, c.c_void_p, c.c_size_t, c.c_void_p],
         "gm_symmetry": [c.c_int, c.c_int, c.c_void_p, c.c_size_t, c.c_void_p],
+        "gm_abi_sizes": [c.c_void_p],
         "gm_plan": [c.c_int, c.c_uint64, c.c_uint32, c.c_uint64,
                     P(gm_plan_t)],
         "gm_solver_create": [c.c_int, P(gm_buffers), P(c.c_void_p)],

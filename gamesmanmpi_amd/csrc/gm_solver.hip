@@ -1184,6 +1184,14 @@ extern "C" {
 const char* gm_last_error(void) { return g_err.c_str(); }
 const char* gm_version(void) { return "gamesmanmpi_amd 0.1 (gfx950)"; }
 
+int gm_abi_sizes(uint32_t out[3]) {
+  if (!out) return fail(GM_EINVAL, "null argument");
+  out[0] = (uint32_t)sizeof(gm_plan_t);
+  out[1] = (uint32_t)sizeof(gm_buffers);
+  out[2] = (uint32_t)sizeof(gm_result);
+  return 0;
+}
+
 int gm_game_lookup(const char* name, const char* params, int* game_id) {
   if (!name || !game_id) return fail(GM_EINVAL, "null argument");
   Desc d;

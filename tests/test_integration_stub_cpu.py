@@ -20,3 +20,13 @@ def test_integration_stub_struct_sizes_match_the_binding():
     assert ctypes.sizeof(ns["Plan"]) == ctypes.sizeof(_lib.gm_plan_t)
     assert ctypes.sizeof(ns["Buffers"]) == ctypes.sizeof(_lib.gm_buffers)
     assert ctypes.sizeof(ns["Result"]) == ctypes.sizeof(_lib.gm_result)
+
+
+def test_binding_structs_match_the_compiled_abi():
+    """_lib's ctypes structs against sizeof() inside the library."""
+    import numpy as np
+    from gamesmanmpi_amd import _lib
+    out = np.zeros(3, np.uint32)
+    _lib.check(_lib.load().gm_abi_sizes(out.ctypes.data))
+    assert out.tolist() == [ctypes.sizeof(_lib.gm_plan_t), ctypes.sizeof(_lib.gm_buffers),
+                            ctypes.sizeof(_lib.gm_result)]
