@@ -2,22 +2,30 @@
 """Benchmark: positions solved per second on the synthetic sum-of-Four-To-One
 state space (BASELINE.json config 4).
 
-A "step" is one complete strong solve from the root: table reset, forward
+A "step" is one complete strong solve from the root: state reset, forward
 expansion of every level, retrograde pass of every level, root word back on
 the host.  N=1 workload: heaps 31^6 = 2^30 = 1,073,741,824 positions,
 187 levels, 12,280,922,112 edges.  For N>1 (one process per GPU, launched by
 torch.distributed.run) the heaps are 31^5 x (32N-1): 2^30 positions per
 GPU; the ranks split the last heap's values into blocks of 8 dealt round
 robin and exchange two boundary slices per block and level over RCCL
-(DESIGN.md §Multi-GPU).  Every step's counts and root value
-are checked against closed forms; a wrong solve aborts the run.
+(DESIGN.md §6).  Every step's counts, root value AND root remoteness are
+checked: counts and value by closed forms, the remoteness against the
+CPU restatement's solve of the same workload (tests/golden/checksums.json,
+or this run's cpu_baseline).
 
 Prints ONE JSON line (rank 0).  Fields beyond the driver contract:
-  roofline      dominant kernel's algorithmic bytes per launch / its
-                HIP-event-timed average duration, vs 8 TB/s; traffic from
-                the committed PMC passes
-  cpu_baseline  the oracle (oracle/, one core) on a bounded sample of the
-                same game family, timed on this host
+  roofline      dominant kernel, HIP-event-timed average launch duration;
+                achieved/frac on the bytes the layout must move (compulsory:
+                own words written, live words of the two child rows read once,
+                reach bits), plus frac_pmc (HBM bytes the counters saw,
+                profiles/pmc_traffic.json) and frac_per_edge_model (one child
+                word read per edge, the round-1 figure) -- DESIGN.md §5
+  keyed         BASELINE config 3 as shipped (toot 6x4, 1.19e9 positions) on
+                the keyed-table path: solve time, positions/s, per-kernel
+                §8d rooflines, fingerprint parity vs the CPU restatement
+  cpu_baseline  the multi-threaded CPU restatement (oracle/oracle_mt.c row
+                solver, all host threads) on the SAME workload
 """
 import argparse
 import json
@@ -35,9 +43,9 @@ def heaps_for(world):
     """Weak scaling, 2^30 positions per GPU: heaps 31^5 x (32N - 1).  N=1 is
     SURVEY §8d's 31^6 (2^30 positions, 187 levels, b = 11.4375).  The ranks
     split the last heap into blocks of 8 values dealt round robin, four per
-    rank (round robin keeps the ranks' per-level work
-    within 1.11 / 1.19 / 1.41x of the mean at N = 2 / 4 / 8; one contiguous
-    block of 32 per rank would give 1.51 / 2.53 / 4.58x)."""
+    rank (round robin keeps the ranks' per-level work within
+    1.11 / 1.19 / 1.41x of the mean at N = 2 / 4 / 8; one contiguous block
+    of 32 per rank would give 1.51 / 2.53 / 4.58x)."""
     if world not in (1, 2, 4, 8):
         raise SystemExit("--gpus must be 1, 2, 4 or 8")
     return [31] * 5 + [32 * world - 1]
@@ -59,28 +67,51 @@ def expected(heaps):
     return P, E, ("LOSS" if g == 0 else "WIN")
 
 
-def algorithmic_bytes(positions, edges, layout, word_bytes=4):
-    """Bytes each kernel family must move, per DESIGN.md §Roofline.
-    hashed (SURVEY §8d keyed model): expand 24 B/position + 8 B/edge,
-      resolve 12 B/position + 12 B/edge (8-B keys, 4-B value words).
-    dense (level-major perfect hash, key implicit in the slot):
-      pull: one reach bit per parent link + one written bit per position
-            = (edges + positions) / 8 B (parent links = edges);
-      resolve: own reach bit + one word written per position, one child
-            word per edge = 4.125 B/position + 4 B/edge with 32-bit words,
-            2.125 B/position + 2 B/edge with the 16-bit table (word_bytes 2,
-            DESIGN.md §3: K_SUM remoteness < 2^15)."""
-    if layout == "dense":
-        return ((edges + positions) / 8.0,
-                (word_bytes + 0.125) * positions + word_bytes * edges)
+def level_counts(heaps):
+    """Positions per level (level L = root_sum - digit sum): coefficients of
+    prod_i (1 + x + ... + x^h_i), reversed."""
+    c = [1]
+    for h in heaps:
+        n = [0] * (len(c) + h)
+        for i, v in enumerate(c):
+            for j in range(h + 1):
+                n[i + j] += v
+        c = n
+    return c[::-1]
+
+
+def dense_bytes(heaps, word_bytes):
+    """Per-solve byte models of the dense layout.
+    compulsory -- what any schedule of this layout must move from HBM:
+      resolve(L): own words written + the live words of rows L+1 and L+2
+                  read once + own reach bits = (3w + 1/8) B per position;
+      pull(L):    own reach bits written + rows L-1, L-2 read = 3/8 B.
+    per_edge -- the round-1 model: one child word per edge (2.125 B/position
+      + 2 B/edge at w = 2), which counts L2/MALL hits as HBM bytes."""
+    n = level_counts(heaps)
+    T = len(n)
+    res = pull = 0.0
+    for L in range(T):
+        nx = lambda k: n[k] if 0 <= k < T else 0  # noqa: E731
+        res += word_bytes * (n[L] + nx(L + 1) + nx(L + 2)) + n[L] / 8.0
+        pull += (n[L] + nx(L - 1) + nx(L - 2)) / 8.0
+    P, E, _ = expected(heaps)
+    return {"resolve_compulsory": res, "pull_compulsory": pull,
+            "resolve_per_edge": (word_bytes + 0.125) * P + word_bytes * E,
+            "pull_per_edge": (E + P) / 8.0}
+
+
+def keyed_bytes(positions, edges):
+    """SURVEY §8d algorithmic bytes of the keyed table: expand 24 B/position
+    + 8 B/edge, resolve 12 B/position + 12 B/edge (8-B keys, 4-B words)."""
     return 24 * positions + 8 * edges, 12 * positions + 12 * edges
 
 
 def pmc_traffic(kernel, workload):
     """HBM bytes per launch of `kernel` from the committed PMC summary
-    (profiles/pmc_traffic.json, written by tools/pmc_summary.py --traffic
-    from separate rocprofv3 --pmc passes of this bench), or None when no
-    pass of this workload is recorded."""
+    (profiles/pmc_traffic.json, tools/pmc_summary.py --traffic over separate
+    rocprofv3 --pmc passes of this bench), or None when no pass of this
+    workload and kernel is recorded."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as fh:
@@ -92,45 +123,87 @@ def pmc_traffic(kernel, workload):
     return row["bytes_per_launch"], "profiles/pmc_traffic.json (%s)" % row.get("source", "?")
 
 
-def dense_resolve_kernel(word_bits, world=1):
-    """Name of the dense resolve kernel the library launches for the bench
-    shape (power-of-two heaps, base >= 8): over the live-group lists, the
-    software-pipelined eight-prefixes-per-lane form on the 16-bit table (the
-    solve reports word_bits 16), else the four-prefixes-per-lane form, unless
-    the A/B knobs (GM_DENSE_RESOLVE / GM_DENSE_SWEEP / GM_DENSE_PIPE) select
-    another."""
-    if word_bits == 16:
-        return "k_dense_resolve8p" if world == 1 else "k_dense_resolve8c"
-    if os.environ.get("GM_DENSE_RESOLVE") == "scalar":
-        return "k_dense_resolve"
-    sweep = os.environ.get("GM_DENSE_SWEEP", "list")
-    if sweep == "cols":
-        return "k_dense_resolve4c"
-    if sweep == "walk":
-        return "k_dense_resolve4w"
-    if os.environ.get("GM_DENSE_PIPE") == "0":
-        return "k_dense_resolve4"
-    return "k_dense_resolve4p"
+def golden(name):
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "checksums.json")) as fh:
+            return json.load(fh).get(name)
+    except (OSError, ValueError):
+        return None
 
 
-def model_8d_bytes(positions, edges):
-    """SURVEY §8d per-position figure 36 + 20*b (whole solve)."""
-    return 36 * positions + 20 * edges
+def golden_for_params(game, params):
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "checksums.json")) as fh:
+            data = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    for e in data.values():
+        if e.get("game") == game and e.get("params") == params:
+            return e
+    return None
 
 
-def cpu_baseline(sample_heaps="31:31:31:31:31"):
-    """Oracle (one core, scalar C port) on a bounded sample: the same game
-    family at 2^25 positions (about 10-20 s)."""
-    from oracle.oracle import Game
-    g = Game("sum_four_to_one", "heaps=" + sample_heaps)
+def cpu_baseline(params):
+    """The multi-threaded CPU restatement (oracle_mt.c row solver, every
+    OpenMP thread of this host) on the same workload: solve time only
+    (reachability + retrograde of every position)."""
+    from oracle.oracle import Game, threads
+    g = Game("sum_four_to_one", params)
     t0 = time.perf_counter()
-    sol = g.solve(1 << 25)
+    sol = g.solve_rows()
     dt = time.perf_counter() - t0
-    return {"value": sol.count / dt, "unit": "positions/s", "cores": 1,
-            "kind": "port",
-            "sample": "oracle/ scalar C retrograde, sum_four_to_one heaps=%s "
-                      "(%d positions, %d edges, root %s), %.2f s"
-                      % (sample_heaps, sol.count, sol.edges, sol.root_line, dt)}
+    out = {"value": sol.count / dt, "unit": "positions/s", "cores": threads(),
+           "kind": "port",
+           "sample": "full workload: oracle/oracle_mt.c row solver (OpenMP, %d threads; "
+                     "host nproc %d), sum_four_to_one %s: %d positions, %d edges, root %s, %.2f s"
+                     % (threads(), os.cpu_count() or 0, params, sol.count, sol.edges,
+                        sol.root_line, dt)}
+    return out, sol.root_line
+
+
+def keyed_record(device):
+    """BASELINE config 3 as shipped: toot_and_otto_bitstring 6x4 on the
+    keyed-table path (one warm-up solve, one timed, one with kernel
+    timing), fingerprint vs tests/golden/checksums.json."""
+    from gamesmanmpi_amd.games import GameSpec
+    from gamesmanmpi_amd.solver import Solver
+    import torch
+    params = "length=6,height=4"
+    s = Solver(GameSpec("toot_and_otto_bitstring", params), device=device)
+    s.solve()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    r = s.solve()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    s.set_kernel_timing(True)
+    tr = s.solve()
+    s.set_kernel_timing(False)
+    fwd_b, bwd_b = keyed_bytes(r.positions, r.edges)
+    out = {"workload": "toot_and_otto_bitstring " + params,
+           "layout": r.extra["layout"],
+           "positions": r.positions, "edges": r.edges, "root": r.root_line,
+           "solve_ms": wall * 1e3, "positions_per_s": r.positions / wall,
+           "ms_forward": r.ms_forward, "ms_backward": r.ms_backward,
+           "kernels": {}}
+    for name, b, ms, n in (("expand", fwd_b, tr.ms_expand_kernels, tr.n_expand_launches),
+                           ("resolve", bwd_b, tr.ms_resolve_kernels, tr.n_resolve_launches)):
+        if n and ms > 0:
+            out["kernels"][name] = {"launches": n, "ms_total": ms,
+                                    "model_8d_bytes": b,
+                                    "achieved_GBps": b / (ms / 1e3) / 1e9,
+                                    "frac": b / (ms / 1e3) / 1e9 / HBM_PEAK_GBS}
+    out["model_8d_frac_whole_solve"] = (fwd_b + bwd_b) / wall / 1e9 / HBM_PEAK_GBS
+    e = golden("toot_6x4")
+    if e is not None:
+        ck = s.checksum()
+        out["parity"] = {"vs": "tests/golden/checksums.json toot_6x4 (oracle_mt)",
+                         "checksum": ck["checksum"],
+                         "ok": (ck["checksum"] == e["checksum"] and r.positions == e["positions"]
+                                and r.edges == e["edges"] and r.root_line == e["root_line"])}
+    del s
+    torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -141,6 +214,8 @@ def main():
     ap.add_argument("--heaps", default=None,
                     help="override the synthetic heaps, e.g. 31:31:31:31")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-keyed", action="store_true",
+                    help="skip the toot 6x4 keyed-table sub-record")
     ap.add_argument("--layout", default="auto", choices=["auto", "dense", "hashed"])
     args = ap.parse_args()
 
@@ -188,8 +263,6 @@ def main():
         elapsed = float(t.item())
     r = results[-1]
     layout = r.extra["layout"]
-    # whole-job position count: sharded results are already summed over ranks
-    positions_total = r.positions if world > 1 else r.positions
     P, E, root_value = expected(heaps)
     for x in results:
         if (x.positions, x.edges) != (P, E) or x.root_line.split()[0] != root_value:
@@ -201,26 +274,62 @@ def main():
     solver.set_kernel_timing(True)
     tr = solver.solve()
     solver.set_kernel_timing(False)
-    if world > 1:
-        tr_pos, tr_edges = tr.positions // world, tr.edges // world  # per GPU
-    else:
-        tr_pos, tr_edges = tr.positions, tr.edges
     word_bits = tr.extra.get("word_bits", 32) or 32
-    fwd_b, bwd_b = algorithmic_bytes(tr_pos, tr_edges, layout, word_bits // 8)
-    if tr.ms_resolve_kernels >= tr.ms_expand_kernels:
-        kname, kb, kms, kn = (dense_resolve_kernel(word_bits, world) if layout == "dense"
-                              else "k_resolve", bwd_b, tr.ms_resolve_kernels,
-                              tr.n_resolve_launches)
-    else:
-        kname, kb, kms, kn = ("k_dense_pull" if layout == "dense"
-                              else "k_expand", fwd_b, tr.ms_expand_kernels,
-                              tr.n_expand_launches)
-    achieved = (kb / kn) / (kms / kn / 1e3) / 1e9  # GB/s
     workload = "sum_four_to_one heaps=%s" % ":".join(map(str, heaps))
+    if layout == "dense":
+        model = dense_bytes(heaps if world == 1 else heaps[:-1] + [(heaps[-1] + 1) // world - 1],
+                            word_bits // 8)
+        resolve_k, pull_k = tr.extra.get("resolve_kernel", "?"), tr.extra.get("pull_kernel", "?")
+    else:
+        fwd, bwd = keyed_bytes(tr.positions // world, tr.edges // world)
+        model = {"resolve_compulsory": bwd, "pull_compulsory": fwd,
+                 "resolve_per_edge": bwd, "pull_per_edge": fwd}
+        resolve_k, pull_k = "k_resolve", "k_expand"
+    if tr.ms_resolve_kernels >= tr.ms_expand_kernels:
+        kname, kb, ke, kms, kn = (resolve_k, model["resolve_compulsory"], model["resolve_per_edge"],
+                                  tr.ms_resolve_kernels, tr.n_resolve_launches)
+    else:
+        kname, kb, ke, kms, kn = (pull_k, model["pull_compulsory"], model["pull_per_edge"],
+                                  tr.ms_expand_kernels, tr.n_expand_launches)
+    t_launch = kms / kn / 1e3  # seconds per launch
+    achieved = (kb / kn) / t_launch / 1e9  # GB/s
     traffic, traffic_src = pmc_traffic(kname, workload)
+    roof = {"bound": "hbm", "kernel": kname,
+            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "traffic_unit": "HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE)",
+            "traffic_source": traffic_src,
+            "frac_pmc": (traffic / t_launch / 1e9 / HBM_PEAK_GBS) if traffic else None,
+            "frac_per_edge_model": (ke / kn) / t_launch / 1e9 / HBM_PEAK_GBS,
+            "algorithmic_bytes_per_launch": kb / kn,
+            "per_edge_model_bytes_per_launch": ke / kn,
+            "model": ("compulsory bytes of the dense layout: resolve (3w + 1/8) B per position "
+                      "(own %d-bit word written, live words of rows L+1 and L+2 read once, reach "
+                      "bit); pull 3/8 B per position" % word_bits if layout == "dense" else
+                      "SURVEY 8d keyed: expand 24 B/position + 8 B/edge, resolve 12 B/position + 12 B/edge"),
+            "launches": kn, "ms_kernel_total": kms, "ms_per_launch": kms / kn,
+            "algorithmic_bytes_total": kb}
+
+    # root remoteness: the CPU restatement's solve of the same workload
+    root_ref, root_src = None, None
+    g = golden_for_params("sum_four_to_one", params)
+    if g is not None:
+        root_ref, root_src = g["root_line"], "tests/golden/checksums.json (oracle_mt)"
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu, cpu_root = cpu_baseline(params)
+        if root_ref is None:
+            root_ref, root_src = cpu_root, "cpu_baseline (oracle_mt) of this run"
+        elif cpu_root != root_ref:
+            raise SystemExit("CPU restatement disagrees with its golden: %s vs %s" % (cpu_root, root_ref))
+    if root_ref is not None:
+        for x in results + [tr]:
+            if x.root_line != root_ref:
+                raise SystemExit("WRONG ROOT: %s, the CPU restatement gives %s" % (x.root_line, root_ref))
+
     line = {
         "metric": "positions solved/sec (node)",
-        "value": positions_total * args.steps / elapsed,
+        "value": P * args.steps / elapsed,
         "unit": "positions/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -229,39 +338,27 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u64 keys / u%d words (integer)" % word_bits,
+        "dtype": ("u%d order-form words, integer (dense table: keys implicit in the slot)" % word_bits
+                  if layout == "dense" else "u64 keys / u32 words, integer"),
         "data": "synthetic: sum of Four-To-One heaps, fully determined state space",
         "config": {"workload": workload,
-                   "positions_per_gpu": r.positions // world, "edges_per_gpu": r.edges // world,
-                   "levels": r.levels, "root": r.root_line,
+                   "positions_per_gpu": P // world, "edges_per_gpu": E // world,
+                   "levels": r.levels, "root": r.root_line, "root_checked_against": root_src,
                    "layout": layout,
                    "parallelism": ("round-robin top-heap blocks x%d, RCCL halo exchange" % world
                                    if world > 1 else "1 GPU")},
-        "roofline": {"bound": "hbm", "kernel": kname,
-                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_unit": "HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE)",
-                     "traffic_source": traffic_src,
-                     "algorithmic_bytes_per_launch": kb / kn,
-                     "model": ("dense: resolve %.3f B/position + %d B/edge (%d-bit words), pull (edges + positions)/8 B"
-                               % (word_bits / 8 + 0.125, word_bits // 8, word_bits)
-                               if layout == "dense" else
-                               "SURVEY 8d keyed: expand 24 B/position + 8 B/edge, resolve 12 B/position + 12 B/edge"),
-                     "launches": kn, "ms_kernel_total": kms,
-                     "ms_per_launch": kms / kn,
-                     "algorithmic_bytes_total": kb},
+        "roofline": roof,
         "phase_ms": {"forward": r.ms_forward, "backward": r.ms_backward,
                      "solve_wall": r.ms_total,
                      "expand_kernels": tr.ms_expand_kernels,
                      "resolve_kernels": tr.ms_resolve_kernels},
-        "model_8d": {"bytes_per_position": model_8d_bytes(r.positions, r.edges) / r.positions,
-                     "equiv_GBps_per_gpu": model_8d_bytes(r.positions, r.edges) / world
-                     * args.steps / elapsed / 1e9,
-                     "frac_of_peak": model_8d_bytes(r.positions, r.edges) / world
-                     * args.steps / elapsed / 1e9 / HBM_PEAK_GBS},
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline()
+    if rank == 0 and world == 1 and not args.no_keyed:
+        del solver
+        torch.cuda.empty_cache()
+        line["keyed"] = keyed_record("cuda:%d" % local)
+    if cpu is not None:
+        line["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:

@@ -17,6 +17,16 @@ GM_EINVAL, GM_EHIP, GM_EFULL, GM_ECORRUPT, GM_ENOGPU = -1, -2, -3, -4, -5
 GM_PARTIAL = 1  # gm_solver_solve stopped at the gm_solver_set_steps bound
 GM_F_KERNEL_TIMING = 1
 GM_F_FORCE_HASHED = 2
+# kernel-family flags: given to gm_plan AND gm_buffers.flags (fixed for the
+# solver's lifetime; include/gamesman.h)
+GM_F_WORDS32 = 4
+GM_F_RESOLVE_SCALAR = 8
+GM_F_SHARD_INORDER = 16
+KERNEL_FLAGS = GM_F_WORDS32 | GM_F_RESOLVE_SCALAR | GM_F_SHARD_INORDER
+# gm_result.kernels codes (gm_solver.hip DenseResolveKind / DensePullKind)
+RESOLVE_KERNELS = {1: "k_dense_resolve8p", 2: "k_dense_resolve8c", 3: "k_dense_resolve4p",
+                   4: "k_dense_resolve4c", 5: "k_dense_resolve4", 6: "k_dense_resolve"}
+PULL_KERNELS = {1: "k_dense_pull_words", 2: "k_dense_pull"}
 GM_MODE_HASHED, GM_MODE_DENSE = 0, 1
 GM_MAXCHILD = 32
 GM_COMM_ID_BYTES = 128
@@ -51,7 +61,8 @@ class gm_buffers(ctypes.Structure):
                 ("scratch_bytes", ctypes.c_uint64),
                 ("stream", ctypes.c_void_p),
                 ("flags", ctypes.c_uint32),
-                ("mode", ctypes.c_uint32)]
+                ("mode", ctypes.c_uint32),
+                ("table_bytes", ctypes.c_uint64)]
 
 
 class gm_result(ctypes.Structure):
@@ -71,7 +82,7 @@ class gm_result(ctypes.Structure):
                 ("n_expand_launches", ctypes.c_uint64),
                 ("n_resolve_launches", ctypes.c_uint64),
                 ("word_bits", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint32)]
+                ("kernels", ctypes.c_uint32)]
 
 
 # every symbol include/gamesman.h declares (tests check the exports)
@@ -79,6 +90,7 @@ EXPORTS = (
     "gm_game_lookup", "gm_game_info", "gm_root", "gm_encode", "gm_decode",
     "gm_encode_batch", "gm_decode_batch", "gm_str_utf8", "gm_host_expand", "gm_host_level", "gm_symmetry", "gm_abi_sizes", "gm_plan", "gm_solver_create",
     "gm_solver_solve", "gm_solver_query", "gm_solver_positions",
+    "gm_solver_checksum",
     "gm_solver_destroy", "gm_solve", "gm_owner", "gm_owner_host",
     "gm_plan_shard", "gm_solver_create_shard", "gm_comm_unique_id",
     "gm_solver_comm_init", "gm_solve_group", "gm_solver_set_flags", "gm_solver_set_steps",
@@ -130,6 +142,7 @@ def load():
         "gm_solver_query": [c.c_void_p, c.c_void_p, c.c_uint64, c.c_void_p],
         "gm_solver_positions": [c.c_void_p, c.c_void_p, c.c_uint64,
                                 P(c.c_uint64)],
+        "gm_solver_checksum": [c.c_void_p, c.c_void_p],
         "gm_solve": [c.c_int, c.c_uint64, c.c_int, P(gm_buffers),
                      P(gm_result)],
         "gm_owner": [c.c_int, c.c_void_p, c.c_uint64, c.c_int, c.c_void_p,

@@ -7,22 +7,28 @@ counters, so a run restarts from the root.  Here a solve is 2T steps
 (forward levels 0..T-1, backward levels T-1..0; include/gamesman.h
 gm_solver_set_steps) and the whole of its state lives in three caller-owned
 device buffers -- table, level store, scratch.  A checkpoint is those
-buffers written to a directory after some step, plus the plan they were
-sized by; resuming loads them into a fresh solver of the same plan and runs
-the remaining steps.  The solution itself is identical to an uninterrupted
-solve (tests/test_gpu_checkpoint.py).
+buffers written to a directory after some step, plus the plan and the
+kernel-family flags they were sized by; resuming loads them into a fresh
+solver of the same plan and runs the remaining steps.  The solution is the
+oracle's (tests/test_gpu_checkpoint.py).
 
     save(solver, directory, step)          # after solve_steps(.., step) stopped
     solver, step = restore(directory)      # a fresh Solver holding the state
     result = solve_checkpointed(solver, directory, every=16)
 
 Layout of `directory`: meta.json, table.bin, levels.bin, scratch.bin (raw
-bytes of the buffers).  save() writes into `directory`.tmp and renames, so
-a crash mid-write leaves the previous checkpoint intact.
+bytes of the buffers).  Safety rules:
+  * a directory that exists and holds anything but a checkpoint of ours
+    (meta.json with our format, our .bin files) is refused, never touched;
+  * save() writes `directory`.tmp, then moves the previous checkpoint to
+    `directory`.old and the new one into place; only our own files are ever
+    removed.  A crash between the two moves leaves the previous checkpoint
+    in `directory`.old, which restore() and latest() fall back to;
+  * buffers stream to and from disk in fixed-size chunks through one pinned
+    host buffer: a checkpoint of a 200+ GB table needs no host copy of it.
 """
 import json
 import os
-import shutil
 
 import numpy as np
 
@@ -30,8 +36,14 @@ from . import _lib
 from .games import GameSpec
 from .solver import Solver
 
-FORMAT = 1
+FORMAT = 2
 _NAMES = ("table", "levels", "scratch")
+_OURS = {"meta.json"} | {n + ".bin" for n in _NAMES}
+CHUNK = 256 << 20  # bytes per host staging chunk
+
+
+class NotACheckpoint(ValueError):
+    """The directory exists and is not a checkpoint this module wrote."""
 
 
 def _plan_dict(solver):
@@ -43,31 +55,104 @@ def _plan_dict(solver):
             "max_levels": int(p.max_levels)}
 
 
+def is_checkpoint(directory):
+    """True if `directory` holds a checkpoint of this format."""
+    try:
+        read_meta(directory)
+        return True
+    except (OSError, ValueError):
+        return False
+
+
+def check_target(directory):
+    """Refuse a directory that exists, is not empty and is not one of our
+    checkpoints (raises NotACheckpoint; nothing is modified)."""
+    if not os.path.exists(directory):
+        return
+    if not os.path.isdir(directory):
+        raise NotACheckpoint("%s exists and is not a directory" % directory)
+    names = set(os.listdir(directory))
+    if not names:
+        return
+    if not is_checkpoint(directory) or not names <= _OURS:
+        raise NotACheckpoint("%s exists and holds files that are not a gamesmanmpi_amd "
+                             "checkpoint; refusing to overwrite it" % directory)
+
+
+def _remove_ours(directory):
+    """Delete only the files a checkpoint consists of, then the directory if
+    that left it empty."""
+    if not os.path.isdir(directory):
+        return
+    for n in _OURS:
+        try:
+            os.remove(os.path.join(directory, n))
+        except FileNotFoundError:
+            pass
+    try:
+        os.rmdir(directory)
+    except OSError:
+        pass
+
+
+def _stream_out(t, path, torch):
+    """Device tensor -> file, CHUNK bytes at a time through pinned memory."""
+    flat = t.view(torch.uint8).reshape(-1)
+    n = flat.numel()
+    stage = torch.empty(min(CHUNK, max(n, 1)), dtype=torch.uint8, pin_memory=True)
+    with open(path, "wb") as fh:
+        for a in range(0, n, CHUNK):
+            b = min(n, a + CHUNK)
+            stage[:b - a].copy_(flat[a:b])
+            fh.write(stage[:b - a].numpy().tobytes())
+
+
+def _stream_in(t, path, torch):
+    flat = t.view(torch.uint8).reshape(-1)
+    n = flat.numel()
+    if os.path.getsize(path) != n:
+        raise ValueError("%s holds %d bytes, the plan %d" % (path, os.path.getsize(path), n))
+    stage = torch.empty(min(CHUNK, max(n, 1)), dtype=torch.uint8, pin_memory=True)
+    with open(path, "rb") as fh:
+        for a in range(0, n, CHUNK):
+            b = min(n, a + CHUNK)
+            raw = np.frombuffer(fh.read(b - a), dtype=np.uint8)
+            stage[:b - a].copy_(torch.from_numpy(raw))
+            flat[a:b].copy_(stage[:b - a])
+
+
 def save(solver, directory, step):
     """Write `solver`'s buffers after step `step` (its last solve_steps call
     stopped there) to `directory`."""
     if solver.world != 1:
         raise ValueError("checkpoints cover one-GPU solves")
-    solver.torch.cuda.synchronize(solver.device)
-    tmp = directory.rstrip("/") + ".tmp"
-    shutil.rmtree(tmp, ignore_errors=True)
+    directory = directory.rstrip("/")
+    check_target(directory)
+    torch = solver.torch
+    torch.cuda.synchronize(solver.device)
+    tmp, old = directory + ".tmp", directory + ".old"
+    check_target(tmp)
+    check_target(old)
+    _remove_ours(tmp)
     os.makedirs(tmp)
     for name, t in zip(_NAMES, solver.buffers):
-        t.cpu().numpy().view(np.uint8).tofile(os.path.join(tmp, name + ".bin"))
+        _stream_out(t, os.path.join(tmp, name + ".bin"), torch)
     meta = {"format": FORMAT, "game": solver.spec.name,
             "params": solver.spec.params, "layout": solver.layout,
             "positions_hint": solver.positions_hint,
             "max_table_bytes": solver.max_table_bytes,
+            "flags": solver.flags,
             "plan": _plan_dict(solver), "step": int(step),
             "steps": solver.steps}
     with open(os.path.join(tmp, "meta.json"), "w") as fh:
         json.dump(meta, fh, indent=1)
-    old = directory.rstrip("/") + ".old"
-    shutil.rmtree(old, ignore_errors=True)
-    if os.path.isdir(directory):
+    _remove_ours(old)
+    if os.path.isdir(directory) and os.listdir(directory):
         os.replace(directory, old)
+    elif os.path.isdir(directory):
+        os.rmdir(directory)
     os.replace(tmp, directory)
-    shutil.rmtree(old, ignore_errors=True)
+    _remove_ours(old)
 
 
 def read_meta(directory):
@@ -78,42 +163,68 @@ def read_meta(directory):
     return meta
 
 
+def latest(directory):
+    """The directory holding the newest complete checkpoint: `directory`,
+    or `directory`.old when a save was interrupted between its two moves;
+    None if neither holds one."""
+    directory = directory.rstrip("/")
+    for d in (directory, directory + ".old"):
+        if is_checkpoint(d):
+            return d
+    return None
+
+
 def restore(directory, device=None):
     """A fresh Solver holding the checkpointed state, and the step to
-    resume at."""
+    resume at.  The plan and the kernel-family flags come from meta.json,
+    not from the environment."""
     import torch
-    meta = read_meta(directory)
+    src = latest(directory)
+    if src is None:
+        raise FileNotFoundError("no checkpoint in %s (or %s.old)" % (directory, directory.rstrip("/")))
+    meta = read_meta(src)
     spec = GameSpec(meta["game"], meta["params"])
     solver = Solver(spec, positions=meta["positions_hint"], device=device,
                     layout=meta["layout"],
-                    max_table_bytes=meta["max_table_bytes"])
+                    max_table_bytes=meta["max_table_bytes"],
+                    flags=meta.get("flags", 0))
     if _plan_dict(solver) != meta["plan"]:
         raise ValueError("checkpoint plan %r does not match this build's %r"
                          % (meta["plan"], _plan_dict(solver)))
     for name, t in zip(_NAMES, solver.buffers):
-        raw = np.fromfile(os.path.join(directory, name + ".bin"), dtype=np.uint8)
-        dst = t.view(torch.uint8).reshape(-1)
-        if raw.size != dst.numel():
-            raise ValueError("%s.bin holds %d bytes, the plan %d"
-                             % (name, raw.size, dst.numel()))
-        dst.copy_(torch.from_numpy(raw))
+        _stream_in(t, os.path.join(src, name + ".bin"), torch)
     torch.cuda.synchronize(solver.device)
     return solver, int(meta["step"])
 
 
-def solve_checkpointed(solver, directory, every, first=0, keep=False):
+def solve_checkpointed(solver, directory, every, first=0, keep=False, max_regrow=4):
     """Run `solver` from step `first` to the end, checkpointing into
-    `directory` every `every` steps; removes the checkpoint when the solve
-    completes unless keep=True."""
+    `directory` every `every` steps; removes the checkpoint's files when the
+    solve completes unless keep=True.  A keyed table that fills during the
+    forward pass (positions_hint too small) is regrown and the solve
+    restarted from step 0, as Solver.solve() does; a resumed solve
+    (first > 0) cannot regrow and raises TableFull."""
     if every < 1:
         raise ValueError("every must be >= 1")
+    check_target(directory)
     step, total = int(first), solver.steps
+    grown = 0
     while True:
         stop = step + every
-        r = solver.solve_steps(step, stop if stop < total else 0)
+        try:
+            r = solver.solve_steps(step, stop if stop < total else 0)
+        except _lib.TableFull:
+            if first > 0 or grown >= max_regrow:
+                raise
+            grown += 1
+            solver.positions_hint *= 2
+            solver._alloc(solver.positions_hint)
+            step = 0
+            continue
         if r is not None:
             if not keep:
-                shutil.rmtree(directory, ignore_errors=True)
+                _remove_ours(directory.rstrip("/"))
+                _remove_ours(directory.rstrip("/") + ".old")
             return r
         save(solver, directory, stop)
         step = stop

@@ -125,4 +125,23 @@ GM_HD int str_utf8_from_key(const Desc& d, uint64_t k, uint8_t* out) {
   return canon_from_key(d, k, out);  // str(int)
 }
 
+// Order-independent fingerprint of one solved position: FNV-1a over its
+// canonical bytes, then a mix with its value and remoteness.  A solve's
+// checksum is the sum (mod 2^64) over every reachable position, so it is
+// independent of storage order, layout and sharding (shards add up), and
+// equal to oracle/oracle_mt.c's ck_term sum over the same positions.
+GM_HD uint64_t pos_checksum(const uint8_t* c, int n, uint32_t value, uint32_t rem) {
+  uint64_t a = 0xcbf29ce484222325ull;
+  for (int i = 0; i < n; i++) {
+    a ^= c[i];
+    a *= 0x100000001b3ull;
+  }
+  a ^= (uint64_t)n << 56;
+  a = a * 0x9E3779B97F4A7C15ull + ((uint64_t)value << 40) + rem;
+  a ^= a >> 29;
+  a *= 0xBF58476D1CE4E5B9ull;
+  a ^= a >> 32;
+  return a;
+}
+
 }  // namespace gm

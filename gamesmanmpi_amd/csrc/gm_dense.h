@@ -214,7 +214,7 @@ __device__ __forceinline__ u64 bits64_at(const u64* bits, u64 pos) {
   return sh ? (lo >> sh) | (bits[w + 1] << (64 - sh)) : lo;
 }
 
-// Column-job tables (k_dense_resolve8c / k_dense_resolve4c / k_dense_pull_cols)
+// Column-job tables (k_dense_resolve8c / k_dense_resolve4c)
 constexpr int kMaxColJobs = 96;
 struct ColJobs {
   uint32_t n;                     // slices
@@ -302,42 +302,6 @@ __global__ __launch_bounds__(256) void k_dense_pull_words(Desc d, DenseView v, u
     if (!run) continue;  // another launch's slice, or a halo
     const u64 V0 = qi + 64 > v.p_hi ? (1ull << (v.p_hi - qi)) - 1 : ~0ull;
     pull_word<MAXH>(d, v.Wbl, bits, L, root_p, q, pg, V0, M, M);
-  }
-}
-
-// Column jobs (shards): the words of each listed slice's live 256-prefix
-// columns only (ColJobs, as k_dense_resolve8c), instead of every word of
-// the slices' band.  Words of dead columns hold only holes, which readers
-// mask.  The job tables go to LDS with the mask tables; a thread finds its
-// column by a binary search there.
-template <int MAXH>
-__global__ __launch_bounds__(256) void k_dense_pull_cols(Desc d, RowGeom g, u64* bits, u64 L, u64 root_p,
-                                                         const u64* __restrict__ masks,
-                                                         const uint32_t* __restrict__ colperm, ColJobs J) {
-  __shared__ u64 M[64 * (MAXH + 1)];
-  __shared__ uint32_t cum[kMaxColJobs + 1], lo[kMaxColJobs], us[kMaxColJobs], ts[kMaxColJobs];
-  for (int k = threadIdx.x; k < 64 * (MAXH + 1); k += blockDim.x) M[k] = masks[k];
-  for (int k = threadIdx.x; k <= (int)J.n; k += blockDim.x) {
-    cum[k] = J.cum[k];
-    if (k < (int)J.n) {
-      lo[k] = J.lo[k];
-      us[k] = J.u[k];
-      ts[k] = J.t[k];
-    }
-  }
-  __syncthreads();
-  const u64 nwords = (u64)cum[J.n] * 4;
-  for (u64 gi = (u64)blockIdx.x * blockDim.x + threadIdx.x; gi < nwords; gi += (u64)gridDim.x * blockDim.x) {
-    const uint32_t c = (uint32_t)(gi >> 2);
-    uint32_t a = 0, b = J.n;  // slice i: cum[i] <= c < cum[i + 1]
-    while (b - a > 1) {
-      const uint32_t m = (a + b) >> 1;
-      if (cum[m] <= c) a = m;
-      else b = m;
-    }
-    const u64 k = colperm[lo[a] + (c - cum[a])];
-    const u64 off = k * 256 + ((gi & 3) << 6);
-    pull_word<MAXH>(d, g.Wbl, bits, L, root_p, (u64)us[a] * g.Z + off, (u64)ts[a] * g.Z + off, ~0ull, M, M);
   }
 }
 
@@ -547,16 +511,9 @@ __device__ __forceinline__ void lane_digits4(const Desc& d, uint32_t (&hl)[MAXH]
     sl += hl[i];
   }
 }
-// WALK (a wave walks one column up the top digit, k_dense_resolve4w): the
-// top-digit children come from the previous steps' own-prefix quads, kept
-// in registers -- H1 = row L+1 at top - 1, H2b = row L+2 at top - 2 (H2a =
-// row L+2 at top - 1 shifts into it) -- instead of two loads 4-8 MB away.
-struct WalkHist {
-  u32x4 H1, H2a, H2b;
-};
-template <int MAXH, bool WALK = false>
+template <int MAXH>
 __device__ __forceinline__ void resolve_quad(const Desc& d, Quad4& Q, const uint32_t (&hl)[MAXH], uint32_t sl, u64 q,
-                                             u64 pw, u64 qi, u64 qlo, u64 qhi, WalkHist* wh = nullptr) {
+                                             u64 pw, u64 qi, u64 qlo, u64 qhi) {
   const uint32_t S = Q.S;
   uint32_t h[MAXH];
   uint32_t s = sl;
@@ -574,32 +531,11 @@ __device__ __forceinline__ void resolve_quad(const Desc& d, Quad4& Q, const uint
     const bool ok = qi + e >= qlo && qi + e < qhi && se <= S && S - se <= Q.H0;
     valid |= (uint32_t)ok << e;
   }
-  u32x4 A1, A2;
-  if (WALK) {  // the history needs this step's quads even when nothing here resolves
-    A1 = Q.n1.at(q, true);
-    A2 = Q.n2.at(q, true);
-  }
-  auto shift = [&]() {
-    if (WALK) {
-      wh->H2b = wh->H2a;
-      wh->H2a = A2;
-      wh->H1 = A1;
-    }
-  };
-  if (!__ballot(valid != 0)) {  // a wave of holes
-    shift();
-    return;
-  }
-  if (!valid) {
-    shift();
-    return;
-  }
+  if (!__ballot(valid != 0)) return;  // a wave of holes
+  if (!valid) return;
   const u64 bw = (Q.Lb + q) >> 6;
   const uint32_t rbits = (uint32_t)(Q.bits[bw] >> ((Q.Lb + q) & 63)) & 15u;
-  if (!WALK) {
-    A1 = Q.n1.at(q, true);
-    A2 = Q.n2.at(q, true);
-  }
+  const u32x4 A1 = Q.n1.at(q, true), A2 = Q.n2.at(q, true);
 #ifdef GM_DIAG_SKIP
   constexpr uint32_t kDiag = GM_DIAG_SKIP;
 #else
@@ -607,16 +543,9 @@ __device__ __forceinline__ void resolve_quad(const Desc& d, Quad4& Q, const uint
 #endif
   u32x4 P1 = Q.n1.at(q - 4, !(kDiag & 64) && q >= 4), P2 = Q.n2.at(q - 4, !(kDiag & 64) && q >= 4);
   u32x4 C1[MAXH], C2[MAXH];
-  constexpr int TOPI = MAXH - 1;  // WALK: exact heap count (MAXH <= 8)
 #pragma unroll
   for (int i = 2; i < MAXH; i++) {
     const bool live = (MAXH <= 8) || i < d.nheaps;
-    if (WALK && i == TOPI) {
-      const u32x4 z = {0u, 0u, 0u, 0u};
-      C1[i] = h[i] >= 1 ? wh->H1 : z;
-      C2[i] = h[i] >= 2 ? wh->H2b : z;
-      continue;
-    }
     const bool on = !((kDiag >> i) & 1u);
     C1[i] = Q.n1.at(q - d.pstride[i], on && live && h[i] >= 1);
     C2[i] = Q.n2.at(q - 2 * d.pstride[i], on && live && h[i] >= 2);
@@ -652,7 +581,6 @@ __device__ __forceinline__ void resolve_quad(const Desc& d, Quad4& Q, const uint
     for (int e = 0; e < 4; e++)
       if ((valid >> e) & 1u) Q.mine[q + e] = out[e];
   }
-  shift();
 }
 // Software-pipelined form (k_dense_resolve4p): quad_issue computes a
 // lane's digits and issues every load of one group; quad_finish reduces and
@@ -1098,62 +1026,6 @@ __global__ __launch_bounds__(256) void k_dense_resolve8c(Desc d, RowGeom g, uint
   }
   block_count(bc, (u64)Q.npos, (u64)Q.edges);
   if (Q.S == 0) block_add(&st->prims, (u64)Q.npos);  // one launch per solve
-}
-
-// Column walks (world 1): a wave takes one column k and walks up to
-// kWalkSeg consecutive top values t of it, carrying the top-digit children
-// in registers (WalkHist).  Items are ordered by the column's digit sum g
-// (colperm order): every column of sum g is live for the same top range
-// [tlo(g), thi(g)] at level L and splits into the same number of segments,
-// so item w -> (g, column, segment) is a scalar search over the per-level
-// prefix counts IC (kernel arguments) and two divisions.
-constexpr int kWalkSeg = 8;
-constexpr int kMaxWalkG = 128;
-struct WalkJobs {
-  uint32_t ng;                  // digit sums g0 .. g0 + ng - 1
-  uint32_t g0;
-  uint32_t IC[kMaxWalkG + 1];   // items before sum g0 + i
-  uint32_t CS[kMaxWalkG];       // colperm start of sum g0 + i
-};
-template <int MAXH>
-__global__ __launch_bounds__(256) void k_dense_resolve4w(Desc d, RowGeom g, uint32_t* words, const u64* bits, u64 L,
-                                                         DevState* st, const uint32_t* __restrict__ colperm,
-                                                         WalkJobs J) {
-  Quad4 Q;
-  quad_init(Q, d, words, bits, L, g.Wl, g.Wbl);
-  uint32_t hl[MAXH], sl;
-  lane_digits4<MAXH>(d, hl, sl);
-  constexpr int TOPI = MAXH - 1;
-  const int64_t S = (int64_t)Q.S, H0 = (int64_t)d.heap[0], E1 = (int64_t)d.heap[TOPI];
-  int mj = 0;
-  for (int i = 1; i < TOPI; i++) mj += (int)((255u >> d.pshift[i]) & (d.base[i] - 1));
-  const u64 lane_off = 4ull * __lane_id();
-  const XcdRange r = xcd_range((u64)J.IC[J.ng] * 64);
-  for (u64 iu = r.first; iu < r.end; iu += r.stride) {
-    const uint32_t w = __builtin_amdgcn_readfirstlane((uint32_t)(iu >> 6));
-    uint32_t a = 0, b = J.ng;
-    while (b - a > 1) {
-      const uint32_t m = (a + b) >> 1;
-      if (J.IC[m] <= w) a = m;
-      else b = m;
-    }
-    const int64_t gs = (int64_t)J.g0 + a;
-    const int64_t tlo = max((int64_t)0, S - H0 - mj - gs), thi = min(E1, S - gs);
-    const uint32_t ns = (uint32_t)((thi - tlo + kWalkSeg) / kWalkSeg);
-    const uint32_t rr = w - J.IC[a], ci = rr / ns, seg = rr - ci * ns;
-    const u64 k = colperm[J.CS[a] + ci];
-    const int64_t t0 = tlo + (int64_t)seg * kWalkSeg, t1 = min(t0 + kWalkSeg, thi + 1);
-    const u64 qk = k * 256 + lane_off;
-    WalkHist wh;
-    wh.H1 = Q.n1.at((u64)(t0 - 1) * g.Z + qk, t0 >= 1);
-    wh.H2a = Q.n2.at((u64)(t0 - 1) * g.Z + qk, t0 >= 1);
-    wh.H2b = Q.n2.at((u64)(t0 - 2) * g.Z + qk, t0 >= 2);
-    for (int64_t t = t0; t < t1; t++) {
-      const u64 gb = (u64)t * g.Z + k * 256;
-      resolve_quad<MAXH, true>(d, Q, hl, sl, gb + lane_off, gb, lane_off, 0, 256, &wh);
-    }
-  }
-  quad_done(Q, st);
 }
 
 // Packed word halos (shards, gm_solver.hip exchange_words): the non-hole

@@ -232,7 +232,8 @@ static int build_desc(const char* name, const char* params, Desc* out) {
 // halo slices [kB-2, kB) (children: one move lowers a heap by 1 or 2) and
 // [kB+B, kB+B+2) (parents, for the pull-form forward pass).  B = 8 when
 // every rank gets at least two blocks, else ceil(E / world) (one block per
-// rank); GM_SHARD_BLOCK overrides.
+// rank).  The geometry is a function of (descriptor, rank, world) alone, so
+// every rank derives the same halo sizes.
 struct DenseGeom {
   DenseView v;
   u64 nblocks, nb;
@@ -243,7 +244,6 @@ static int dense_geom(const Desc* d, int rank, int world, DenseGeom* g) {
     g->v.p_lo = 0;
     g->v.p_hi = d->W;
     g->v.Wl = d->W;
-    if (const char* e = getenv("GM_ROW_PAD")) g->v.Wl += (u64)atoll(e) & ~3ull;  // A/B: row stride padding (words)
     g->v.Wbl = (d->W + 63) & ~63ull;
     g->v.world = 1;
     g->v.zshift = -1;
@@ -255,8 +255,7 @@ static int dense_geom(const Desc* d, int rank, int world, DenseGeom* g) {
   const int k = d->nheaps - 1;
   const u64 E = d->base[k], Z = d->pstride[k];
   if (Z % 64) return fail(GM_EINVAL, "shard slices must hold a multiple of 64 prefixes (got %llu)", (unsigned long long)Z);
-  u64 B = E >= 16 * (u64)world ? 8 : (E + world - 1) / world;
-  if (const char* e = getenv("GM_SHARD_BLOCK")) B = (u64)atoll(e);
+  const u64 B = E >= 16 * (u64)world ? 8 : (E + world - 1) / world;
   const u64 nblocks = B ? (E + B - 1) / B : 0;
   if (B < 2 || nblocks < (u64)world)
     return fail(GM_EINVAL, "top heap of %llu values cannot give %d ranks blocks of >= 2", (unsigned long long)E, world);
@@ -281,8 +280,7 @@ static int dense_geom(const Desc* d, int rank, int world, DenseGeom* g) {
   v.p_hi = v.Wl;
   return 0;
 }
-static bool dense_resolve_knob_set();
-static bool dense_plan16(const Desc* d, int world);
+static bool dense_plan16(const Desc* d, int world, uint32_t flags);
 // word area of a dense table: 16-bit order forms when the plan chose them
 // (dense_plan16: one-GPU K_SUM tables the octet kernels handle), else 32-bit
 static u64 dense_words_bytes(const Desc* d, const DenseGeom& g, bool w16) {
@@ -317,6 +315,7 @@ struct DevState {
   u64 red[5];     // cross-shard reduction: positions, edges, prims, root word + 1, err
   uint32_t word_bits;  // dense: table word width of the solve in progress (resume reads it back)
   uint32_t pad_;
+  u64 ck[6];        // gm_solver_checksum: checksum, positions, W, L, T, D
   LevelSeg seg[1];  // [max_levels + 2]
 };
 static size_t devstate_bytes(int max_levels) {
@@ -412,15 +411,16 @@ static GroupGeom group_geom(const Desc* d, int world) {
   return g;
 }
 // Plan-time choice of 16-bit table words (half the HBM of the word area):
-// one-GPU tables whose solves run the octet kernel (run_dense's w16 rule)
-// unless GM_WORDS32 or a 32-bit resolve knob is set when the solver is
-// planned and created.  A solve of such a table refuses 32-bit kernels.
-static bool dense_plan16(const Desc* d, int world) {
+// one-GPU tables the octet kernel (k_dense_resolve8p) can solve, unless the
+// plan flags ask for 32-bit words or the one-prefix kernel.  The same flags
+// must reach gm_solver_create_shard (gm_buffers.flags), which sizes the
+// table against them: a table planned with 16-bit words cannot be handed a
+// 32-bit kernel (GM_EINVAL at creation, never a fault).
+static bool dense_plan16(const Desc* d, int world, uint32_t flags) {
   if (world != 1 || d->kind != K_SUM || !d->pow2 || d->nheaps < 2 || d->nheaps > 8 || d->base[1] < 8 ||
       d->root_sum >= 0x7FFF || d->W * 2 > 0xFFFFFFF0ull || !group_geom(d, 1).on)
     return false;
-  const char* w32 = getenv("GM_WORDS32");
-  return !(w32 && atoi(w32)) && !dense_resolve_knob_set();
+  return !(flags & (GM_F_WORDS32 | GM_F_RESOLVE_SCALAR));
 }
 static void group_sums(const Desc* d, const GroupGeom& g, std::vector<uint16_t>& gs) {
   gs.resize(g.groups);
@@ -800,8 +800,78 @@ __global__ void k_owner(Desc d, const u64* keys, u64 n, uint32_t P, uint32_t* ow
 #include "gm_keyed_shard.h"
 
 // ---------------------------------------------------------------------------
+// whole-solve fingerprint (gm_solver_checksum): per block partial sums of
+// pos_checksum and the value histogram, one atomic per block and field
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void ck_block_add(u64* acc, u64 (&v)[6]) {
+  __shared__ u64 part[16][6];
+#pragma unroll
+  for (int f = 0; f < 6; f++)
+    for (int o = 32; o > 0; o >>= 1) v[f] += __shfl_xor(v[f], o);
+  const int w = threadIdx.x >> 6;
+  if (__lane_id() == 0)
+    for (int f = 0; f < 6; f++) part[w][f] = v[f];
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    u64 t = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); i++) t += part[i][threadIdx.x];
+    if (t) atomicAdd(&acc[threadIdx.x], t);
+  }
+}
+__device__ __forceinline__ void ck_add(const Desc& d, u64 key, uint32_t word, u64 (&v)[6]) {
+  uint8_t c[40];
+  const int n = canon_from_key(d, key, c);
+  v[0] += pos_checksum(c, n, word & 3u, word >> 2);
+  v[1] += 1;
+  v[2 + (word & 3u)] += 1;
+}
+__global__ __launch_bounds__(256) void k_checksum_hashed(Desc d, const gm_slot* tab, u64 mask, const u64* lv, u64 lcap,
+                                                         const DevState* st, u64* acc) {
+  u64 v[6] = {0, 0, 0, 0, 0, 0};
+  const u64 nf = st->cursor_front, nb = st->cursor_back;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < nf + nb; i += (u64)gridDim.x * blockDim.x) {
+    const u64 key = i < nf ? lv[i] : lv[lcap - 1 - (i - nf)];
+    const u64 h = table_find(tab, mask, key);
+    ck_add(d, key, h == ~0ull ? NO_WORD : tab[h].word, v);
+  }
+  ck_block_add(acc, v);
+}
+__global__ __launch_bounds__(256) void k_checksum_dense(Desc d, DenseView v, const uint32_t* words, const u64* bits,
+                                                        u64 levels, bool w16, u64* acc) {
+  u64 a[6] = {0, 0, 0, 0, 0, 0};
+  const u64 n = v.Wl;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < levels * n; i += (u64)gridDim.x * blockDim.x) {
+    const u64 L = i / n, q = i - L * n;
+    bool run;
+    const u64 p = dense_global(v, q, &run);
+    if (!run) continue;
+    const int64_t h0 = dense_h0(d, L, p);
+    if (h0 < 0 || !reach_bit(bits, L * v.Wbl + q)) continue;
+    const uint32_t w = w16 ? dense_word16(((const uint16_t*)words)[L * v.Wl + q]) : dense_word(words[L * v.Wl + q]);
+    ck_add(d, p * d.base[0] + (u64)h0, w, a);
+  }
+  ck_block_add(acc, a);
+}
+
+// ---------------------------------------------------------------------------
 // solver object
 // ---------------------------------------------------------------------------
+// Dense kernel families, fixed when the solver is created (dense_choose,
+// from the descriptor, the shard geometry and the GM_F_* flags of
+// gm_buffers): nothing later -- no environment variable, no flag change --
+// can hand a table a kernel of another word width.  The codes are reported
+// in gm_result.kernels (resolve | pull << 16).
+enum DenseResolveKind : uint32_t {
+  RK_NONE = 0,
+  RK_OCT_LIST = 1,   // k_dense_resolve8p: world 1, 16-bit table, live-group lists
+  RK_OCT_COLS = 2,   // k_dense_resolve8c: shards, 16-bit table, column jobs
+  RK_QUAD_LIST = 3,  // k_dense_resolve4p: world 1, 32-bit table, live-group lists
+  RK_QUAD_COLS = 4,  // k_dense_resolve4c: shards, 32-bit table, column jobs
+  RK_QUAD_BAND = 5,  // k_dense_resolve4: 32-bit band sweeps (no list)
+  RK_SCALAR = 6,     // k_dense_resolve: one prefix per lane (any bases; GM_F_RESOLVE_SCALAR)
+};
+enum DensePullKind : uint32_t { PK_NONE = 0, PK_WORDS = 1, PK_LANE = 2 };
+
 struct gm_solver {
   Desc d;
   uint32_t mode;
@@ -847,6 +917,8 @@ struct gm_solver {
   uint32_t flags;
   int grid;
   uint32_t step_first = 0, step_stop = 0;  // gm_solver_set_steps (one solve)
+  uint32_t rk = RK_NONE, pk = PK_NONE;      // dense kernel families (dense_choose)
+  bool launch_err = false;                  // a launch found no kernel of the table's word width
 };
 
 static const int kBlock = 256;
@@ -891,24 +963,6 @@ static void do_resolve(gm_solver* s, int L) {
   }
 }
 
-// Kernel choice for power-of-two dense layouts (measured on MI355X, 2^30
-// solve): pull -- word-parallel 4.2 ms vs per-lane 46 ms.
-// GM_DENSE_PER_LANE=pull forces the per-lane pull (A/B runs).
-static bool dense_per_lane_pull() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("GM_DENSE_PER_LANE");
-    v = (e && (!strcmp(e, "pull") || atoi(e))) ? 1 : 0;
-  }
-  return v == 1;
-}
-// resolve: four prefixes per lane (k_dense_resolve4) unless
-// GM_DENSE_RESOLVE=scalar (A/B runs)
-static bool dense_scalar_resolve() {
-  const char* e = getenv("GM_DENSE_RESOLVE");  // read per launch: tests switch it in-process
-  return e && !strcmp(e, "scalar");
-}
-
 // Blocks of 256 threads of `kernel` that fit on the device at once (a
 // multiple of 8, one share per XCD): list sweeps launch exactly that many,
 // since blocks that start late would sweep their grid-stride items out of
@@ -928,39 +982,22 @@ static int resident_blocks(const void* kernel) {
   return r;
 }
 
-// world-1 quad resolve sweep: the level's live-group list (0, default),
-// column jobs (1, GM_DENSE_SWEEP=cols) or column walks (2, =walk)
-static int dense_sweep_mode() {
-  const char* e = getenv("GM_DENSE_SWEEP");
-  return !e ? 0 : !strcmp(e, "cols") ? 1 : !strcmp(e, "walk") ? 2 : 0;
-}
-static bool dense_sweep_cols() { return dense_sweep_mode() == 1; }
-// list sweep: software-pipelined kernel (default) or the plain one
-// (GM_DENSE_PIPE=0, A/B)
-static bool dense_pipelined() {
-  const char* e = getenv("GM_DENSE_PIPE");
-  return !(e && !strcmp(e, "0"));
-}
-// any A/B knob that selects a non-default (32-bit word) resolve kernel
-static bool dense_resolve_knob_set() { return dense_scalar_resolve() || dense_sweep_mode() != 0 || !dense_pipelined(); }
-
-// Column jobs of level L over the view's slices (a shard's listed slices,
-// or every top value of a single table): each slice's live columns are one
-// range of the digit-sum-sorted permutation.  False if no column is live.
+// Column jobs of level L over a shard view's listed slices: each slice's
+// live columns are one range of the digit-sum-sorted permutation.  False
+// if no column is live.
 static bool build_col_jobs(const gm_solver* s, const DenseView& v, u64 L, ColJobs& J) {
   J.n = 0;
   J.cum[0] = 0;
   const int64_t S = (int64_t)s->d.root_sum - (int64_t)L;
-  const uint32_t nsl = v.blk ? v.nsl : s->d.base[s->cg.top];
-  for (uint32_t i = 0; i < nsl; i++) {
-    const int64_t t = v.blk ? (int64_t)v.st[i] : (int64_t)i;
+  for (uint32_t i = 0; i < v.nsl; i++) {
+    const int64_t t = (int64_t)v.st[i];
     const int64_t hi = std::min<int64_t>(S - t, s->cg.maxgs);
     const int64_t lo = std::max<int64_t>(S - t - (int64_t)s->d.heap[0] - s->cg.mj, 0);
     if (hi < lo) continue;
     const uint32_t a = s->cstart[(size_t)lo], b = s->cstart[(size_t)hi + 1];
     if (a == b) continue;
     J.lo[J.n] = a;
-    J.u[J.n] = v.blk ? (uint32_t)v.sl[i] : i;
+    J.u[J.n] = (uint32_t)v.sl[i];
     J.t[J.n] = (uint32_t)t;
     J.cum[J.n + 1] = J.cum[J.n] + (b - a);
     J.n++;
@@ -968,30 +1005,15 @@ static bool build_col_jobs(const gm_solver* s, const DenseView& v, u64 L, ColJob
   return J.n > 0;
 }
 
+// Forward (pull): power-of-two tables run one thread per 64-prefix bitmap
+// word (k_dense_pull_words; world 1 over the level's live-group list), other
+// bases one prefix per lane (k_dense_pull).
 template <int MAXH, bool POW2>
 static void dense_launch_pull_t(gm_solver* s, const DenseView& v, int grid, u64 L, u64 root_p) {
-  // shards, A/B (GM_PULL_COLS=1): the listed slices' live columns only.
-  // Measured slower than the band sweep (9.6 vs 8.3 us per launch in the
-  // 2-shard group: the per-thread column search and permutation load cost
-  // more than the dead words they skip; profiles/r01_ab_pull_cols.jsonl)
-  if constexpr (POW2 && MAXH >= 3) {
-    const char* pc = getenv("GM_PULL_COLS");
-    if (pc && atoi(pc) && v.blk && s->colperm && v.nsl > 0 && v.nsl <= (uint32_t)kMaxColJobs &&
-        v.Z % 256 == 0 && !dense_per_lane_pull()) {
-      ColJobs J;
-      if (!build_col_jobs(s, v, L, J)) return;
-      const u64 words = (u64)J.cum[J.n] * 4;
-      const int g = (int)std::min<u64>((words + kBlock - 1) / kBlock, (u64)s->grid);
-      const RowGeom rg{v.Wl, v.Wbl, v.Z};
-      hipLaunchKernelGGL((k_dense_pull_cols<MAXH>), dim3(g), dim3(kBlock), 0, s->stream, s->d, rg, s->bits, L,
-                         root_p, s->masks, s->colperm, J);
-      return;
-    }
-  }
-  if (POW2 && !dense_per_lane_pull()) {  // word-parallel form: one thread per 64-prefix group
+  if (POW2 && s->pk == PK_WORDS) {
     const uint32_t* gl = nullptr;
     u64 groups = (v.p_hi - v.p_lo + 63) / 64;
-    if (s->glist && !v.blk && !getenv("GM_PULL_BAND")) {  // the level's live 256-prefix groups
+    if (s->glist && !v.blk) {  // the level's live 256-prefix groups
       gl = s->glist + s->goff[L];
       groups = (s->goff[L + 1] - s->goff[L]) * 4;
       if (!groups) return;
@@ -1004,117 +1026,84 @@ static void dense_launch_pull_t(gm_solver* s, const DenseView& v, int grid, u64 
   hipLaunchKernelGGL((k_dense_pull<MAXH, POW2>), dim3(grid), dim3(kBlock), 0, s->stream, s->d, v, s->bits, L,
                      root_p);
 }
+// Backward (resolve) by the family fixed at creation (s->rk, dense_choose).
 template <int MAXH, bool POW2>
 static void dense_launch_resolve_t(gm_solver* s, const DenseView& v, int grid, u64 L) {
-  // buffer loads need every row's byte offsets to fit 32 bits
-  // one grid-stride round per iteration: two rounds (24 loads in flight,
-  // fewer waves per SIMD) measured 21.6 vs 17.4 ms per 2^30 resolve.  The
-  // block-layout mapping (shards) is a separate instantiation so the
-  // single-table kernel carries none of it.
-  // quad form: pow2 digits with base[1] >= 4 (the four prefixes of a lane
-  // share every digit but the lowest), 32-bit row offsets, and waves of 256
-  // prefixes that never straddle a slice of a block layout
   if constexpr (POW2 && MAXH >= 2) {
-  if (s->d.nheaps >= 2 && s->d.base[1] >= 4 && v.Wl * 4 <= 0xFFFFFFF0ull && (!v.blk || v.Z % 256 == 0) &&
-      !dense_scalar_resolve()) {
-    const uint32_t* gl = nullptr;
-    u64 units = (v.p_hi - (v.p_lo & ~255ull) + 3) / 4;
-    if (s->glist && !v.blk && dense_sweep_mode() == 0) {  // live groups of level L, 64 units each
-      gl = s->glist + s->goff[L];
-      units = (s->goff[L + 1] - s->goff[L]) * 64;
-      if (!units) return;
-    }
-    // a grid of exactly the blocks that fit at once (a multiple of 8):
-    // blocks that start late would sweep their grid-stride items out of the
-    // list order the L2 reuse relies on
-    const int resident = resident_blocks((const void*)k_dense_resolve4<MAXH, false>);
-    // column walks (world 1, GM_DENSE_SWEEP=walk)
-    if constexpr (MAXH >= 3 && MAXH <= 8) {
-      if (s->colperm && !v.blk && dense_sweep_mode() == 2 && s->cg.maxgs + 1 <= kMaxWalkG) {
-        WalkJobs J;
-        J.g0 = 0;
-        J.ng = (uint32_t)s->cg.maxgs + 1;
-        J.IC[0] = 0;
-        const int64_t S = (int64_t)s->d.root_sum - (int64_t)L, H0 = s->d.heap[0];
-        const int64_t E1 = s->d.heap[s->cg.top];
-        for (uint32_t i = 0; i < J.ng; i++) {
-          const int64_t gs = i;
-          const int64_t tlo = std::max<int64_t>(0, S - H0 - s->cg.mj - gs), thi = std::min<int64_t>(E1, S - gs);
-          const u64 cnt = s->cstart[i + 1] - s->cstart[i];
-          const u64 ns = thi >= tlo ? (u64)((thi - tlo + kWalkSeg) / kWalkSeg) : 0;
-          J.IC[i + 1] = J.IC[i] + (uint32_t)(cnt * ns);
-          J.CS[i] = s->cstart[i];
-        }
-        if (!J.IC[J.ng]) return;
-        const u64 cu = (u64)J.IC[J.ng] * 64;
-        const int gc = (int)std::min<u64>(((cu + kBlock - 1) / kBlock + 7) & ~7ull, (u64)resident);
-        const RowGeom rg{v.Wl, v.Wbl, s->d.pstride[s->cg.top]};
-        hipLaunchKernelGGL((k_dense_resolve4w<MAXH>), dim3(gc), dim3(kBlock), 0, s->stream, s->d, rg, s->words,
-                           s->bits, L, s->st, s->colperm, J);
-        return;
+    if (s->rk != RK_SCALAR) {
+      const uint32_t* gl = nullptr;
+      u64 units = (v.p_hi - (v.p_lo & ~255ull) + 3) / 4;
+      if (s->glist && !v.blk) {  // live groups of level L, 64 units each
+        gl = s->glist + s->goff[L];
+        units = (s->goff[L + 1] - s->goff[L]) * 64;
+        if (!units) return;
       }
-    }
-    // column jobs: a shard's listed slices (or, with GM_DENSE_SWEEP=cols,
-    // every top value of a single table), each with its live columns
-    if constexpr (MAXH >= 3) {
-      const bool cols = s->colperm && (v.blk ? (v.nsl > 0 && v.nsl <= (uint32_t)kMaxColJobs)
-                                             : (dense_sweep_cols() && s->d.base[s->cg.top] <= (uint32_t)kMaxColJobs));
-      if (cols) {
-        ColJobs J;
-        if (!build_col_jobs(s, v, L, J)) return;
-        const RowGeom rg{v.Wl, v.Wbl, v.blk ? v.Z : s->d.pstride[s->cg.top]};
-        if (s->w16) {  // 16-bit shard table: octets, two columns per wave
-          const u64 cu8 = (u64)((J.cum[J.n] + 1) / 2) * 64;
-          const int g8 = (int)std::min<u64>(
-              std::min<u64>(((cu8 + kBlock - 1) / kBlock + 7) & ~7ull,
-                            (u64)resident_blocks((const void*)k_dense_resolve8c<MAXH>)),
-              (u64)kCountSlots);
-          hipLaunchKernelGGL((k_dense_resolve8c<MAXH>), dim3(g8), dim3(kBlock), 0, s->stream, s->d, rg,
-                             (uint16_t*)s->words, s->bits, L, s->st, s->colperm, J, s->bcount);
+      const int resident = resident_blocks((const void*)k_dense_resolve4<MAXH, false>);
+      // shards: column jobs over the level's listed slices (a view that
+      // lists no slices -- too many to list -- takes the band sweep)
+      if constexpr (MAXH >= 3) {
+        if (v.blk && s->colperm && v.nsl > 0 && v.nsl <= (uint32_t)kMaxColJobs) {
+          ColJobs J;
+          if (!build_col_jobs(s, v, L, J)) return;
+          const RowGeom rg{v.Wl, v.Wbl, v.Z};
+          if (s->w16) {  // 16-bit shard table: octets, two columns per wave
+            const u64 cu8 = (u64)((J.cum[J.n] + 1) / 2) * 64;
+            const int g8 = (int)std::min<u64>(
+                std::min<u64>(((cu8 + kBlock - 1) / kBlock + 7) & ~7ull,
+                              (u64)resident_blocks((const void*)k_dense_resolve8c<MAXH>)),
+                (u64)kCountSlots);
+            hipLaunchKernelGGL((k_dense_resolve8c<MAXH>), dim3(g8), dim3(kBlock), 0, s->stream, s->d, rg,
+                               (uint16_t*)s->words, s->bits, L, s->st, s->colperm, J, s->bcount);
+            return;
+          }
+          const u64 cu = (u64)J.cum[J.n] * 64;
+          const int gc = (int)std::min<u64>(((cu + kBlock - 1) / kBlock + 7) & ~7ull,
+                                            (u64)resident_blocks((const void*)k_dense_resolve4c<MAXH>));
+          hipLaunchKernelGGL((k_dense_resolve4c<MAXH>), dim3(gc), dim3(kBlock), 0, s->stream, s->d, rg, s->words,
+                             s->bits, L, s->st, s->colperm, J);
           return;
         }
-        const u64 cu = (u64)J.cum[J.n] * 64;
-        const int gc = (int)std::min<u64>(((cu + kBlock - 1) / kBlock + 7) & ~7ull,
-                                          (u64)resident_blocks((const void*)k_dense_resolve4c<MAXH>));
-        hipLaunchKernelGGL((k_dense_resolve4c<MAXH>), dim3(gc), dim3(kBlock), 0, s->stream, s->d, rg, s->words,
-                           s->bits, L, s->st, s->colperm, J);
+      }
+      if (s->w16) {
+        // 16-bit table: octets over the live-group list (world 1).  A 16-bit
+        // shard table always lists its slices (dense_choose), so reaching
+        // here without a list is a bug: flag it instead of running a kernel
+        // of the wrong word width.
+        if (!gl) {
+          s->launch_err = true;
+          return;
+        }
+        XcdShares xs;
+        for (int x = 0; x < 9; x++) xs.o[x] = s->gxcd[(size_t)L * 9 + x];
+        for (int x = 1; x < 8; x++) xs.o[x] &= ~1u;  // shares start at even entries: a wave = two whole groups
+        const u64 u8 = (u64)xs.o[8] * 32;
+        const int rp = resident_blocks((const void*)k_dense_resolve8p<MAXH>);
+        const int gp = (int)std::min<u64>(std::min<u64>(((u8 + kBlock - 1) / kBlock + 7) & ~7ull, (u64)rp),
+                                          (u64)kCountSlots);
+        hipLaunchKernelGGL((k_dense_resolve8p<MAXH>), dim3(gp), dim3(kBlock), 0, s->stream, s->d, v,
+                           (uint16_t*)s->words, s->bits, L, s->st, gl, xs, s->bcount);
         return;
       }
-    }
-    if (s->w16) {  // 16-bit table: octets over the live-group list (run_dense chose it for this solve)
-      XcdShares xs;
-      for (int x = 0; x < 9; x++) xs.o[x] = s->gxcd[(size_t)L * 9 + x];
-      for (int x = 1; x < 8; x++) xs.o[x] &= ~1u;  // shares start at even entries: a wave = two whole groups
-      const u64 u8 = (u64)xs.o[8] * 32;
-      const int rp = resident_blocks((const void*)k_dense_resolve8p<MAXH>);
-      const int gp = (int)std::min<u64>(std::min<u64>(((u8 + kBlock - 1) / kBlock + 7) & ~7ull, (u64)rp),
-                                        (u64)kCountSlots);
-      hipLaunchKernelGGL((k_dense_resolve8p<MAXH>), dim3(gp), dim3(kBlock), 0, s->stream, s->d, v,
-                         (uint16_t*)s->words, s->bits, L, s->st, gl, xs, s->bcount);
-      return;
-    }
-    const int g = (int)std::min<u64>(((units + kBlock - 1) / kBlock + 7) & ~7ull, (u64)resident);
-    if (gl) {
-      XcdShares xs;
-      for (int x = 0; x < 9; x++) xs.o[x] = s->gxcd[(size_t)L * 9 + x];
-      if (dense_pipelined()) {
+      const int g = (int)std::min<u64>(((units + kBlock - 1) / kBlock + 7) & ~7ull, (u64)resident);
+      if (gl) {  // 32-bit words over the list, software-pipelined
+        XcdShares xs;
+        for (int x = 0; x < 9; x++) xs.o[x] = s->gxcd[(size_t)L * 9 + x];
         const int rp = resident_blocks((const void*)k_dense_resolve4p<MAXH>);
         const int gp = (int)std::min<u64>(((units + kBlock - 1) / kBlock + 7) & ~7ull, (u64)rp);
         hipLaunchKernelGGL((k_dense_resolve4p<MAXH>), dim3(gp), dim3(kBlock), 0, s->stream, s->d, v, s->words,
                            s->bits, L, s->st, gl, xs);
-      } else {
+      } else if (v.blk)
+        hipLaunchKernelGGL((k_dense_resolve4<MAXH, true>), dim3(g), dim3(kBlock), 0, s->stream, s->d, v, s->words,
+                           s->bits, L, s->st, nullptr, XcdShares{});
+      else
         hipLaunchKernelGGL((k_dense_resolve4<MAXH, false>), dim3(g), dim3(kBlock), 0, s->stream, s->d, v, s->words,
-                           s->bits, L, s->st, gl, xs);
-      }
+                           s->bits, L, s->st, nullptr, XcdShares{});
+      return;
     }
-    else if (v.blk)
-      hipLaunchKernelGGL((k_dense_resolve4<MAXH, true>), dim3(g), dim3(kBlock), 0, s->stream, s->d, v, s->words,
-                         s->bits, L, s->st, nullptr, XcdShares{});
-    else
-      hipLaunchKernelGGL((k_dense_resolve4<MAXH, false>), dim3(g), dim3(kBlock), 0, s->stream, s->d, v, s->words,
-                         s->bits, L, s->st, nullptr, XcdShares{});
-    return;
   }
+  if (s->w16) {  // never chosen with the one-prefix kernel (dense_choose)
+    s->launch_err = true;
+    return;
   }
   if (v.blk)
     hipLaunchKernelGGL((k_dense_resolve<MAXH, POW2, true, 1, true>), dim3(grid), dim3(kBlock), 0, s->stream, s->d,
@@ -1381,11 +1370,12 @@ int gm_owner_host(int game, const uint64_t* keys, size_t n, int world_size, uint
   return 0;
 }
 
-static int plan_dense(const Desc* d, int rank, int world, uint64_t max_table_bytes, gm_plan_t* out, bool* fits) {
+static int plan_dense(const Desc* d, int rank, int world, uint32_t flags, uint64_t max_table_bytes, gm_plan_t* out,
+                      bool* fits) {
   DenseGeom g;
   int rc = dense_geom(d, rank, world, &g);
   if (rc) return rc;
-  const u64 bytes = dense_words_bytes(d, g, dense_plan16(d, world)) + dense_bits_bytes(d, g);
+  const u64 bytes = dense_words_bytes(d, g, dense_plan16(d, world, flags)) + dense_bits_bytes(d, g);
   *fits = max_table_bytes == 0 || bytes <= max_table_bytes;
   out->mode = GM_MODE_DENSE;
   out->table_slots = (u64)d->max_levels * g.v.Wl;
@@ -1419,7 +1409,7 @@ int gm_plan_shard(int game, int rank, int world, uint32_t flags, uint64_t max_ta
   if (grc) return grc;
   out->scratch_bytes += halo_bytes(halo_geom(d, world, g.nb)) + col_bytes(d);
   bool fits = false;
-  int rc = plan_dense(d, rank, world, max_table_bytes, out, &fits);
+  int rc = plan_dense(d, rank, world, flags, max_table_bytes, out, &fits);
   if (rc) return rc;
   if (!fits) return fail(GM_EFULL, "dense shard needs %llu bytes", (unsigned long long)out->table_bytes);
   return 0;
@@ -1433,7 +1423,7 @@ int gm_plan(int game, uint64_t positions, uint32_t flags, uint64_t max_table_byt
   out->scratch_bytes = scratch_bytes_for(d->max_levels);
   if (d->dense_ok && !(flags & GM_F_FORCE_HASHED)) {
     bool fits = false;
-    int rc = plan_dense(d, 0, 1, max_table_bytes, out, &fits);
+    int rc = plan_dense(d, 0, 1, flags, max_table_bytes, out, &fits);
     if (rc) return rc;
     out->scratch_bytes += col_bytes(d) + group_bytes(d, 1);
     if (fits) return 0;
@@ -1509,6 +1499,39 @@ static void build_halo_cols(const Desc& d, const HaloGeom& h, const std::vector<
   }
 }
 
+static u64 blk_count(const gm_solver* s);
+// Kernel families of a dense solver (DenseResolveKind / DensePullKind),
+// chosen once from the descriptor, the geometry, the scratch the caller
+// provided and the flags.  16-bit tables: world 1 needs the live-group
+// lists (octets sweep only listed groups); shards need the column
+// permutation, packed 16-bit halos and every level's slices in one job list.
+static int dense_choose(gm_solver* s) {
+  const Desc& d = s->d;
+  const DenseView& v = s->view;
+  s->pk = d.pow2 ? PK_WORDS : PK_LANE;
+  const bool scalar = (s->flags & GM_F_RESOLVE_SCALAR) != 0;
+  const bool quad = d.pow2 && d.nheaps >= 2 && d.base[1] >= 4 && v.Wl * 4 <= 0xFFFFFFF0ull && (!v.blk || v.Z % 256 == 0);
+  const bool base16 = d.pow2 && d.kind == K_SUM && d.nheaps >= 2 && d.nheaps <= 8 && d.base[1] >= 8 &&
+                      d.root_sum < 0x7FFF && v.Wl * 2 <= 0xFFFFFFF0ull &&
+                      !(s->flags & (GM_F_WORDS32 | GM_F_RESOLVE_SCALAR));
+  if (!v.blk) {
+    if (s->plan16) {
+      if (!s->glist)
+        return fail(GM_EINVAL, "16-bit dense table without live-group lists: scratch smaller than gm_plan's");
+      s->w16 = true;
+      s->rk = RK_OCT_LIST;
+      return 0;
+    }
+    s->w16 = false;
+    s->rk = (scalar || !quad) ? RK_SCALAR : s->glist ? RK_QUAD_LIST : RK_QUAD_BAND;
+    return 0;
+  }
+  s->w16 = base16 && d.nheaps >= 3 && s->colperm && s->hg.on && s->halo16 && v.Z % 256 == 0 && v.E <= 0xFFFF &&
+           blk_count(s) * (v.B + 4) <= (u64)kMaxColJobs;
+  s->rk = s->w16 ? RK_OCT_COLS : (scalar || !quad) ? RK_SCALAR : s->colperm ? RK_QUAD_COLS : RK_QUAD_BAND;
+  return 0;
+}
+
 int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf, gm_solver** out) {
   const Desc* d = get_game(game);
   if (!d || !buf || !out) return fail(GM_EINVAL, "bad argument");
@@ -1521,11 +1544,20 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
     int rc = dense_geom(d, rank, world, &g);
     if (rc) return rc;
     if (buf->table_slots != (u64)d->max_levels * g.v.Wl) return fail(GM_EINVAL, "dense table must hold levels * Wl words (use gm_plan_shard)");
+    // the word width follows from the flags: a table planned with 16-bit
+    // words is too small for the 32-bit kernels other flags select
+    const u64 need = dense_words_bytes(d, g, dense_plan16(d, world, buf->flags)) + dense_bits_bytes(d, g);
+    if (buf->table_bytes < need)
+      return fail(GM_EINVAL, "dense table of %llu bytes, these flags need %llu (plan with the flags the solver is "
+                             "created with)", (unsigned long long)buf->table_bytes, (unsigned long long)need);
   } else if (buf->mode == GM_MODE_HASHED) {
     if (world < 1 || rank < 0 || rank >= world) return fail(GM_EINVAL, "bad shard %d/%d", rank, world);
     if (!buf->levels || buf->level_capacity < 1) return fail(GM_EINVAL, "null level store");
     if (buf->table_slots < 2 || (buf->table_slots & (buf->table_slots - 1)))
       return fail(GM_EINVAL, "table_slots must be a power of two");
+    if (buf->table_bytes < buf->table_slots * sizeof(gm_slot))
+      return fail(GM_EINVAL, "keyed table of %llu bytes holds fewer than %llu slots",
+                  (unsigned long long)buf->table_bytes, (unsigned long long)buf->table_slots);
   } else {
     return fail(GM_EINVAL, "unknown mode %u", buf->mode);
   }
@@ -1537,7 +1569,7 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
   s->words = (uint32_t*)buf->table;
   s->nslots = buf->table_slots;
   s->view = g.v;
-  s->plan16 = buf->mode == GM_MODE_DENSE && dense_plan16(d, world);
+  s->plan16 = buf->mode == GM_MODE_DENSE && dense_plan16(d, world, buf->flags);
   s->bits = (u64*)((char*)buf->table + (buf->mode == GM_MODE_DENSE ? dense_words_bytes(d, g, s->plan16) : 0));
   s->rank = rank;
   s->world = world;
@@ -1606,7 +1638,7 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
       s->ht = HaloTabs{pb, ny, cs, s->hg.NG, s->hg.NYn, s->hg.top};
       s->halo_send = (uint32_t*)(base + halo_tab_bytes(s->hg));
       s->halo_recv = s->halo_send + s->hg.nb * 2 * s->hg.Z;
-      s->halo16 = d->kind == K_SUM && d->root_sum < 32768 && !getenv("GM_HALO32");
+      s->halo16 = d->kind == K_SUM && d->root_sum < 32768;
     } else {
       s->hg.on = false;  // scratch from an older plan: whole-slice halos
     }
@@ -1623,12 +1655,7 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
       const int top = d->nheaps - 1;
       const u64 C = d->pstride[top] / 256;  // groups per top-digit slice
       bool cols = top >= 2 && d->pstride[top] % 256 == 0 && C >= 8;
-      u64 tile = 0;  // columns per top-major tile (0: the XCD's whole range)
-      if (const char* e = getenv("GM_GROUP_TILE")) {  // A/B: -1 = address order
-        const long long v = atoll(e);
-        if (v < 0) cols = false;
-        else tile = (u64)v;
-      }
+      const u64 tile = 0;  // columns per top-major tile (0: the XCD's whole range; tiles measured no gain)
       const u64 NT = cols ? gg.groups / C : 1, NC = cols ? C : gg.groups;
       std::vector<u64> live(NC);
       for (int L = 0; L < d->max_levels; L++) {
@@ -1665,6 +1692,13 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
         return fail(GM_EHIP, "group lists: %s", hipGetErrorString(e));
       }
       s->glist = dl;
+    }
+  }
+  if (s->mode == GM_MODE_DENSE) {
+    int rc = dense_choose(s);
+    if (rc) {
+      gm_solver_destroy(s);
+      return rc;
     }
   }
   *out = s;
@@ -1708,6 +1742,9 @@ int gm_solver_set_steps(gm_solver* s, uint32_t first, uint32_t stop) {
 
 int gm_solver_set_flags(gm_solver* s, uint32_t flags) {
   if (!s) return fail(GM_EINVAL, "null solver");
+  if ((flags & ~GM_F_KERNEL_TIMING) != (s->flags & ~GM_F_KERNEL_TIMING))
+    return fail(GM_EINVAL, "only GM_F_KERNEL_TIMING changes after creation: the kernel families and word width "
+                           "are fixed by the flags the solver was planned and created with");
   s->flags = flags;
   return 0;
 }
@@ -2010,8 +2047,7 @@ static u64 halo_move_all(gm_solver* s, u64 L, int pack, uint32_t* buf, hipStream
     const int grid = (int)std::min<u64>(((units + kBlock - 1) / kBlock + 7) & ~7ull, (u64)s->grid);
     uint32_t* lw = s->words + L * s->view.Wl;
     uint16_t* lw16 = (uint16_t*)s->words + L * s->view.Wl;
-    const char* hc4 = getenv("GM_HALO_COLS4");  // A/B: one column per wave, four slots per lane
-    if (s->w16 && !(hc4 && atoi(hc4))) {  // two columns per wave, eight slots per lane
+    if (s->w16) {  // two columns per wave, eight slots per lane
       const u64 u2 = (u64)((J.cum[J.n] + 1) / 2) * 64;
       const int g2 = (int)std::min<u64>(((u2 + kBlock - 1) / kBlock + 7) & ~7ull, (u64)s->grid);
       if (pack)
@@ -2020,13 +2056,7 @@ static u64 halo_move_all(gm_solver* s, u64 L, int pack, uint32_t* buf, hipStream
       else
         hipLaunchKernelGGL((k_halo_cols16<false>), dim3(g2), dim3(kBlock), 0, cs, s->d, J, s->view.Z, s->colperm,
                            s->ht, lw16, (uint16_t*)buf);
-    } else if (s->w16 && pack)
-      hipLaunchKernelGGL((k_halo_cols<true, true, true>), dim3(grid), dim3(kBlock), 0, cs, s->d, J, s->view.Z,
-                         s->colperm, s->ht, (void*)lw16, (void*)buf);
-    else if (s->w16)
-      hipLaunchKernelGGL((k_halo_cols<false, true, true>), dim3(grid), dim3(kBlock), 0, cs, s->d, J, s->view.Z,
-                         s->colperm, s->ht, (void*)lw16, (void*)buf);
-    else if (pack && s->halo16)
+    } else if (pack && s->halo16)
       hipLaunchKernelGGL((k_halo_cols<true, true>), dim3(grid), dim3(kBlock), 0, cs, s->d, J, s->view.Z, s->colperm,
                          s->ht, lw, (void*)buf);
     else if (pack)
@@ -2170,31 +2200,17 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
   s0->step_first = s0->step_stop = 0;
   const bool timing = (s0->flags & GM_F_KERNEL_TIMING) && first == 0 && stop == 2 * T;
   hipStream_t st = s0->stream;
-  // 16-bit words (k_dense_resolve8p) for the default world-1 sweep: K_SUM
-  // remoteness <= root_sum < 2^15, octets need base[1] >= 8.  GM_WORDS32=1
-  // keeps 32-bit words (A/B); any other resolve knob selects a 32-bit kernel.
-  // Shards (column jobs, k_dense_resolve8c) additionally need the packed
-  // 16-bit halos and every level's slice list to fit one ColJobs.
+  // the kernel families and word width were fixed at creation (dense_choose);
+  // a resume checks the interrupted solve used the same width
   for (gm_solver* s : ss) {
-    if (first > 0) {  // resume: the word width the interrupted solve chose
+    s->launch_err = false;
+    if (first > 0) {
       uint32_t wb = 0;
       HIPCHK(hipMemcpy(&wb, &s->st->word_bits, sizeof wb, hipMemcpyDeviceToHost));
       if (wb != 16 && wb != 32) return fail(GM_EINVAL, "resume: scratch holds no solve in progress");
-      s->w16 = wb == 16;
-      if (s->plan16 && !s->w16) return fail(GM_EINVAL, "resume: 32-bit state in a 16-bit table");
-      continue;
+      if ((wb == 16) != s->w16) return fail(GM_EINVAL, "resume: the interrupted solve used %u-bit words, this solver %u",
+                                            wb, s->w16 ? 16u : 32u);
     }
-    const char* w32 = getenv("GM_WORDS32");
-    const bool base_ok = d.pow2 && d.kind == K_SUM && d.nheaps >= 2 && d.nheaps <= 8 && d.base[1] >= 8 &&
-                         d.root_sum < 0x7FFF && s->view.Wl * 2 <= 0xFFFFFFF0ull && !(w32 && atoi(w32));
-    if (mode == 0)
-      s->w16 = base_ok && s->glist && !s->view.blk && !dense_resolve_knob_set();
-    else
-      s->w16 = base_ok && d.nheaps >= 3 && s->view.blk && s->colperm && s->hg.on && s->halo16 &&
-               s->view.Z % 256 == 0 && s->view.E <= 0xFFFF &&
-               blk_count(s) * (s->view.B + 4) <= (u64)kMaxColJobs && !dense_scalar_resolve();
-    if (s->plan16 && !s->w16)  // a 16-bit table cannot take a 32-bit kernel
-      return fail(GM_EINVAL, "table planned with 16-bit words: set GM_WORDS32 / resolve knobs before creating the solver");
   }
   std::vector<hipEvent_t> ev;
   auto new_event = [&](hipEvent_t* e) -> int {
@@ -2241,8 +2257,7 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
   bool pipe = mode != 0;
   for (gm_solver* s : ss)
     if (s->view.B < 4) pipe = false;
-  if (const char* e = getenv("GM_SHARD_NOPIPE"))  // A/B: exchange in order
-    if (atoi(e)) pipe = false;
+  if (s0->flags & GM_F_SHARD_INORDER) pipe = false;  // A/B: exchange in order
   hipStream_t cs = st;
   hipEvent_t* E = nullptr;  // [0, T): own part done, [T, 2T): exchange done (forward); reused backward
   if (pipe) {
@@ -2415,6 +2430,9 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
   out->levels = (uint32_t)T;
   out->max_level_width = 0;
   out->word_bits = s0->w16 ? 16u : 32u;
+  out->kernels = s0->rk | (s0->pk << 16);
+  for (gm_solver* s : ss)
+    if (s->launch_err) return fail(GM_ECORRUPT, "a level found no resolve kernel of the table's word width");
   const uint32_t word = red[3] ? (uint32_t)(red[3] - 1) : NO_WORD;
   out->root_word = word;
   if (red[4]) return fail(GM_ECORRUPT, "solve failed:%s", err_text((uint32_t)red[4]).c_str());
@@ -2469,6 +2487,22 @@ int gm_solver_positions(gm_solver* s, uint64_t* keys_dev, uint64_t cap, uint64_t
   hipLaunchKernelGGL(k_gather_positions, dim3(s->grid), dim3(kBlock), 0, s->stream, s->lv, s->lcap, s->st,
                      (u64*)keys_dev);
   HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s->stream));
+  return 0;
+}
+
+int gm_solver_checksum(gm_solver* s, uint64_t out[6]) {
+  if (!s || !out) return fail(GM_EINVAL, "bad argument");
+  u64* acc = s->st->ck;
+  HIPCHK(hipMemsetAsync(acc, 0, 6 * sizeof(u64), s->stream));
+  if (s->mode == GM_MODE_DENSE)
+    hipLaunchKernelGGL(k_checksum_dense, dim3(s->grid), dim3(kBlock), 0, s->stream, s->d, s->view, s->words, s->bits,
+                       (u64)s->d.max_levels, s->w16, acc);
+  else
+    hipLaunchKernelGGL(k_checksum_hashed, dim3(s->grid), dim3(kBlock), 0, s->stream, s->d, s->tab, s->mask, s->lv,
+                       s->lcap, s->st, acc);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out, acc, 6 * sizeof(u64), hipMemcpyDeviceToHost, s->stream));
   HIPCHK(hipStreamSynchronize(s->stream));
   return 0;
 }

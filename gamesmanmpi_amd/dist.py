@@ -43,7 +43,7 @@ class ShardedSolver(Solver):
             _lib.check(L.gm_solver_comm_init(self._h, buf))
 
 
-def group_solve(spec, world, device=None, kernel_timing=False):
+def group_solve(spec, world, device=None, kernel_timing=False, flags=0):
     """Solve all `world` shards in this process (one GPU, one stream).
     Returns (SolveResult of the whole job, [shard Solvers])."""
     import torch
@@ -53,7 +53,7 @@ def group_solve(spec, world, device=None, kernel_timing=False):
     # 0, which the ABI reads as "library-owned stream per solver")
     stream = torch.cuda.Stream(device=dev)
     shards = [Solver(spec, device=dev, rank=g, world=world, layout="dense",
-                     kernel_timing=kernel_timing, stream=stream)
+                     kernel_timing=kernel_timing, stream=stream, flags=flags)
               for g in range(world)]
     arr = (ctypes.c_void_p * world)(*[s.handle.value for s in shards])
     r = _lib.gm_result()

@@ -48,9 +48,11 @@ class Solver:
 
     def __init__(self, spec, positions=0, device=None, kernel_timing=False,
                  layout="auto", max_table_bytes=0, rank=0, world=1,
-                 stream=None):
+                 stream=None, flags=0):
         """layout: "auto" (dense when the descriptor supports it and the
         table fits max_table_bytes, else hashed), "dense" or "hashed".
+        flags: kernel-family flags (_lib.GM_F_WORDS32 / GM_F_RESOLVE_SCALAR /
+        GM_F_SHARD_INORDER, A/B runs), fixed for this solver's lifetime.
         rank/world > 1: this object is one shard of a dense multi-GPU solve
         (gamesmanmpi_amd.dist), or with layout="hashed" one md5 shard of a
         keyed solve (gamesmanmpi_amd.keyed; `positions` is then this
@@ -69,6 +71,9 @@ class Solver:
         self.max_table_bytes = int(max_table_bytes)
         self.rank, self.world = int(rank), int(world)
         self.stream = stream
+        if flags & ~_lib.KERNEL_FLAGS:
+            raise ValueError("flags: kernel-family flags only (%#x)" % _lib.KERNEL_FLAGS)
+        self.flags = int(flags)
         self.positions_hint = int(positions or self.spec.positions_bound)
         self._h = None
         self._bufs = None
@@ -79,7 +84,7 @@ class Solver:
         L = _lib.load()
         self._free()
         plan = _lib.gm_plan_t()
-        flags = _lib.GM_F_FORCE_HASHED if self.layout == "hashed" else 0
+        flags = self.flags | (_lib.GM_F_FORCE_HASHED if self.layout == "hashed" else 0)
         if self.world > 1 and self.layout != "hashed":
             _lib.check(L.gm_plan_shard(self.spec.id, self.rank, self.world,
                                        flags, self.max_table_bytes,
@@ -107,8 +112,9 @@ class Solver:
         b.scratch = scratch.data_ptr()
         b.scratch_bytes = plan.scratch_bytes
         b.stream = stream.cuda_stream
-        b.flags = _lib.GM_F_KERNEL_TIMING if self.kernel_timing else 0
+        b.flags = self.flags | (_lib.GM_F_KERNEL_TIMING if self.kernel_timing else 0)
         b.mode = plan.mode
+        b.table_bytes = plan.table_bytes
         self._bufs = b
         self.plan = plan
         h = ctypes.c_void_p()
@@ -137,7 +143,7 @@ class Solver:
         """Time every kernel launch with HIP events (on the solve stream)."""
         self.kernel_timing = bool(on)
         _lib.check(_lib.load().gm_solver_set_flags(
-            self._h, _lib.GM_F_KERNEL_TIMING if on else 0))
+            self._h, self.flags | (_lib.GM_F_KERNEL_TIMING if on else 0)))
 
     def solve(self, max_retries=4):
         """Full solve from the root; grows the buffers on GM_EFULL."""
@@ -200,6 +206,8 @@ class Solver:
             extra={"layout": "dense" if self.plan.mode == _lib.GM_MODE_DENSE
                    else "hashed",
                    "word_bits": r.word_bits,
+                   "resolve_kernel": _lib.RESOLVE_KERNELS.get(r.kernels & 0xFFFF),
+                   "pull_kernel": _lib.PULL_KERNELS.get(r.kernels >> 16),
                    "table_bytes": self.plan.table_bytes})
 
     # -- reading the table -------------------------------------------------
@@ -231,6 +239,19 @@ class Solver:
             _lib.check(L.gm_solver_positions(self._h, out.data_ptr(),
                                              n.value, ctypes.byref(n)))
         return out[:n.value].cpu().numpy().view(np.uint64)
+
+    def checksum(self):
+        """Whole-solve fingerprint (gm_solver_checksum): dict with the
+        order-independent checksum of every reachable position's
+        (canonical bytes, value, remoteness), the position count and the
+        W/L/T/D histogram."""
+        out = np.zeros(6, np.uint64)
+        with self.torch.cuda.device(self.device):
+            _lib.check(_lib.load().gm_solver_checksum(self._h,
+                                                      out.ctypes.data))
+        v = [int(x) for x in out]
+        return {"checksum": "%016x" % v[0], "positions": v[1], "win": v[2],
+                "loss": v[3], "tie": v[4], "draw": v[5]}
 
     def dump(self):
         """(keys u64, value u8, remoteness u32) for every reachable

@@ -197,6 +197,14 @@ def main(argv=None):
 
     if args.checkpoint and world > 1:
         raise SystemExit("-ck/--checkpoint covers one-GPU solves (a sharded solve's state spans ranks)")
+    if args.checkpoint:
+        # never write into (or later delete) a directory that holds anything
+        # but a checkpoint of ours
+        from gamesmanmpi_amd import checkpoint
+        try:
+            checkpoint.check_target(args.checkpoint)
+        except checkpoint.NotACheckpoint as e:
+            raise SystemExit("-ck: %s" % e)
     import torch
     torch.cuda.set_device(local)
     if world > 1:
@@ -217,11 +225,12 @@ def main(argv=None):
         from gamesmanmpi_amd import checkpoint
         from gamesmanmpi_amd.solver import Solver
         first = 0
-        if os.path.isfile(os.path.join(args.checkpoint, "meta.json")):
-            meta = checkpoint.read_meta(args.checkpoint)
+        src = checkpoint.latest(args.checkpoint)  # DIR, or DIR.old after an interrupted save
+        if src is not None:
+            meta = checkpoint.read_meta(src)
             if (meta["game"], meta["params"]) != (spec.name, spec.params):
                 raise SystemExit("%s holds a checkpoint of %s %s, not %s %s"
-                                 % (args.checkpoint, meta["game"], meta["params"],
+                                 % (src, meta["game"], meta["params"],
                                     spec.name, spec.params))
             solver, first = checkpoint.restore(args.checkpoint, device="cuda:%d" % local)
             logging.debug("resuming %r at step %d of %d", spec, first, solver.steps)

@@ -731,3 +731,6 @@ void or_free(void *hs) {
   free(S->tab);
   free(S);
 }
+
+/* multi-threaded restatements (same translation unit: reuses the game code) */
+#include "oracle_mt.c"

@@ -53,6 +53,22 @@ def lib():
         L.or_lookup.restype = ctypes.c_uint32
         L.or_free.argtypes = [ctypes.c_void_p]
         L.or_last_error.restype = ctypes.c_char_p
+        # multi-threaded restatements (oracle_mt.c)
+        L.or_threads.restype = ctypes.c_int
+        L.or_solve_levels.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.or_solve_levels.restype = ctypes.c_void_p
+        L.or_lsolve_stats.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.or_lsolve_lookup.argtypes = [ctypes.c_void_p, ctypes.c_char_p,
+                                       ctypes.c_int]
+        L.or_lsolve_lookup.restype = ctypes.c_uint32
+        L.or_lsolve_free.argtypes = [ctypes.c_void_p]
+        L.or_solve_rows.argtypes = [ctypes.c_int]
+        L.or_solve_rows.restype = ctypes.c_void_p
+        L.or_rsolve_stats.argtypes = [ctypes.c_void_p, ctypes.c_int,
+                                      ctypes.c_void_p]
+        L.or_rsolve_word.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+        L.or_rsolve_word.restype = ctypes.c_uint32
+        L.or_rsolve_free.argtypes = [ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -92,6 +108,86 @@ class Game:
 
     def solve(self, max_positions=1 << 20):
         return Solution(self, max_positions)
+
+    def solve_levels(self, keep=True):
+        """Multi-threaded tier-synchronous solve (oracle_mt.c, all
+        OpenMP threads); keep=False frees levels as the backward pass goes
+        (large games: only stats and the checksum remain)."""
+        return LevelSolution(self, keep)
+
+    def solve_rows(self):
+        """Multi-threaded row solve of an int game (sum_four_to_one /
+        four_to_one; oracle_mt.c)."""
+        return RowSolution(self)
+
+
+def threads():
+    """OpenMP threads the multi-threaded solvers use."""
+    return lib().or_threads()
+
+
+STAT_KEYS = ("positions", "edges", "primitives", "root_word", "checksum",
+             "win", "loss", "tie", "draw")
+
+
+class _Stats:
+    def _fill(self, raw):
+        self.stats = dict(zip(STAT_KEYS, [int(x) for x in raw]))
+        self.count = self.stats["positions"]
+        self.edges = self.stats["edges"]
+        w = self.stats["root_word"]
+        self.root_value, self.root_remoteness = w & 3, w >> 2
+
+    @property
+    def root_line(self):
+        return "%s in %d moves" % (NAMES[self.root_value],
+                                   self.root_remoteness)
+
+
+class LevelSolution(_Stats):
+    def __init__(self, game, keep):
+        self.game = game
+        self.h = lib().or_solve_levels(game.h, 1 if keep else 0)
+        if not self.h:
+            raise RuntimeError(_err())
+        raw = np.zeros(9, np.uint64)
+        lib().or_lsolve_stats(self.h, raw.ctypes.data)
+        self._fill(raw)
+
+    def lookup(self, canon):
+        w = lib().or_lsolve_lookup(self.h, canon, len(canon))
+        if w == 0xFFFFFFFF:
+            raise KeyError(canon)
+        return w & 3, w >> 2
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().or_lsolve_free(self.h)
+            self.h = None
+
+
+class RowSolution(_Stats):
+    def __init__(self, game):
+        self.game = game
+        self.h = lib().or_solve_rows(game.h)
+        if not self.h:
+            raise RuntimeError(_err())
+        self.refresh(False)
+
+    def refresh(self, with_checksum=True):
+        raw = np.zeros(9, np.uint64)
+        lib().or_rsolve_stats(self.h, 1 if with_checksum else 0,
+                              raw.ctypes.data)
+        self._fill(raw)
+        return self.stats
+
+    def word(self, rank):
+        return lib().or_rsolve_word(self.h, int(rank))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().or_rsolve_free(self.h)
+            self.h = None
 
 
 class Solution:

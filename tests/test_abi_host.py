@@ -133,10 +133,15 @@ def test_plan_sizes():
     assert p.table_slots == 187 * 32 ** 5
     # 16-bit order-form words (one-GPU octet kernels) + reach bitmap
     assert p.table_bytes == 2 * 187 * 32 ** 5 + 187 * 32 ** 5 // 8
-    os.environ["GM_WORDS32"] = "1"  # the A/B knob plans 32-bit words
+    # the kernel-family flags plan 32-bit words (and the environment does
+    # not: no knob is read from it)
+    for f in (_lib.GM_F_WORDS32, _lib.GM_F_RESOLVE_SCALAR):
+        _lib.check(_lib.load().gm_plan(s.id, 0, f, 0, ctypes.byref(p)))
+        assert p.table_bytes == 4 * 187 * 32 ** 5 + 187 * 32 ** 5 // 8
+    os.environ["GM_WORDS32"] = "1"
     try:
         _lib.check(_lib.load().gm_plan(s.id, 0, 0, 0, ctypes.byref(p)))
-        assert p.table_bytes == 4 * 187 * 32 ** 5 + 187 * 32 ** 5 // 8
+        assert p.table_bytes == 2 * 187 * 32 ** 5 + 187 * 32 ** 5 // 8
     finally:
         del os.environ["GM_WORDS32"]
     # a byte budget below the dense table falls back to the keyed table

@@ -31,20 +31,34 @@ def test_closed_forms_match_the_oracle(heaps):
     assert (sol.count, sol.edges, sol.root_line.split()[0]) == (P, E, root)
 
 
-def test_roofline_byte_model():
-    fwd, bwd = bench.algorithmic_bytes(1000, 10000, "dense", word_bytes=2)
-    assert fwd == (10000 + 1000) / 8 and bwd == 2.125 * 1000 + 2 * 10000
-    fwd, bwd = bench.algorithmic_bytes(1000, 10000, "dense")
-    assert bwd == 4.125 * 1000 + 4 * 10000
-    assert bench.algorithmic_bytes(10, 100, "hashed") == (24 * 10 + 8 * 100, 12 * 10 + 12 * 100)
-    assert bench.model_8d_bytes(10, 100) == 36 * 10 + 20 * 100
+def test_level_counts_and_compulsory_bytes():
+    """Per-level position counts (digit-sum distribution) and the dense
+    layout's compulsory byte model."""
+    import itertools
+    heaps = [3, 2, 4]
+    n = bench.level_counts(heaps)
+    root = sum(heaps)
+    want = [0] * (root + 1)
+    for hs in itertools.product(*[range(h + 1) for h in heaps]):
+        want[root - sum(hs)] += 1
+    assert n == want
+    m = bench.dense_bytes(heaps, 2)
+    P, E, _ = bench.expected(heaps)
+    assert abs(m["resolve_compulsory"] - sum(2 * (n[L] + (n[L + 1] if L + 1 <= root else 0)
+                                                  + (n[L + 2] if L + 2 <= root else 0)) + n[L] / 8
+                                             for L in range(root + 1))) < 1e-6
+    assert m["resolve_per_edge"] == 2.125 * P + 2 * E
+    assert m["pull_per_edge"] == (E + P) / 8
+    # the bench shape: about 6.1 B per position must move per resolve
+    big = bench.dense_bytes([31] * 6, 2)
+    assert 6.0 * 2 ** 30 < big["resolve_compulsory"] < 6.2 * 2 ** 30
 
 
-def test_roofline_kernel_names(monkeypatch):
-    for k in ("GM_DENSE_RESOLVE", "GM_DENSE_SWEEP", "GM_DENSE_PIPE"):
-        monkeypatch.delenv(k, raising=False)
-    assert bench.dense_resolve_kernel(16) == "k_dense_resolve8p"
-    assert bench.dense_resolve_kernel(16, world=4) == "k_dense_resolve8c"
-    assert bench.dense_resolve_kernel(32) == "k_dense_resolve4p"
-    monkeypatch.setenv("GM_DENSE_PIPE", "0")
-    assert bench.dense_resolve_kernel(32) == "k_dense_resolve4"
+def test_keyed_model():
+    assert bench.keyed_bytes(10, 100) == (24 * 10 + 8 * 100, 12 * 10 + 12 * 100)
+
+
+def test_kernel_names_come_from_the_library():
+    from gamesmanmpi_amd import _lib
+    assert _lib.RESOLVE_KERNELS[1] == "k_dense_resolve8p"
+    assert _lib.PULL_KERNELS[1] == "k_dense_pull_words"

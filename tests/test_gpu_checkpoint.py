@@ -2,7 +2,9 @@
 gm_solver_set_steps, gamesmanmpi_amd/checkpoint.py): a solve interrupted
 after any step -- forward or backward, HASHED or DENSE (16- and 32-bit
 words) -- and resumed, in the same solver or in a fresh one restored from
-disk, gives exactly the uninterrupted solve's counts, root and words."""
+disk, gives the ORACLE's counts, root line and every position's value and
+remoteness (oracle/, the CPU restatement pinned to the reference's golden
+tables) -- not merely the GPU's own uninterrupted solve."""
 import os
 import subprocess
 import sys
@@ -18,42 +20,47 @@ CASES = [
     ("tic_tac_toe_np", "", "hashed", {}),
     ("othello_bit_new", "length=4,height=4", "hashed", {}),
     ("sum_four_to_one", "heaps=15:15:15:15", "dense", {}),
-    ("sum_four_to_one", "heaps=15:15:15:15", "dense", {"GM_WORDS32": "1"}),
+    ("sum_four_to_one", "heaps=15:15:15:15", "dense", {"flags": 4}),  # GM_F_WORDS32
     ("four_to_one", "start=40", "dense", {}),
 ]
 
 
-def _full(name, params, layout):
-    from gamesmanmpi_amd.games import GameSpec
-    from gamesmanmpi_amd.solver import Solver
-    s = Solver(GameSpec(name, params), layout=layout)
-    r = s.solve()
-    keys, val, rem = s.dump()
-    o = np.argsort(keys)
-    return r, (keys[o], val[o], rem[o])
+class _Oracle:
+    """The oracle's solve of (name, params): counts, root line and a table
+    sorted by canonical bytes."""
+    def __init__(self, name, params, layout):
+        from oracle.oracle import Game
+        sol = Game(name, params).solve(1 << 20)
+        self.positions, self.edges, self.root_line = sol.count, sol.edges, sol.root_line
+        self.canon, self.clen, self.val, self.rem = sol.dump(stride=24)
+
+
+def _full(name, params, layout, flags=0):
+    return _Oracle(name, params, layout), None
 
 
 def _same(r, d, r0, d0):
-    assert (r.positions, r.edges, r.primitives, r.root_line) == (
-        r0.positions, r0.edges, r0.primitives, r0.root_line)
-    for a, b in zip(d, d0):
-        np.testing.assert_array_equal(a, b)
+    """r / d: the resumed solve's result and its solver; r0: the oracle."""
+    assert (r.positions, r.edges, r.root_line) == (r0.positions, r0.edges, r0.root_line)
+    keys, val, rem = d.dump()
+    canon, clen = d.spec.decode_batch(keys, stride=24)
+    order = sorted(range(len(keys)), key=lambda i: bytes(canon[i, :clen[i]]))
+    order = np.array(order, np.int64)
+    np.testing.assert_array_equal(canon[order], r0.canon)
+    np.testing.assert_array_equal(val[order], r0.val)
+    np.testing.assert_array_equal(rem[order], r0.rem)
 
 
 def _dump(s):
-    keys, val, rem = s.dump()
-    o = np.argsort(keys)
-    return keys[o], val[o], rem[o]
+    return s
 
 
 @pytest.mark.parametrize("name,params,layout,env", CASES)
-def test_stop_resume_same_solver(name, params, layout, env, monkeypatch):
+def test_stop_resume_same_solver(name, params, layout, env):
     from gamesmanmpi_amd.games import GameSpec
     from gamesmanmpi_amd.solver import Solver
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
     r0, d0 = _full(name, params, layout)
-    s = Solver(GameSpec(name, params), layout=layout)
+    s = Solver(GameSpec(name, params), layout=layout, flags=env.get("flags", 0))
     n = s.steps
     for cut in sorted({1, n // 4, n // 2, n // 2 + 1, (3 * n) // 4, n - 1}):
         assert s.solve_steps(0, cut) is None
@@ -65,14 +72,12 @@ def test_stop_resume_same_solver(name, params, layout, env, monkeypatch):
 
 
 @pytest.mark.parametrize("name,params,layout,env", CASES)
-def test_checkpoint_on_disk(name, params, layout, env, monkeypatch, tmp_path):
+def test_checkpoint_on_disk(name, params, layout, env, tmp_path):
     from gamesmanmpi_amd import checkpoint
     from gamesmanmpi_amd.games import GameSpec
     from gamesmanmpi_amd.solver import Solver
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
     r0, d0 = _full(name, params, layout)
-    s = Solver(GameSpec(name, params), layout=layout)
+    s = Solver(GameSpec(name, params), layout=layout, flags=env.get("flags", 0))
     cut = s.steps // 2 + 1  # inside the backward pass
     assert s.solve_steps(0, cut) is None
     ck = str(tmp_path / "ck")
@@ -80,7 +85,7 @@ def test_checkpoint_on_disk(name, params, layout, env, monkeypatch, tmp_path):
     del s
     s2, step = checkpoint.restore(ck)
     assert step == cut
-    monkeypatch.delenv("GM_WORDS32", raising=False)  # the width travels in the checkpoint
+    assert s2.flags == env.get("flags", 0)  # the kernel flags travel in the checkpoint
     r = s2.solve_steps(step, 0)
     _same(r, _dump(s2), r0, d0)
 

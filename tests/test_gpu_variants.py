@@ -1,26 +1,22 @@
-"""GPU parity of every dense resolve variant: the A/B knobs
-select other kernels / sweep orders for the same solve, and each must give
-the same words as the default path, the closed-form counts and the
-Sprague-Grundy values.  Shapes exercise the quad kernels' paths: live-group
-lists with top-major XCD shares (C >= 8 columns), column jobs, column walks,
-the unpipelined and the one-prefix kernels, and shard halos in 16 and 32
-bits."""
+"""GPU parity of every dense kernel family: the kernel-family
+flags (include/gamesman.h GM_F_WORDS32 / GM_F_RESOLVE_SCALAR /
+GM_F_SHARD_INORDER, fixed when a solver is created) select other kernels
+for the same solve, and each must give the same words as the default path,
+the closed-form counts and the Sprague-Grundy values.  Shapes exercise the
+live-group lists with top-major XCD shares (C >= 8 columns), column jobs,
+the one-prefix kernel, shard halos in 16 and 32 bits, and in-order
+exchanges.  A table planned for 16-bit words refuses a 32-bit kernel with
+GM_EINVAL instead of running it."""
+import ctypes
+
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
-WORLD1 = [
-    {},
-    {"GM_WORDS32": "1"},
-    {"GM_DENSE_PIPE": "0"},
-    {"GM_DENSE_SWEEP": "cols"},
-    {"GM_DENSE_SWEEP": "walk"},
-    {"GM_DENSE_RESOLVE": "scalar"},
-    {"GM_PULL_BAND": "1"},
-    {"GM_GROUP_TILE": "-1"},
-    {"GM_GROUP_TILE": "4"},
-]
+WORDS32, SCALAR, INORDER = 4, 8, 16  # _lib.GM_F_*
+WORLD1 = [0, WORDS32, SCALAR]
+KERNELS1 = {0: "k_dense_resolve8p", WORDS32: "k_dense_resolve4p", SCALAR: "k_dense_resolve"}
 
 
 def _expected(heaps):
@@ -34,28 +30,24 @@ def _expected(heaps):
     return P, E, "LOSS" if g == 0 else "WIN"
 
 
-def _solve(params, monkeypatch, env):
+def _solve(params, flags):
     from gamesmanmpi_amd.games import GameSpec
     from gamesmanmpi_amd.solver import Solver
-    for k in ("GM_DENSE_PIPE", "GM_DENSE_SWEEP", "GM_DENSE_RESOLVE", "GM_PULL_BAND", "GM_GROUP_TILE",
-              "GM_WORDS32"):
-        monkeypatch.delenv(k, raising=False)
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    s = Solver(GameSpec("sum_four_to_one", params), layout="dense")
+    s = Solver(GameSpec("sum_four_to_one", params), layout="dense", flags=flags)
     r = s.solve()
+    assert r.extra["resolve_kernel"] == KERNELS1[flags], r.extra
     keys, val, rem = s.dump()
     order = np.argsort(keys)
     return r, keys[order], val[order], rem[order]
 
 
 @pytest.mark.parametrize("params", ["heaps=15:15:15:15:7", "heaps=31:7:31:15"])
-def test_world1_variants_agree(params, monkeypatch):
+def test_world1_variants_agree(params):
     heaps = [int(h) for h in params.split("=")[1].split(":")]
     P, E, root = _expected(heaps)
     base = None
     for env in WORLD1:
-        r, keys, val, rem = _solve(params, monkeypatch, env)
+        r, keys, val, rem = _solve(params, env)
         assert (r.positions, r.edges, r.root_line.split()[0]) == (P, E, root), env
         if base is None:
             base = (keys, val, rem)
@@ -72,27 +64,25 @@ def test_world1_variants_agree(params, monkeypatch):
         np.testing.assert_array_equal(rem, base[2], err_msg=str(env))
 
 
-@pytest.mark.parametrize("env", [{}, {"GM_HALO_COLS4": "1"}, {"GM_WORDS32": "1"}, {"GM_HALO32": "1"},
-                                 {"GM_PULL_COLS": "1"}])
+@pytest.mark.parametrize("flags", [0, WORDS32, INORDER, WORDS32 | INORDER, SCALAR])
 @pytest.mark.parametrize("world", [2, 3])
-def test_shard_halo_word_widths(env, world, monkeypatch):
+def test_shard_halo_word_widths(flags, world):
     """Column-order halos (Z % 256 == 0): 16-bit shard tables with 16-bit
-    halos (default, k_dense_resolve8c), 32-bit tables with 16-bit halos,
-    32-bit tables and halos -- each against the single-table solve."""
+    halos (default, k_dense_resolve8c), 32-bit tables with 16-bit halos
+    (k_dense_resolve4c), the one-prefix kernel, overlapped and in-order
+    exchanges -- each against the single-table solve."""
     from gamesmanmpi_amd.dist import group_solve
     from gamesmanmpi_amd.games import GameSpec
     from gamesmanmpi_amd.solver import Solver
     params = "heaps=15:15:15:15:31"  # Z = 16^3 = 4096 prefixes (16 columns) per slice
-    for k in ("GM_HALO32", "GM_WORDS32", "GM_HALO_COLS4", "GM_PULL_COLS"):
-        monkeypatch.delenv(k, raising=False)
     s1 = Solver(GameSpec("sum_four_to_one", params), layout="dense")
     r1 = s1.solve()
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    rg, shards = group_solve(GameSpec("sum_four_to_one", params), world)
+    rg, shards = group_solve(GameSpec("sum_four_to_one", params), world, flags=flags)
     assert (rg.positions, rg.edges, rg.root_line) == (r1.positions, r1.edges, r1.root_line)
-    wide = "GM_WORDS32" in env or "GM_HALO32" in env
+    wide = bool(flags & (WORDS32 | SCALAR))
     assert rg.extra["word_bits"] == (32 if wide else 16), rg.extra
+    want = "k_dense_resolve" if flags & SCALAR else "k_dense_resolve4c" if wide else "k_dense_resolve8c"
+    assert rg.extra["resolve_kernel"] == want, rg.extra
     keys, val, rem = s1.dump()
     out = np.full(len(keys), 0xFFFFFFFF, np.uint32)
     for s in shards:
@@ -130,3 +120,35 @@ def test_shard_geometries_like_the_bench(world, params):
     assert (hits == 1).all()
     np.testing.assert_array_equal(out & 3, val)
     np.testing.assert_array_equal(out >> 2, rem)
+
+
+def test_16bit_table_refuses_32bit_kernels():
+    """The round-1 fault class (a 32-bit kernel writing past a 16-bit word
+    area): kernel families are fixed at creation from the flags the table
+    was planned with.  A 16-bit plan handed GM_F_WORDS32 at creation, or a
+    16-bit solver asked to switch afterwards, returns GM_EINVAL; the solver
+    keeps solving correctly."""
+    import torch
+    from gamesmanmpi_amd import _lib
+    from gamesmanmpi_amd.games import GameSpec
+    from gamesmanmpi_amd.solver import Solver
+    L = _lib.load()
+    spec = GameSpec("sum_four_to_one", "heaps=15:15:15:15:7")
+    plan = _lib.gm_plan_t()
+    _lib.check(L.gm_plan(spec.id, 0, 0, 0, ctypes.byref(plan)))
+    assert plan.mode == _lib.GM_MODE_DENSE
+    table = torch.empty(plan.table_bytes, dtype=torch.uint8, device="cuda")
+    scratch = torch.empty(plan.scratch_bytes, dtype=torch.uint8, device="cuda")
+    b = _lib.gm_buffers()
+    b.table, b.table_slots, b.table_bytes = table.data_ptr(), plan.table_slots, plan.table_bytes
+    b.scratch, b.scratch_bytes = scratch.data_ptr(), plan.scratch_bytes
+    b.mode, b.flags = plan.mode, _lib.GM_F_WORDS32
+    h = ctypes.c_void_p()
+    assert L.gm_solver_create(spec.id, ctypes.byref(b), ctypes.byref(h)) == _lib.GM_EINVAL
+    assert b"flags need" in L.gm_last_error()
+    s = Solver(spec, layout="dense")
+    r = s.solve()
+    assert r.extra["word_bits"] == 16
+    assert L.gm_solver_set_flags(s.handle, _lib.GM_F_WORDS32) == _lib.GM_EINVAL
+    assert L.gm_solver_set_flags(s.handle, _lib.GM_F_RESOLVE_SCALAR) == _lib.GM_EINVAL
+    assert s.solve().root_line == r.root_line

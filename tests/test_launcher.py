@@ -174,3 +174,51 @@ def test_launcher_graph_path_for_file_without_descriptor(tmp_path):
     assert out.getvalue().strip().splitlines()[0] == "TIE in 9 moves"
     z = np.load(tmp_path / "sd" / "stats" / "0" / "solution.npz")
     assert len(z["names"]) == 5478
+
+
+def test_checkpoint_flag_refuses_foreign_directory(tmp_path):
+    """-ck on a directory holding files that are not a checkpoint exits
+    non-zero before touching anything (no GPU needed: the check comes
+    first); the directory and its files stay as they were."""
+    from gamesmanmpi_amd import solver_launcher as sl
+    game = tmp_path / "sum_four_to_one.py"
+    game.write_text(open(OWN_SUM).read().replace(
+        "HEAPS = (31, 31, 31, 31, 31, 31)", "HEAPS = (4, 6, 3)"))
+    results = tmp_path / "results"
+    results.mkdir()
+    (results / "notes.txt").write_text("precious")
+    (results / "sub").mkdir()
+    with pytest.raises(SystemExit) as ei:
+        sl.main([str(game), "-ck", str(results)])
+    assert ei.value.code not in (0, None)
+    assert sorted(os.listdir(results)) == ["notes.txt", "sub"]
+    assert (results / "notes.txt").read_text() == "precious"
+
+
+def test_checkpoint_helpers_only_touch_their_own_files(tmp_path):
+    """checkpoint.check_target / latest / _remove_ours on the host: a
+    foreign directory is refused, an interrupted save's DIR.old is found,
+    and removal deletes exactly the checkpoint's files."""
+    import json
+    from gamesmanmpi_amd import checkpoint as ck
+    d = tmp_path / "ck"
+    ck.check_target(str(d))  # absent: fine
+    d.mkdir()
+    ck.check_target(str(d))  # empty: fine
+    (d / "x.txt").write_text("x")
+    with pytest.raises(ck.NotACheckpoint):
+        ck.check_target(str(d))
+    (d / "x.txt").unlink()
+    meta = {"format": ck.FORMAT, "game": "g", "params": "", "step": 3}
+    (d / "meta.json").write_text(json.dumps(meta))
+    for n in ("table", "levels", "scratch"):
+        (d / (n + ".bin")).write_bytes(b"\0" * 8)
+    ck.check_target(str(d))
+    assert ck.latest(str(d)) == str(d)
+    # an interrupted save: only DIR.old holds the checkpoint
+    os.replace(d, str(d) + ".old")
+    assert ck.latest(str(d)) == str(d) + ".old"
+    extra = tmp_path / "ck.old" / "keep.txt"
+    extra.write_text("k")
+    ck._remove_ours(str(d) + ".old")
+    assert os.listdir(tmp_path / "ck.old") == ["keep.txt"]
