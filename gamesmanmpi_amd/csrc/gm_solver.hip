@@ -798,6 +798,7 @@ __global__ void k_owner(Desc d, const u64* keys, u64 n, uint32_t P, uint32_t* ow
 
 #include "gm_dense.h"
 #include "gm_keyed_shard.h"
+#include "gm_bucketed.h"
 
 // ---------------------------------------------------------------------------
 // whole-solve fingerprint (gm_solver_checksum): per block partial sums of
@@ -834,6 +835,12 @@ __global__ __launch_bounds__(256) void k_checksum_hashed(Desc d, const gm_slot* 
     const u64 h = table_find(tab, mask, key);
     ck_add(d, key, h == ~0ull ? NO_WORD : tab[h].word, v);
   }
+  ck_block_add(acc, v);
+}
+__global__ __launch_bounds__(256) void k_checksum_flat(Desc d, const u64* K, const uint32_t* W, u64 n, u64* acc) {
+  u64 v[6] = {0, 0, 0, 0, 0, 0};
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x)
+    ck_add(d, K[i], W[i], v);
   ck_block_add(acc, v);
 }
 __global__ __launch_bounds__(256) void k_checksum_dense(Desc d, DenseView v, const uint32_t* words, const u64* bits,
@@ -919,6 +926,21 @@ struct gm_solver {
   uint32_t step_first = 0, step_stop = 0;  // gm_solver_set_steps (one solve)
   uint32_t rk = RK_NONE, pk = PK_NONE;      // dense kernel families (dense_choose)
   bool launch_err = false;                  // a launch found no kernel of the table's word width
+  // BUCKETED (gm_bucketed.h): level store, words, in-edges, partition scratch
+  u64* bkK = nullptr;
+  uint32_t* bkW = nullptr;
+  uint32_t *REp = nullptr, *REc = nullptr;
+  u64* S1k = nullptr;
+  uint32_t* S1p = nullptr;
+  u64* S2k = nullptr;
+  uint32_t* S2p = nullptr;
+  u64 Pcap = 0, Ecap = 0, Emax = 0;
+  BkLevel* bkL = nullptr;  // device level table (scratch)
+  uint32_t *pbase = nullptr, *bh = nullptr, *ph = nullptr, *boff = nullptr, *tot = nullptr, *cbase = nullptr;
+  uint32_t *fo = nullptr, *ucnt = nullptr, *fo2 = nullptr, *meta = nullptr;
+  u64* bktotal = nullptr;
+  u64 meta_cap = 0;
+  std::vector<BkLevel> lvh;  // host copy of the level table
 };
 
 static const int kBlock = 256;
@@ -1162,6 +1184,8 @@ static std::string err_text(uint32_t e) {
   if (e & ERR_CHILD_UNRESOLVED) s += " child-unresolved";
   if (e & ERR_NO_MOVES) s += " non-primitive-without-moves";
   if (e & ERR_SELF_MISSING) s += " self-missing";
+  if (e & ERR_BUCKET_FULL) s += " hash-bucket-over-capacity";
+  if (e & ERR_EDGE_COUNT) s += " edge-count-mismatch";
   return s;
 }
 
@@ -1415,6 +1439,53 @@ int gm_plan_shard(int game, int rank, int world, uint32_t flags, uint64_t max_ta
   return 0;
 }
 
+// ---- BUCKETED plan ---------------------------------------------------------
+// keyed games whose every move advances one level (the tier is the number
+// of pieces placed): the bucketed pipeline applies (gm_bucketed.h)
+static bool bk_ok(const Desc* d) { return d->kind == K_TTT || d->kind == K_TOOT || d->kind == K_OTHELLO; }
+// edges bound for a positions bound: the known counts where the board and
+// bound match (SURVEY Appendix B / tests/golden), else a branching factor
+// above every known board's
+static u64 bk_edges_bound(const Desc* d, u64 P) {
+  struct Known { int kind, L, H; u64 P, E; };
+  static const Known kn[] = {
+      {K_TOOT, 3, 3, 11097ull, 27774ull},          {K_TOOT, 4, 3, 200127ull, 640648ull},
+      {K_TOOT, 4, 4, 3468773ull, 9932808ull},      {K_TOOT, 5, 4, 70184763ull, 226547754ull},
+      {K_TOOT, 6, 4, 1187212827ull, 4243234712ull}, {K_OTHELLO, 4, 4, 54089ull, 69916ull},
+      {K_TTT, 0, 0, 5478ull, 16167ull}};
+  for (const Known& k : kn)
+    if (k.kind == d->kind && (d->kind == K_TTT || (k.L == d->L && k.H == d->H)) && P <= k.P)
+      return k.E + 1024;
+  const double ratio = d->kind == K_TOOT ? 3.6 : d->kind == K_TTT ? 3.0 : 2.0;
+  return (u64)(ratio * (double)P) + 1024;
+}
+// in-edges of the widest level: a quarter of all edges (every known board
+// is below a fifth; a level over it returns GM_EFULL and the host re-plans)
+static u64 bk_emax_bound(u64 E) { return std::min<u64>(E, std::max<u64>(E / 4, 1u << 20)); }
+struct BkScratch {
+  size_t lv, pbase, bh, ph, boff, tot, cbase, fo, ucnt, fo2, total, meta, end;
+};
+static BkScratch bk_scratch(int T) {
+  auto r = [](size_t b) { return (b + 255) / 256 * 256; };
+  BkScratch x;
+  size_t o = r(devstate_bytes(T));
+  x.lv = o; o += r(sizeof(BkLevel) * (size_t)T);
+  x.pbase = o; o += r((size_t)T * (kBkC + 1) * 4);
+  x.bh = o; o += r((size_t)kBkBlocks * kBkC * 4);
+  x.ph = o; o += r((size_t)kBkBlocks * kBkC * 4);
+  x.boff = o; o += r((size_t)kBkBlocks * kBkC * 4);
+  x.tot = o; o += r(2 * kBkC * 4);
+  x.cbase = o; o += r((kBkC + 1) * 4);
+  const size_t NBmax = (size_t)kBkC << kBkMaxFineBits;
+  x.fo = o; o += r((NBmax + 1) * 4);
+  x.ucnt = o; o += r(NBmax * 4);
+  x.fo2 = o; o += r((NBmax + 1) * 4);
+  x.total = o; o += r(2 * 8);
+  x.meta = o; o += r((size_t)T * (NBmax + 1) * 4);
+  x.end = o;
+  return x;
+}
+
 int gm_plan(int game, uint64_t positions, uint32_t flags, uint64_t max_table_bytes, gm_plan_t* out) {
   const Desc* d = get_game(game);
   if (!d || !out) return fail(GM_EINVAL, "bad argument");
@@ -1434,6 +1505,18 @@ int gm_plan(int game, uint64_t positions, uint32_t flags, uint64_t max_table_byt
   if (positions == 0) {
     gm_game_info(game, &positions, nullptr, nullptr);
     if (positions == 0) return fail(GM_EINVAL, "no known position bound for this board; pass an estimate");
+  }
+  if (bk_ok(d) && !(flags & GM_F_HASH_TABLE)) {
+    // bucketed levels: keys (levels buffer), words + in-edges + two
+    // partition buffers of the widest level's in-edges (table buffer)
+    const u64 P = positions + 64, E = bk_edges_bound(d, positions), Em = bk_emax_bound(E);
+    if (Em >= 0xFFFFFFF0ull) return fail(GM_EINVAL, "a level of more than 2^32 edges: not supported");
+    out->mode = GM_MODE_BUCKETED;
+    out->level_capacity = P;
+    out->table_slots = E;
+    out->table_bytes = 4 * P + 8 * E + 24 * Em;
+    out->scratch_bytes = bk_scratch(d->max_levels).end;
+    return 0;
   }
   uint64_t slots = 1024;
   while (slots < 2 * positions) slots <<= 1;  // load factor <= 0.5
@@ -1550,6 +1633,13 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
     if (buf->table_bytes < need)
       return fail(GM_EINVAL, "dense table of %llu bytes, these flags need %llu (plan with the flags the solver is "
                              "created with)", (unsigned long long)buf->table_bytes, (unsigned long long)need);
+  } else if (buf->mode == GM_MODE_BUCKETED) {
+    if (world != 1 || rank != 0) return fail(GM_EINVAL, "bucketed levels solve on one GPU (md5 shards use keyed tables)");
+    if (!bk_ok(d)) return fail(GM_EINVAL, "bucketed levels need every move to advance one level");
+    if (!buf->levels || buf->level_capacity < 2) return fail(GM_EINVAL, "null level store");
+    if (buf->scratch_bytes < bk_scratch(d->max_levels).end) return fail(GM_EINVAL, "scratch too small (use gm_plan)");
+    const u64 fixed = 4 * buf->level_capacity + 8 * buf->table_slots;
+    if (buf->table_bytes < fixed + 24 * 1024ull) return fail(GM_EINVAL, "bucketed table too small (use gm_plan)");
   } else if (buf->mode == GM_MODE_HASHED) {
     if (world < 1 || rank < 0 || rank >= world) return fail(GM_EINVAL, "bad shard %d/%d", rank, world);
     if (!buf->levels || buf->level_capacity < 1) return fail(GM_EINVAL, "null level store");
@@ -1694,6 +1784,41 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
       s->glist = dl;
     }
   }
+  if (s->mode == GM_MODE_BUCKETED) {
+    char* t = (char*)buf->table;
+    s->Pcap = buf->level_capacity;
+    s->Ecap = buf->table_slots;
+    s->Emax = std::min<u64>((buf->table_bytes - 4 * s->Pcap - 8 * s->Ecap) / 24, 0xFFFFFFF0ull);
+    s->bkK = (u64*)buf->levels;
+    s->bkW = (uint32_t*)t;
+    t += (4 * s->Pcap + 7) & ~7ull;
+    s->REp = (uint32_t*)t;
+    t += 4 * s->Ecap;
+    s->REc = (uint32_t*)t;
+    t += (4 * s->Ecap + 7) & ~7ull;
+    s->S1k = (u64*)t;
+    t += 8 * s->Emax;
+    s->S2k = (u64*)t;
+    t += 8 * s->Emax;
+    s->S1p = (uint32_t*)t;
+    t += 4 * s->Emax;
+    s->S2p = (uint32_t*)t;
+    const BkScratch x = bk_scratch(d->max_levels);
+    char* sc = (char*)buf->scratch;
+    s->bkL = (BkLevel*)(sc + x.lv);
+    s->pbase = (uint32_t*)(sc + x.pbase);
+    s->bh = (uint32_t*)(sc + x.bh);
+    s->ph = (uint32_t*)(sc + x.ph);
+    s->boff = (uint32_t*)(sc + x.boff);
+    s->tot = (uint32_t*)(sc + x.tot);
+    s->cbase = (uint32_t*)(sc + x.cbase);
+    s->fo = (uint32_t*)(sc + x.fo);
+    s->ucnt = (uint32_t*)(sc + x.ucnt);
+    s->fo2 = (uint32_t*)(sc + x.fo2);
+    s->bktotal = (u64*)(sc + x.total);
+    s->meta = (uint32_t*)(sc + x.meta);
+    s->meta_cap = (x.end - x.meta) / 4;
+  }
   if (s->mode == GM_MODE_DENSE) {
     int rc = dense_choose(s);
     if (rc) {
@@ -1759,11 +1884,13 @@ void gm_solver_destroy(gm_solver* s) {
 }
 
 static int solve_dense(gm_solver* s, gm_result* out);
+static int solve_bucketed(gm_solver* s, gm_result* out);
 
 int gm_solver_solve(gm_solver* s, gm_result* out) {
   if (!s || !out) return fail(GM_EINVAL, "bad argument");
   memset(out, 0, sizeof *out);
   if (s->mode == GM_MODE_DENSE) return solve_dense(s, out);
+  if (s->mode == GM_MODE_BUCKETED) return solve_bucketed(s, out);
   if (s->world > 1) return fail(GM_EINVAL, "keyed-table shard %d/%d: drive it with gm_ks_* (md5 exchange)", s->rank, s->world);
   const int T = s->d.max_levels;
   // steps [first, stop) of the 2T (gm_solver_set_steps); forward level L is
@@ -2444,6 +2571,292 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
 
 static int solve_dense(gm_solver* s, gm_result* out) { return run_dense({s}, out); }
 
+// ---------------------------------------------------------------------------
+// BUCKETED solve (gm_bucketed.h).  Steps as in the other layouts: forward
+// step L (L < T - 1) builds level L + 1 from level L; backward step
+// 2T - 1 - L resolves level L.  The host reads back two small arrays per
+// forward level (partition sizes, then the level's unique count) to size
+// the next launches and check capacities BEFORE any kernel writes past
+// them; the backward pass is enqueued without host round trips.
+// ---------------------------------------------------------------------------
+static uint32_t bitlen64(u64 x) { return x ? 64u - (uint32_t)__builtin_clzll(x) : 0u; }
+// parent-range geometry of a level of n positions (B3-B5): coarse ranges
+// index >> pshift (< 256 of them), fine ranges index >> fb (<= 2^13 parents,
+// <= 256 per coarse range)
+static bool bk_ranges(u64 n, uint32_t* pshift, uint32_t* fb) {
+  const uint32_t bl = bitlen64(n ? n - 1 : 0);
+  *pshift = bl > 8 ? bl - 8 : 0;
+  *fb = std::min<uint32_t>(*pshift, (uint32_t)kBkRangeBits);
+  return *pshift - *fb <= (uint32_t)kBkMaxFineBits;
+}
+#define BK_KIND_LAUNCH(KERNEL, GRID, BLOCK, S, ...)                                                          \
+  switch ((S)->d.kind) {                                                                                     \
+    case K_TTT: hipLaunchKernelGGL(KERNEL<K_TTT>, dim3(GRID), dim3(BLOCK), 0, (S)->stream, __VA_ARGS__); break;   \
+    case K_TOOT: hipLaunchKernelGGL(KERNEL<K_TOOT>, dim3(GRID), dim3(BLOCK), 0, (S)->stream, __VA_ARGS__); break; \
+    default: hipLaunchKernelGGL(KERNEL<K_OTHELLO>, dim3(GRID), dim3(BLOCK), 0, (S)->stream, __VA_ARGS__); break;  \
+  }
+
+static int solve_bucketed(gm_solver* s, gm_result* out) {
+  const Desc& d = s->d;
+  const int T = d.max_levels;
+  const int first = (int)s->step_first, stop = s->step_stop ? (int)s->step_stop : 2 * T;
+  s->step_first = s->step_stop = 0;
+  const bool timing = (s->flags & GM_F_KERNEL_TIMING) && first == 0 && stop == 2 * T;
+  hipStream_t st = s->stream;
+  std::vector<hipEvent_t> ev;
+  auto new_event = [&](hipEvent_t* e) -> int {
+    HIPCHK(hipEventCreate(e));
+    ev.push_back(*e);
+    return 0;
+  };
+  auto cleanup = [&]() {
+    for (auto e : ev) (void)hipEventDestroy(e);
+    ev.clear();
+  };
+  hipEvent_t e0, e1, e2;
+  if (new_event(&e0) || new_event(&e1) || new_event(&e2)) return GM_EHIP;
+  // kernel-time spans (timing): [start, stop, forward?]
+  struct Span {
+    hipEvent_t a, b;
+    bool fwd;
+  };
+  std::vector<Span> spans;
+  u64 nfwd = 0, nbwd = 0;
+  auto span = [&](bool fwd) -> hipEvent_t* {  // opens a span; returns its stop event to record later
+    if (!timing) return nullptr;
+    Span x{};
+    x.fwd = fwd;
+    if (new_event(&x.a) || new_event(&x.b)) return nullptr;
+    if (hipEventRecord(x.a, st) != hipSuccess) return nullptr;
+    spans.push_back(x);
+    return &spans.back().b;
+  };
+  auto span_end = [&](hipEvent_t* b) -> int {
+    if (b) HIPCHK(hipEventRecord(*b, st));
+    return 0;
+  };
+  int rc = 0;
+  auto bail = [&](int code) {
+    (void)hipStreamSynchronize(st);
+    cleanup();
+    return code;
+  };
+  auto t0 = std::chrono::steady_clock::now();
+  HIPCHK(hipEventRecord(e0, st));
+  std::vector<BkLevel>& lv = s->lvh;
+  if (first == 0) {
+    HIPCHK(hipMemsetAsync(s->st, 0, devstate_bytes(T), st));
+    HIPCHK(hipMemsetAsync(s->bkL, 0, sizeof(BkLevel) * (size_t)T, st));
+    lv.assign((size_t)T, BkLevel{});
+    lv[0].n = 1;
+    HIPCHK(hipMemcpyAsync(s->bkK, &s->d.root, sizeof(u64), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(s->bkL, lv.data(), sizeof(BkLevel), hipMemcpyHostToDevice, st));
+  } else {
+    lv.assign((size_t)T, BkLevel{});
+    HIPCHK(hipMemcpyAsync(lv.data(), s->bkL, sizeof(BkLevel) * (size_t)T, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  std::vector<uint32_t> htot(2 * kBkC);
+  std::vector<std::vector<uint32_t>> keep;  // host arrays of async H2D copies, alive until the end
+  uint32_t herr = 0;
+  // ---- forward ----
+  for (int L = first; L < T && L < stop; L++) {
+    if (L + 1 >= T) continue;  // the last level expands nothing (backward checks it holds only primitives)
+    BkLevel& P = lv[(size_t)L];
+    BkLevel& X = lv[(size_t)L + 1];
+    u64 re_used = P.rb + P.ein;
+    u64 meta_used = 0;
+    for (int i = 1; i <= L; i++)
+      if (lv[(size_t)i].nbits) meta_used = std::max<u64>(meta_used, lv[(size_t)i].cst_off + (1ull << lv[(size_t)i].nbits) + 1);
+    X = BkLevel{};
+    X.lb = P.lb + P.n;
+    X.rb = re_used;
+    if (!bk_ranges(P.n, &P.pshift, &P.fb))
+      return bail(fail(GM_EFULL, "level %d holds %llu positions: more than the 2^29 a bucketed level supports", L,
+                       (unsigned long long)P.n));
+    P.eout = 0;
+    if (P.n) {
+      const u64 nblk = std::min<u64>(kBkBlocks, (P.n + 255) / 256), chunk = (P.n + nblk - 1) / nblk;
+      hipEvent_t* sp = span(true);
+      BK_KIND_LAUNCH(k_bk_count, nblk, 256, s, s->d, s->bkK + P.lb, P.n, chunk, P.pshift, s->bh, s->ph, s->st);
+      hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, st, s->bh, (uint32_t)nblk, s->boff, s->tot);
+      hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, st, s->ph, (uint32_t)nblk, s->ph, s->tot + kBkC);
+      if ((rc = span_end(sp))) return bail(rc);
+      nfwd += 3;
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipMemcpyAsync(htot.data(), s->tot, 2 * kBkC * 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(&herr, &s->st->err, 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      if (herr) return bail(fail(GM_ECORRUPT, "level %d:%s", L, err_text(herr).c_str()));
+      keep.emplace_back(2 * (kBkC + 1));
+      std::vector<uint32_t>& hb = keep.back();  // [coarse bases | parent-range bases]
+      u64 E = 0, Ep = 0;
+      for (int j = 0; j < kBkC; j++) {
+        hb[(size_t)j] = (uint32_t)E;
+        hb[(size_t)kBkC + 1 + j] = (uint32_t)Ep;
+        E += htot[(size_t)j];
+        Ep += htot[(size_t)kBkC + j];
+      }
+      if (E != Ep) return bail(fail(GM_ECORRUPT, "level %d: %llu children by partition, %llu by parent", L,
+                                    (unsigned long long)E, (unsigned long long)Ep));
+      if (E > s->Emax) return bail(fail(GM_EFULL, "level %d emits %llu children; the plan holds %llu per level", L,
+                                        (unsigned long long)E, (unsigned long long)s->Emax));
+      if (re_used + E > s->Ecap) return bail(fail(GM_EFULL, "edges exceed the plan's %llu", (unsigned long long)s->Ecap));
+      hb[(size_t)kBkC] = (uint32_t)E;
+      hb[(size_t)2 * kBkC + 1] = (uint32_t)Ep;
+      P.eout = E;
+      X.ein = E;
+      HIPCHK(hipMemcpyAsync(s->cbase, hb.data(), (kBkC + 1) * 4, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(s->pbase + (size_t)L * (kBkC + 1), hb.data() + kBkC + 1, (kBkC + 1) * 4,
+                            hipMemcpyHostToDevice, st));
+      if (E) {
+        uint32_t f = 0;
+        while (f < (uint32_t)kBkMaxFineBits && (E >> f) > (u64)kBkC * 4096) f++;
+        const uint32_t F = 1u << f, NB = (uint32_t)kBkC << f;
+        X.nbits = 8 + f;
+        if (meta_used + NB + 1 > s->meta_cap) return bail(fail(GM_ECORRUPT, "bucket tables exceed the scratch"));
+        X.cst_off = (uint32_t)meta_used;
+        const int gd = (int)std::min<uint32_t>(NB, 512);
+        sp = span(true);
+        BK_KIND_LAUNCH(k_bk_expand, nblk, 256, s, s->d, s->bkK + P.lb, P.n, chunk, s->boff, s->cbase, s->S1k, s->S1p);
+        const u64* fk = s->S1k;
+        const uint32_t* fp = s->S1p;
+        const uint32_t* fof = s->cbase;
+        if (F > 1) {
+          hipLaunchKernelGGL((k_bk_fine<true, u64>), dim3(kBkC), dim3(kBkFineThreads), 0, st, s->S1k, s->S1p,
+                             s->cbase, 56u - f, F, s->S2k, s->S2p, s->fo);
+          fk = s->S2k;
+          fp = s->S2p;
+          fof = s->fo;
+          nfwd++;
+        }
+        hipLaunchKernelGGL(k_bk_dedup_count, dim3(gd), dim3(kBkDedupThreads), 0, st, fk, fof, NB, s->ucnt, s->st);
+        hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, st, s->ucnt, NB, s->meta + X.cst_off, s->bktotal);
+        if ((rc = span_end(sp))) return bail(rc);
+        nfwd += 3;
+        HIPCHK(hipGetLastError());
+        u64 n1 = 0;
+        HIPCHK(hipMemcpyAsync(&n1, s->bktotal, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(&herr, &s->st->err, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        if (herr) {
+          const bool full = herr & ERR_BUCKET_FULL;
+          return bail(fail(full ? GM_EFULL : GM_ECORRUPT, "level %d:%s", L + 1, err_text(herr).c_str()));
+        }
+        if (X.lb + n1 > s->Pcap) return bail(fail(GM_EFULL, "positions exceed the plan's %llu", (unsigned long long)s->Pcap));
+        X.n = n1;
+        sp = span(true);
+        hipLaunchKernelGGL(k_bk_dedup_write, dim3(gd), dim3(kBkDedupThreads), 0, st, fk, fp, fof,
+                           (const uint32_t*)s->meta + X.cst_off, NB, s->bkK + X.lb, s->REp + X.rb, s->REc + X.rb,
+                           s->st);
+        if ((rc = span_end(sp))) return bail(rc);
+        nfwd++;
+        HIPCHK(hipGetLastError());
+      }
+    }
+    HIPCHK(hipMemcpyAsync(s->bkL + L, &lv[(size_t)L], 2 * sizeof(BkLevel), hipMemcpyHostToDevice, st));
+  }
+  HIPCHK(hipEventRecord(e1, st));
+  // ---- backward ----
+  for (int L = T - 1; L >= 0; L--) {
+    const int k = 2 * T - 1 - L;
+    if (k < first) continue;
+    if (k >= stop) break;
+    BkLevel& P = lv[(size_t)L];
+    if (!P.n) continue;
+    if (!bk_ranges(P.n, &P.pshift, &P.fb)) return bail(fail(GM_EFULL, "level %d too wide", L));
+    const uint32_t NR = (uint32_t)((P.n + (1ull << P.fb) - 1) >> P.fb);
+    const int gr = (int)std::min<uint32_t>(NR, 512);
+    hipEvent_t* sp = span(false);
+    if (L + 1 < T && P.eout) {
+      const BkLevel& X = lv[(size_t)L + 1];
+      const u64 m = P.eout;
+      const u64 nblk = std::min<u64>(kBkBlocks, (m + 255) / 256), chunk = (m + nblk - 1) / nblk;
+      const uint32_t* pb = s->pbase + (size_t)L * (kBkC + 1);
+      uint32_t* Ap = (uint32_t*)s->S1k;
+      hipLaunchKernelGGL(k_bk_acount, dim3(nblk), dim3(256), 0, st, s->REp + X.rb, m, chunk, P.pshift, s->bh);
+      hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, st, s->bh, (uint32_t)nblk, s->boff, s->tot);
+      hipLaunchKernelGGL(k_bk_answer, dim3(nblk), dim3(256), 0, st, s->REp + X.rb, s->REc + X.rb, m, chunk, P.pshift,
+                         s->boff, pb, s->bkW + X.lb, Ap, s->S1p);
+      nbwd += 3;
+      const uint32_t Fp = 1u << (P.pshift - P.fb);
+      const uint32_t *ap = Ap, *aw = s->S1p, *fo = pb;
+      if (Fp > 1) {
+        hipLaunchKernelGGL((k_bk_fine<false, uint32_t>), dim3(kBkC), dim3(kBkFineThreads), 0, st, Ap, s->S1p, pb,
+                           P.fb, Fp, (uint32_t*)s->S2k, s->S2p, s->fo2);
+        ap = (uint32_t*)s->S2k;
+        aw = s->S2p;
+        fo = s->fo2;
+        nbwd++;
+      }
+      BK_KIND_LAUNCH(k_bk_reduce, gr, kBkDedupThreads, s, s->d, s->bkK + P.lb, P.n, ap, aw, fo, P.fb, NR,
+                     s->bkW + P.lb, s->st);
+    } else {
+      BK_KIND_LAUNCH(k_bk_reduce, gr, kBkDedupThreads, s, s->d, s->bkK + P.lb, P.n, (const uint32_t*)nullptr,
+                     (const uint32_t*)nullptr, (const uint32_t*)nullptr, P.fb, NR, s->bkW + P.lb, s->st);
+    }
+    nbwd++;
+    if ((rc = span_end(sp))) return bail(rc);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipEventRecord(e2, st));
+  if (stop < 2 * T) {  // stopped early: the state stays in the buffers for a resume
+    HIPCHK(hipMemcpyAsync(s->bkL, lv.data(), sizeof(BkLevel) * (size_t)T, hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));
+    cleanup();
+    out->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return GM_PARTIAL;
+  }
+  HIPCHK(hipMemcpyAsync(s->bkL, lv.data(), sizeof(BkLevel) * (size_t)T, hipMemcpyHostToDevice, st));
+  uint32_t root_word = NO_WORD;
+  HIPCHK(hipMemcpyAsync(&root_word, s->bkW, 4, hipMemcpyDeviceToHost, st));
+  std::vector<unsigned char> host(devstate_bytes(T));
+  HIPCHK(hipMemcpyAsync(host.data(), s->st, host.size(), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  auto t1 = std::chrono::steady_clock::now();
+  const DevState* hs = (const DevState*)host.data();
+  float f = 0, b = 0;
+  HIPCHK(hipEventElapsedTime(&f, e0, e1));
+  HIPCHK(hipEventElapsedTime(&b, e1, e2));
+  out->ms_forward = f;
+  out->ms_backward = b;
+  out->ms_total = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  if (timing) {
+    double sx = 0, sr = 0;
+    for (const Span& x : spans) {
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, x.a, x.b));
+      (x.fwd ? sx : sr) += ms;
+    }
+    out->ms_expand_kernels = sx;
+    out->ms_resolve_kernels = sr;
+    out->n_expand_launches = nfwd;
+    out->n_resolve_launches = nbwd;
+  }
+  cleanup();
+  u64 pos = 0, wmax = 0;
+  uint32_t nlev = 0;
+  for (const BkLevel& x : lv) {
+    pos += x.n;
+    wmax = std::max<u64>(wmax, x.n);
+    nlev += x.n > 0;
+  }
+  out->positions = pos;
+  out->edges = hs->edges;
+  out->primitives = hs->prims;
+  out->levels = nlev;
+  out->max_level_width = (uint32_t)std::min<u64>(wmax, 0xFFFFFFFFull);
+  out->root_word = root_word;
+  if (hs->err) {
+    const bool full = hs->err & (ERR_TABLE_FULL | ERR_LEVELS_FULL | ERR_BUCKET_FULL);
+    return fail(full ? GM_EFULL : GM_ECORRUPT, "solve failed:%s", err_text(hs->err).c_str());
+  }
+  if (root_word == NO_WORD) return fail(GM_ECORRUPT, "root unresolved");
+  out->root_value = (int32_t)(root_word & 3u);
+  out->root_remoteness = root_word >> 2;
+  return 0;
+}
+
 int gm_solve_group(gm_solver** shards, int n, gm_result* out) {
   if (!shards || n < 1 || !out) return fail(GM_EINVAL, "bad argument");
   memset(out, 0, sizeof *out);
@@ -2460,6 +2873,9 @@ int gm_solver_query(gm_solver* s, const uint64_t* keys_dev, uint64_t n, uint32_t
   if (s->mode == GM_MODE_DENSE)
     hipLaunchKernelGGL(k_dense_query, dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->view, s->words, s->bits,
                        (const u64*)keys_dev, n, words_dev, s->w16);
+  else if (s->mode == GM_MODE_BUCKETED)
+    hipLaunchKernelGGL(k_bk_query, dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->bkK, s->bkW, s->bkL,
+                       s->d.max_levels, s->meta, (const u64*)keys_dev, n, words_dev);
   else
     hipLaunchKernelGGL(k_query, dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->tab, s->mask, (const u64*)keys_dev, n,
                        words_dev);
@@ -2470,6 +2886,15 @@ int gm_solver_query(gm_solver* s, const uint64_t* keys_dev, uint64_t n, uint32_t
 
 int gm_solver_positions(gm_solver* s, uint64_t* keys_dev, uint64_t cap, uint64_t* n) {
   if (!s || !n) return fail(GM_EINVAL, "bad argument");
+  if (s->mode == GM_MODE_BUCKETED) {  // every level's keys, contiguous
+    u64 tot = 0;
+    for (const BkLevel& x : s->lvh) tot += x.n;
+    *n = tot;
+    if (tot > cap || !keys_dev) return cap < tot ? fail(GM_EFULL, "need %llu slots", (unsigned long long)tot) : 0;
+    HIPCHK(hipMemcpyAsync(keys_dev, s->bkK, tot * sizeof(u64), hipMemcpyDeviceToDevice, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return 0;
+  }
   u64 cur[2];
   HIPCHK(hipStreamSynchronize(s->stream));
   HIPCHK(hipMemcpy(cur, s->st, sizeof cur, hipMemcpyDeviceToHost));
@@ -2498,7 +2923,11 @@ int gm_solver_checksum(gm_solver* s, uint64_t out[6]) {
   if (s->mode == GM_MODE_DENSE)
     hipLaunchKernelGGL(k_checksum_dense, dim3(s->grid), dim3(kBlock), 0, s->stream, s->d, s->view, s->words, s->bits,
                        (u64)s->d.max_levels, s->w16, acc);
-  else
+  else if (s->mode == GM_MODE_BUCKETED) {
+    u64 tot = 0;
+    for (const BkLevel& x : s->lvh) tot += x.n;
+    hipLaunchKernelGGL(k_checksum_flat, dim3(s->grid), dim3(kBlock), 0, s->stream, s->d, s->bkK, s->bkW, tot, acc);
+  } else
     hipLaunchKernelGGL(k_checksum_hashed, dim3(s->grid), dim3(kBlock), 0, s->stream, s->d, s->tab, s->mask, s->lv,
                        s->lcap, s->st, acc);
   HIPCHK(hipGetLastError());

@@ -50,7 +50,9 @@ class Solver:
                  layout="auto", max_table_bytes=0, rank=0, world=1,
                  stream=None, flags=0):
         """layout: "auto" (dense when the descriptor supports it and the
-        table fits max_table_bytes, else hashed), "dense" or "hashed".
+        table fits max_table_bytes; else bucketed levels when every move
+        advances one level; else the keyed hash table), "dense", "bucketed"
+        or "hashed" (the open-addressing hash table).
         flags: kernel-family flags (_lib.GM_F_WORDS32 / GM_F_RESOLVE_SCALAR /
         GM_F_SHARD_INORDER, A/B runs), fixed for this solver's lifetime.
         rank/world > 1: this object is one shard of a dense multi-GPU solve
@@ -65,8 +67,8 @@ class Solver:
         self.spec = spec if isinstance(spec, GameSpec) else GameSpec(*spec)
         self.device = torch.device(device if device is not None else "cuda")
         self.kernel_timing = kernel_timing
-        if layout not in ("auto", "dense", "hashed"):
-            raise ValueError("layout must be auto, dense or hashed")
+        if layout not in ("auto", "dense", "hashed", "bucketed"):
+            raise ValueError("layout must be auto, dense, bucketed or hashed")
         self.layout = layout
         self.max_table_bytes = int(max_table_bytes)
         self.rank, self.world = int(rank), int(world)
@@ -84,7 +86,8 @@ class Solver:
         L = _lib.load()
         self._free()
         plan = _lib.gm_plan_t()
-        flags = self.flags | (_lib.GM_F_FORCE_HASHED if self.layout == "hashed" else 0)
+        flags = self.flags | {"hashed": _lib.GM_F_FORCE_HASHED | _lib.GM_F_HASH_TABLE,
+                              "bucketed": _lib.GM_F_FORCE_HASHED}.get(self.layout, 0)
         if self.world > 1 and self.layout != "hashed":
             _lib.check(L.gm_plan_shard(self.spec.id, self.rank, self.world,
                                        flags, self.max_table_bytes,
@@ -95,6 +98,9 @@ class Solver:
         if self.layout == "dense" and plan.mode != _lib.GM_MODE_DENSE:
             raise ValueError("%r has no dense layout (or it does not fit)"
                              % (self.spec,))
+        if self.layout == "bucketed" and plan.mode != _lib.GM_MODE_BUCKETED:
+            raise ValueError("%r: bucketed levels need every move to advance "
+                             "one level" % (self.spec,))
         with torch.cuda.device(self.device):
             table = torch.empty(plan.table_bytes, dtype=torch.uint8,
                                 device=self.device)
@@ -203,8 +209,7 @@ class Solver:
             ms_resolve_kernels=r.ms_resolve_kernels,
             n_expand_launches=r.n_expand_launches,
             n_resolve_launches=r.n_resolve_launches,
-            extra={"layout": "dense" if self.plan.mode == _lib.GM_MODE_DENSE
-                   else "hashed",
+            extra={"layout": _lib.MODE_NAMES[self.plan.mode],
                    "word_bits": r.word_bits,
                    "resolve_kernel": _lib.RESOLVE_KERNELS.get(r.kernels & 0xFFFF),
                    "pull_kernel": _lib.PULL_KERNELS.get(r.kernels >> 16),

@@ -76,7 +76,7 @@ def build_parser():
                    help="location to store statistics about game",
                    action="store")
     # additions
-    p.add_argument("--layout", choices=["auto", "dense", "hashed", "graph"],
+    p.add_argument("--layout", choices=["auto", "dense", "bucketed", "hashed", "graph"],
                    default="auto",
                    help="table layout (DESIGN.md §Layout); graph = host-"
                         "enumerated positions, for files without a descriptor")

@@ -56,6 +56,13 @@ typedef struct gm_slot {
  * four_to_one, sum_four_to_one). */
 #define GM_MODE_HASHED 0u
 #define GM_MODE_DENSE 1u
+/* BUCKETED (keyed games whose every move advances one level: tic-tac-toe,
+ * toot-and-otto, othello; one GPU): no hash table.  Each level's unique keys
+ * grouped by hash bucket in the levels buffer (level_capacity keys), 32-bit
+ * words + the level's in-edges + partition scratch in the table buffer
+ * (table_slots = edge capacity); dedup and lookups happen in LDS
+ * (gamesmanmpi_amd/csrc/gm_bucketed.h). */
+#define GM_MODE_BUCKETED 2u
 
 /* Sizes the caller must allocate for a solve (see gm_plan). */
 typedef struct gm_plan_t {
@@ -95,6 +102,8 @@ typedef struct gm_buffers {
 #define GM_F_RESOLVE_SCALAR 8u /* dense: one-prefix-per-lane resolve, 32-bit */
 #define GM_F_SHARD_INORDER 16u /* dense shards: exchange each level's halo in
                                   order instead of overlapping it */
+#define GM_F_HASH_TABLE 32u    /* gm_plan, keyed games: the open-addressing
+                                  hash table (HASHED) instead of BUCKETED */
 
 typedef struct gm_result {
   uint32_t root_word;

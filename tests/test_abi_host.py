@@ -149,4 +149,10 @@ def test_plan_sizes():
     assert p.mode == _lib.GM_MODE_HASHED
     t = GameSpec("toot_and_otto_bitstring", "length=4,height=4")
     _lib.check(_lib.load().gm_plan(t.id, 0, 0, 0, ctypes.byref(p)))
+    assert p.mode == _lib.GM_MODE_BUCKETED  # keyed game, every move one level
+    assert p.level_capacity == 3468773 + 64 and p.table_slots == 9932808 + 1024
+    _lib.check(_lib.load().gm_plan(t.id, 0, _lib.GM_F_HASH_TABLE, 0, ctypes.byref(p)))
+    assert p.mode == _lib.GM_MODE_HASHED
+    # step-2 games (sums) never take the bucketed layout
+    _lib.check(_lib.load().gm_plan(s.id, 0, _lib.GM_F_FORCE_HASHED, 0, ctypes.byref(p)))
     assert p.mode == _lib.GM_MODE_HASHED

@@ -19,6 +19,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CASES = [
     ("tic_tac_toe_np", "", "hashed", {}),
     ("othello_bit_new", "length=4,height=4", "hashed", {}),
+    ("tic_tac_toe_np", "", "bucketed", {}),
+    ("othello_bit_new", "length=4,height=4", "bucketed", {}),
+    ("toot_and_otto_bitstring", "length=4,height=3", "bucketed", {}),
     ("sum_four_to_one", "heaps=15:15:15:15", "dense", {}),
     ("sum_four_to_one", "heaps=15:15:15:15", "dense", {"flags": 4}),  # GM_F_WORDS32
     ("four_to_one", "start=40", "dense", {}),

@@ -44,3 +44,37 @@ def test_edge_shape_matches_oracle(name, params, root, layout):
     assert len(keys) == sol.count
     for k, v, m in zip(keys.tolist(), val.tolist(), rem.tolist()):
         assert (v, m) == tuple(sol.lookup(spec.decode(k))), (k, v, m)
+
+
+KEYED_SHAPES = [
+    ("toot_and_otto_bitstring", "length=1,height=1"),
+    ("toot_and_otto_bitstring", "length=2,height=1"),
+    ("toot_and_otto_bitstring", "length=1,height=3"),
+    ("toot_and_otto_bitstring", "length=2,height=2"),
+    ("toot_and_otto_bitstring", "length=3,height=2"),
+    ("toot_and_otto_bitstring", "length=2,height=4"),
+    ("othello_bit_new", "length=2,height=2"),   # the root is primitive: one level
+    ("othello_bit_new", "length=4,height=4"),
+    ("mttt", ""),
+]
+
+
+@pytest.mark.parametrize("layout", ["bucketed", "hashed"])
+@pytest.mark.parametrize("name,params", KEYED_SHAPES)
+def test_keyed_edge_shape_matches_oracle(name, params, layout):
+    """Small and degenerate boards through both keyed layouts: a primitive
+    root, levels of one position, single-bucket levels (bucketed levels:
+    partitions mostly empty) -- every position against the oracle."""
+    from gamesmanmpi_amd.games import GameSpec
+    from gamesmanmpi_amd.solver import Solver
+    from oracle.oracle import Game  # checker only
+    spec = GameSpec(name, params)
+    sol = Game(name, params).solve(1 << 22)
+    s = Solver(spec, layout=layout, positions=max(64, sol.count))
+    r = s.solve()
+    assert r.extra["layout"] == layout
+    assert (r.positions, r.edges, r.root_line) == (sol.count, sol.edges, sol.root_line)
+    keys, val, rem = s.dump()
+    assert len(keys) == sol.count
+    for k, v, m in zip(keys.tolist(), val.tolist(), rem.tolist()):
+        assert (v, m) == tuple(sol.lookup(spec.decode(k))), (k, v, m)

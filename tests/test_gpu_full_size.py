@@ -62,7 +62,13 @@ def test_gpu_sum_15x5_checksum_both_layouts():
 
 
 def test_gpu_toot_5x4_checksum():
-    _check("toot_5x4")
+    s, r = _check("toot_5x4")
+    assert r.extra["layout"] == "bucketed"
+
+
+def test_gpu_toot_5x4_checksum_hash_table():
+    s, r = _check("toot_5x4", layout="hashed")
+    assert r.extra["layout"] == "hashed"
 
 
 def test_gpu_toot_6x4_checksum():
