@@ -67,6 +67,7 @@ struct Desc {
   uint64_t tmask[4];
   int tstep[4];
   uint64_t full;   // all-cells mask
+  uint64_t col0;   // K_TOOT: the cells of column 0 (bit L*y for every y)
   uint64_t root;   // root key
   int max_levels;  // levels the pipeline must provision (root level = 0)
   // K_SUM dense (perfect-hash) layout: slot = level * W + prefix, where
@@ -283,9 +284,10 @@ GM_HD int toot_children(const Desc& d, uint64_t k, F&& emit) {
   int n = 0;
   for (int x = 0; x < L; x++) {
     if ((occ >> (L * (H - 1) + x)) & 1) continue;  // column full (:95)
-    int y = 0;
-    while ((occ >> (L * y + x)) & 1) y++;          // lowest blank (:112-115)
-    uint64_t cell = 1ull << (L * y + x);
+    // lowest blank cell of column x (:112-115): the lowest clear bit of the
+    // column's cells, isolated (no loop; exact for any key)
+    const uint64_t blank = ~(occ >> x) & d.col0;
+    const uint64_t cell = (blank & (~blank + 1)) << x;
     if (nT > 0) { emit((k - (1ull << hb)) ^ turn ^ cell, 1); n++; }
     if (nO > 0) { emit((k - (1ull << (hb + 3))) ^ turn ^ (cell << A), 1); n++; }
   }

@@ -171,6 +171,7 @@ static int build_desc(const char* name, const char* params, Desc* out) {
       return fail(GM_EINVAL, "toot board %dx%d does not fit a 64-bit key (area <= 25)", d.L, d.H);
     d.nbits = (2 * d.A + 17 + 7) / 8 * 8;
     d.full = (1ull << d.A) - 1;
+    for (int y = 0; y < d.H; y++) d.col0 |= 1ull << (d.L * y);
     // word starts per direction: (1,0) (0,1) (1,1) (1,-1); steps in cell index
     const int dxs[4] = {1, 0, 1, 1}, dys[4] = {0, 1, 1, -1};
     for (int i = 0; i < 4; i++) {
@@ -1481,7 +1482,7 @@ static BkScratch bk_scratch(int T) {
   x.ucnt = o; o += r(NBmax * 4);
   x.fo2 = o; o += r((NBmax + 1) * 4);
   x.total = o; o += r(2 * 8);
-  x.meta = o; o += r((size_t)T * (NBmax + 1) * 4);
+  x.meta = o; o += r((size_t)T * 2 * (NBmax + 1) * 4);  // per level: cst, fo
   x.end = o;
   return x;
 }
@@ -2667,7 +2668,8 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
     u64 re_used = P.rb + P.ein;
     u64 meta_used = 0;
     for (int i = 1; i <= L; i++)
-      if (lv[(size_t)i].nbits) meta_used = std::max<u64>(meta_used, lv[(size_t)i].cst_off + (1ull << lv[(size_t)i].nbits) + 1);
+      if (lv[(size_t)i].nbits)
+        meta_used = std::max<u64>(meta_used, lv[(size_t)i].cst_off + 2 * ((1ull << lv[(size_t)i].nbits) + 1));
     X = BkLevel{};
     X.lb = P.lb + P.n;
     X.rb = re_used;
@@ -2676,9 +2678,10 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
                        (unsigned long long)P.n));
     P.eout = 0;
     if (P.n) {
-      const u64 nblk = std::min<u64>(kBkBlocks, (P.n + 255) / 256), chunk = (P.n + nblk - 1) / nblk;
+      const u64 nblk = std::min<u64>(kBkBlocks, (P.n + kBkStreamThreads - 1) / kBkStreamThreads),
+                chunk = (P.n + nblk - 1) / nblk;
       hipEvent_t* sp = span(true);
-      BK_KIND_LAUNCH(k_bk_count, nblk, 256, s, s->d, s->bkK + P.lb, P.n, chunk, P.pshift, s->bh, s->ph, s->st);
+      BK_KIND_LAUNCH(k_bk_count, nblk, kBkStreamThreads, s, s->d, s->bkK + P.lb, P.n, chunk, P.pshift, s->bh, s->ph, s->st);
       hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, st, s->bh, (uint32_t)nblk, s->boff, s->tot);
       hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, st, s->ph, (uint32_t)nblk, s->ph, s->tot + kBkC);
       if ((rc = span_end(sp))) return bail(rc);
@@ -2714,26 +2717,28 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
         while (f < (uint32_t)kBkMaxFineBits && (E >> f) > (u64)kBkC * 4096) f++;
         const uint32_t F = 1u << f, NB = (uint32_t)kBkC << f;
         X.nbits = 8 + f;
-        if (meta_used + NB + 1 > s->meta_cap) return bail(fail(GM_ECORRUPT, "bucket tables exceed the scratch"));
+        if (meta_used + 2 * (NB + 1) > s->meta_cap) return bail(fail(GM_ECORRUPT, "bucket tables exceed the scratch"));
         X.cst_off = (uint32_t)meta_used;
-        const int gd = (int)std::min<uint32_t>(NB, 512);
+        uint32_t* cst = s->meta + X.cst_off;
+        uint32_t* fo = cst + NB + 1;  // kept: the backward pass walks the level's in-edges bucket by bucket
+        // parents per expand round: about a stage (8192 records) of children
+        const double avg = (double)E / (double)P.n;
+        uint32_t ppr = 256;
+        while (ppr < 4096 && (double)(2 * ppr) * avg <= 6144.0) ppr *= 2;
+        const int gd = (int)std::min<uint32_t>(NB, 512);  // two workgroups per CU
         sp = span(true);
-        BK_KIND_LAUNCH(k_bk_expand, nblk, 256, s, s->d, s->bkK + P.lb, P.n, chunk, s->boff, s->cbase, s->S1k, s->S1p);
-        const u64* fk = s->S1k;
-        const uint32_t* fp = s->S1p;
-        const uint32_t* fof = s->cbase;
-        if (F > 1) {
-          hipLaunchKernelGGL((k_bk_fine<true, u64>), dim3(kBkC), dim3(kBkFineThreads), 0, st, s->S1k, s->S1p,
-                             s->cbase, 56u - f, F, s->S2k, s->S2p, s->fo);
-          fk = s->S2k;
-          fp = s->S2p;
-          fof = s->fo;
-          nfwd++;
-        }
-        hipLaunchKernelGGL(k_bk_dedup_count, dim3(gd), dim3(kBkDedupThreads), 0, st, fk, fof, NB, s->ucnt, s->st);
-        hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, st, s->ucnt, NB, s->meta + X.cst_off, s->bktotal);
+        BK_KIND_LAUNCH(k_bk_expand, nblk, kBkStreamThreads, s, s->d, s->bkK + P.lb, P.n, chunk, s->boff, s->cbase, ppr,
+                       s->S1k, s->S1p);
+        // the fine partition writes the parents straight into the level's
+        // in-edge parents (REp); F3 adds the child indices (REc)
+        hipLaunchKernelGGL((k_bk_fine<true, u64>), dim3(kBkC), dim3(kBkFineThreads), 0, st, s->S1k, s->S1p,
+                           s->cbase, 56u - f, F, s->S2k, s->REp + X.rb, fo);
+        // unique keys of bucket b to S1k[fo[b] ..), compacted into the level
+        hipLaunchKernelGGL(k_bk_dedup, dim3(gd), dim3(kBkDedupThreads), 0, st, s->S2k, (const uint32_t*)fo, NB, s->S1k,
+                           s->ucnt, s->REc + X.rb, s->st);
+        hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, st, s->ucnt, NB, cst, s->bktotal);
         if ((rc = span_end(sp))) return bail(rc);
-        nfwd += 3;
+        nfwd += 4;
         HIPCHK(hipGetLastError());
         u64 n1 = 0;
         HIPCHK(hipMemcpyAsync(&n1, s->bktotal, 8, hipMemcpyDeviceToHost, st));
@@ -2746,9 +2751,8 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
         if (X.lb + n1 > s->Pcap) return bail(fail(GM_EFULL, "positions exceed the plan's %llu", (unsigned long long)s->Pcap));
         X.n = n1;
         sp = span(true);
-        hipLaunchKernelGGL(k_bk_dedup_write, dim3(gd), dim3(kBkDedupThreads), 0, st, fk, fp, fof,
-                           (const uint32_t*)s->meta + X.cst_off, NB, s->bkK + X.lb, s->REp + X.rb, s->REc + X.rb,
-                           s->st);
+        hipLaunchKernelGGL(k_bk_compact, dim3(std::min<uint32_t>(NB, 4096)), dim3(256), 0, st, (const u64*)s->S1k,
+                           (const uint32_t*)fo, (const uint32_t*)cst, NB, s->bkK + X.lb);
         if ((rc = span_end(sp))) return bail(rc);
         nfwd++;
         HIPCHK(hipGetLastError());
@@ -2770,29 +2774,32 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
     hipEvent_t* sp = span(false);
     if (L + 1 < T && P.eout) {
       const BkLevel& X = lv[(size_t)L + 1];
-      const u64 m = P.eout;
-      const u64 nblk = std::min<u64>(kBkBlocks, (m + 255) / 256), chunk = (m + nblk - 1) / nblk;
+      const uint32_t NB = 1u << X.nbits;
+      const uint32_t bpb = (NB + kBkBlocks - 1) / kBkBlocks;  // <= 256 buckets per block
+      const uint32_t nblk = (NB + bpb - 1) / bpb;
+      const uint32_t* cst = s->meta + X.cst_off;
+      const uint32_t* fo = cst + NB + 1;
       const uint32_t* pb = s->pbase + (size_t)L * (kBkC + 1);
       uint32_t* Ap = (uint32_t*)s->S1k;
-      hipLaunchKernelGGL(k_bk_acount, dim3(nblk), dim3(256), 0, st, s->REp + X.rb, m, chunk, P.pshift, s->bh);
-      hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, st, s->bh, (uint32_t)nblk, s->boff, s->tot);
-      hipLaunchKernelGGL(k_bk_answer, dim3(nblk), dim3(256), 0, st, s->REp + X.rb, s->REc + X.rb, m, chunk, P.pshift,
-                         s->boff, pb, s->bkW + X.lb, Ap, s->S1p);
+      hipLaunchKernelGGL(k_bk_acount, dim3(nblk), dim3(kBkStreamThreads), 0, st, s->REp + X.rb, fo, NB, bpb, P.pshift, s->bh);
+      hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, st, s->bh, nblk, s->boff, s->tot);
+      hipLaunchKernelGGL(k_bk_answer, dim3(nblk), dim3(kBkStreamThreads), 0, st, s->REp + X.rb, s->REc + X.rb, fo, cst,
+                         NB, bpb, P.pshift, s->boff, pb, s->bkW + X.lb, Ap, s->S1p);
       nbwd += 3;
       const uint32_t Fp = 1u << (P.pshift - P.fb);
-      const uint32_t *ap = Ap, *aw = s->S1p, *fo = pb;
+      const uint32_t *ap = Ap, *aw = s->S1p, *fr = pb;
       if (Fp > 1) {
         hipLaunchKernelGGL((k_bk_fine<false, uint32_t>), dim3(kBkC), dim3(kBkFineThreads), 0, st, Ap, s->S1p, pb,
                            P.fb, Fp, (uint32_t*)s->S2k, s->S2p, s->fo2);
         ap = (uint32_t*)s->S2k;
         aw = s->S2p;
-        fo = s->fo2;
+        fr = s->fo2;
         nbwd++;
       }
-      BK_KIND_LAUNCH(k_bk_reduce, gr, kBkDedupThreads, s, s->d, s->bkK + P.lb, P.n, ap, aw, fo, P.fb, NR,
+      BK_KIND_LAUNCH(k_bk_reduce, gr, kBkReduceThreads, s, s->d, s->bkK + P.lb, P.n, ap, aw, fr, P.fb, NR,
                      s->bkW + P.lb, s->st);
     } else {
-      BK_KIND_LAUNCH(k_bk_reduce, gr, kBkDedupThreads, s, s->d, s->bkK + P.lb, P.n, (const uint32_t*)nullptr,
+      BK_KIND_LAUNCH(k_bk_reduce, gr, kBkReduceThreads, s, s->d, s->bkK + P.lb, P.n, (const uint32_t*)nullptr,
                      (const uint32_t*)nullptr, (const uint32_t*)nullptr, P.fb, NR, s->bkW + P.lb, s->st);
     }
     nbwd++;
