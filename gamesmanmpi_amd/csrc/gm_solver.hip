@@ -938,7 +938,7 @@ struct gm_solver {
   u64 Pcap = 0, Ecap = 0, Emax = 0;
   BkLevel* bkL = nullptr;  // device level table (scratch)
   uint32_t *pbase = nullptr, *bh = nullptr, *ph = nullptr, *boff = nullptr, *tot = nullptr, *cbase = nullptr;
-  uint32_t *fo = nullptr, *ucnt = nullptr, *fo2 = nullptr, *meta = nullptr;
+  uint32_t *bkah = nullptr, *ucnt = nullptr, *meta = nullptr;
   u64* bktotal = nullptr;
   u64 meta_cap = 0;
   std::vector<BkLevel> lvh;  // host copy of the level table
@@ -1443,7 +1443,10 @@ int gm_plan_shard(int game, int rank, int world, uint32_t flags, uint64_t max_ta
 // ---- BUCKETED plan ---------------------------------------------------------
 // keyed games whose every move advances one level (the tier is the number
 // of pieces placed): the bucketed pipeline applies (gm_bucketed.h)
-static bool bk_ok(const Desc* d) { return d->kind == K_TTT || d->kind == K_TOOT || d->kind == K_OTHELLO; }
+// every move advances one level, and remoteness < 256 (packed backward answers)
+static bool bk_ok(const Desc* d) {
+  return (d->kind == K_TTT || d->kind == K_TOOT || d->kind == K_OTHELLO) && d->max_levels <= 256;
+}
 // edges bound for a positions bound: the known counts where the board and
 // bound match (SURVEY Appendix B / tests/golden), else a branching factor
 // above every known board's
@@ -1464,7 +1467,7 @@ static u64 bk_edges_bound(const Desc* d, u64 P) {
 // is below a fifth; a level over it returns GM_EFULL and the host re-plans)
 static u64 bk_emax_bound(u64 E) { return std::min<u64>(E, std::max<u64>(E / 4, 1u << 20)); }
 struct BkScratch {
-  size_t lv, pbase, bh, ph, boff, tot, cbase, fo, ucnt, fo2, total, meta, end;
+  size_t lv, pbase, bh, ph, boff, tot, cbase, ah, ucnt, total, meta, end;
 };
 static BkScratch bk_scratch(int T) {
   auto r = [](size_t b) { return (b + 255) / 256 * 256; };
@@ -1478,11 +1481,11 @@ static BkScratch bk_scratch(int T) {
   x.tot = o; o += r(2 * kBkC * 4);
   x.cbase = o; o += r((kBkC + 1) * 4);
   const size_t NBmax = (size_t)kBkC << kBkMaxFineBits;
-  x.fo = o; o += r((NBmax + 1) * 4);
+  x.ah = o; o += r((size_t)T * kBkC * kBkC * 4);  // per level: answers per (child partition, parent range)
   x.ucnt = o; o += r(NBmax * 4);
-  x.fo2 = o; o += r((NBmax + 1) * 4);
   x.total = o; o += r(2 * 8);
-  x.meta = o; o += r((size_t)T * 2 * (NBmax + 1) * 4);  // per level: cst, fo
+  const size_t NRmax = (size_t)1 << (29 - kBkRangeBits);
+  x.meta = o; o += r((size_t)T * (2 * (NBmax + 1) + NRmax + 1) * 4);  // per level: cst, fo, rfo
   x.end = o;
   return x;
 }
@@ -1813,9 +1816,8 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
     s->boff = (uint32_t*)(sc + x.boff);
     s->tot = (uint32_t*)(sc + x.tot);
     s->cbase = (uint32_t*)(sc + x.cbase);
-    s->fo = (uint32_t*)(sc + x.fo);
+    s->bkah = (uint32_t*)(sc + x.ah);
     s->ucnt = (uint32_t*)(sc + x.ucnt);
-    s->fo2 = (uint32_t*)(sc + x.fo2);
     s->bktotal = (u64*)(sc + x.total);
     s->meta = (uint32_t*)(sc + x.meta);
     s->meta_cap = (x.end - x.meta) / 4;
@@ -2666,10 +2668,12 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
     BkLevel& P = lv[(size_t)L];
     BkLevel& X = lv[(size_t)L + 1];
     u64 re_used = P.rb + P.ein;
-    u64 meta_used = 0;
-    for (int i = 1; i <= L; i++)
-      if (lv[(size_t)i].nbits)
-        meta_used = std::max<u64>(meta_used, lv[(size_t)i].cst_off + 2 * ((1ull << lv[(size_t)i].nbits) + 1));
+    u64 meta_used = 0;  // end of the meta tables of the levels so far
+    for (int i = 0; i <= L; i++) {
+      const BkLevel& Q = lv[(size_t)i];
+      if (Q.nbits) meta_used = std::max<u64>(meta_used, Q.cst_off + 2 * ((1ull << Q.nbits) + 1));
+      if (i < L && Q.eout) meta_used = std::max<u64>(meta_used, Q.rfo_off + ((Q.n + (1ull << Q.fb) - 1) >> Q.fb) + 1);
+    }
     X = BkLevel{};
     X.lb = P.lb + P.n;
     X.rb = re_used;
@@ -2680,12 +2684,20 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
     if (P.n) {
       const u64 nblk = std::min<u64>(kBkBlocks, (P.n + kBkStreamThreads - 1) / kBkStreamThreads),
                 chunk = (P.n + nblk - 1) / nblk;
+      const uint32_t NR = (uint32_t)((P.n + (1ull << P.fb) - 1) >> P.fb);
+      if (meta_used + NR + 1 > s->meta_cap) return bail(fail(GM_ECORRUPT, "bucket tables exceed the scratch"));
+      P.rfo_off = (uint32_t)meta_used;
+      meta_used += NR + 1;
+      uint32_t* rfo = s->meta + P.rfo_off;  // answers per fine parent range -> their starts
+      HIPCHK(hipMemsetAsync(rfo, 0, (NR + 1) * 4, st));
       hipEvent_t* sp = span(true);
-      BK_KIND_LAUNCH(k_bk_count, nblk, kBkStreamThreads, s, s->d, s->bkK + P.lb, P.n, chunk, P.pshift, s->bh, s->ph, s->st);
+      BK_KIND_LAUNCH(k_bk_count, nblk, kBkStreamThreads, s, s->d, s->bkK + P.lb, P.n, chunk, P.pshift, P.fb, s->bh,
+                     s->ph, rfo, s->st);
       hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, st, s->bh, (uint32_t)nblk, s->boff, s->tot);
       hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, st, s->ph, (uint32_t)nblk, s->ph, s->tot + kBkC);
+      hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, st, rfo, NR + 1, rfo, s->bktotal + 1);
       if ((rc = span_end(sp))) return bail(rc);
-      nfwd += 3;
+      nfwd += 4;
       HIPCHK(hipGetLastError());
       HIPCHK(hipMemcpyAsync(htot.data(), s->tot, 2 * kBkC * 4, hipMemcpyDeviceToHost, st));
       HIPCHK(hipMemcpyAsync(&herr, &s->st->err, 4, hipMemcpyDeviceToHost, st));
@@ -2732,7 +2744,8 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
         // the fine partition writes the parents straight into the level's
         // in-edge parents (REp); F3 adds the child indices (REc)
         hipLaunchKernelGGL((k_bk_fine<true, u64>), dim3(kBkC), dim3(kBkFineThreads), 0, st, s->S1k, s->S1p,
-                           s->cbase, 56u - f, F, s->S2k, s->REp + X.rb, fo);
+                           s->cbase, 56u - f, F, s->S2k, s->REp + X.rb, fo, (const uint32_t*)nullptr, P.pshift,
+                           s->bkah + (size_t)L * kBkC * kBkC);
         // unique keys of bucket b to S1k[fo[b] ..), compacted into the level
         hipLaunchKernelGGL(k_bk_dedup, dim3(gd), dim3(kBkDedupThreads), 0, st, s->S2k, (const uint32_t*)fo, NB, s->S1k,
                            s->ucnt, s->REc + X.rb, s->st);
@@ -2775,32 +2788,31 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
     if (L + 1 < T && P.eout) {
       const BkLevel& X = lv[(size_t)L + 1];
       const uint32_t NB = 1u << X.nbits;
-      const uint32_t bpb = (NB + kBkBlocks - 1) / kBkBlocks;  // <= 256 buckets per block
-      const uint32_t nblk = (NB + bpb - 1) / bpb;
+      const uint32_t bpb = NB / kBkC;  // block j: the children's coarse partition j
       const uint32_t* cst = s->meta + X.cst_off;
       const uint32_t* fo = cst + NB + 1;
+      const uint32_t* rfo = s->meta + P.rfo_off;
       const uint32_t* pb = s->pbase + (size_t)L * (kBkC + 1);
       uint32_t* Ap = (uint32_t*)s->S1k;
-      hipLaunchKernelGGL(k_bk_acount, dim3(nblk), dim3(kBkStreamThreads), 0, st, s->REp + X.rb, fo, NB, bpb, P.pshift, s->bh);
-      hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, st, s->bh, nblk, s->boff, s->tot);
-      hipLaunchKernelGGL(k_bk_answer, dim3(nblk), dim3(kBkStreamThreads), 0, st, s->REp + X.rb, s->REc + X.rb, fo, cst,
-                         NB, bpb, P.pshift, s->boff, pb, s->bkW + X.lb, Ap, s->S1p);
-      nbwd += 3;
+      hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, st, s->bkah + (size_t)L * kBkC * kBkC, (uint32_t)kBkC,
+                         s->boff, s->tot);
+      hipLaunchKernelGGL(k_bk_answer, dim3(kBkC), dim3(kBkStreamThreads), 0, st, s->REp + X.rb, s->REc + X.rb, fo, cst,
+                         NB, bpb, P.pshift, s->boff, pb, s->bkW + X.lb, Ap, s->st);
+      nbwd += 2;
       const uint32_t Fp = 1u << (P.pshift - P.fb);
-      const uint32_t *ap = Ap, *aw = s->S1p, *fr = pb;
+      const uint32_t* ap = Ap;
       if (Fp > 1) {
-        hipLaunchKernelGGL((k_bk_fine<false, uint32_t>), dim3(kBkC), dim3(kBkFineThreads), 0, st, Ap, s->S1p, pb,
-                           P.fb, Fp, (uint32_t*)s->S2k, s->S2p, s->fo2);
+        hipLaunchKernelGGL((k_bk_fine<false, uint32_t>), dim3(kBkC), dim3(kBkFineThreads), 0, st, Ap,
+                           (const uint32_t*)nullptr, pb, 10u + P.fb, Fp, (uint32_t*)s->S2k, (uint32_t*)nullptr,
+                           (uint32_t*)nullptr, rfo, 0u, (uint32_t*)nullptr);
         ap = (uint32_t*)s->S2k;
-        aw = s->S2p;
-        fr = s->fo2;
         nbwd++;
       }
-      BK_KIND_LAUNCH(k_bk_reduce, gr, kBkReduceThreads, s, s->d, s->bkK + P.lb, P.n, ap, aw, fr, P.fb, NR,
+      BK_KIND_LAUNCH(k_bk_reduce, gr, kBkReduceThreads, s, s->d, s->bkK + P.lb, P.n, ap, rfo, P.fb, Fp - 1, NR,
                      s->bkW + P.lb, s->st);
     } else {
       BK_KIND_LAUNCH(k_bk_reduce, gr, kBkReduceThreads, s, s->d, s->bkK + P.lb, P.n, (const uint32_t*)nullptr,
-                     (const uint32_t*)nullptr, (const uint32_t*)nullptr, P.fb, NR, s->bkW + P.lb, s->st);
+                     (const uint32_t*)nullptr, P.fb, 0u, NR, s->bkW + P.lb, s->st);
     }
     nbwd++;
     if ((rc = span_end(sp))) return bail(rc);
