@@ -15,3 +15,4 @@ pass sq SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_
 pass sq2 SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES SQ_WAVES
 pass fetch FETCH_SIZE
 pass write WRITE_SIZE
+pass tcc TCC_HIT_sum TCC_MISS_sum
