@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("name,world", [
     ("othello_4x4", 8), ("othello_4x4", 3), ("tic_tac_toe_np", 2),
     ("mttt", 5), ("toot_3x3", 4), ("toot_4x3", 8), ("four_to_one_64", 3),
-    ("sum_fto_6_6_6_6", 7),
+    ("sum_fto_6_6_6_6", 7), ("four_to_one", 5),  # README.md:13: four_to_one over 5 ranks
 ])
 def test_gpu_group_keyed_matches_golden(name, world, golden_summary):
     from gamesmanmpi_amd.games import GameSpec

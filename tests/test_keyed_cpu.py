@@ -38,7 +38,7 @@ def _check_tables(name, spec, dumps, world):
 
 @pytest.mark.parametrize("name,world", [
     ("tic_tac_toe_np", 1), ("tic_tac_toe_np", 4), ("mttt", 3),
-    ("four_to_one_20", 2), ("sum_fto_2_5_7", 5), ("toot_3x3", 8),
+    ("four_to_one_20", 2), ("sum_fto_2_5_7", 5), ("toot_3x3", 8), ("four_to_one", 5),
 ])
 def test_group_keyed_matches_golden(name, world, golden_summary):
     from gamesmanmpi_amd.keyed import GroupExchange, keyed_solve
