@@ -23,10 +23,12 @@ GM_F_WORDS32 = 4
 GM_F_RESOLVE_SCALAR = 8
 GM_F_SHARD_INORDER = 16
 GM_F_HASH_TABLE = 32  # gm_plan, keyed games: open-addressing table, not BUCKETED
-KERNEL_FLAGS = GM_F_WORDS32 | GM_F_RESOLVE_SCALAR | GM_F_SHARD_INORDER
+GM_F_WORDS16 = 64  # dense: 16-bit words where 8-bit ones would be chosen
+KERNEL_FLAGS = GM_F_WORDS32 | GM_F_RESOLVE_SCALAR | GM_F_SHARD_INORDER | GM_F_WORDS16
 # gm_result.kernels codes (gm_solver.hip DenseResolveKind / DensePullKind)
 RESOLVE_KERNELS = {1: "k_dense_resolve8p", 2: "k_dense_resolve8c", 3: "k_dense_resolve4p",
-                   4: "k_dense_resolve4c", 5: "k_dense_resolve4", 6: "k_dense_resolve"}
+                   4: "k_dense_resolve4c", 5: "k_dense_resolve4", 6: "k_dense_resolve",
+                   7: "k_dense_resolve16p"}
 PULL_KERNELS = {1: "k_dense_pull_words", 2: "k_dense_pull"}
 GM_MODE_HASHED, GM_MODE_DENSE, GM_MODE_BUCKETED = 0, 1, 2
 MODE_NAMES = {0: "hashed", 1: "dense", 2: "bucketed"}

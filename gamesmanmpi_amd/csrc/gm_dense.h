@@ -785,6 +785,16 @@ __device__ __forceinline__ uint32_t dense_parent16(uint32_t m) {
 __host__ __device__ __forceinline__ uint32_t dense_word16(uint32_t h) {
   return dense_word((h & 0x8000u) ? (0xFFFF8000u | h) : h);
 }
+// 8-bit order form (k_dense_resolve16p) -> the 32-bit one -> value | rem << 2
+__host__ __device__ __forceinline__ uint32_t dense_word8(uint32_t h) {
+  return dense_word((h & 0x80u) ? 0x80000000u | (0x7FFFFFFFu - 2u * (0x7Fu - (h & 0x7Fu))) : 2u * h + 1u);
+}
+// the word at index i of a table of wbits-bit words
+__host__ __device__ __forceinline__ uint32_t dense_word_at(const void* words, u64 i, uint32_t wbits) {
+  return wbits == 8 ? dense_word8(((const uint8_t*)words)[i])
+         : wbits == 16 ? dense_word16(((const uint16_t*)words)[i])
+                       : dense_word(((const uint32_t*)words)[i]);
+}
 struct WordRow8 {
   __amdgpu_buffer_rsrc_t r;
   __device__ __forceinline__ void init(const uint16_t* base, u64 nwords) {
@@ -978,6 +988,216 @@ __global__ __launch_bounds__(256) void k_dense_resolve8p(Desc d, DenseView v, ui
 }
 // (held to 128 VGPRs for 4 waves per SIMD it spills 88 B per lane and runs
 // 1.5x slower: profiles/r01_ab_occupancy.jsonl)
+
+// ---------------------------------------------------------------------------
+// 8-bit tables (k_dense_resolve16p): SIXTEEN consecutive prefixes per lane,
+// one 16-B load per child row, a wave four 256-prefix groups of the level's
+// live-group list.  Half the bytes of the 16-bit octet form per position.
+// In a game of WIN / LOSS positions only (every K_SUM table) the parity of
+// the remoteness carries the value -- a LOSS has even remoteness (0 at a
+// primitive, 1 + an odd WIN remoteness), a WIN odd (1 + an even one) -- so
+// a byte holds remoteness up to 255 as an order form:
+//   WIN  r (odd)  -> y = (r - 1) / 2             (0x00 .. 0x7F)
+//   LOSS r (even) -> y = 0x80 | (0x7F - r / 2)   (0x80 .. 0xFF)
+// The unsigned max over a parent's children picks the LOSS child of least
+// remoteness if there is one, else the WIN child of greatest (0 = WIN 1 is
+// the least element, so an absent child read as 0 never wins the max).
+// Plan-time condition: every remoteness < 255 (root_sum <= 253).
+// ---------------------------------------------------------------------------
+typedef uint8_t u8x16 __attribute__((ext_vector_type(16)));
+constexpr uint32_t W8_UNREACHED = 0xFFu;
+constexpr uint32_t DENSE_PRIMITIVE8 = 0xFFu;  // LOSS, remoteness 0
+__device__ __forceinline__ uint32_t dense_parent8(uint32_t m) {
+  return (m & 0x80u) ? 0x7Fu - (m & 0x7Fu) : 0x80u | (0x7Fu - (m + 1u));
+}
+struct WordRow16 {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ __forceinline__ void init(const uint8_t* base, u64 nwords) {
+    r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(uint32_t)nwords, 0x00020000);
+  }
+  // words [idx, idx + 16), idx 16-aligned; !ok reads zeros with no memory access
+  __device__ __forceinline__ u8x16 at(u64 idx, bool ok) const {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, ok ? (uint32_t)idx : 0xFFFFFFF0u, 0, 0);
+    return __builtin_bit_cast(u8x16, v);
+  }
+};
+struct Hex16 {
+  WordRow16 n1, n2;  // levels L+1, L+2 (empty rows past the last level)
+  uint8_t* mine;
+  const u64* bits;
+  u64 Lb;  // L * Wbl
+  uint32_t S, H0;
+  uint32_t npos = 0, edges = 0;
+};
+template <int MAXH>
+struct HexLoads {
+  u8x16 A1, A2, P1, P2, C1[MAXH], C2[MAXH];
+  u64 bitsw;
+  u64 q;
+  uint32_t h1, s, valid, nch_hi;
+};
+__device__ __forceinline__ void hex_init(Hex16& Q, const Desc& d, uint8_t* words, const u64* bits, u64 L, u64 Wl,
+                                         u64 Wbl) {
+  Q.S = d.root_sum - (uint32_t)L;
+  Q.H0 = d.heap[0];
+  Q.mine = words + L * Wl;
+  Q.n1.init(words + (L + 1) * Wl, Q.S >= 1 ? Wl : 0);
+  Q.n2.init(words + (L + 2) * Wl, Q.S >= 2 ? Wl : 0);
+  Q.bits = bits;
+  Q.Lb = L * Wbl;
+}
+template <int MAXH>
+__device__ __forceinline__ void hex_issue(const Desc& d, const Hex16& Q, u64 q, bool on, HexLoads<MAXH>& X) {
+  const uint32_t S = Q.S;
+  uint32_t h[MAXH];
+  uint32_t s = 0;
+#pragma unroll
+  for (int i = 1; i < MAXH; i++) {
+    h[i] = ((MAXH <= 8) || i < d.nheaps) ? (uint32_t)((q >> d.pshift[i]) & (d.base[i] - 1)) : 0u;
+    s += h[i];
+  }
+  // valid e: s + e <= S and S - (s + e) <= H0, i.e. e in [S - s - H0, S - s]
+  const int hi = min((int)S - (int)s, 15), lo = max((int)S - (int)s - (int)Q.H0, 0);
+  const uint32_t valid = (on && hi >= lo) ? ((2u << hi) - 1u) & ~((1u << lo) - 1u) : 0u;
+  X.q = q;
+  X.h1 = h[1];
+  X.s = s;
+  X.valid = valid;
+  uint32_t nch_hi = 0;
+#pragma unroll
+  for (int i = 2; i < MAXH; i++) nch_hi += ((MAXH <= 8) || i < d.nheaps) ? min(h[i], 2u) : 0u;
+  X.nch_hi = nch_hi;
+  const bool any = valid != 0;
+  X.bitsw = any ? Q.bits[(Q.Lb + q) >> 6] : 0ull;
+  X.A1 = Q.n1.at(q, any);
+  X.A2 = Q.n2.at(q, any);
+  X.P1 = Q.n1.at(q - 16, any && h[1] >= 16);
+  X.P2 = Q.n2.at(q - 16, any && h[1] >= 16);
+#pragma unroll
+  for (int i = 2; i < MAXH; i++) {
+    const bool live = (MAXH <= 8) || i < d.nheaps;
+    X.C1[i] = Q.n1.at(q - d.pstride[i], any && live && h[i] >= 1);
+    X.C2[i] = Q.n2.at(q - 2 * d.pstride[i], any && live && h[i] >= 2);
+  }
+}
+// Byte arithmetic on the packed 16-B vectors (SWAR), so a lane keeps 4 VGPRs
+// per vector and a byte max costs half a packed instruction: every loaded
+// vector is split once into its even and odd bytes, each byte in a 16-bit
+// lane (u32 & 0x00FF00FF, (u32 >> 8) & 0x00FF00FF), the maxes run as
+// v_pk_max_u16 on the halves, and the parent words are formed in the halves
+// and merged once for the store.
+struct Half2 {
+  u32x4 e, o;  // bytes 2k / 2k+1 of 16, in the low byte of 16-bit lane k
+};
+__device__ __forceinline__ Half2 hsplit(u32x4 v) {
+  const u32x4 M = {0x00FF00FFu, 0x00FF00FFu, 0x00FF00FFu, 0x00FF00FFu};
+  return Half2{v & M, (v >> 8) & M};
+}
+__device__ __forceinline__ u32x4 hmax(u32x4 a, u32x4 b) {
+  typedef uint16_t h16x8 __attribute__((ext_vector_type(8)));
+  return __builtin_bit_cast(u32x4, __builtin_elementwise_max(__builtin_bit_cast(h16x8, a), __builtin_bit_cast(h16x8, b)));
+}
+// 16-bit lanes shifted up one lane, lane 0 from the top lane of prev
+__device__ __forceinline__ u32x4 hshift(u32x4 v, u32x4 prev) {
+  u32x4 r;
+  r[0] = __builtin_amdgcn_alignbit(v[0], prev[3], 16);
+#pragma unroll
+  for (int k = 1; k < 4; k++) r[k] = __builtin_amdgcn_alignbit(v[k], v[k - 1], 16);
+  return r;
+}
+// 16-bit lanes [0, n) all ones (n clamped to [0, 8])
+__device__ __forceinline__ u32x4 hprefix(int n) {
+  u32x4 m;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int c = min(max(n - 2 * k, 0), 2);
+    m[k] = c == 2 ? ~0u : c == 1 ? 0xFFFFu : 0u;
+  }
+  return m;
+}
+// dense_parent8 in each 16-bit lane (a byte value; never 0x7F: remoteness < 255)
+__device__ __forceinline__ uint32_t parent8x2(uint32_t m) {
+  const uint32_t L = ((m & 0x00800080u) >> 7) * 0xFFu;  // lanes with a LOSS child
+  return ((~m & 0x007F007Fu) & L) | ((0x00FE00FEu - (m & ~L)) & ~L);
+}
+__device__ __forceinline__ uint32_t bits4_to_bytes(uint32_t b4) {  // 4 bits -> 4 byte masks
+  return ((b4 * 0x00204081u) & 0x01010101u) * 0xFFu;
+}
+template <int MAXH>
+__device__ __forceinline__ void hex_finish(Hex16& Q, const HexLoads<MAXH>& X) {
+  const uint32_t valid = X.valid;
+  if (!valid) return;
+  const uint32_t S = Q.S;
+  const uint32_t rbits = (uint32_t)(X.bitsw >> ((Q.Lb + X.q) & 63)) & 0xFFFFu;
+  const Half2 A1 = hsplit(__builtin_bit_cast(u32x4, X.A1)), A2 = hsplit(__builtin_bit_cast(u32x4, X.A2));
+  const Half2 P1 = hsplit(__builtin_bit_cast(u32x4, X.P1)), P2 = hsplit(__builtin_bit_cast(u32x4, X.P2));
+  // heap 1: byte e -1 / -2 (P = 0 when the unit starts the digit: no child there)
+  u32x4 me = hshift(A1.o, P1.o), mo = A1.e;
+  me = hmax(me, hshift(A2.e, P2.e));
+  mo = hmax(mo, hshift(A2.o, P2.o));
+  // heaps >= 2: never holes under a valid parent
+#pragma unroll
+  for (int i = 2; i < MAXH; i++) {
+    const Half2 c1 = hsplit(__builtin_bit_cast(u32x4, X.C1[i])), c2 = hsplit(__builtin_bit_cast(u32x4, X.C2[i]));
+    me = hmax(me, hmax(c1.e, c2.e));
+    mo = hmax(mo, hmax(c1.o, c2.o));
+  }
+  // heap 0 -1 / -2 where h0 = S - s - e >= 1 / >= 2, i.e. e <= t1 / e <= t1 - 1
+  const int t1 = (int)S - (int)X.s - 1;
+  me = hmax(me, hmax(A1.e & hprefix((t1 + 2) >> 1), A2.e & hprefix((t1 + 1) >> 1)));
+  mo = hmax(mo, hmax(A1.o & hprefix((t1 + 1) >> 1), A2.o & hprefix(t1 >> 1)));
+  u32x4 o;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t w = S == 0 ? 0xFFFFFFFFu : parent8x2(me[k]) | (parent8x2(mo[k]) << 8);  // DENSE_PRIMITIVE8
+    o[k] = w | ~bits4_to_bytes((rbits >> (4 * k)) & 0xFu);  // unreached -> W8_UNREACHED
+  }
+  const uint32_t V = rbits & valid;
+  if (V) {
+    const uint32_t n = (uint32_t)__popc(V);
+    auto pre = [](int t) -> uint32_t { return t < 0 ? 0u : t >= 15 ? 0xFFFFu : (2u << t) - 1u; };
+    Q.npos += n;
+    // min(h0, 2) + min(h1, 2) + heaps >= 2 per reached valid position
+    // (h1 = the unit's first heap-1 digit: 0, or a multiple of 16)
+    Q.edges += n * X.nch_hi + (uint32_t)__popc(V & pre(t1)) + (uint32_t)__popc(V & pre(t1 - 1)) +
+               (X.h1 >= 2 ? 2 * n : (uint32_t)__popc(V & 0xFFFEu) + (uint32_t)__popc(V & 0xFFFCu));
+  }
+  *(u32x4*)(Q.mine + X.q) = o;
+}
+// Live-group list sweep; the host starts every XCD share at an entry
+// divisible by 4, so a wave's 64 units are four whole groups (lanes 16k ..
+// 16k+15), read with four scalar loads.  Not software-pipelined: one unit in
+// flight per lane keeps 91 VGPRs (5 waves per SIMD) and measured 3.90 ms per
+// 2^30 backward pass against 4.25 ms for the two-stage pipeline at 166 VGPRs
+// (3 waves per SIMD).
+template <int MAXH>
+__global__ __launch_bounds__(256) void k_dense_resolve16p(Desc d, DenseView v, uint8_t* words, const u64* bits, u64 L,
+                                                          DevState* st, const uint32_t* __restrict__ glist,
+                                                          XcdShares xs, BlockCount* bc) {
+  Hex16 Q;
+  hex_init(Q, d, words, bits, L, v.Wl, v.Wbl);
+  const uint32_t lane = __lane_id();
+  const uint32_t x = blockIdx.x % kXcds;
+  const u64 first = (u64)xs.o[x] * 16 + (u64)(blockIdx.x / kXcds) * blockDim.x + threadIdx.x;
+  const u64 end = (u64)xs.o[x + 1] * 16, stride = (u64)(gridDim.x / kXcds) * blockDim.x;
+  const uint32_t last = xs.o[8] - 1;  // last entry of the level's list (the host launches only non-empty lists)
+  auto issue = [&](u64 iu, HexLoads<MAXH>& X) {
+    const bool on = iu < end;
+    const uint32_t g0 = min(__builtin_amdgcn_readfirstlane((uint32_t)((iu - lane) >> 4)), last);
+    const uint32_t e0 = glist[g0], e1 = glist[min(g0 + 1, last)], e2 = glist[min(g0 + 2, last)],
+                   e3 = glist[min(g0 + 3, last)];
+    const uint32_t k = lane >> 4;
+    const uint32_t e = k == 0 ? e0 : k == 1 ? e1 : k == 2 ? e2 : e3;
+    hex_issue<MAXH>(d, Q, ((u64)e << 8) + 16 * (lane & 15), on, X);
+  };
+  for (u64 iu = first; iu < end; iu += stride) {
+    HexLoads<MAXH> X;
+    issue(iu, X);
+    hex_finish<MAXH>(Q, X);
+  }
+  block_count(bc, (u64)Q.npos, (u64)Q.edges);
+  if (Q.S == 0) block_add(&st->prims, (u64)Q.npos);  // one launch per solve
+}
 
 // Column jobs over a 16-bit table (shards): the octet body of
 // k_dense_resolve8p, a wave = two consecutive columns of the jobs'
@@ -1224,18 +1444,19 @@ __global__ __launch_bounds__(256) void k_halo_cols16(Desc d, HaloColJobs J, u64 
 
 // root word (on the shard that owns the root, root_q = its local prefix;
 // others pass ~0 and report NO_WORD)
-__global__ void k_dense_root(DenseView v, const uint32_t* words, const u64* bits, u64 root_q, DevState* st, bool w16) {
+__global__ void k_dense_root(DenseView v, const uint32_t* words, const u64* bits, u64 root_q, DevState* st,
+                             uint32_t wbits) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     uint32_t w = NO_WORD;
     if (root_q != ~0ull && reach_bit(bits, root_q))  // level 0
-      w = w16 ? dense_word16(((const uint16_t*)words)[root_q]) : dense_word(words[root_q]);
+      w = dense_word_at(words, root_q, wbits);
     st->root_word = w;
   }
 }
 
 // word of each key this table owns (NO_WORD for unreachable / not owned)
 __global__ void k_dense_query(Desc d, DenseView v, const uint32_t* words, const u64* bits, const u64* keys, u64 n,
-                              uint32_t* out, bool w16) {
+                              uint32_t* out, uint32_t wbits) {
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
     u64 slot, L, p;
     uint32_t w = NO_WORD;
@@ -1243,7 +1464,7 @@ __global__ void k_dense_query(Desc d, DenseView v, const uint32_t* words, const 
       slot_split(d, slot, &L, &p);
       uint64_t q;
       if (dense_local(v, p, &q) && reach_bit(bits, L * v.Wbl + q))
-        w = w16 ? dense_word16(((const uint16_t*)words)[L * v.Wl + q]) : dense_word(words[L * v.Wl + q]);
+        w = dense_word_at(words, L * v.Wl + q, wbits);
     }
     out[i] = w;
   }

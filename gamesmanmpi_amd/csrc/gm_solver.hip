@@ -281,11 +281,12 @@ static int dense_geom(const Desc* d, int rank, int world, DenseGeom* g) {
   v.p_hi = v.Wl;
   return 0;
 }
-static bool dense_plan16(const Desc* d, int world, uint32_t flags);
-// word area of a dense table: 16-bit order forms when the plan chose them
-// (dense_plan16: one-GPU K_SUM tables the octet kernels handle), else 32-bit
-static u64 dense_words_bytes(const Desc* d, const DenseGeom& g, bool w16) {
-  return ((u64)d->max_levels * g.v.Wl * (w16 ? 2 : 4) + 255) & ~255ull;
+static uint32_t dense_plan_bits(const Desc* d, int world, uint32_t flags);
+// word area of a dense table: 8- or 16-bit order forms when the plan chose
+// them (dense_plan_bits: one-GPU K_SUM tables the 16- / 8-prefix kernels
+// handle), else 32-bit
+static u64 dense_words_bytes(const Desc* d, const DenseGeom& g, uint32_t wbits) {
+  return ((u64)d->max_levels * g.v.Wl * (wbits / 8) + 255) & ~255ull;
 }
 static u64 dense_bits_bytes(const Desc* d, const DenseGeom& g) {
   return (u64)d->max_levels * g.v.Wbl / 8;
@@ -417,11 +418,15 @@ static GroupGeom group_geom(const Desc* d, int world) {
 // must reach gm_solver_create_shard (gm_buffers.flags), which sizes the
 // table against them: a table planned with 16-bit words cannot be handed a
 // 32-bit kernel (GM_EINVAL at creation, never a fault).
-static bool dense_plan16(const Desc* d, int world, uint32_t flags) {
+static uint32_t dense_plan_bits(const Desc* d, int world, uint32_t flags) {
   if (world != 1 || d->kind != K_SUM || !d->pow2 || d->nheaps < 2 || d->nheaps > 8 || d->base[1] < 8 ||
-      d->root_sum >= 0x7FFF || d->W * 2 > 0xFFFFFFF0ull || !group_geom(d, 1).on)
-    return false;
-  return !(flags & (GM_F_WORDS32 | GM_F_RESOLVE_SCALAR));
+      d->root_sum >= 0x7FFF || d->W * 2 > 0xFFFFFFF0ull || !group_geom(d, 1).on ||
+      (flags & (GM_F_WORDS32 | GM_F_RESOLVE_SCALAR)))
+    return 32;
+  // 8-bit words (k_dense_resolve16p): 16 prefixes per lane, every
+  // remoteness < 255 (dense_parent8)
+  if (d->base[1] >= 16 && d->root_sum <= 253 && !(flags & GM_F_WORDS16)) return 8;
+  return 16;
 }
 static void group_sums(const Desc* d, const GroupGeom& g, std::vector<uint16_t>& gs) {
   gs.resize(g.groups);
@@ -845,7 +850,7 @@ __global__ __launch_bounds__(256) void k_checksum_flat(Desc d, const u64* K, con
   ck_block_add(acc, v);
 }
 __global__ __launch_bounds__(256) void k_checksum_dense(Desc d, DenseView v, const uint32_t* words, const u64* bits,
-                                                        u64 levels, bool w16, u64* acc) {
+                                                        u64 levels, uint32_t wbits, u64* acc) {
   u64 a[6] = {0, 0, 0, 0, 0, 0};
   const u64 n = v.Wl;
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < levels * n; i += (u64)gridDim.x * blockDim.x) {
@@ -855,7 +860,7 @@ __global__ __launch_bounds__(256) void k_checksum_dense(Desc d, DenseView v, con
     if (!run) continue;
     const int64_t h0 = dense_h0(d, L, p);
     if (h0 < 0 || !reach_bit(bits, L * v.Wbl + q)) continue;
-    const uint32_t w = w16 ? dense_word16(((const uint16_t*)words)[L * v.Wl + q]) : dense_word(words[L * v.Wl + q]);
+    const uint32_t w = dense_word_at(words, L * v.Wl + q, wbits);
     ck_add(d, p * d.base[0] + (u64)h0, w, a);
   }
   ck_block_add(acc, a);
@@ -877,6 +882,7 @@ enum DenseResolveKind : uint32_t {
   RK_QUAD_COLS = 4,  // k_dense_resolve4c: shards, 32-bit table, column jobs
   RK_QUAD_BAND = 5,  // k_dense_resolve4: 32-bit band sweeps (no list)
   RK_SCALAR = 6,     // k_dense_resolve: one prefix per lane (any bases; GM_F_RESOLVE_SCALAR)
+  RK_HEX_LIST = 7,   // k_dense_resolve16p: world 1, 8-bit table, live-group lists
 };
 enum DensePullKind : uint32_t { PK_NONE = 0, PK_WORDS = 1, PK_LANE = 2 };
 
@@ -905,8 +911,10 @@ struct gm_solver {
   HaloGeom hg;
   HaloTabs ht{};
   bool halo16 = false;  // words travel as 16 bits (k_halo_cols)
-  bool w16 = false;     // this solve's table holds 16-bit order-form words (k_dense_resolve8p)
-  bool plan16 = false;  // the table was planned with 16-bit words only (dense_plan16)
+  bool w16 = false;     // this solve's table holds 16-bit order-form words (k_dense_resolve8p / 8c)
+  bool w8 = false;      // 8-bit order-form words (k_dense_resolve16p)
+  uint32_t wbits() const { return w8 ? 8u : w16 ? 16u : 32u; }
+  uint32_t plan_bits = 32;  // the table's word width as planned (dense_plan_bits)
   BlockCount* bcount = nullptr;  // per-block counts in scratch (block_count)
   uint32_t* halo_send = nullptr;
   uint32_t* halo_recv = nullptr;
@@ -1087,6 +1095,22 @@ static void dense_launch_resolve_t(gm_solver* s, const DenseView& v, int grid, u
           return;
         }
       }
+      if (s->w8) {  // 8-bit table: sixteen prefixes per lane over the live-group list (world 1)
+        if (!gl) {
+          s->launch_err = true;
+          return;
+        }
+        XcdShares xs;
+        for (int x = 0; x < 9; x++) xs.o[x] = s->gxcd[(size_t)L * 9 + x];
+        for (int x = 1; x < 8; x++) xs.o[x] &= ~3u;  // shares start at entries divisible by 4: a wave = four groups
+        const u64 u16 = (u64)xs.o[8] * 16;
+        const int rp = resident_blocks((const void*)k_dense_resolve16p<MAXH>);
+        const int gp = (int)std::min<u64>(std::min<u64>(((u16 + kBlock - 1) / kBlock + 7) & ~7ull, (u64)rp),
+                                          (u64)kCountSlots);
+        hipLaunchKernelGGL((k_dense_resolve16p<MAXH>), dim3(gp), dim3(kBlock), 0, s->stream, s->d, v,
+                           (uint8_t*)s->words, s->bits, L, s->st, gl, xs, s->bcount);
+        return;
+      }
       if (s->w16) {
         // 16-bit table: octets over the live-group list (world 1).  A 16-bit
         // shard table always lists its slices (dense_choose), so reaching
@@ -1124,7 +1148,7 @@ static void dense_launch_resolve_t(gm_solver* s, const DenseView& v, int grid, u
       return;
     }
   }
-  if (s->w16) {  // never chosen with the one-prefix kernel (dense_choose)
+  if (s->w16 || s->w8) {  // never chosen with the one-prefix kernel (dense_choose)
     s->launch_err = true;
     return;
   }
@@ -1400,7 +1424,7 @@ static int plan_dense(const Desc* d, int rank, int world, uint32_t flags, uint64
   DenseGeom g;
   int rc = dense_geom(d, rank, world, &g);
   if (rc) return rc;
-  const u64 bytes = dense_words_bytes(d, g, dense_plan16(d, world, flags)) + dense_bits_bytes(d, g);
+  const u64 bytes = dense_words_bytes(d, g, dense_plan_bits(d, world, flags)) + dense_bits_bytes(d, g);
   *fits = max_table_bytes == 0 || bytes <= max_table_bytes;
   out->mode = GM_MODE_DENSE;
   out->table_slots = (u64)d->max_levels * g.v.Wl;
@@ -1601,12 +1625,15 @@ static int dense_choose(gm_solver* s) {
   const bool base16 = d.pow2 && d.kind == K_SUM && d.nheaps >= 2 && d.nheaps <= 8 && d.base[1] >= 8 &&
                       d.root_sum < 0x7FFF && v.Wl * 2 <= 0xFFFFFFF0ull &&
                       !(s->flags & (GM_F_WORDS32 | GM_F_RESOLVE_SCALAR));
+  s->w8 = false;
   if (!v.blk) {
-    if (s->plan16) {
+    if (s->plan_bits < 32) {
       if (!s->glist)
-        return fail(GM_EINVAL, "16-bit dense table without live-group lists: scratch smaller than gm_plan's");
-      s->w16 = true;
-      s->rk = RK_OCT_LIST;
+        return fail(GM_EINVAL, "%u-bit dense table without live-group lists: scratch smaller than gm_plan's",
+                    s->plan_bits);
+      s->w16 = s->plan_bits == 16;
+      s->w8 = s->plan_bits == 8;
+      s->rk = s->w8 ? RK_HEX_LIST : RK_OCT_LIST;
       return 0;
     }
     s->w16 = false;
@@ -1633,7 +1660,7 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
     if (buf->table_slots != (u64)d->max_levels * g.v.Wl) return fail(GM_EINVAL, "dense table must hold levels * Wl words (use gm_plan_shard)");
     // the word width follows from the flags: a table planned with 16-bit
     // words is too small for the 32-bit kernels other flags select
-    const u64 need = dense_words_bytes(d, g, dense_plan16(d, world, buf->flags)) + dense_bits_bytes(d, g);
+    const u64 need = dense_words_bytes(d, g, dense_plan_bits(d, world, buf->flags)) + dense_bits_bytes(d, g);
     if (buf->table_bytes < need)
       return fail(GM_EINVAL, "dense table of %llu bytes, these flags need %llu (plan with the flags the solver is "
                              "created with)", (unsigned long long)buf->table_bytes, (unsigned long long)need);
@@ -1663,8 +1690,8 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
   s->words = (uint32_t*)buf->table;
   s->nslots = buf->table_slots;
   s->view = g.v;
-  s->plan16 = buf->mode == GM_MODE_DENSE && dense_plan16(d, world, buf->flags);
-  s->bits = (u64*)((char*)buf->table + (buf->mode == GM_MODE_DENSE ? dense_words_bytes(d, g, s->plan16) : 0));
+  s->plan_bits = buf->mode == GM_MODE_DENSE ? dense_plan_bits(d, world, buf->flags) : 32;
+  s->bits = (u64*)((char*)buf->table + (buf->mode == GM_MODE_DENSE ? dense_words_bytes(d, g, s->plan_bits) : 0));
   s->rank = rank;
   s->world = world;
   s->nblocks = g.nblocks;
@@ -2337,9 +2364,9 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
     if (first > 0) {
       uint32_t wb = 0;
       HIPCHK(hipMemcpy(&wb, &s->st->word_bits, sizeof wb, hipMemcpyDeviceToHost));
-      if (wb != 16 && wb != 32) return fail(GM_EINVAL, "resume: scratch holds no solve in progress");
-      if ((wb == 16) != s->w16) return fail(GM_EINVAL, "resume: the interrupted solve used %u-bit words, this solver %u",
-                                            wb, s->w16 ? 16u : 32u);
+      if (wb != 8 && wb != 16 && wb != 32) return fail(GM_EINVAL, "resume: scratch holds no solve in progress");
+      if (wb != s->wbits())
+        return fail(GM_EINVAL, "resume: the interrupted solve used %u-bit words, this solver %u", wb, s->wbits());
     }
   }
   std::vector<hipEvent_t> ev;
@@ -2369,11 +2396,11 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
   auto t0 = std::chrono::steady_clock::now();
   HIPCHK(hipEventRecord(e0, st));
   if (first == 0) {
-    static const uint32_t kWordBits[2] = {32u, 16u};
+    static const uint32_t kWordBits[3] = {32u, 16u, 8u};
     for (gm_solver* s : ss) {
       HIPCHK(hipMemsetAsync(s->st, 0, devstate_bytes(T), st));
       HIPCHK(hipMemsetAsync(s->bcount, 0, kCountSlots * sizeof(BlockCount), st));
-      HIPCHK(hipMemcpyAsync(&s->st->word_bits, &kWordBits[s->w16 ? 1 : 0], sizeof(uint32_t),
+      HIPCHK(hipMemcpyAsync(&s->st->word_bits, &kWordBits[s->w8 ? 2 : s->w16 ? 1 : 0], sizeof(uint32_t),
                             hipMemcpyHostToDevice, st));
     }
   }
@@ -2511,13 +2538,13 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
     HIPCHK(hipStreamSynchronize(st));
     for (auto e : ev) (void)hipEventDestroy(e);
     out->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    out->word_bits = s0->w16 ? 16u : 32u;
+    out->word_bits = s0->wbits();
     return GM_PARTIAL;
   }
   for (gm_solver* s : ss) {
     uint64_t root_q = ~0ull;
     if (!dense_local(s->view, root_p, &root_q)) root_q = ~0ull;
-    hipLaunchKernelGGL(k_dense_root, dim3(1), dim3(64), 0, st, s->view, s->words, s->bits, root_q, s->st, s->w16);
+    hipLaunchKernelGGL(k_dense_root, dim3(1), dim3(64), 0, st, s->view, s->words, s->bits, root_q, s->st, s->wbits());
     hipLaunchKernelGGL(k_fill_red, dim3(1), dim3(1024), 0, st, s->st, s->bcount);
   }
   if (mode == 1) {
@@ -2559,7 +2586,7 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
   out->primitives = red[2];
   out->levels = (uint32_t)T;
   out->max_level_width = 0;
-  out->word_bits = s0->w16 ? 16u : 32u;
+  out->word_bits = s0->wbits();
   out->kernels = s0->rk | (s0->pk << 16);
   for (gm_solver* s : ss)
     if (s->launch_err) return fail(GM_ECORRUPT, "a level found no resolve kernel of the table's word width");
@@ -2891,7 +2918,7 @@ int gm_solver_query(gm_solver* s, const uint64_t* keys_dev, uint64_t n, uint32_t
   int grid = (int)std::min<u64>((n + kBlock - 1) / kBlock, (u64)s->grid);
   if (s->mode == GM_MODE_DENSE)
     hipLaunchKernelGGL(k_dense_query, dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->view, s->words, s->bits,
-                       (const u64*)keys_dev, n, words_dev, s->w16);
+                       (const u64*)keys_dev, n, words_dev, s->wbits());
   else if (s->mode == GM_MODE_BUCKETED)
     hipLaunchKernelGGL(k_bk_query, dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->bkK, s->bkW, s->bkL,
                        s->d.max_levels, s->meta, (const u64*)keys_dev, n, words_dev);
@@ -2941,7 +2968,7 @@ int gm_solver_checksum(gm_solver* s, uint64_t out[6]) {
   HIPCHK(hipMemsetAsync(acc, 0, 6 * sizeof(u64), s->stream));
   if (s->mode == GM_MODE_DENSE)
     hipLaunchKernelGGL(k_checksum_dense, dim3(s->grid), dim3(kBlock), 0, s->stream, s->d, s->view, s->words, s->bits,
-                       (u64)s->d.max_levels, s->w16, acc);
+                       (u64)s->d.max_levels, s->wbits(), acc);
   else if (s->mode == GM_MODE_BUCKETED) {
     u64 tot = 0;
     for (const BkLevel& x : s->lvh) tot += x.n;

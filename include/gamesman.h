@@ -104,6 +104,8 @@ typedef struct gm_buffers {
                                   order instead of overlapping it */
 #define GM_F_HASH_TABLE 32u    /* gm_plan, keyed games: the open-addressing
                                   hash table (HASHED) instead of BUCKETED */
+#define GM_F_WORDS16 64u       /* dense: 16-bit table words (octet kernels)
+                                  where 8-bit ones would be chosen */
 
 typedef struct gm_result {
   uint32_t root_word;
@@ -122,7 +124,7 @@ typedef struct gm_result {
   double ms_resolve_kernels;
   uint64_t n_expand_launches;
   uint64_t n_resolve_launches;
-  uint32_t word_bits;        /* DENSE: bits per table word this solve used (16 or 32); 0 HASHED */
+  uint32_t word_bits;        /* DENSE: bits per table word this solve used (8, 16 or 32); 0 keyed */
   uint32_t kernels;          /* DENSE: resolve family | pull family << 16 (gm_solver.hip DenseResolveKind) */
 } gm_result;
 

@@ -131,19 +131,25 @@ def test_plan_sizes():
     _lib.check(_lib.load().gm_plan(s.id, 0, 0, 0, ctypes.byref(p)))
     assert p.mode == _lib.GM_MODE_DENSE
     assert p.table_slots == 187 * 32 ** 5
-    # 16-bit order-form words (one-GPU octet kernels) + reach bitmap
+    # 8-bit order-form words (one-GPU, remoteness < 255) + reach bitmap
+    assert p.table_bytes == 1 * 187 * 32 ** 5 + 187 * 32 ** 5 // 8
+    # the kernel-family flags plan 16- or 32-bit words (and the environment
+    # does not: no knob is read from it)
+    _lib.check(_lib.load().gm_plan(s.id, 0, _lib.GM_F_WORDS16, 0, ctypes.byref(p)))
     assert p.table_bytes == 2 * 187 * 32 ** 5 + 187 * 32 ** 5 // 8
-    # the kernel-family flags plan 32-bit words (and the environment does
-    # not: no knob is read from it)
     for f in (_lib.GM_F_WORDS32, _lib.GM_F_RESOLVE_SCALAR):
         _lib.check(_lib.load().gm_plan(s.id, 0, f, 0, ctypes.byref(p)))
         assert p.table_bytes == 4 * 187 * 32 ** 5 + 187 * 32 ** 5 // 8
     os.environ["GM_WORDS32"] = "1"
     try:
         _lib.check(_lib.load().gm_plan(s.id, 0, 0, 0, ctypes.byref(p)))
-        assert p.table_bytes == 2 * 187 * 32 ** 5 + 187 * 32 ** 5 // 8
+        assert p.table_bytes == 1 * 187 * 32 ** 5 + 187 * 32 ** 5 // 8
     finally:
         del os.environ["GM_WORDS32"]
+    # remoteness past 254 keeps 16-bit words (heaps 127 + 127 + 7 = 261 levels)
+    w = GameSpec("sum_four_to_one", "heaps=127:127:7")
+    _lib.check(_lib.load().gm_plan(w.id, 0, 0, 0, ctypes.byref(p)))
+    assert p.table_bytes == 2 * 262 * 128 * 8 + 262 * 128 * 8 // 8
     # a byte budget below the dense table falls back to the keyed table
     _lib.check(_lib.load().gm_plan(s.id, 0, 0, 1 << 30, ctypes.byref(p)))
     assert p.mode == _lib.GM_MODE_HASHED

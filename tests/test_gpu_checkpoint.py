@@ -1,6 +1,6 @@
 """Level-granular stop / resume and on-disk checkpoints (include/gamesman.h
 gm_solver_set_steps, gamesmanmpi_amd/checkpoint.py): a solve interrupted
-after any step -- forward or backward, HASHED or DENSE (16- and 32-bit
+after any step -- forward or backward, HASHED, BUCKETED or DENSE (8-, 16- and 32-bit
 words) -- and resumed, in the same solver or in a fresh one restored from
 disk, gives the ORACLE's counts, root line and every position's value and
 remoteness (oracle/, the CPU restatement pinned to the reference's golden
@@ -22,7 +22,8 @@ CASES = [
     ("tic_tac_toe_np", "", "bucketed", {}),
     ("othello_bit_new", "length=4,height=4", "bucketed", {}),
     ("toot_and_otto_bitstring", "length=4,height=3", "bucketed", {}),
-    ("sum_four_to_one", "heaps=15:15:15:15", "dense", {}),
+    ("sum_four_to_one", "heaps=15:15:15:15", "dense", {}),                # 8-bit words
+    ("sum_four_to_one", "heaps=15:15:15:15", "dense", {"flags": 64}),     # GM_F_WORDS16
     ("sum_four_to_one", "heaps=15:15:15:15", "dense", {"flags": 4}),  # GM_F_WORDS32
     ("four_to_one", "start=40", "dense", {}),
 ]
@@ -71,7 +72,8 @@ def test_stop_resume_same_solver(name, params, layout, env):
         assert r is not None
         _same(r, _dump(s), r0, d0)
         if layout == "dense":
-            assert r.extra["word_bits"] == (32 if env else 16) or name == "four_to_one"
+            want = {0: 8, 64: 16, 4: 32}[env.get("flags", 0)]
+            assert r.extra["word_bits"] == want or name == "four_to_one"
 
 
 @pytest.mark.parametrize("name,params,layout,env", CASES)

@@ -14,9 +14,15 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-WORDS32, SCALAR, INORDER = 4, 8, 16  # _lib.GM_F_*
-WORLD1 = [0, WORDS32, SCALAR]
-KERNELS1 = {0: "k_dense_resolve8p", WORDS32: "k_dense_resolve4p", SCALAR: "k_dense_resolve"}
+WORDS32, SCALAR, INORDER, WORDS16 = 4, 8, 16, 64  # _lib.GM_F_*
+WORLD1 = [0, WORDS16, WORDS32, SCALAR]
+KERNELS1 = {WORDS16: "k_dense_resolve8p", WORDS32: "k_dense_resolve4p", SCALAR: "k_dense_resolve"}
+
+
+def _default_kernel(heaps):
+    """8-bit words (k_dense_resolve16p) when the second heap's base is >= 16
+    and every remoteness fits (root_sum <= 253), else 16-bit octets."""
+    return "k_dense_resolve16p" if heaps[1] + 1 >= 16 and sum(heaps) <= 253 else "k_dense_resolve8p"
 
 
 def _expected(heaps):
@@ -33,15 +39,17 @@ def _expected(heaps):
 def _solve(params, flags):
     from gamesmanmpi_amd.games import GameSpec
     from gamesmanmpi_amd.solver import Solver
+    heaps = [int(h) for h in params.split("=")[1].split(":")]
     s = Solver(GameSpec("sum_four_to_one", params), layout="dense", flags=flags)
     r = s.solve()
-    assert r.extra["resolve_kernel"] == KERNELS1[flags], r.extra
+    assert r.extra["resolve_kernel"] == (KERNELS1[flags] if flags else _default_kernel(heaps)), r.extra
     keys, val, rem = s.dump()
     order = np.argsort(keys)
     return r, keys[order], val[order], rem[order]
 
 
-@pytest.mark.parametrize("params", ["heaps=15:15:15:15:7", "heaps=31:7:31:15"])
+@pytest.mark.parametrize("params", ["heaps=15:15:15:15:7", "heaps=31:7:31:15", "heaps=63:31:31:31:63",
+                                    "heaps=127:15:127"])
 def test_world1_variants_agree(params):
     heaps = [int(h) for h in params.split("=")[1].split(":")]
     P, E, root = _expected(heaps)
@@ -125,30 +133,34 @@ def test_shard_geometries_like_the_bench(world, params):
 def test_16bit_table_refuses_32bit_kernels():
     """The round-1 fault class (a 32-bit kernel writing past a 16-bit word
     area): kernel families are fixed at creation from the flags the table
-    was planned with.  A 16-bit plan handed GM_F_WORDS32 at creation, or a
-    16-bit solver asked to switch afterwards, returns GM_EINVAL; the solver
-    keeps solving correctly."""
+    was planned with.  A 16-bit plan (GM_F_WORDS16) handed GM_F_WORDS32 at
+    creation, an 8-bit plan handed GM_F_WORDS16, or a solver asked to switch
+    afterwards, returns GM_EINVAL; the solver keeps solving correctly."""
     import torch
     from gamesmanmpi_amd import _lib
     from gamesmanmpi_amd.games import GameSpec
     from gamesmanmpi_amd.solver import Solver
     L = _lib.load()
     spec = GameSpec("sum_four_to_one", "heaps=15:15:15:15:7")
-    plan = _lib.gm_plan_t()
-    _lib.check(L.gm_plan(spec.id, 0, 0, 0, ctypes.byref(plan)))
-    assert plan.mode == _lib.GM_MODE_DENSE
-    table = torch.empty(plan.table_bytes, dtype=torch.uint8, device="cuda")
-    scratch = torch.empty(plan.scratch_bytes, dtype=torch.uint8, device="cuda")
-    b = _lib.gm_buffers()
-    b.table, b.table_slots, b.table_bytes = table.data_ptr(), plan.table_slots, plan.table_bytes
-    b.scratch, b.scratch_bytes = scratch.data_ptr(), plan.scratch_bytes
-    b.mode, b.flags = plan.mode, _lib.GM_F_WORDS32
-    h = ctypes.c_void_p()
-    assert L.gm_solver_create(spec.id, ctypes.byref(b), ctypes.byref(h)) == _lib.GM_EINVAL
-    assert b"flags need" in L.gm_last_error()
+    for planned, given in ((_lib.GM_F_WORDS16, _lib.GM_F_WORDS32), (0, _lib.GM_F_WORDS16)):
+        plan = _lib.gm_plan_t()
+        _lib.check(L.gm_plan(spec.id, 0, planned, 0, ctypes.byref(plan)))
+        assert plan.mode == _lib.GM_MODE_DENSE
+        table = torch.empty(plan.table_bytes, dtype=torch.uint8, device="cuda")
+        scratch = torch.empty(plan.scratch_bytes, dtype=torch.uint8, device="cuda")
+        b = _lib.gm_buffers()
+        b.table, b.table_slots, b.table_bytes = table.data_ptr(), plan.table_slots, plan.table_bytes
+        b.scratch, b.scratch_bytes = scratch.data_ptr(), plan.scratch_bytes
+        b.mode, b.flags = plan.mode, given
+        h = ctypes.c_void_p()
+        assert L.gm_solver_create(spec.id, ctypes.byref(b), ctypes.byref(h)) == _lib.GM_EINVAL
+        assert b"flags need" in L.gm_last_error()
+    s16 = Solver(spec, layout="dense", flags=_lib.GM_F_WORDS16)
+    assert s16.solve().extra["word_bits"] == 16
     s = Solver(spec, layout="dense")
     r = s.solve()
-    assert r.extra["word_bits"] == 16
+    assert r.extra["word_bits"] == 8
     assert L.gm_solver_set_flags(s.handle, _lib.GM_F_WORDS32) == _lib.GM_EINVAL
     assert L.gm_solver_set_flags(s.handle, _lib.GM_F_RESOLVE_SCALAR) == _lib.GM_EINVAL
+    assert L.gm_solver_set_flags(s.handle, _lib.GM_F_WORDS16) == _lib.GM_EINVAL
     assert s.solve().root_line == r.root_line
