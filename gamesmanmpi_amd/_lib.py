@@ -31,6 +31,10 @@ RESOLVE_KERNELS = {1: "k_dense_resolve8p", 2: "k_dense_resolve8c", 3: "k_dense_r
                    7: "k_dense_resolve16p"}
 PULL_KERNELS = {1: "k_dense_pull_words", 2: "k_dense_pull"}
 GM_MODE_HASHED, GM_MODE_DENSE, GM_MODE_BUCKETED = 0, 1, 2
+# host-staged transport (include/gamesman.h gm_xfer_fn)
+GM_XFER_SENDRECV, GM_XFER_ALLGATHER = 0, 1
+XFER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,
+                           ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int)
 MODE_NAMES = {0: "hashed", 1: "dense", 2: "bucketed"}
 GM_MAXCHILD = 32
 GM_COMM_ID_BYTES = 128
@@ -98,7 +102,7 @@ EXPORTS = (
     "gm_solver_destroy", "gm_solve", "gm_owner", "gm_owner_host",
     "gm_plan_shard", "gm_solver_create_shard", "gm_comm_unique_id",
     "gm_solver_comm_init", "gm_solve_group", "gm_solver_set_flags", "gm_solver_set_steps",
-    "gm_shard_info",
+    "gm_shard_info", "gm_solver_set_transport", "gm_shard_halo_sigs",
     "gm_ks_begin", "gm_ks_level_size", "gm_ks_expand", "gm_ks_insert",
     "gm_ks_finalize", "gm_ks_counts", "gm_ks_children", "gm_ks_reduce",
     "gm_ks_end", "gm_graph_solve",
@@ -163,6 +167,8 @@ def load():
         "gm_solver_set_flags": [c.c_void_p, c.c_uint32],
         "gm_solver_set_steps": [c.c_void_p, c.c_uint32, c.c_uint32],
         "gm_shard_info": [c.c_int, c.c_int, c.c_int, P(c.c_uint64)],
+        "gm_solver_set_transport": [c.c_void_p, XFER_FN, c.c_void_p],
+        "gm_shard_halo_sigs": [c.c_int, c.c_int, c.c_int, c.c_uint32, c.c_void_p, c.c_uint32],
         "gm_ks_begin": [c.c_void_p, c.c_int],
         "gm_ks_level_size": [c.c_void_p, c.c_int, P(c.c_uint64)],
         "gm_ks_expand": [c.c_void_p, c.c_int, c.c_void_p, c.c_void_p,

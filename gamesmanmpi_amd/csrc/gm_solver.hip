@@ -42,6 +42,7 @@
 #include <mutex>
 #include <string>
 #include <vector>
+#include <memory>
 #include <map>
 #include <mutex>
 
@@ -897,6 +898,10 @@ struct gm_solver {
   int rank, world;
   u64 nblocks;  // blocks of the top digit over all ranks (view.B values each)
   ncclComm_t comm;  // RCCL communicator (world > 1), or null
+  gm_xfer_fn xfer = nullptr;  // host-staged transport (gm_solver_set_transport), replaces comm
+  void* xfer_ctx = nullptr;
+  bool halo_ok = false;       // the exchange plan was checked against the other ranks'
+  std::vector<uint8_t> hstage;  // host staging of the transport
   gm_slot* tab;
   u64 mask;
   u64* lv;
@@ -1885,6 +1890,58 @@ int gm_solver_comm_init(gm_solver* s, const void* id) {
   return 0;
 }
 
+static void halo_sigs(const gm_solver* s, u64 L, u64 out[4]);
+// host half of a dense shard's halo geometry, as gm_solver_create_shard
+// builds it from a gm_plan_shard scratch (column permutation present)
+static int shard_host_geom(const Desc* d, int rank, int world, gm_solver* s) {
+  DenseGeom g;
+  memset(&g, 0, sizeof g);
+  int rc = dense_geom(d, rank, world, &g);
+  if (rc) return rc;
+  s->d = *d;
+  s->mode = GM_MODE_DENSE;
+  s->view = g.v;
+  s->rank = rank;
+  s->world = world;
+  s->nblocks = g.nblocks;
+  s->hg.on = false;
+  if (d->pow2) {
+    const ColGeom cg = col_geom(d);
+    std::vector<uint32_t> perm;
+    if (cg.on) build_colperm(d, cg, perm, s->cstart);
+    s->hg = halo_geom(d, world, (u64)(s->view.blk ? s->view.Wl / ((s->view.B + 4) * s->view.Z) : 1));
+    if (s->hg.on && cg.on) {
+      std::vector<uint32_t> PB, NY, CS;
+      build_halo_cols(*d, s->hg, s->cstart, PB, NY, CS, s->halo_tot);
+      s->halo16 = d->kind == K_SUM && d->root_sum < 32768;
+    } else {
+      s->hg.on = false;
+    }
+  }
+  return 0;
+}
+
+int gm_shard_halo_sigs(int game, int rank, int world, uint32_t flags, uint64_t* out, uint32_t levels) {
+  (void)flags;  // the halo geometry does not depend on the kernel families
+  const Desc* d = get_game(game);
+  if (!d || !out || world < 1 || rank < 0 || rank >= world) return fail(GM_EINVAL, "bad argument");
+  if (!d->dense_ok) return fail(GM_EINVAL, "game has no dense layout");
+  if (levels < (uint32_t)d->max_levels) return fail(GM_EINVAL, "out holds %u levels, the game has %d", levels, d->max_levels);
+  std::unique_ptr<gm_solver> s(new gm_solver());
+  int rc = shard_host_geom(d, rank, world, s.get());
+  if (rc) return rc;
+  for (int L = 0; L < d->max_levels; L++) halo_sigs(s.get(), (u64)L, (u64*)out + (size_t)L * 4);
+  return 0;
+}
+
+int gm_solver_set_transport(gm_solver* s, gm_xfer_fn fn, void* ctx) {
+  if (!s) return fail(GM_EINVAL, "bad argument");
+  if (s->mode != GM_MODE_DENSE || s->world <= 1) return fail(GM_EINVAL, "a transport serves dense shards of a world > 1");
+  s->xfer = fn;
+  s->xfer_ctx = ctx;
+  return 0;
+}
+
 int gm_solver_set_steps(gm_solver* s, uint32_t first, uint32_t stop) {
   if (!s) return fail(GM_EINVAL, "bad argument");
   const uint32_t n = 2u * (uint32_t)s->d.max_levels;
@@ -2129,11 +2186,74 @@ static bool band_pair(const gm_solver* s, u64 L, int64_t t0, u64* lo, u64* hi) {
   return true;
 }
 
+static int xfer_call(gm_solver* s, int op, const void* sb, u64 sn, int sp, void* rb, u64 rn, int rp) {
+  const int rc = s->xfer(s->xfer_ctx, op, sb, sn, sp, rb, rn, rp);
+  return rc ? fail(GM_EHIP, "transport callback failed (%d) on rank %d", rc, s->rank) : 0;
+}
+// host-staged copy of device ranges into / out of s->hstage
+struct HostRange {
+  void* dev;
+  u64 bytes;
+};
+static int stage_out(gm_solver* s, const std::vector<HostRange>& rs, u64 at, hipStream_t cs) {
+  for (const HostRange& r : rs) {
+    HIPCHK(hipMemcpyAsync(s->hstage.data() + at, r.dev, r.bytes, hipMemcpyDeviceToHost, cs));
+    at += r.bytes;
+  }
+  HIPCHK(hipStreamSynchronize(cs));
+  return 0;
+}
+static int stage_in(gm_solver* s, const std::vector<HostRange>& rs, u64 at, hipStream_t cs) {
+  for (const HostRange& r : rs) {
+    HIPCHK(hipMemcpyAsync(r.dev, s->hstage.data() + at, r.bytes, hipMemcpyHostToDevice, cs));
+    at += r.bytes;
+  }
+  HIPCHK(hipStreamSynchronize(cs));
+  return 0;
+}
+static u64 ranges_bytes(const std::vector<HostRange>& rs) {
+  u64 n = 0;
+  for (const HostRange& r : rs) n += r.bytes;
+  return n;
+}
+// one paired transfer through the host: send ranges `out` to rank sp, receive
+// ranges `in` from rank rp
+static int xfer_ranges(gm_solver* s, const std::vector<HostRange>& out, int sp, const std::vector<HostRange>& in, int rp,
+                       hipStream_t cs) {
+  const u64 ns = ranges_bytes(out), nr = ranges_bytes(in);
+  if (s->hstage.size() < ns + nr) s->hstage.resize(ns + nr);
+  int rc = stage_out(s, out, 0, cs);
+  if (rc) return rc;
+  rc = xfer_call(s, GM_XFER_SENDRECV, s->hstage.data(), ns, sp, s->hstage.data() + ns, nr, rp);
+  if (rc) return rc;
+  return stage_in(s, in, ns, cs);
+}
+
 // after pull(L): bits of every block's bottom two own slices go down
 static int exchange_bits(std::vector<gm_solver*>& ss, u64 L, int mode, hipStream_t cs) {
   auto bits_at = [&](gm_solver* s, u64 j, u64 o, u64 off) {
     return s->bits + (L * s->view.Wbl + blk_slice(s, j, o) * s->view.Z + off) / 64;
   };
+  if (mode == 3) {  // host-staged: the same ranges, in the same order as the RCCL form
+    gm_solver* s = ss[0];
+    const int down = (s->rank + s->world - 1) % s->world, up = (s->rank + 1) % s->world;
+    const u64 nb = blk_count(s), B = s->view.B;
+    std::vector<HostRange> out, in;
+    for (u64 j = 0; j < nb; j++) {
+      u64 lo, hi;
+      if (blk_global(s, j) >= 1 && band_pair(s, L, blk_top(s, j, 2), &lo, &hi)) {
+        lo &= ~63ull;
+        hi = (hi + 63) & ~63ull;
+        out.push_back({bits_at(s, j, 2, lo), (hi - lo) / 8});
+      }
+      if (blk_global(s, j) + 1 < s->nblocks && band_pair(s, L, blk_top(s, j, B + 2), &lo, &hi)) {
+        lo &= ~63ull;
+        hi = (hi + 63) & ~63ull;
+        in.push_back({bits_at(s, j, B + 2, lo), (hi - lo) / 8});
+      }
+    }
+    return xfer_ranges(s, out, down, in, up, cs);
+  }
   if (mode == 1) {
     gm_solver* s = ss[0];
     const int down = (s->rank + s->world - 1) % s->world, up = (s->rank + 1) % s->world;
@@ -2257,6 +2377,107 @@ static u64 halo_recv_count(const gm_solver* s, u64 L) {
     if (blk_global(s, j) >= 1) n += halo_count(s, L, blk_top(s, j, 0));
   return n;
 }
+// words halo_move_all packs on the send side (its count, without the kernels)
+static u64 halo_send_count(const gm_solver* s, u64 L) {
+  u64 n = 0;
+  for (u64 j = 0; j < blk_count(s); j++)
+    if (blk_global(s, j) + 1 < s->nblocks) n += halo_count(s, L, blk_top(s, j, s->view.B));
+  return n;
+}
+
+// Fail-fast check of a sharded solve's exchange plan.  Every message of
+// every level is fixed by the geometry, so before level 0 each rank
+// fingerprints, per level, the ordered byte counts it will send and receive
+// for the bits (down) and words (up) halos; the fingerprints are gathered
+// and a sender's must equal its receiver's.  A mismatch -- which under RCCL
+// would leave a receive of the wrong size waiting forever -- is GM_ECORRUPT
+// on every rank at once, before any transfer.
+struct SigAcc {
+  u64 h = 1469598103934665603ull, n = 0;
+  void add(u64 bytes) {
+    h = (h ^ bytes) * 1099511628211ull;
+    n++;
+  }
+  u64 get() const { return h ^ (n << 56); }
+};
+static void halo_sigs(const gm_solver* s, u64 L, u64 out[4]) {
+  SigAcc bs, br, ws, wr;
+  const u64 nb = blk_count(s), B = s->view.B;
+  for (u64 j = 0; j < nb; j++) {
+    u64 lo, hi;
+    if (blk_global(s, j) >= 1 && band_pair(s, L, blk_top(s, j, 2), &lo, &hi))
+      bs.add(((hi + 63) & ~63ull) / 8 - (lo & ~63ull) / 8);
+    if (blk_global(s, j) + 1 < s->nblocks && band_pair(s, L, blk_top(s, j, B + 2), &lo, &hi))
+      br.add(((hi + 63) & ~63ull) / 8 - (lo & ~63ull) / 8);
+  }
+  if (s->hg.on) {
+    const u64 wb = s->halo16 ? 2 : 4;
+    const u64 ns = halo_send_count(s, L), nr = halo_recv_count(s, L);
+    if (ns) ws.add(ns * wb);
+    if (nr) wr.add(nr * wb);
+  } else {
+    for (u64 j = 0; j < nb; j++) {
+      u64 lo, hi;
+      if (blk_global(s, j) + 1 < s->nblocks && band_pair(s, L, blk_top(s, j, B), &lo, &hi)) ws.add((hi - lo) * 4);
+      if (blk_global(s, j) >= 1 && band_pair(s, L, blk_top(s, j, 0), &lo, &hi)) wr.add((hi - lo) * 4);
+    }
+  }
+  out[0] = bs.get();
+  out[1] = br.get();
+  out[2] = ws.get();
+  out[3] = wr.get();
+}
+// all ranks' fingerprints, rank-major [world][T][4]: bits go down (rank r
+// sends what r - 1 receives), words go up
+static int halo_sigs_match(const std::vector<u64>& all, int world, int T) {
+  auto at = [&](int r, int L, int k) { return all[((size_t)r * T + L) * 4 + k]; };
+  for (int r = 0; r < world; r++) {
+    const int down = (r + world - 1) % world, up = (r + 1) % world;
+    for (int L = 0; L < T; L++) {
+      if (at(r, L, 0) != at(down, L, 1))
+        return fail(GM_ECORRUPT, "bits halo of level %d: rank %d would send what rank %d does not expect", L, r, down);
+      if (at(r, L, 2) != at(up, L, 3))
+        return fail(GM_ECORRUPT, "words halo of level %d: rank %d would send what rank %d does not expect", L, r, up);
+    }
+  }
+  return 0;
+}
+// gather every rank's fingerprints and compare (once per solver: the
+// geometry never changes)
+static int check_halo_plan(std::vector<gm_solver*>& ss, int mode, hipStream_t st) {
+  gm_solver* s0 = ss[0];
+  if (s0->halo_ok) return 0;
+  const int T = s0->d.max_levels, W = s0->world;
+  std::vector<u64> all((size_t)W * T * 4);
+  if (mode == 2) {
+    for (gm_solver* s : ss)
+      for (int L = 0; L < T; L++) halo_sigs(s, (u64)L, &all[((size_t)s->rank * T + L) * 4]);
+  } else {
+    std::vector<u64> mine((size_t)T * 4);
+    for (int L = 0; L < T; L++) halo_sigs(s0, (u64)L, &mine[(size_t)L * 4]);
+    if (mode == 3) {
+      int rc = xfer_call(s0, GM_XFER_ALLGATHER, mine.data(), mine.size() * 8, -1, all.data(), all.size() * 8, -1);
+      if (rc) return rc;
+    } else {
+      void* dev = nullptr;
+      HIPCHK(hipMalloc(&dev, (all.size() + mine.size()) * 8));
+      u64* dall = (u64*)dev;
+      u64* dmine = dall + all.size();
+      hipError_t e = hipMemcpyAsync(dmine, mine.data(), mine.size() * 8, hipMemcpyHostToDevice, st);
+      ncclResult_t r = ncclSuccess;
+      if (e == hipSuccess) r = ncclAllGather(dmine, dall, mine.size(), ncclUint64, s0->comm, st);
+      if (e == hipSuccess && r == ncclSuccess) e = hipMemcpyAsync(all.data(), dall, all.size() * 8, hipMemcpyDeviceToHost, st);
+      if (e == hipSuccess) e = hipStreamSynchronize(st);
+      (void)hipFree(dev);
+      if (r != ncclSuccess) return fail(GM_EHIP, "RCCL allgather of the halo plan: %s", ncclGetErrorString(r));
+      if (e != hipSuccess) return fail(GM_EHIP, "halo plan: %s", hipGetErrorString(e));
+    }
+  }
+  int rc = halo_sigs_match(all, W, T);
+  if (rc) return rc;
+  for (gm_solver* s : ss) s->halo_ok = true;
+  return 0;
+}
 
 // after resolve(L): words of every block's top two own slices go up.
 // Power-of-two tables send only the non-hole words (about a fifth of the
@@ -2267,6 +2488,34 @@ static int exchange_words(std::vector<gm_solver*>& ss, u64 L, int mode, hipStrea
   auto words_at = [&](gm_solver* s, u64 j, u64 o, u64 off) {
     return s->words + L * s->view.Wl + blk_slice(s, j, o) * s->view.Z + off;
   };
+  if (mode == 3) {  // host-staged: the RCCL form's buffers and order
+    gm_solver* s = ss[0];
+    const int down = (s->rank + s->world - 1) % s->world, up = (s->rank + 1) % s->world;
+    const u64 nb = blk_count(s), B = s->view.B;
+    std::vector<HostRange> out, in;
+    u64 nrecv = 0;
+    if (packed) {
+      const u64 wb = s->halo16 ? 2 : 4;
+      const u64 nsend = halo_move_all(s, L, 1, s->halo_send, cs);
+      HIPCHK(hipGetLastError());
+      nrecv = halo_recv_count(s, L);
+      if (nsend) out.push_back({s->halo_send, nsend * wb});
+      if (nrecv) in.push_back({s->halo_recv, nrecv * wb});
+    } else {
+      for (u64 j = 0; j < nb; j++) {
+        u64 lo, hi;
+        if (blk_global(s, j) + 1 < s->nblocks && band_pair(s, L, blk_top(s, j, B), &lo, &hi))
+          out.push_back({words_at(s, j, B, lo), (hi - lo) * 4});
+        if (blk_global(s, j) >= 1 && band_pair(s, L, blk_top(s, j, 0), &lo, &hi))
+          in.push_back({words_at(s, j, 0, lo), (hi - lo) * 4});
+      }
+    }
+    int rc = xfer_ranges(s, out, up, in, down, cs);
+    if (rc) return rc;
+    if (packed && nrecv) halo_move_all(s, L, 0, s->halo_recv, cs);
+    HIPCHK(hipGetLastError());
+    return 0;
+  }
   if (mode == 1) {
     gm_solver* s = ss[0];
     const int down = (s->rank + s->world - 1) % s->world, up = (s->rank + 1) % s->world;
@@ -2342,7 +2591,9 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
   gm_solver* s0 = ss[0];
   const Desc& d = s0->d;
   const int T = d.max_levels;
-  const int mode = s0->world <= 1 ? 0 : (ss.size() == 1 ? 1 : 2);
+  // 0: one table; 1: one shard per process over RCCL; 2: in-process group;
+  // 3: one shard per process over a host-staged transport
+  const int mode = s0->world <= 1 ? 0 : ss.size() != 1 ? 2 : s0->xfer ? 3 : 1;
   if (mode == 1 && !s0->comm) return fail(GM_EINVAL, "shard %d/%d has no communicator (gm_solver_comm_init)", s0->rank, s0->world);
   if (mode == 2) {
     if ((int)ss.size() != s0->world) return fail(GM_EINVAL, "group solve needs all %d shards", s0->world);
@@ -2411,7 +2662,7 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
   // halo.  Per level: own part -> event -> exchange on the comm stream ->
   // event; the boundary part of the NEXT level waits for that exchange.  A
   // block narrower than 4 top values has no such split: exchange in order.
-  bool pipe = mode != 0;
+  bool pipe = mode == 1 || mode == 2;  // the host-staged transport runs in order
   for (gm_solver* s : ss)
     if (s->view.B < 4) pipe = false;
   if (s0->flags & GM_F_SHARD_INORDER) pipe = false;  // A/B: exchange in order
@@ -2463,6 +2714,10 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
     }
     return c;
   };
+  if (mode != 0) {
+    int rc = check_halo_plan(ss, mode, st);
+    if (rc) return rc;
+  }
   // forward (pull): level 0 .. T-1, each level's bitmap written exactly once.
   // Parents are one or two top values ABOVE: the boundary is the top two
   // slices [b-2, b), whose parents sit in the halo [b, b+2) sent down by the
@@ -2547,16 +2802,29 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
     hipLaunchKernelGGL(k_dense_root, dim3(1), dim3(64), 0, st, s->view, s->words, s->bits, root_q, s->st, s->wbits());
     hipLaunchKernelGGL(k_fill_red, dim3(1), dim3(1024), 0, st, s->st, s->bcount);
   }
-  if (mode == 1) {
-    ncclResult_t r = ncclAllReduce(s0->st->red, s0->st->red, 5, ncclUint64, ncclSum, s0->comm, st);
-    if (r != ncclSuccess) return fail(GM_EHIP, "RCCL allreduce: %s", ncclGetErrorString(r));
+  if (mode == 1) {  // counts and root word summed; the error masks max-reduced (a sum would carry)
+    ncclGroupStart();
+    ncclResult_t r = ncclAllReduce(s0->st->red, s0->st->red, 4, ncclUint64, ncclSum, s0->comm, st);
+    ncclResult_t r2 = ncclAllReduce(s0->st->red + 4, s0->st->red + 4, 1, ncclUint64, ncclMax, s0->comm, st);
+    ncclResult_t r3 = ncclGroupEnd();
+    if (r != ncclSuccess || r2 != ncclSuccess || r3 != ncclSuccess)
+      return fail(GM_EHIP, "RCCL allreduce: %s", ncclGetErrorString(r != ncclSuccess ? r : r2 != ncclSuccess ? r2 : r3));
   }
-  // totals (host): RCCL has already summed red[] across ranks; a group sums here
+  // totals (host): RCCL has already reduced red[] across ranks; a group and
+  // the host-staged transport reduce here (counts summed, error masks OR-ed)
   u64 red[5] = {0, 0, 0, 0, 0};
   for (gm_solver* s : ss) {
     u64 r[5];
     HIPCHK(hipMemcpyAsync(r, s->st->red, sizeof r, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    if (mode == 3) {
+      std::vector<u64> all((size_t)5 * s->world);
+      int rc = xfer_call(s, GM_XFER_ALLGATHER, r, sizeof r, -1, all.data(), all.size() * 8, -1);
+      if (rc) return rc;
+      for (int g = 0; g < s->world; g++)
+        for (int i = 0; i < 5; i++) red[i] = (i == 4) ? (red[i] | all[(size_t)g * 5 + i]) : red[i] + all[(size_t)g * 5 + i];
+      continue;
+    }
     for (int i = 0; i < 5; i++) red[i] = (i == 4) ? (red[i] | r[i]) : red[i] + r[i];
   }
   auto t1 = std::chrono::steady_clock::now();

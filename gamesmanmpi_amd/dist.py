@@ -7,7 +7,10 @@ and the library exchanges two boundary slices per level over RCCL, inside
 one enqueued solve (no host round trip per level).
 
   ShardedSolver   one process per GPU (torch.distributed.run); RCCL id
-                  bootstrapped with torch.distributed
+                  bootstrapped with torch.distributed, or -- transport="host"
+                  -- halos staged through host memory and carried by the
+                  default torch.distributed group (gloo on a CPU box or when
+                  ranks share a GPU), the same geometry and reductions
   group_solve     every shard of a job in ONE process on one GPU, halos by
                   device-to-device copies -- the same kernels and halo
                   geometry, for parity tests on a single device
@@ -23,11 +26,18 @@ class ShardedSolver(Solver):
     """Shard `rank` of `world` of a dense solve; needs an initialised
     torch.distributed default group (any backend) for the bootstrap."""
 
-    def __init__(self, spec, rank, world, device=None, **kw):
+    def __init__(self, spec, rank, world, device=None, transport="rccl", **kw):
         super().__init__(spec, device=device, rank=rank, world=world,
                          layout="dense", **kw)
+        self._xfer = None
         if world > 1:
-            self._comm_init()
+            if transport == "host":
+                self._xfer = HostTransport()
+                _lib.check(_lib.load().gm_solver_set_transport(self._h, self._xfer.fn, None))
+            elif transport == "rccl":
+                self._comm_init()
+            else:
+                raise ValueError("transport: 'rccl' or 'host'")
 
     def _comm_init(self):
         import torch.distributed as dist
@@ -41,6 +51,61 @@ class ShardedSolver(Solver):
         buf = ctypes.create_string_buffer(raw, len(raw))
         with self.torch.cuda.device(self.device):
             _lib.check(L.gm_solver_comm_init(self._h, buf))
+
+
+class HostTransport:
+    """gm_xfer_fn over the default torch.distributed group: the library hands
+    halo bytes in host memory; paired send / receive with isend + irecv,
+    all-gathers with all_gather.  Errors become a non-zero return (the solve
+    fails with GM_EHIP instead of hanging)."""
+
+    def __init__(self):
+        self.fn = _lib.XFER_FN(self._call)
+
+    @staticmethod
+    def _view(ptr, n):
+        import numpy as np
+        import torch
+        if not n:
+            return torch.empty(0, dtype=torch.uint8)
+        arr = np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctypes.c_uint8)), shape=(n,))
+        return torch.from_numpy(arr)
+
+    def _call(self, ctx, op, sbuf, sbytes, speer, rbuf, rbytes, rpeer):
+        import torch.distributed as dist
+        try:
+            send, recv = self._view(sbuf, sbytes), self._view(rbuf, rbytes)
+            if op == _lib.GM_XFER_SENDRECV:
+                reqs = []
+                if sbytes:
+                    reqs.append(dist.isend(send, speer))
+                if rbytes:
+                    reqs.append(dist.irecv(recv, rpeer))
+                for r in reqs:
+                    r.wait()
+            elif op == _lib.GM_XFER_ALLGATHER:
+                world = dist.get_world_size()
+                parts = list(recv.view(world, sbytes).unbind(0))
+                dist.all_gather(parts, send.clone())
+            else:
+                return 1
+            return 0
+        except Exception:  # noqa: BLE001 -- reported to the library as a failed transfer
+            import traceback
+            traceback.print_exc()
+            return 1
+
+
+def halo_sigs(spec, rank, world, flags=0):
+    """The per-level halo fingerprints shard `rank` of `world` checks against
+    its neighbours before level 0 (host only): uint64 [levels, 4] = bits
+    sent down, bits received from above, words sent up, words received."""
+    import numpy as np
+    spec = spec if isinstance(spec, GameSpec) else GameSpec(*spec)
+    T = int(spec.max_levels)
+    out = np.zeros((T, 4), np.uint64)
+    _lib.check(_lib.load().gm_shard_halo_sigs(spec.id, rank, world, flags, out.ctypes.data, T))
+    return out
 
 
 def group_solve(spec, world, device=None, kernel_timing=False, flags=0):

@@ -249,6 +249,24 @@ int gm_shard_info(int game, int rank, int world, uint64_t out[8]);
 #define GM_COMM_ID_BYTES 128
 int gm_comm_unique_id(void *id_out);
 int gm_solver_comm_init(gm_solver *s, const void *id);
+/* Host-staged transport (one shard per process without RCCL, e.g.
+ * torch.distributed over gloo): the solver stages every halo in host memory
+ * and calls fn, which returns 0 once the transfer is complete.
+ *   GM_XFER_SENDRECV  send sbytes of sbuf to rank speer and receive rbytes
+ *                     into rbuf from rank rpeer (either may be 0 bytes)
+ *   GM_XFER_ALLGATHER every rank's sbytes of sbuf into rbuf, rank order
+ *                     (world * sbytes; speer / rpeer unused)
+ * Replaces the communicator for gm_solver_solve; NULL fn restores RCCL. */
+#define GM_XFER_SENDRECV 0
+#define GM_XFER_ALLGATHER 1
+typedef int (*gm_xfer_fn)(void *ctx, int op, const void *sbuf, uint64_t sbytes, int speer, void *rbuf,
+                          uint64_t rbytes, int rpeer);
+int gm_solver_set_transport(gm_solver *s, gm_xfer_fn fn, void *ctx);
+/* The per-level halo fingerprints a shard checks against its neighbours'
+ * before level 0 (gm_solver.hip halo_sigs): out[T][4] = bits sent down,
+ * bits received from above, words sent up, words received from below.
+ * Host only: no device memory, no GPU needed. */
+int gm_shard_halo_sigs(int game, int rank, int world, uint32_t flags, uint64_t *out, uint32_t levels);
 /* All `n` shards of one job in ONE process on one stream, halos moved by
  * device-to-device copies: the same kernels and halo geometry as the RCCL
  * path, runnable on a single GPU (parity tests). */
