@@ -163,8 +163,9 @@ def cpu_baseline(params):
 
 def keyed_record(device):
     """BASELINE config 3 as shipped: toot_and_otto_bitstring 6x4 on the
-    keyed-table path (one warm-up solve, one timed, one with kernel
-    timing), fingerprint vs tests/golden/checksums.json."""
+    keyed path the planner picks (BUCKETED levels; one warm-up solve, one
+    timed, one with kernel timing), fingerprint vs
+    tests/golden/checksums.json."""
     from gamesmanmpi_amd.games import GameSpec
     from gamesmanmpi_amd.solver import Solver
     import torch
@@ -186,8 +187,11 @@ def keyed_record(device):
            "solve_ms": wall * 1e3, "positions_per_s": r.positions / wall,
            "ms_forward": r.ms_forward, "ms_backward": r.ms_backward,
            "kernels": {}}
-    for name, b, ms, n in (("expand", fwd_b, tr.ms_expand_kernels, tr.n_expand_launches),
-                           ("resolve", bwd_b, tr.ms_resolve_kernels, tr.n_resolve_launches)):
+    # HASHED: the expand / resolve kernels; BUCKETED: every kernel of the
+    # forward / backward passes (gm_bucketed.h F0-F5 / B3-B5)
+    names = ("expand", "resolve") if r.extra["layout"] == "hashed" else ("forward", "backward")
+    for name, b, ms, n in ((names[0], fwd_b, tr.ms_expand_kernels, tr.n_expand_launches),
+                           (names[1], bwd_b, tr.ms_resolve_kernels, tr.n_resolve_launches)):
         if n and ms > 0:
             out["kernels"][name] = {"launches": n, "ms_total": ms,
                                     "model_8d_bytes": b,

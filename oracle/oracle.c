@@ -419,7 +419,15 @@ static int parse_kv(const char *params, const char *key, int dflt) {
 /* name: four_to_one | sum_four_to_one | tic_tac_toe_np | mttt |
  *       toot_and_otto_bitstring | othello_bit_new
  * params: "length=4,height=4" / "start=20" / "heaps=31:31:31" */
+static char g_keys[MAXGAMES][256]; /* "name|params" of each registered game */
+
 int or_game(const char *name, const char *params) {
+  /* a game already described returns its handle: descriptors are immutable,
+   * so a test process may ask for the same game any number of times */
+  char key[256];
+  snprintf(key, sizeof key, "%s|%s", name, params ? params : "");
+  for (int i = 0; i < g_ngames; i++)
+    if (!strcmp(g_keys[i], key)) return i;
   if (g_ngames >= MAXGAMES) { snprintf(g_err, sizeof g_err, "too many games"); return -1; }
   game g;
   memset(&g, 0, sizeof g);
@@ -460,6 +468,7 @@ int or_game(const char *name, const char *params) {
     return -1;
   }
   g_games[g_ngames] = g;
+  memcpy(g_keys[g_ngames], key, sizeof key);
   return g_ngames++;
 }
 
