@@ -113,11 +113,12 @@ def _stream_in(t, path, torch):
     if os.path.getsize(path) != n:
         raise ValueError("%s holds %d bytes, the plan %d" % (path, os.path.getsize(path), n))
     stage = torch.empty(min(CHUNK, max(n, 1)), dtype=torch.uint8, pin_memory=True)
+    view = stage.numpy()  # the pinned chunk as a writable host array: read straight into it
     with open(path, "rb") as fh:
         for a in range(0, n, CHUNK):
             b = min(n, a + CHUNK)
-            raw = np.frombuffer(fh.read(b - a), dtype=np.uint8)
-            stage[:b - a].copy_(torch.from_numpy(raw))
+            if fh.readinto(memoryview(view[:b - a])) != b - a:
+                raise ValueError("%s ended early" % path)
             flat[a:b].copy_(stage[:b - a])
 
 

@@ -952,6 +952,7 @@ struct gm_solver {
   BkLevel* bkL = nullptr;  // device level table (scratch)
   uint32_t *pbase = nullptr, *bh = nullptr, *ph = nullptr, *boff = nullptr, *tot = nullptr, *cbase = nullptr;
   uint32_t *bkah = nullptr, *ucnt = nullptr, *meta = nullptr;
+  uint32_t* bkgc = nullptr;  // [256 partition cursors | 256 parent-range totals | overflow flag]
   u64* bktotal = nullptr;
   u64 meta_cap = 0;
   std::vector<BkLevel> lvh;  // host copy of the level table
@@ -1494,9 +1495,11 @@ static u64 bk_edges_bound(const Desc* d, u64 P) {
 }
 // in-edges of the widest level: a quarter of all edges (every known board
 // is below a fifth; a level over it returns GM_EFULL and the host re-plans)
-static u64 bk_emax_bound(u64 E) { return std::min<u64>(E, std::max<u64>(E / 4, 1u << 20)); }
+// (+5% and a run per partition: the count-free expand provisions each of the
+// 256 coarse partitions a 1/256 share of it, k_bk_expand<OVER>)
+static u64 bk_emax_bound(u64 E) { return std::min<u64>(E, std::max<u64>(E / 4, 1u << 20)) / 20 * 21 + (u64)kBkC * 4096; }
 struct BkScratch {
-  size_t lv, pbase, bh, ph, boff, tot, cbase, ah, ucnt, total, meta, end;
+  size_t lv, pbase, bh, ph, boff, tot, cbase, ah, ucnt, total, gc, meta, end;
 };
 static BkScratch bk_scratch(int T) {
   auto r = [](size_t b) { return (b + 255) / 256 * 256; };
@@ -1513,6 +1516,7 @@ static BkScratch bk_scratch(int T) {
   x.ah = o; o += r((size_t)T * kBkC * kBkC * 4);  // per level: answers per (child partition, parent range)
   x.ucnt = o; o += r(NBmax * 4);
   x.total = o; o += r(2 * 8);
+  x.gc = o; o += r((2 * kBkC + 4) * 4);  // k_bk_expand<OVER>: partition cursors, parent-range totals, overflow flag
   const size_t NRmax = (size_t)1 << (29 - kBkRangeBits);
   x.meta = o; o += r((size_t)T * (2 * (NBmax + 1) + NRmax + 1) * 4);  // per level: cst, fo, rfo
   x.end = o;
@@ -1849,6 +1853,7 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
     s->tot = (uint32_t*)(sc + x.tot);
     s->cbase = (uint32_t*)(sc + x.cbase);
     s->bkah = (uint32_t*)(sc + x.ah);
+    s->bkgc = (uint32_t*)(sc + x.gc);
     s->ucnt = (uint32_t*)(sc + x.ucnt);
     s->bktotal = (u64*)(sc + x.total);
     s->meta = (uint32_t*)(sc + x.meta);
@@ -2984,28 +2989,83 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
       P.rfo_off = (uint32_t)meta_used;
       meta_used += NR + 1;
       uint32_t* rfo = s->meta + P.rfo_off;  // answers per fine parent range -> their starts
-      HIPCHK(hipMemsetAsync(rfo, 0, (NR + 1) * 4, st));
-      hipEvent_t* sp = span(true);
-      BK_KIND_LAUNCH(k_bk_count, nblk, kBkStreamThreads, s, s->d, s->bkK + P.lb, P.n, chunk, P.pshift, P.fb, s->bh,
-                     s->ph, rfo, s->st);
-      hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, st, s->bh, (uint32_t)nblk, s->boff, s->tot);
-      hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, st, s->ph, (uint32_t)nblk, s->ph, s->tot + kBkC);
-      hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, st, rfo, NR + 1, rfo, s->bktotal + 1);
-      if ((rc = span_end(sp))) return bail(rc);
-      nfwd += 4;
-      HIPCHK(hipGetLastError());
-      HIPCHK(hipMemcpyAsync(htot.data(), s->tot, 2 * kBkC * 4, hipMemcpyDeviceToHost, st));
-      HIPCHK(hipMemcpyAsync(&herr, &s->st->err, 4, hipMemcpyDeviceToHost, st));
-      HIPCHK(hipStreamSynchronize(st));
-      if (herr) return bail(fail(GM_ECORRUPT, "level %d:%s", L, err_text(herr).c_str()));
       keep.emplace_back(2 * (kBkC + 1));
       std::vector<uint32_t>& hb = keep.back();  // [coarse bases | parent-range bases]
       u64 E = 0, Ep = 0;
-      for (int j = 0; j < kBkC; j++) {
-        hb[(size_t)j] = (uint32_t)E;
-        hb[(size_t)kBkC + 1 + j] = (uint32_t)Ep;
-        E += htot[(size_t)j];
-        Ep += htot[(size_t)kBkC + j];
+      // Count-free form first (k_bk_expand<OVER>): children go straight to
+      // provisioned partitions; a partition past its share -> the exact
+      // form (F0 counts, then k_bk_expand<false>) for this level.
+      const uint32_t cap = (uint32_t)(s->Emax / kBkC);
+      uint32_t incap = 0;
+      bool exact = true;
+      hipEvent_t* sp = nullptr;
+      if (!(s->flags & GM_F_BK_EXACT)) {
+        HIPCHK(hipMemsetAsync(rfo, 0, (NR + 1) * 4, st));
+        HIPCHK(hipMemsetAsync(s->bkgc, 0, (2 * kBkC + 4) * 4, st));
+        // parents per round from the previous level's branching (a round's
+        // children should fill most of the 8192-record stage)
+        const double avg = (L > 0 && lv[(size_t)L - 1].n) ? std::max(1.0, (double)P.ein / (double)lv[(size_t)L - 1].n) : 4.0;
+        uint32_t ppr = 256;
+        while (ppr < 4096 && (double)(2 * ppr) * avg <= 6144.0) ppr *= 2;
+        sp = span(true);
+        switch (s->d.kind) {
+          case K_TTT:
+            hipLaunchKernelGGL((k_bk_expand<K_TTT, true>), dim3(nblk), dim3(kBkStreamThreads), 0, st, s->d,
+                               s->bkK + P.lb, P.n, chunk, (const uint32_t*)nullptr, (const uint32_t*)nullptr, ppr,
+                               s->S1k, s->S1p, cap, s->bkgc, P.pshift, P.fb, s->bkgc + kBkC, rfo, s->bkgc + 2 * kBkC, s->st);
+            break;
+          case K_TOOT:
+            hipLaunchKernelGGL((k_bk_expand<K_TOOT, true>), dim3(nblk), dim3(kBkStreamThreads), 0, st, s->d,
+                               s->bkK + P.lb, P.n, chunk, (const uint32_t*)nullptr, (const uint32_t*)nullptr, ppr,
+                               s->S1k, s->S1p, cap, s->bkgc, P.pshift, P.fb, s->bkgc + kBkC, rfo, s->bkgc + 2 * kBkC, s->st);
+            break;
+          default:
+            hipLaunchKernelGGL((k_bk_expand<K_OTHELLO, true>), dim3(nblk), dim3(kBkStreamThreads), 0, st, s->d,
+                               s->bkK + P.lb, P.n, chunk, (const uint32_t*)nullptr, (const uint32_t*)nullptr, ppr,
+                               s->S1k, s->S1p, cap, s->bkgc, P.pshift, P.fb, s->bkgc + kBkC, rfo, s->bkgc + 2 * kBkC, s->st);
+            break;
+        }
+        hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, st, rfo, NR + 1, rfo, s->bktotal + 1);
+        if ((rc = span_end(sp))) return bail(rc);
+        nfwd += 2;
+        HIPCHK(hipGetLastError());
+        std::vector<uint32_t> g(2 * kBkC + 1);
+        HIPCHK(hipMemcpyAsync(g.data(), s->bkgc, g.size() * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(&herr, &s->st->err, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        if (herr) return bail(fail(GM_ECORRUPT, "level %d:%s", L, err_text(herr).c_str()));
+        if (!g[2 * kBkC]) {
+          exact = false;
+          incap = cap;
+          for (int j = 0; j < kBkC; j++) {
+            hb[(size_t)j] = (uint32_t)E;
+            hb[(size_t)kBkC + 1 + j] = (uint32_t)Ep;
+            E += g[(size_t)j];
+            Ep += g[(size_t)kBkC + j];
+          }
+        }
+      }
+      if (exact) {
+        HIPCHK(hipMemsetAsync(rfo, 0, (NR + 1) * 4, st));
+        sp = span(true);
+        BK_KIND_LAUNCH(k_bk_count, nblk, kBkStreamThreads, s, s->d, s->bkK + P.lb, P.n, chunk, P.pshift, P.fb, s->bh,
+                       s->ph, rfo, s->st);
+        hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, st, s->bh, (uint32_t)nblk, s->boff, s->tot);
+        hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, st, s->ph, (uint32_t)nblk, s->ph, s->tot + kBkC);
+        hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, st, rfo, NR + 1, rfo, s->bktotal + 1);
+        if ((rc = span_end(sp))) return bail(rc);
+        nfwd += 4;
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(htot.data(), s->tot, 2 * kBkC * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(&herr, &s->st->err, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        if (herr) return bail(fail(GM_ECORRUPT, "level %d:%s", L, err_text(herr).c_str()));
+        for (int j = 0; j < kBkC; j++) {
+          hb[(size_t)j] = (uint32_t)E;
+          hb[(size_t)kBkC + 1 + j] = (uint32_t)Ep;
+          E += htot[(size_t)j];
+          Ep += htot[(size_t)kBkC + j];
+        }
       }
       if (E != Ep) return bail(fail(GM_ECORRUPT, "level %d: %llu children by partition, %llu by parent", L,
                                     (unsigned long long)E, (unsigned long long)Ep));
@@ -3028,25 +3088,35 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
         X.cst_off = (uint32_t)meta_used;
         uint32_t* cst = s->meta + X.cst_off;
         uint32_t* fo = cst + NB + 1;  // kept: the backward pass walks the level's in-edges bucket by bucket
-        // parents per expand round: about a stage (8192 records) of children
-        const double avg = (double)E / (double)P.n;
-        uint32_t ppr = 256;
-        while (ppr < 4096 && (double)(2 * ppr) * avg <= 6144.0) ppr *= 2;
         const int gd = (int)std::min<uint32_t>(NB, 512);  // two workgroups per CU
         sp = span(true);
-        BK_KIND_LAUNCH(k_bk_expand, nblk, kBkStreamThreads, s, s->d, s->bkK + P.lb, P.n, chunk, s->boff, s->cbase, ppr,
-                       s->S1k, s->S1p);
+        if (exact) {  // parents per expand round: about a stage (8192 records) of children
+          const double avg = (double)E / (double)P.n;
+          uint32_t ppr = 256;
+          while (ppr < 4096 && (double)(2 * ppr) * avg <= 6144.0) ppr *= 2;
+#define BK_EXPAND_EXACT(K)                                                                                        \
+  hipLaunchKernelGGL((k_bk_expand<K, false>), dim3(nblk), dim3(kBkStreamThreads), 0, st, s->d, s->bkK + P.lb, P.n, \
+                     chunk, (const uint32_t*)s->boff, (const uint32_t*)s->cbase, ppr, s->S1k, s->S1p, 0u,          \
+                     (uint32_t*)nullptr, 0u, 0u, (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr, s->st)
+          switch (s->d.kind) {
+            case K_TTT: BK_EXPAND_EXACT(K_TTT); break;
+            case K_TOOT: BK_EXPAND_EXACT(K_TOOT); break;
+            default: BK_EXPAND_EXACT(K_OTHELLO); break;
+          }
+#undef BK_EXPAND_EXACT
+          nfwd++;
+        }
         // the fine partition writes the parents straight into the level's
         // in-edge parents (REp); F3 adds the child indices (REc)
         hipLaunchKernelGGL((k_bk_fine<true, u64>), dim3(kBkC), dim3(kBkFineThreads), 0, st, s->S1k, s->S1p,
                            s->cbase, 56u - f, F, s->S2k, s->REp + X.rb, fo, (const uint32_t*)nullptr, P.pshift,
-                           s->bkah + (size_t)L * kBkC * kBkC);
+                           s->bkah + (size_t)L * kBkC * kBkC, incap);
         // unique keys of bucket b to S1k[fo[b] ..), compacted into the level
         hipLaunchKernelGGL(k_bk_dedup, dim3(gd), dim3(kBkDedupThreads), 0, st, s->S2k, (const uint32_t*)fo, NB, s->S1k,
                            s->ucnt, s->REc + X.rb, s->st);
         hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, st, s->ucnt, NB, cst, s->bktotal);
         if ((rc = span_end(sp))) return bail(rc);
-        nfwd += 4;
+        nfwd += 3;
         HIPCHK(hipGetLastError());
         u64 n1 = 0;
         HIPCHK(hipMemcpyAsync(&n1, s->bktotal, 8, hipMemcpyDeviceToHost, st));
@@ -3099,7 +3169,7 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
       if (Fp > 1) {
         hipLaunchKernelGGL((k_bk_fine<false, uint32_t>), dim3(kBkC), dim3(kBkFineThreads), 0, st, Ap,
                            (const uint32_t*)nullptr, pb, 10u + P.fb, Fp, (uint32_t*)s->S2k, (uint32_t*)nullptr,
-                           (uint32_t*)nullptr, rfo, 0u, (uint32_t*)nullptr);
+                           (uint32_t*)nullptr, rfo, 0u, (uint32_t*)nullptr, 0u);
         ap = (uint32_t*)s->S2k;
         nbwd++;
       }

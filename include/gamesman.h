@@ -106,6 +106,9 @@ typedef struct gm_buffers {
                                   hash table (HASHED) instead of BUCKETED */
 #define GM_F_WORDS16 64u       /* dense: 16-bit table words (octet kernels)
                                   where 8-bit ones would be chosen */
+#define GM_F_BK_EXACT 128u     /* BUCKETED: count every level's children first
+                                  (exact partition offsets) instead of writing
+                                  into provisioned partitions */
 
 typedef struct gm_result {
   uint32_t root_word;

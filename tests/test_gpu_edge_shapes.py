@@ -59,18 +59,19 @@ KEYED_SHAPES = [
 ]
 
 
-@pytest.mark.parametrize("layout", ["bucketed", "hashed"])
+@pytest.mark.parametrize("layout,flags", [("bucketed", 0), ("bucketed", 128), ("hashed", 0)])
 @pytest.mark.parametrize("name,params", KEYED_SHAPES)
-def test_keyed_edge_shape_matches_oracle(name, params, layout):
-    """Small and degenerate boards through both keyed layouts: a primitive
-    root, levels of one position, single-bucket levels (bucketed levels:
-    partitions mostly empty) -- every position against the oracle."""
+def test_keyed_edge_shape_matches_oracle(name, params, layout, flags):
+    """Small and degenerate boards through both keyed layouts (bucketed:
+    provisioned partitions, and GM_F_BK_EXACT = 128, the counted form): a
+    primitive root, levels of one position, single-bucket levels (partitions
+    mostly empty) -- every position against the oracle."""
     from gamesmanmpi_amd.games import GameSpec
     from gamesmanmpi_amd.solver import Solver
     from oracle.oracle import Game  # checker only
     spec = GameSpec(name, params)
     sol = Game(name, params).solve(1 << 22)
-    s = Solver(spec, layout=layout, positions=max(64, sol.count))
+    s = Solver(spec, layout=layout, positions=max(64, sol.count), flags=flags)
     r = s.solve()
     assert r.extra["layout"] == layout
     assert (r.positions, r.edges, r.root_line) == (sol.count, sol.edges, sol.root_line)

@@ -32,12 +32,12 @@ def _gold(name):
     return gold[name]
 
 
-def _check(name, layout="auto"):
+def _check(name, layout="auto", flags=0):
     from gamesmanmpi_amd.games import GameSpec
     from gamesmanmpi_amd.solver import Solver
     e = _gold(name)
     spec = GameSpec(e["game"], e["params"])
-    s = Solver(spec, layout=layout)
+    s = Solver(spec, layout=layout, flags=flags)
     r = s.solve()
     assert (r.positions, r.edges, r.primitives) == (e["positions"], e["edges"], e["primitives"])
     assert r.root_line == e["root_line"]
@@ -63,6 +63,13 @@ def test_gpu_sum_15x5_checksum_both_layouts():
 
 def test_gpu_toot_5x4_checksum():
     s, r = _check("toot_5x4")
+    assert r.extra["layout"] == "bucketed"
+
+
+def test_gpu_toot_5x4_checksum_counted_partitions():
+    """GM_F_BK_EXACT: every level counted first (the form a level falls back
+    to when a provisioned partition overflows)."""
+    s, r = _check("toot_5x4", flags=128)
     assert r.extra["layout"] == "bucketed"
 
 
