@@ -951,7 +951,7 @@ struct gm_solver {
   u64 Pcap = 0, Ecap = 0, Emax = 0;
   BkLevel* bkL = nullptr;  // device level table (scratch)
   uint32_t *pbase = nullptr, *bh = nullptr, *ph = nullptr, *boff = nullptr, *tot = nullptr, *cbase = nullptr;
-  uint32_t *bkah = nullptr, *ucnt = nullptr, *meta = nullptr;
+  uint32_t *bkcur = nullptr, *bkah = nullptr, *ucnt = nullptr, *meta = nullptr;
   uint32_t* bkgc = nullptr;  // [256 partition cursors | 256 parent-range totals | overflow flag]
   u64* bktotal = nullptr;
   u64 meta_cap = 0;
@@ -1499,7 +1499,7 @@ static u64 bk_edges_bound(const Desc* d, u64 P) {
 // 256 coarse partitions a 1/256 share of it, k_bk_expand<OVER>)
 static u64 bk_emax_bound(u64 E) { return std::min<u64>(E, std::max<u64>(E / 4, 1u << 20)) / 20 * 21 + (u64)kBkC * 4096; }
 struct BkScratch {
-  size_t lv, pbase, bh, ph, boff, tot, cbase, ah, ucnt, total, gc, meta, end;
+  size_t lv, pbase, bh, ph, boff, tot, cbase, ah, cur, ucnt, total, gc, meta, end;
 };
 static BkScratch bk_scratch(int T) {
   auto r = [](size_t b) { return (b + 255) / 256 * 256; };
@@ -1514,6 +1514,7 @@ static BkScratch bk_scratch(int T) {
   x.cbase = o; o += r((kBkC + 1) * 4);
   const size_t NBmax = (size_t)kBkC << kBkMaxFineBits;
   x.ah = o; o += r((size_t)T * kBkC * kBkC * 4);  // per level: answers per (child partition, parent range)
+  x.cur = o; o += r((((size_t)1 << (29 - kBkRangeBits)) + 1) * 4);  // B4 run cursors
   x.ucnt = o; o += r(NBmax * 4);
   x.total = o; o += r(2 * 8);
   x.gc = o; o += r((2 * kBkC + 4) * 4);  // k_bk_expand<OVER>: partition cursors, parent-range totals, overflow flag
@@ -1852,6 +1853,7 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
     s->boff = (uint32_t*)(sc + x.boff);
     s->tot = (uint32_t*)(sc + x.tot);
     s->cbase = (uint32_t*)(sc + x.cbase);
+    s->bkcur = (uint32_t*)(sc + x.cur);
     s->bkah = (uint32_t*)(sc + x.ah);
     s->bkgc = (uint32_t*)(sc + x.gc);
     s->ucnt = (uint32_t*)(sc + x.ucnt);
@@ -2899,6 +2901,13 @@ static bool bk_ranges(u64 n, uint32_t* pshift, uint32_t* fb) {
     default: hipLaunchKernelGGL(KERNEL<K_OTHELLO>, dim3(GRID), dim3(BLOCK), 0, (S)->stream, __VA_ARGS__); break;  \
   }
 
+// parents per expand round for a mean branching avg: the round's children
+// should fill about 3/4 of the 8192-record stage (whole waves, 256..4096)
+static uint32_t bk_ppr(double avg) {
+  const double p = 6144.0 / std::max(avg, 0.25);
+  return (uint32_t)std::min<double>(4096.0, std::max<double>(256.0, std::floor(p / 64.0) * 64.0));
+}
+
 static int solve_bucketed(gm_solver* s, gm_result* out) {
   const Desc& d = s->d;
   const int T = d.max_levels;
@@ -3005,8 +3014,7 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
         // parents per round from the previous level's branching (a round's
         // children should fill most of the 8192-record stage)
         const double avg = (L > 0 && lv[(size_t)L - 1].n) ? std::max(1.0, (double)P.ein / (double)lv[(size_t)L - 1].n) : 4.0;
-        uint32_t ppr = 256;
-        while (ppr < 4096 && (double)(2 * ppr) * avg <= 6144.0) ppr *= 2;
+        const uint32_t ppr = bk_ppr(avg);
         sp = span(true);
         switch (s->d.kind) {
           case K_TTT:
@@ -3092,8 +3100,7 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
         sp = span(true);
         if (exact) {  // parents per expand round: about a stage (8192 records) of children
           const double avg = (double)E / (double)P.n;
-          uint32_t ppr = 256;
-          while (ppr < 4096 && (double)(2 * ppr) * avg <= 6144.0) ppr *= 2;
+          const uint32_t ppr = bk_ppr(avg);
 #define BK_EXPAND_EXACT(K)                                                                                        \
   hipLaunchKernelGGL((k_bk_expand<K, false>), dim3(nblk), dim3(kBkStreamThreads), 0, st, s->d, s->bkK + P.lb, P.n, \
                      chunk, (const uint32_t*)s->boff, (const uint32_t*)s->cbase, ppr, s->S1k, s->S1p, 0u,          \
@@ -3152,24 +3159,26 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
     hipEvent_t* sp = span(false);
     if (L + 1 < T && P.eout) {
       const BkLevel& X = lv[(size_t)L + 1];
-      const uint32_t NB = 1u << X.nbits;
-      const uint32_t bpb = NB / kBkC;  // block j: the children's coarse partition j
+      const uint32_t NB = 1u << X.nbits, F = NB / kBkC;
       const uint32_t* cst = s->meta + X.cst_off;
       const uint32_t* fo = cst + NB + 1;
       const uint32_t* rfo = s->meta + P.rfo_off;
       const uint32_t* pb = s->pbase + (size_t)L * (kBkC + 1);
       uint32_t* Ap = (uint32_t*)s->S1k;
+      constexpr uint32_t K = 4;  // B4 workgroups per range (two resident per CU)
+      // B3: one workgroup per children's partition, exact offsets per
+      // (partition, parent range) from the counts F2 kept (ah)
       hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, st, s->bkah + (size_t)L * kBkC * kBkC, (uint32_t)kBkC,
                          s->boff, s->tot);
       hipLaunchKernelGGL(k_bk_answer, dim3(kBkC), dim3(kBkStreamThreads), 0, st, s->REp + X.rb, s->REc + X.rb, fo, cst,
-                         NB, bpb, P.pshift, s->boff, pb, s->bkW + X.lb, Ap, s->st);
+                         NB, F, P.pshift, s->boff, pb, s->bkW + X.lb, Ap, s->st);
       nbwd += 2;
       const uint32_t Fp = 1u << (P.pshift - P.fb);
       const uint32_t* ap = Ap;
       if (Fp > 1) {
-        hipLaunchKernelGGL((k_bk_fine<false, uint32_t>), dim3(kBkC), dim3(kBkFineThreads), 0, st, Ap,
-                           (const uint32_t*)nullptr, pb, 10u + P.fb, Fp, (uint32_t*)s->S2k, (uint32_t*)nullptr,
-                           (uint32_t*)nullptr, rfo, 0u, (uint32_t*)nullptr, 0u);
+        HIPCHK(hipMemcpyAsync(s->bkcur + kBkC, rfo, (size_t)NR * 4, hipMemcpyDeviceToDevice, st));
+        hipLaunchKernelGGL(k_bk_split, dim3(kBkC * K), dim3(kBkStreamThreads), 0, st, (const uint32_t*)Ap, pb,
+                           10u + P.fb, Fp, K, s->bkcur + kBkC, (uint32_t*)s->S2k);
         ap = (uint32_t*)s->S2k;
         nbwd++;
       }
