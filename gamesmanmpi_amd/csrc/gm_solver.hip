@@ -947,7 +947,7 @@ struct gm_solver {
   u64* S1k = nullptr;
   uint32_t* S1p = nullptr;
   u64* S2k = nullptr;
-  uint32_t* S2p = nullptr;
+  uint8_t* S1f = nullptr;  // per staged child: the byte under mix64's top byte (fine bucket bits)
   u64 Pcap = 0, Ecap = 0, Emax = 0;
   BkLevel* bkL = nullptr;  // device level table (scratch)
   uint32_t *pbase = nullptr, *bh = nullptr, *ph = nullptr, *boff = nullptr, *tot = nullptr, *cbase = nullptr;
@@ -1843,7 +1843,7 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
     t += 8 * s->Emax;
     s->S1p = (uint32_t*)t;
     t += 4 * s->Emax;
-    s->S2p = (uint32_t*)t;
+    s->S1f = (uint8_t*)t;  // (4 Emax bytes of the plan; one is used)
     const BkScratch x = bk_scratch(d->max_levels);
     char* sc = (char*)buf->scratch;
     s->bkL = (BkLevel*)(sc + x.lv);
@@ -3020,17 +3020,17 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
           case K_TTT:
             hipLaunchKernelGGL((k_bk_expand<K_TTT, true>), dim3(nblk), dim3(kBkStreamThreads), 0, st, s->d,
                                s->bkK + P.lb, P.n, chunk, (const uint32_t*)nullptr, (const uint32_t*)nullptr, ppr,
-                               s->S1k, s->S1p, cap, s->bkgc, P.pshift, P.fb, s->bkgc + kBkC, rfo, s->bkgc + 2 * kBkC, s->st);
+                               s->S1k, s->S1p, s->S1f, cap, s->bkgc, P.pshift, P.fb, s->bkgc + kBkC, rfo, s->bkgc + 2 * kBkC, s->st);
             break;
           case K_TOOT:
             hipLaunchKernelGGL((k_bk_expand<K_TOOT, true>), dim3(nblk), dim3(kBkStreamThreads), 0, st, s->d,
                                s->bkK + P.lb, P.n, chunk, (const uint32_t*)nullptr, (const uint32_t*)nullptr, ppr,
-                               s->S1k, s->S1p, cap, s->bkgc, P.pshift, P.fb, s->bkgc + kBkC, rfo, s->bkgc + 2 * kBkC, s->st);
+                               s->S1k, s->S1p, s->S1f, cap, s->bkgc, P.pshift, P.fb, s->bkgc + kBkC, rfo, s->bkgc + 2 * kBkC, s->st);
             break;
           default:
             hipLaunchKernelGGL((k_bk_expand<K_OTHELLO, true>), dim3(nblk), dim3(kBkStreamThreads), 0, st, s->d,
                                s->bkK + P.lb, P.n, chunk, (const uint32_t*)nullptr, (const uint32_t*)nullptr, ppr,
-                               s->S1k, s->S1p, cap, s->bkgc, P.pshift, P.fb, s->bkgc + kBkC, rfo, s->bkgc + 2 * kBkC, s->st);
+                               s->S1k, s->S1p, s->S1f, cap, s->bkgc, P.pshift, P.fb, s->bkgc + kBkC, rfo, s->bkgc + 2 * kBkC, s->st);
             break;
         }
         hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, st, rfo, NR + 1, rfo, s->bktotal + 1);
@@ -3103,7 +3103,7 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
           const uint32_t ppr = bk_ppr(avg);
 #define BK_EXPAND_EXACT(K)                                                                                        \
   hipLaunchKernelGGL((k_bk_expand<K, false>), dim3(nblk), dim3(kBkStreamThreads), 0, st, s->d, s->bkK + P.lb, P.n, \
-                     chunk, (const uint32_t*)s->boff, (const uint32_t*)s->cbase, ppr, s->S1k, s->S1p, 0u,          \
+                     chunk, (const uint32_t*)s->boff, (const uint32_t*)s->cbase, ppr, s->S1k, s->S1p, s->S1f, 0u, \
                      (uint32_t*)nullptr, 0u, 0u, (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr, s->st)
           switch (s->d.kind) {
             case K_TTT: BK_EXPAND_EXACT(K_TTT); break;
@@ -3115,9 +3115,9 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
         }
         // the fine partition writes the parents straight into the level's
         // in-edge parents (REp); F3 adds the child indices (REc)
-        hipLaunchKernelGGL((k_bk_fine<true, u64>), dim3(kBkC), dim3(kBkFineThreads), 0, st, s->S1k, s->S1p,
-                           s->cbase, 56u - f, F, s->S2k, s->REp + X.rb, fo, (const uint32_t*)nullptr, P.pshift,
-                           s->bkah + (size_t)L * kBkC * kBkC, incap);
+        hipLaunchKernelGGL(k_bk_fine, dim3(kBkC), dim3(kBkFineThreads), 0, st, (const u64*)s->S1k,
+                           (const uint32_t*)s->S1p, (const uint8_t*)s->S1f, (const uint32_t*)s->cbase, 8u - f, F, s->S2k,
+                           s->REp + X.rb, fo, P.pshift, s->bkah + (size_t)L * kBkC * kBkC, incap);
         // unique keys of bucket b to S1k[fo[b] ..), compacted into the level
         hipLaunchKernelGGL(k_bk_dedup, dim3(gd), dim3(kBkDedupThreads), 0, st, s->S2k, (const uint32_t*)fo, NB, s->S1k,
                            s->ucnt, s->REc + X.rb, s->st);
