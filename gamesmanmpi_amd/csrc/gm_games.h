@@ -297,6 +297,78 @@ GM_HD int toot_level(const Desc& d, uint64_t k) {
   return popc64((k | (k >> d.A)) & d.full);
 }
 
+// The same rules with the board size fixed at compile time (the bucketed
+// kernels instantiate it for the BASELINE board, 6x4, and the test boards):
+// every mask, shift and the column loop fold to constants.  Bit-identical
+// to toot_prim / toot_children (tests: both forms solve to the same
+// fingerprints).
+template <int L, int H>
+struct TootFixed {
+  static constexpr int A = L * H;
+  static constexpr uint64_t full = (1ull << A) - 1;
+  static constexpr uint64_t col0() {
+    uint64_t m = 0;
+    for (int y = 0; y < H; y++) m |= 1ull << (L * y);
+    return m;
+  }
+  static constexpr uint64_t tmask(int i) {
+    const int dxs[4] = {1, 0, 1, 1}, dys[4] = {0, 1, 1, -1};
+    uint64_t m = 0;
+    for (int x = 0; x < L; x++)
+      for (int y = 0; y < H; y++) {
+        const int ex = x + 3 * dxs[i], ey = y + 3 * dys[i];
+        if (ex >= 0 && ex < L && ey >= 0 && ey < H) m |= 1ull << (L * y + x);
+      }
+    return m;
+  }
+  static constexpr int tstep(int i) {
+    const int dxs[4] = {1, 0, 1, 1}, dys[4] = {0, 1, 1, -1};
+    return dxs[i] + L * dys[i];
+  }
+  template <int S>
+  static GM_HD uint64_t shr(uint64_t v) {
+    if constexpr (S >= 0) return v >> S;
+    else return v << (-S);
+  }
+  template <int I>
+  static GM_HD int count_dir(uint64_t first, uint64_t mid) {
+    constexpr int s = tstep(I);
+    constexpr uint64_t m = tmask(I);
+    if constexpr (m == 0) return 0;
+    else return popc64(m & first & shr<s>(mid) & shr<2 * s>(mid) & shr<3 * s>(first));
+  }
+  static GM_HD int count(uint64_t first, uint64_t mid) {
+    return count_dir<0>(first, mid) + count_dir<1>(first, mid) + count_dir<2>(first, mid) + count_dir<3>(first, mid);
+  }
+  static GM_HD int prim(const Desc&, uint64_t k) {
+    const uint64_t t = k & full, o = (k >> A) & full;
+    const int toot = count(t, o), otto = count(o, t);
+    const bool p1 = (k >> (2 * A + 12)) & 1;
+    if (toot == otto) return ((t | o) == full) ? TIE : UNDECIDED;
+    return ((toot > otto) != p1) ? LOSS : WIN;
+  }
+  template <class F>
+  static GM_HD int children(const Desc&, uint64_t k, F&& emit) {
+    const uint64_t occ = (k | (k >> A)) & full;
+    const int p1 = (int)((k >> (2 * A + 12)) & 1);
+    const int hb = 2 * A + (p1 ? 0 : 6);
+    const bool hasT = ((k >> hb) & 7) != 0, hasO = ((k >> (hb + 3)) & 7) != 0;
+    constexpr uint64_t turn = 1ull << (2 * A + 12);
+    const uint64_t kT = (k - (1ull << hb)) ^ turn, kO = (k - (1ull << (hb + 3))) ^ turn;
+    int n = 0;
+#pragma unroll
+    for (int x = 0; x < L; x++) {
+      if ((occ >> (L * (H - 1) + x)) & 1) continue;  // column full
+      const uint64_t blank = ~(occ >> x) & col0();
+      const uint64_t cell = (blank & (~blank + 1)) << x;
+      if (hasT) { emit(kT ^ cell, 1); n++; }
+      if (hasO) { emit(kO ^ (cell << A), 1); n++; }
+    }
+    return n;
+  }
+  static GM_HD int level(const Desc&, uint64_t k) { return popc64((k | (k >> A)) & full); }
+};
+
 // ---------------------------------------------------------------------------
 // Othello (othello_bit_new.py), square boards.  key bits:
 //   [0,A) WHITE plane, [A,2A) BLACK plane (board_get :251-257)
@@ -399,6 +471,16 @@ template <> struct Game<K_TOOT> {
   template <class F> static GM_HD int children(const Desc& d, uint64_t k, F&& f) { return toot_children(d, k, f); }
   static GM_HD int level(const Desc& d, uint64_t k) { return toot_level(d, k); }
 };
+// compile-time toot boards (kernel instantiation ids, not descriptor kinds)
+constexpr int K_TOOT_6x4 = 64, K_TOOT_5x4 = 54, K_TOOT_4x4 = 44;
+template <> struct Game<K_TOOT_6x4> : TootFixed<6, 4> { static constexpr bool kFixed = true; };
+template <> struct Game<K_TOOT_5x4> : TootFixed<5, 4> { static constexpr bool kFixed = true; };
+template <> struct Game<K_TOOT_4x4> : TootFixed<4, 4> { static constexpr bool kFixed = true; };
+// the instantiation id for a descriptor: a fixed toot board where one exists
+GM_HD int fixed_kind(const Desc& d) {
+  if (d.kind == K_TOOT && d.H == 4 && d.L >= 4 && d.L <= 6) return d.L * 10 + 4;
+  return d.kind;
+}
 template <> struct Game<K_OTHELLO> {
   static GM_HD int prim(const Desc& d, uint64_t k) { return oth_prim(d, k); }
   template <class F> static GM_HD int children(const Desc& d, uint64_t k, F&& f) { return oth_children(d, k, f); }

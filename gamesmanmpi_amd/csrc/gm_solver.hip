@@ -43,6 +43,7 @@
 #include <string>
 #include <vector>
 #include <memory>
+#include <type_traits>
 #include <map>
 #include <mutex>
 
@@ -943,7 +944,8 @@ struct gm_solver {
   // BUCKETED (gm_bucketed.h): level store, words, in-edges, partition scratch
   u64* bkK = nullptr;
   uint32_t* bkW = nullptr;
-  uint32_t *REp = nullptr, *REc = nullptr;
+  uint32_t* REp = nullptr;
+  uint16_t* REc = nullptr;  // child index inside its bucket (< kBkMaxUnique)
   u64* S1k = nullptr;
   uint32_t* S1p = nullptr;
   u64* S2k = nullptr;
@@ -1507,9 +1509,9 @@ static BkScratch bk_scratch(int T) {
   size_t o = r(devstate_bytes(T));
   x.lv = o; o += r(sizeof(BkLevel) * (size_t)T);
   x.pbase = o; o += r((size_t)T * (kBkC + 1) * 4);
-  x.bh = o; o += r((size_t)kBkBlocks * kBkC * 4);
-  x.ph = o; o += r((size_t)kBkBlocks * kBkC * 4);
-  x.boff = o; o += r((size_t)kBkBlocks * kBkC * 4);
+  x.bh = o; o += r((size_t)kBkExpandBlocks * kBkC * 4);
+  x.ph = o; o += r((size_t)kBkExpandBlocks * kBkC * 4);
+  x.boff = o; o += r((size_t)kBkExpandBlocks * kBkC * 4);
   x.tot = o; o += r(2 * kBkC * 4);
   x.cbase = o; o += r((kBkC + 1) * 4);
   const size_t NBmax = (size_t)kBkC << kBkMaxFineBits;
@@ -1552,7 +1554,7 @@ int gm_plan(int game, uint64_t positions, uint32_t flags, uint64_t max_table_byt
     out->mode = GM_MODE_BUCKETED;
     out->level_capacity = P;
     out->table_slots = E;
-    out->table_bytes = 4 * P + 8 * E + 24 * Em;
+    out->table_bytes = 4 * P + 6 * E + 24 * Em;  // words, in-edges (u32 parent + u16 child), staging
     out->scratch_bytes = bk_scratch(d->max_levels).end;
     return 0;
   }
@@ -1679,7 +1681,7 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
     if (!bk_ok(d)) return fail(GM_EINVAL, "bucketed levels need every move to advance one level");
     if (!buf->levels || buf->level_capacity < 2) return fail(GM_EINVAL, "null level store");
     if (buf->scratch_bytes < bk_scratch(d->max_levels).end) return fail(GM_EINVAL, "scratch too small (use gm_plan)");
-    const u64 fixed = 4 * buf->level_capacity + 8 * buf->table_slots;
+    const u64 fixed = 4 * buf->level_capacity + 6 * buf->table_slots;
     if (buf->table_bytes < fixed + 24 * 1024ull) return fail(GM_EINVAL, "bucketed table too small (use gm_plan)");
   } else if (buf->mode == GM_MODE_HASHED) {
     if (world < 1 || rank < 0 || rank >= world) return fail(GM_EINVAL, "bad shard %d/%d", rank, world);
@@ -1829,14 +1831,14 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
     char* t = (char*)buf->table;
     s->Pcap = buf->level_capacity;
     s->Ecap = buf->table_slots;
-    s->Emax = std::min<u64>((buf->table_bytes - 4 * s->Pcap - 8 * s->Ecap) / 24, 0xFFFFFFF0ull);
+    s->Emax = std::min<u64>((buf->table_bytes - 4 * s->Pcap - 6 * s->Ecap) / 24, 0xFFFFFFF0ull);
     s->bkK = (u64*)buf->levels;
     s->bkW = (uint32_t*)t;
     t += (4 * s->Pcap + 7) & ~7ull;
     s->REp = (uint32_t*)t;
     t += 4 * s->Ecap;
-    s->REc = (uint32_t*)t;
-    t += (4 * s->Ecap + 7) & ~7ull;
+    s->REc = (uint16_t*)t;
+    t += (2 * s->Ecap + 7) & ~7ull;
     s->S1k = (u64*)t;
     t += 8 * s->Emax;
     s->S2k = (u64*)t;
@@ -2894,18 +2896,32 @@ static bool bk_ranges(u64 n, uint32_t* pshift, uint32_t* fb) {
   *fb = std::min<uint32_t>(*pshift, (uint32_t)kBkRangeBits);
   return *pshift - *fb <= (uint32_t)kBkMaxFineBits;
 }
-#define BK_KIND_LAUNCH(KERNEL, GRID, BLOCK, S, ...)                                                          \
-  switch ((S)->d.kind) {                                                                                     \
-    case K_TTT: hipLaunchKernelGGL(KERNEL<K_TTT>, dim3(GRID), dim3(BLOCK), 0, (S)->stream, __VA_ARGS__); break;   \
-    case K_TOOT: hipLaunchKernelGGL(KERNEL<K_TOOT>, dim3(GRID), dim3(BLOCK), 0, (S)->stream, __VA_ARGS__); break; \
-    default: hipLaunchKernelGGL(KERNEL<K_OTHELLO>, dim3(GRID), dim3(BLOCK), 0, (S)->stream, __VA_ARGS__); break;  \
+}  // extern "C"
+// the bucketed kernels' instantiation for a descriptor (fixed_kind: the
+// compile-time toot boards where one exists)
+template <class Fn>
+static void bk_dispatch(const Desc& d, Fn&& fn) {
+  switch (fixed_kind(d)) {
+    case K_TTT: fn(std::integral_constant<int, K_TTT>{}); break;
+    case K_TOOT_6x4: fn(std::integral_constant<int, K_TOOT_6x4>{}); break;
+    case K_TOOT_5x4: fn(std::integral_constant<int, K_TOOT_5x4>{}); break;
+    case K_TOOT_4x4: fn(std::integral_constant<int, K_TOOT_4x4>{}); break;
+    case K_TOOT: fn(std::integral_constant<int, K_TOOT>{}); break;
+    default: fn(std::integral_constant<int, K_OTHELLO>{}); break;
   }
+}
+extern "C" {
+#define BK_KIND_LAUNCH(KERNEL, GRID, BLOCK, S, ...)                                                      \
+  bk_dispatch((S)->d, [&](auto kind_) {                                                                  \
+    constexpr int K_ = decltype(kind_)::value;                                                           \
+    hipLaunchKernelGGL(KERNEL<K_>, dim3(GRID), dim3(BLOCK), 0, (S)->stream, __VA_ARGS__);               \
+  })
 
 // parents per expand round for a mean branching avg: the round's children
 // should fill about 3/4 of the 8192-record stage (whole waves, 256..4096)
 static uint32_t bk_ppr(double avg) {
-  const double p = 6144.0 / std::max(avg, 0.25);
-  return (uint32_t)std::min<double>(4096.0, std::max<double>(256.0, std::floor(p / 64.0) * 64.0));
+  const double p = 0.75 * kBkExpandCap / std::max(avg, 0.25);
+  return (uint32_t)std::min<double>(4.0 * kBkExpandThreads, std::max<double>(256.0, std::floor(p / 64.0) * 64.0));
 }
 
 static int solve_bucketed(gm_solver* s, gm_result* out) {
@@ -2991,7 +3007,7 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
                        (unsigned long long)P.n));
     P.eout = 0;
     if (P.n) {
-      const u64 nblk = std::min<u64>(kBkBlocks, (P.n + kBkStreamThreads - 1) / kBkStreamThreads),
+      const u64 nblk = std::min<u64>(kBkExpandBlocks, (P.n + kBkExpandThreads - 1) / kBkExpandThreads),
                 chunk = (P.n + nblk - 1) / nblk;
       const uint32_t NR = (uint32_t)((P.n + (1ull << P.fb) - 1) >> P.fb);
       if (meta_used + NR + 1 > s->meta_cap) return bail(fail(GM_ECORRUPT, "bucket tables exceed the scratch"));
@@ -3016,23 +3032,12 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
         const double avg = (L > 0 && lv[(size_t)L - 1].n) ? std::max(1.0, (double)P.ein / (double)lv[(size_t)L - 1].n) : 4.0;
         const uint32_t ppr = bk_ppr(avg);
         sp = span(true);
-        switch (s->d.kind) {
-          case K_TTT:
-            hipLaunchKernelGGL((k_bk_expand<K_TTT, true>), dim3(nblk), dim3(kBkStreamThreads), 0, st, s->d,
-                               s->bkK + P.lb, P.n, chunk, (const uint32_t*)nullptr, (const uint32_t*)nullptr, ppr,
-                               s->S1k, s->S1p, s->S1f, cap, s->bkgc, P.pshift, P.fb, s->bkgc + kBkC, rfo, s->bkgc + 2 * kBkC, s->st);
-            break;
-          case K_TOOT:
-            hipLaunchKernelGGL((k_bk_expand<K_TOOT, true>), dim3(nblk), dim3(kBkStreamThreads), 0, st, s->d,
-                               s->bkK + P.lb, P.n, chunk, (const uint32_t*)nullptr, (const uint32_t*)nullptr, ppr,
-                               s->S1k, s->S1p, s->S1f, cap, s->bkgc, P.pshift, P.fb, s->bkgc + kBkC, rfo, s->bkgc + 2 * kBkC, s->st);
-            break;
-          default:
-            hipLaunchKernelGGL((k_bk_expand<K_OTHELLO, true>), dim3(nblk), dim3(kBkStreamThreads), 0, st, s->d,
-                               s->bkK + P.lb, P.n, chunk, (const uint32_t*)nullptr, (const uint32_t*)nullptr, ppr,
-                               s->S1k, s->S1p, s->S1f, cap, s->bkgc, P.pshift, P.fb, s->bkgc + kBkC, rfo, s->bkgc + 2 * kBkC, s->st);
-            break;
-        }
+        bk_dispatch(s->d, [&](auto kind_) {
+          constexpr int K_ = decltype(kind_)::value;
+          hipLaunchKernelGGL((k_bk_expand<K_, true>), dim3(nblk), dim3(kBkExpandThreads), 0, st, s->d, s->bkK + P.lb, P.n,
+                             chunk, (const uint32_t*)nullptr, (const uint32_t*)nullptr, ppr, s->S1k, s->S1p, s->S1f, cap,
+                             s->bkgc, P.pshift, P.fb, s->bkgc + kBkC, rfo, s->bkgc + 2 * kBkC, s->st);
+        });
         hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, st, rfo, NR + 1, rfo, s->bktotal + 1);
         if ((rc = span_end(sp))) return bail(rc);
         nfwd += 2;
@@ -3101,16 +3106,13 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
         if (exact) {  // parents per expand round: about a stage (8192 records) of children
           const double avg = (double)E / (double)P.n;
           const uint32_t ppr = bk_ppr(avg);
-#define BK_EXPAND_EXACT(K)                                                                                        \
-  hipLaunchKernelGGL((k_bk_expand<K, false>), dim3(nblk), dim3(kBkStreamThreads), 0, st, s->d, s->bkK + P.lb, P.n, \
-                     chunk, (const uint32_t*)s->boff, (const uint32_t*)s->cbase, ppr, s->S1k, s->S1p, s->S1f, 0u, \
-                     (uint32_t*)nullptr, 0u, 0u, (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr, s->st)
-          switch (s->d.kind) {
-            case K_TTT: BK_EXPAND_EXACT(K_TTT); break;
-            case K_TOOT: BK_EXPAND_EXACT(K_TOOT); break;
-            default: BK_EXPAND_EXACT(K_OTHELLO); break;
-          }
-#undef BK_EXPAND_EXACT
+          bk_dispatch(s->d, [&](auto kind_) {
+            constexpr int K_ = decltype(kind_)::value;
+            hipLaunchKernelGGL((k_bk_expand<K_, false>), dim3(nblk), dim3(kBkExpandThreads), 0, st, s->d, s->bkK + P.lb,
+                               P.n, chunk, (const uint32_t*)s->boff, (const uint32_t*)s->cbase, ppr, s->S1k, s->S1p,
+                               s->S1f, 0u, (uint32_t*)nullptr, 0u, 0u, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                               (uint32_t*)nullptr, s->st);
+          });
           nfwd++;
         }
         // the fine partition writes the parents straight into the level's
