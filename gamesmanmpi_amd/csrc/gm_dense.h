@@ -275,19 +275,38 @@ __device__ __forceinline__ void pull_word(const Desc& d, u64 Wbl, u64* bits, u64
 #undef TD
 }
 
+constexpr uint32_t kXcds = 8;
+// Per-level XCD shares of a live-group list: share x = entries [o[x], o[x+1])
+// (contiguous column ranges of ~equal live count, built at solver creation)
+struct XcdShares {
+  uint32_t o[9];
+};
+
 template <int MAXH>
 __global__ __launch_bounds__(256) void k_dense_pull_words(Desc d, DenseView v, u64* bits, u64 L, u64 root_p,
                                                           const u64* __restrict__ masks,
-                                                          const uint32_t* __restrict__ glist, u64 gwords) {
+                                                          const uint32_t* __restrict__ glist, XcdShares xs) {
   // mask tables (built once on the host at solver creation, gm_solver.hip
   // build_mask_tables): M[0..63] = TS, M[64 (i + 1) + t] = TD[i][t]
   __shared__ u64 M[64 * (MAXH + 1)];
   // one thread per 64-prefix bitmap word of the band, or of the level's
   // live 256-prefix groups (glist, world 1: words of groups without a
-  // non-hole are never read unmasked, so they are not written)
-  const u64 ngroups = glist ? gwords : (v.p_hi - v.p_lo + 63) >> 6;
-  const u64 stride = (u64)gridDim.x * blockDim.x;
-  const u64 g_first = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  // non-hole are never read unmasked, so they are not written).  List
+  // sweeps are XCD-chunked (workgroup b runs on XCD b % 8, the host launches
+  // a multiple of 8): the blocks of one XCD take one share, so the parent
+  // words that neighbouring groups share (heap-3..5 parents 128 B - 128 KB
+  // away) are fetched into one L2 instead of all eight.
+  u64 g_first, ngroups, stride;
+  if (glist) {
+    const uint32_t x = blockIdx.x % kXcds;
+    g_first = (u64)xs.o[x] * 4 + (u64)(blockIdx.x / kXcds) * blockDim.x + threadIdx.x;
+    ngroups = (u64)xs.o[x + 1] * 4;
+    stride = (u64)(gridDim.x / kXcds) * blockDim.x;
+  } else {
+    g_first = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    ngroups = (v.p_hi - v.p_lo + 63) >> 6;
+    stride = (u64)gridDim.x * blockDim.x;
+  }
   // the first item's list entry is loaded before the table fill + barrier
   // (most launches give a thread a single item)
   const uint32_t e_first = (glist && g_first < ngroups) ? glist[g_first >> 2] : 0u;
@@ -310,7 +329,6 @@ __global__ __launch_bounds__(256) void k_dense_pull_words(Desc d, DenseView v, u
 // so the child words that neighbouring prefixes share are fetched into ONE
 // XCD's L2 instead of all eight.  Grids that are not a multiple of 8 blocks
 // fall back to one plain grid-stride range.
-constexpr uint32_t kXcds = 8;
 struct XcdRange {
   u64 first, end, stride;
 };
@@ -474,10 +492,6 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // a level's live-group list split into 8 XCD shares: share x = entries
 // [o[x], o[x + 1]) (blocks b with b % 8 == x sweep it)
-struct XcdShares {
-  uint32_t o[9];
-};
-
 struct WordRow4 {
   __amdgpu_buffer_rsrc_t r;
   __device__ __forceinline__ void init(const uint32_t* base, u64 nwords) {

@@ -1052,14 +1052,21 @@ static void dense_launch_pull_t(gm_solver* s, const DenseView& v, int grid, u64 
   if (POW2 && s->pk == PK_WORDS) {
     const uint32_t* gl = nullptr;
     u64 groups = (v.p_hi - v.p_lo + 63) / 64;
-    if (s->glist && !v.blk) {  // the level's live 256-prefix groups
+    XcdShares xs{};
+    int g;
+    if (s->glist && !v.blk) {  // the level's live 256-prefix groups, one share per XCD
       gl = s->glist + s->goff[L];
-      groups = (s->goff[L + 1] - s->goff[L]) * 4;
-      if (!groups) return;
+      if (s->goff[L + 1] == s->goff[L]) return;
+      uint32_t widest = 0;
+      for (int x = 0; x < 9; x++) xs.o[x] = s->gxcd[(size_t)L * 9 + x];
+      for (int x = 0; x < 8; x++) widest = std::max(widest, xs.o[x + 1] - xs.o[x]);
+      const u64 per = ((u64)widest * 4 + kBlock - 1) / kBlock;  // blocks per XCD
+      g = (int)(kXcds * std::min<u64>(per, (u64)s->grid / kXcds));
+    } else {
+      g = (int)std::min<u64>((groups + kBlock - 1) / kBlock, (u64)s->grid);
     }
-    const int g = (int)std::min<u64>((groups + kBlock - 1) / kBlock, (u64)s->grid);
     hipLaunchKernelGGL((k_dense_pull_words<MAXH>), dim3(g), dim3(kBlock), 0, s->stream, s->d, v, s->bits, L,
-                       root_p, s->masks, gl, groups);
+                       root_p, s->masks, gl, xs);
     return;
   }
   hipLaunchKernelGGL((k_dense_pull<MAXH, POW2>), dim3(grid), dim3(kBlock), 0, s->stream, s->d, v, s->bits, L,
