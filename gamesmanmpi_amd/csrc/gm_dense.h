@@ -1096,27 +1096,33 @@ __device__ __forceinline__ void hex_issue(const Desc& d, const Hex16& Q, u64 q, 
 }
 // Byte arithmetic on the packed 16-B vectors (SWAR), so a lane keeps 4 VGPRs
 // per vector and a byte max costs half a packed instruction: every loaded
-// vector is split once into its even and odd bytes, each byte in a 16-bit
-// lane (u32 & 0x00FF00FF, (u32 >> 8) & 0x00FF00FF), the maxes run as
-// v_pk_max_u16 on the halves, and the parent words are formed in the halves
-// and merged once for the store.
+// vector is split once into its even bytes (v & 0x00FF00FF: the LOW byte of
+// each 16-bit lane) and its odd bytes (v & 0xFF00FF00: left in place, the
+// HIGH byte), the maxes run as v_pk_max_u16 on the halves (a 16-bit max of
+// x << 8 is the byte max of x), and the parent words are formed in place and
+// OR-ed for the store.  One AND per dword and half instead of the shift a
+// low-aligned odd half would cost.
 struct Half2 {
-  u32x4 e, o;  // bytes 2k / 2k+1 of 16, in the low byte of 16-bit lane k
+  u32x4 e, o;  // e: bytes 2k in the low byte of 16-bit lane k; o: bytes 2k+1 in its high byte
 };
 __device__ __forceinline__ Half2 hsplit(u32x4 v) {
   const u32x4 M = {0x00FF00FFu, 0x00FF00FFu, 0x00FF00FFu, 0x00FF00FFu};
-  return Half2{v & M, (v >> 8) & M};
+  return Half2{v & M, v & ~M};
 }
 __device__ __forceinline__ u32x4 hmax(u32x4 a, u32x4 b) {
   typedef uint16_t h16x8 __attribute__((ext_vector_type(8)));
   return __builtin_bit_cast(u32x4, __builtin_elementwise_max(__builtin_bit_cast(h16x8, a), __builtin_bit_cast(h16x8, b)));
 }
 // 16-bit lanes shifted up one lane, lane 0 from the top lane of prev
+// (SH = 16); with SH = 24 the HIGH bytes of v (an odd half) arrive as the
+// LOW bytes of the next lane: byte 2k+1 -> byte 2k+2 (high bytes of the
+// result are v's even bytes, zero in an odd half)
+template <int SH>
 __device__ __forceinline__ u32x4 hshift(u32x4 v, u32x4 prev) {
   u32x4 r;
-  r[0] = __builtin_amdgcn_alignbit(v[0], prev[3], 16);
+  r[0] = __builtin_amdgcn_alignbit(v[0], prev[3], SH);
 #pragma unroll
-  for (int k = 1; k < 4; k++) r[k] = __builtin_amdgcn_alignbit(v[k], v[k - 1], 16);
+  for (int k = 1; k < 4; k++) r[k] = __builtin_amdgcn_alignbit(v[k], v[k - 1], SH);
   return r;
 }
 // 16-bit lanes [0, n) all ones (n clamped to [0, 8])
@@ -1129,10 +1135,14 @@ __device__ __forceinline__ u32x4 hprefix(int n) {
   }
   return m;
 }
-// dense_parent8 in each 16-bit lane (a byte value; never 0x7F: remoteness < 255)
+// dense_parent8 in each 16-bit lane, on the byte at bit B of the lane (B = 0:
+// low byte, B = 8: high byte); never 0x7F: remoteness < 255.  No borrow
+// crosses a lane: 0xFE - m >= 0 for the WIN-only (m <= 0x7F) lanes.
+template <int B>
 __device__ __forceinline__ uint32_t parent8x2(uint32_t m) {
-  const uint32_t L = ((m & 0x00800080u) >> 7) * 0xFFu;  // lanes with a LOSS child
-  return ((~m & 0x007F007Fu) & L) | ((0x00FE00FEu - (m & ~L)) & ~L);
+  constexpr uint32_t top = 0x00800080u << B, low7 = 0x007F007Fu << B, fe = 0x00FE00FEu << B;
+  const uint32_t L = ((m & top) >> (7 + B)) * (0xFFu << B);  // lanes with a LOSS child
+  return ((~m & low7) & L) | ((fe - (m & ~L)) & ~L);
 }
 __device__ __forceinline__ uint32_t bits4_to_bytes(uint32_t b4) {  // 4 bits -> 4 byte masks
   return ((b4 * 0x00204081u) & 0x01010101u) * 0xFFu;
@@ -1143,12 +1153,18 @@ __device__ __forceinline__ void hex_finish(Hex16& Q, const HexLoads<MAXH>& X) {
   if (!valid) return;
   const uint32_t S = Q.S;
   const uint32_t rbits = (uint32_t)(X.bitsw >> ((Q.Lb + X.q) & 63)) & 0xFFFFu;
-  const Half2 A1 = hsplit(__builtin_bit_cast(u32x4, X.A1)), A2 = hsplit(__builtin_bit_cast(u32x4, X.A2));
-  const Half2 P1 = hsplit(__builtin_bit_cast(u32x4, X.P1)), P2 = hsplit(__builtin_bit_cast(u32x4, X.P2));
-  // heap 1: byte e -1 / -2 (P = 0 when the unit starts the digit: no child there)
-  u32x4 me = hshift(A1.o, P1.o), mo = A1.e;
-  me = hmax(me, hshift(A2.e, P2.e));
-  mo = hmax(mo, hshift(A2.o, P2.o));
+  const u32x4 EM = {0x00FF00FFu, 0x00FF00FFu, 0x00FF00FFu, 0x00FF00FFu};
+  const u32x4 a1 = __builtin_bit_cast(u32x4, X.A1);
+  const Half2 A2 = hsplit(__builtin_bit_cast(u32x4, X.A2));
+  const u32x4 a1e = a1 & EM, a1o = a1 & ~EM;
+  const u32x4 p1 = __builtin_bit_cast(u32x4, X.P1), p2 = __builtin_bit_cast(u32x4, X.P2);
+  // heap 1: byte e -1 / -2 (P = 0 when the unit starts the digit: no child
+  // there).  Even outputs (low bytes): -1 = the odd byte below (hshift<24> of
+  // the odd half), -2 = the even byte below; odd outputs (high bytes): -1 =
+  // the even byte of the same lane moved up, -2 = the odd byte below.
+  u32x4 me = hshift<24>(a1o, p1 & ~EM), mo = a1e << 8;
+  me = hmax(me, hshift<16>(A2.e, p2 & EM));
+  mo = hmax(mo, hshift<16>(A2.o, p2 & ~EM));
   // heaps >= 2: never holes under a valid parent
 #pragma unroll
   for (int i = 2; i < MAXH; i++) {
@@ -1158,12 +1174,12 @@ __device__ __forceinline__ void hex_finish(Hex16& Q, const HexLoads<MAXH>& X) {
   }
   // heap 0 -1 / -2 where h0 = S - s - e >= 1 / >= 2, i.e. e <= t1 / e <= t1 - 1
   const int t1 = (int)S - (int)X.s - 1;
-  me = hmax(me, hmax(A1.e & hprefix((t1 + 2) >> 1), A2.e & hprefix((t1 + 1) >> 1)));
-  mo = hmax(mo, hmax(A1.o & hprefix((t1 + 1) >> 1), A2.o & hprefix(t1 >> 1)));
+  me = hmax(me, hmax(a1e & hprefix((t1 + 2) >> 1), A2.e & hprefix((t1 + 1) >> 1)));
+  mo = hmax(mo, hmax(a1o & hprefix((t1 + 1) >> 1), A2.o & hprefix(t1 >> 1)));
   u32x4 o;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    const uint32_t w = S == 0 ? 0xFFFFFFFFu : parent8x2(me[k]) | (parent8x2(mo[k]) << 8);  // DENSE_PRIMITIVE8
+    const uint32_t w = S == 0 ? 0xFFFFFFFFu : parent8x2<0>(me[k]) | parent8x2<8>(mo[k]);  // DENSE_PRIMITIVE8
     o[k] = w | ~bits4_to_bytes((rbits >> (4 * k)) & 0xFu);  // unreached -> W8_UNREACHED
   }
   const uint32_t V = rbits & valid;
