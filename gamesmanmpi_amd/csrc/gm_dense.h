@@ -230,10 +230,47 @@ struct RowGeom {
 // One 64-prefix bitmap word of level L: reach bits = OR of the parents'
 // bits (undo-moves +1/+2 on one heap), masked to the word's non-holes.  q =
 // local prefix of lane-bit 0 (multiple of 64), pg = its global prefix, V0 =
-// extra validity mask (band end), TS/TD = the mask tables in LDS.
+// extra validity mask (band end), TS/TD = the mask tables in LDS.  Split in
+// two: pull_issue loads every parent word the word can need (raw, no
+// combining, so no wait is implied), pull_finish masks and ORs them -- the
+// kernel issues the first item's loads BEFORE it fills the mask tables, so
+// both memory rounds overlap.  Unneeded words are read but masked off; every
+// index stays inside the bitmap (rows L-1 / L-2 plus at most two pstrides,
+// i.e. at most into row L - 1 / L).
 template <int MAXH>
-__device__ __forceinline__ void pull_word(const Desc& d, u64 Wbl, u64* bits, u64 L, u64 root_p, u64 q, u64 pg,
-                                          u64 V0, const u64* TS, const u64* M) {
+struct PullLd {
+  u64 w1, w2;                         // heap 0: same prefix, one / two levels up
+  u64 a1[MAXH], b1[MAXH], a2[MAXH], b2[MAXH];  // heap i: the two words around the +1 / +2 parents
+};
+__device__ __forceinline__ u64 bits64_join(u64 lo, u64 hi, unsigned sh) {
+  return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+}
+template <int MAXH>
+__device__ __forceinline__ void pull_issue(const Desc& d, u64 Wbl, const u64* bits, u64 L, u64 q, PullLd<MAXH>& X) {
+  if (L == 0) return;
+  const u64 p1 = (L - 1) * Wbl + q;
+  X.w1 = bits[p1 >> 6];
+#pragma unroll
+  for (int i = 1; i < MAXH; i++) {
+    if (!((MAXH <= 8) || i < d.nheaps)) continue;
+    const u64 w = (p1 + d.pstride[i]) >> 6;
+    X.a1[i] = bits[w];
+    X.b1[i] = (d.pstride[i] & 63) ? bits[w + 1] : 0ull;
+  }
+  if (L < 2) return;
+  const u64 p2 = (L - 2) * Wbl + q;
+  X.w2 = bits[p2 >> 6];
+#pragma unroll
+  for (int i = 1; i < MAXH; i++) {
+    if (!((MAXH <= 8) || i < d.nheaps)) continue;
+    const u64 w = (p2 + 2 * d.pstride[i]) >> 6;
+    X.a2[i] = bits[w];
+    X.b2[i] = ((2 * d.pstride[i]) & 63) ? bits[w + 1] : 0ull;
+  }
+}
+template <int MAXH>
+__device__ __forceinline__ void pull_finish(const Desc& d, u64 Wbl, u64* bits, u64 L, u64 root_p, u64 q, u64 pg,
+                                            u64 V0, const u64* TS, const u64* M, const PullLd<MAXH>& X) {
 #define TD(i) (M + 64 * ((i) + 1))
   const int S = (int)(d.root_sum - (uint32_t)L);
   const int H0 = (int)d.heap[0];
@@ -251,24 +288,20 @@ __device__ __forceinline__ void pull_word(const Desc& d, u64 Wbl, u64* bits, u64
   u64 reached = 0;
   if (L == 0) {
     if (root_p >= pg && root_p < pg + 64) reached = 1ull << (root_p - pg);
-  } else if (V) {
-    const u64 b1 = (L - 1) * Wbl + q, b2 = (L - 2) * Wbl + q;
+  } else {
     // heap 0 +1 / +2: parent at the same prefix, one / two levels up;
     // exists iff h0 + d <= H0  <=>  sj >= lo_s + d
-    reached |= bits[b1 >> 6] & ~mask_le(TS, lo_s);
-    if (L >= 2) reached |= bits[b2 >> 6] & ~mask_le(TS, lo_s + 1);
+    reached |= X.w1 & ~mask_le(TS, lo_s);
+    if (L >= 2) reached |= X.w2 & ~mask_le(TS, lo_s + 1);
 #pragma unroll
     for (int i = 1; i < MAXH; i++) {
       const bool live = (MAXH <= 8) || i < d.nheaps;
       if (!live) continue;
       // heap i +1 / +2: exists iff dg + dj <= H_i - d
       const int Hi = (int)d.heap[i];
-      const u64 m1 = mask_le(TD(i), Hi - 1 - dg[i]);
-      if (m1) reached |= bits64_at(bits, b1 + d.pstride[i]) & m1;
-      if (L >= 2) {
-        const u64 m2 = mask_le(TD(i), Hi - 2 - dg[i]);
-        if (m2) reached |= bits64_at(bits, b2 + 2 * d.pstride[i]) & m2;
-      }
+      reached |= bits64_join(X.a1[i], X.b1[i], (unsigned)(d.pstride[i] & 63)) & mask_le(TD(i), Hi - 1 - dg[i]);
+      if (L >= 2)
+        reached |= bits64_join(X.a2[i], X.b2[i], (unsigned)((2 * d.pstride[i]) & 63)) & mask_le(TD(i), Hi - 2 - dg[i]);
     }
   }
   bits[(L * Wbl + q) >> 6] = reached & V;
@@ -307,20 +340,34 @@ __global__ __launch_bounds__(256) void k_dense_pull_words(Desc d, DenseView v, u
     ngroups = (v.p_hi - v.p_lo + 63) >> 6;
     stride = (u64)gridDim.x * blockDim.x;
   }
-  // the first item's list entry is loaded before the table fill + barrier
-  // (most launches give a thread a single item)
-  const uint32_t e_first = (glist && g_first < ngroups) ? glist[g_first >> 2] : 0u;
+  // the first item (most launches give a thread a single one): its list
+  // entry, then its parent words, are loaded before the table fill and
+  // barrier, so the parent loads and the table loads share one memory round
+  auto item = [&](u64 gi, uint32_t e, uint64_t* q, u64* pg, u64* V0) -> bool {
+    const u64 qi = glist ? ((u64)e << 8) + ((gi & 3) << 6) : v.p_lo + (gi << 6);  // sweep index of lane-bit 0
+    bool run;
+    *pg = dense_sweep(v, qi, q, &run);  // global prefix of lane-bit 0; q = its local prefix
+    *V0 = qi + 64 > v.p_hi ? (1ull << (v.p_hi - qi)) - 1 : ~0ull;
+    return run;  // false: another launch's slice, or a halo
+  };
+  const bool has1 = g_first < ngroups;
+  uint64_t q1 = 0;
+  u64 pg1 = 0, V01 = 0;
+  bool run1 = false;
+  PullLd<MAXH> X;
+  if (has1) {
+    run1 = item(g_first, glist ? glist[g_first >> 2] : 0u, &q1, &pg1, &V01);
+    if (run1) pull_issue<MAXH>(d, v.Wbl, bits, L, q1, X);
+  }
   for (int k = threadIdx.x; k < 64 * (MAXH + 1); k += blockDim.x) M[k] = masks[k];
   __syncthreads();
-  for (u64 gi = g_first; gi < ngroups; gi += stride) {
-    const u64 qi = glist ? ((u64)(gi == g_first ? e_first : glist[gi >> 2]) << 8) + ((gi & 3) << 6)
-                         : v.p_lo + (gi << 6);  // sweep index of lane-bit 0
-    uint64_t q;  // local prefix of lane-bit 0 (multiple of 64)
-    bool run;
-    const u64 pg = dense_sweep(v, qi, &q, &run);  // global prefix of lane-bit 0
-    if (!run) continue;  // another launch's slice, or a halo
-    const u64 V0 = qi + 64 > v.p_hi ? (1ull << (v.p_hi - qi)) - 1 : ~0ull;
-    pull_word<MAXH>(d, v.Wbl, bits, L, root_p, q, pg, V0, M, M);
+  if (run1) pull_finish<MAXH>(d, v.Wbl, bits, L, root_p, q1, pg1, V01, M, M, X);
+  for (u64 gi = g_first + stride; gi < ngroups; gi += stride) {
+    uint64_t q;
+    u64 pg, V0;
+    if (!item(gi, glist ? glist[gi >> 2] : 0u, &q, &pg, &V0)) continue;
+    pull_issue<MAXH>(d, v.Wbl, bits, L, q, X);
+    pull_finish<MAXH>(d, v.Wbl, bits, L, root_p, q, pg, V0, M, M, X);
   }
 }
 

@@ -10,9 +10,10 @@ but each level moves its traffic in two bulk all-to-all(v) exchanges:
                            (gm_ks_expand), deduplicated, bucketed by owner,
                            all-to-all, inserted by their owners (gm_ks_insert)
   backward (L = T-1 .. 0)  own level-L positions -> children in gen_moves
-                           order (gm_ks_counts / gm_ks_children), queried at
-                           their owners (gm_solver_query), words sent back,
-                           reduced (gm_ks_reduce)
+                           order (gm_ks_counts / gm_ks_children), distinct
+                           children queried at their owners
+                           (gm_solver_query), words sent back, expanded to
+                           one per edge, reduced (gm_ks_reduce)
 
 `keyed_solve` is written once over the shards LOCAL to this process and an
 exchange object:
@@ -253,18 +254,30 @@ def keyed_solve(shards, exchange):
             for g, sh in enumerate(shards):
                 offsets, keys, owners = sh.children(L)
                 widths[g][L] = offsets.numel() - 1
+                # one query per distinct child (a position reached from
+                # several parents of this shard is asked for once)
+                inv = None
+                if keys.numel():
+                    keys, inv = torch.unique(keys, return_inverse=True)
+                    own = torch.empty(keys.numel(), dtype=owners.dtype,
+                                      device=owners.device)
+                    own[inv] = owners
+                    owners = own
                 lists, perm = _bucket(torch, keys, owners, world)
                 queries.append(lists)
-                state.append((offsets, perm, keys.numel()))
+                state.append((offsets, perm, keys.numel(), inv))
             replies = []
             for sh, lists in zip(shards, exchange.all_to_all(queries)):
                 sizes = [int(t.numel()) for t in lists]
                 replies.append(list(torch.split(sh.lookup(torch.cat(lists)),
                                                 sizes)))
             answers = exchange.all_to_all(replies)
-            for sh, lists, (offsets, perm, n) in zip(shards, answers, state):
+            for sh, lists, (offsets, perm, n, inv) in zip(shards, answers,
+                                                          state):
                 words = torch.empty(n, dtype=torch.int32, device=sh.device)
                 words[perm] = torch.cat(lists)
+                if inv is not None:
+                    words = words[inv]  # back to one word per edge
                 sh.reduce(L, offsets, words)
         t2 = time.perf_counter()
         res = [sh.end() for sh in shards]
