@@ -1152,10 +1152,16 @@ __device__ __forceinline__ void hex_issue(const Desc& d, const Hex16& Q, u64 q, 
 struct Half2 {
   u32x4 e, o;  // e: bytes 2k in the low byte of 16-bit lane k; o: bytes 2k+1 in its high byte
 };
-__device__ __forceinline__ Half2 hsplit(u32x4 v) {
-  const u32x4 M = {0x00FF00FFu, 0x00FF00FFu, 0x00FF00FFu, 0x00FF00FFu};
-  return Half2{v & M, v & ~M};
+// The byte masks reach the ANDs through an empty asm: with a visible
+// constant the compiler rewrites (v & 0x00FF00FF) feeding 16-bit maxes as
+// per-16-bit-lane ops (v_and + v_and_sdwa + v_perm: three VALU per dword
+// instead of one v_and_b32 with an SGPR operand)
+__device__ __forceinline__ uint32_t opaque_u32(uint32_t x) {
+  asm("" : "+s"(x));
+  return x;
 }
+__device__ __forceinline__ u32x4 splat4(uint32_t m) { return u32x4{m, m, m, m}; }
+__device__ __forceinline__ Half2 hsplit(u32x4 v, u32x4 EM, u32x4 OM) { return Half2{v & EM, v & OM}; }
 __device__ __forceinline__ u32x4 hmax(u32x4 a, u32x4 b) {
   typedef uint16_t h16x8 __attribute__((ext_vector_type(8)));
   return __builtin_bit_cast(u32x4, __builtin_elementwise_max(__builtin_bit_cast(h16x8, a), __builtin_bit_cast(h16x8, b)));
@@ -1200,22 +1206,23 @@ __device__ __forceinline__ void hex_finish(Hex16& Q, const HexLoads<MAXH>& X) {
   if (!valid) return;
   const uint32_t S = Q.S;
   const uint32_t rbits = (uint32_t)(X.bitsw >> ((Q.Lb + X.q) & 63)) & 0xFFFFu;
-  const u32x4 EM = {0x00FF00FFu, 0x00FF00FFu, 0x00FF00FFu, 0x00FF00FFu};
+  const u32x4 EM = splat4(opaque_u32(0x00FF00FFu)), OM = splat4(opaque_u32(0xFF00FF00u));
   const u32x4 a1 = __builtin_bit_cast(u32x4, X.A1);
-  const Half2 A2 = hsplit(__builtin_bit_cast(u32x4, X.A2));
-  const u32x4 a1e = a1 & EM, a1o = a1 & ~EM;
+  const Half2 A2 = hsplit(__builtin_bit_cast(u32x4, X.A2), EM, OM);
+  const u32x4 a1e = a1 & EM, a1o = a1 & OM;
   const u32x4 p1 = __builtin_bit_cast(u32x4, X.P1), p2 = __builtin_bit_cast(u32x4, X.P2);
   // heap 1: byte e -1 / -2 (P = 0 when the unit starts the digit: no child
   // there).  Even outputs (low bytes): -1 = the odd byte below (hshift<24> of
   // the odd half), -2 = the even byte below; odd outputs (high bytes): -1 =
   // the even byte of the same lane moved up, -2 = the odd byte below.
-  u32x4 me = hshift<24>(a1o, p1 & ~EM), mo = a1e << 8;
+  u32x4 me = hshift<24>(a1o, p1 & OM), mo = a1e << 8;
   me = hmax(me, hshift<16>(A2.e, p2 & EM));
-  mo = hmax(mo, hshift<16>(A2.o, p2 & ~EM));
+  mo = hmax(mo, hshift<16>(A2.o, p2 & OM));
   // heaps >= 2: never holes under a valid parent
 #pragma unroll
   for (int i = 2; i < MAXH; i++) {
-    const Half2 c1 = hsplit(__builtin_bit_cast(u32x4, X.C1[i])), c2 = hsplit(__builtin_bit_cast(u32x4, X.C2[i]));
+    const Half2 c1 = hsplit(__builtin_bit_cast(u32x4, X.C1[i]), EM, OM),
+                c2 = hsplit(__builtin_bit_cast(u32x4, X.C2[i]), EM, OM);
     me = hmax(me, hmax(c1.e, c2.e));
     mo = hmax(mo, hmax(c1.o, c2.o));
   }
