@@ -1142,16 +1142,13 @@ __device__ __forceinline__ void hex_issue(const Desc& d, const Hex16& Q, u64 q, 
   }
 }
 // Byte arithmetic on the packed 16-B vectors (SWAR), so a lane keeps 4 VGPRs
-// per vector and a byte max costs half a packed instruction: every loaded
-// vector is split once into its even bytes (v & 0x00FF00FF: the LOW byte of
-// each 16-bit lane) and its odd bytes (v & 0xFF00FF00: left in place, the
-// HIGH byte), the maxes run as v_pk_max_u16 on the halves (a 16-bit max of
-// x << 8 is the byte max of x), and the parent words are formed in place and
-// OR-ed for the store.  One AND per dword and half instead of the shift a
-// low-aligned odd half would cost.
-struct Half2 {
-  u32x4 e, o;  // e: bytes 2k in the low byte of 16-bit lane k; o: bytes 2k+1 in its high byte
-};
+// per vector and a byte max costs half a packed instruction: the even bytes
+// (v & 0x00FF00FF: the LOW byte of each 16-bit lane) and the odd bytes (the
+// HIGH byte, left in place) are reduced with v_pk_max_u16 -- a 16-bit max of
+// x << 8 is the byte max of x, so the odd half needs no shift, and since the
+// high byte of a 16-bit max does not depend on the low bytes, its operands
+// need no mask either (one AND at the end) -- and the parent words are formed
+// in place and OR-ed for the store.
 // The byte masks reach the ANDs through an empty asm: with a visible
 // constant the compiler rewrites (v & 0x00FF00FF) feeding 16-bit maxes as
 // per-16-bit-lane ops (v_and + v_and_sdwa + v_perm: three VALU per dword
@@ -1161,7 +1158,7 @@ __device__ __forceinline__ uint32_t opaque_u32(uint32_t x) {
   return x;
 }
 __device__ __forceinline__ u32x4 splat4(uint32_t m) { return u32x4{m, m, m, m}; }
-__device__ __forceinline__ Half2 hsplit(u32x4 v, u32x4 EM, u32x4 OM) { return Half2{v & EM, v & OM}; }
+
 __device__ __forceinline__ u32x4 hmax(u32x4 a, u32x4 b) {
   typedef uint16_t h16x8 __attribute__((ext_vector_type(8)));
   return __builtin_bit_cast(u32x4, __builtin_elementwise_max(__builtin_bit_cast(h16x8, a), __builtin_bit_cast(h16x8, b)));
@@ -1207,29 +1204,31 @@ __device__ __forceinline__ void hex_finish(Hex16& Q, const HexLoads<MAXH>& X) {
   const uint32_t S = Q.S;
   const uint32_t rbits = (uint32_t)(X.bitsw >> ((Q.Lb + X.q) & 63)) & 0xFFFFu;
   const u32x4 EM = splat4(opaque_u32(0x00FF00FFu)), OM = splat4(opaque_u32(0xFF00FF00u));
-  const u32x4 a1 = __builtin_bit_cast(u32x4, X.A1);
-  const Half2 A2 = hsplit(__builtin_bit_cast(u32x4, X.A2), EM, OM);
-  const u32x4 a1e = a1 & EM, a1o = a1 & OM;
+  const u32x4 a1 = __builtin_bit_cast(u32x4, X.A1), a2 = __builtin_bit_cast(u32x4, X.A2);
+  const u32x4 a1e = a1 & EM, a1o = a1 & OM, a2e = a2 & EM;
   const u32x4 p1 = __builtin_bit_cast(u32x4, X.P1), p2 = __builtin_bit_cast(u32x4, X.P2);
+  // Odd outputs (high bytes) accumulate RAW 16-bit maxes: the high byte of
+  // a 16-bit max is the max of the high bytes whatever the low bytes hold,
+  // so their operands need no mask and the sum is masked once at the end.
+  // Even outputs (low bytes) need every operand's high byte cleared.
   // heap 1: byte e -1 / -2 (P = 0 when the unit starts the digit: no child
-  // there).  Even outputs (low bytes): -1 = the odd byte below (hshift<24> of
-  // the odd half), -2 = the even byte below; odd outputs (high bytes): -1 =
-  // the even byte of the same lane moved up, -2 = the odd byte below.
+  // there).  Even outputs: -1 = the odd byte below (hshift<24> of the odd
+  // half), -2 = the even byte below; odd outputs: -1 = the even byte of the
+  // same lane moved up, -2 = the odd byte below (hshift<16>, raw).
   u32x4 me = hshift<24>(a1o, p1 & OM), mo = a1e << 8;
-  me = hmax(me, hshift<16>(A2.e, p2 & EM));
-  mo = hmax(mo, hshift<16>(A2.o, p2 & OM));
+  me = hmax(me, hshift<16>(a2e, p2 & EM));
+  mo = hmax(mo, hshift<16>(a2, p2));
   // heaps >= 2: never holes under a valid parent
 #pragma unroll
   for (int i = 2; i < MAXH; i++) {
-    const Half2 c1 = hsplit(__builtin_bit_cast(u32x4, X.C1[i]), EM, OM),
-                c2 = hsplit(__builtin_bit_cast(u32x4, X.C2[i]), EM, OM);
-    me = hmax(me, hmax(c1.e, c2.e));
-    mo = hmax(mo, hmax(c1.o, c2.o));
+    const u32x4 c1 = __builtin_bit_cast(u32x4, X.C1[i]), c2 = __builtin_bit_cast(u32x4, X.C2[i]);
+    me = hmax(me, hmax(c1 & EM, c2 & EM));
+    mo = hmax(mo, hmax(c1, c2));
   }
   // heap 0 -1 / -2 where h0 = S - s - e >= 1 / >= 2, i.e. e <= t1 / e <= t1 - 1
   const int t1 = (int)S - (int)X.s - 1;
-  me = hmax(me, hmax(a1e & hprefix((t1 + 2) >> 1), A2.e & hprefix((t1 + 1) >> 1)));
-  mo = hmax(mo, hmax(a1o & hprefix((t1 + 1) >> 1), A2.o & hprefix(t1 >> 1)));
+  me = hmax(me, hmax(a1e & hprefix((t1 + 2) >> 1), a2e & hprefix((t1 + 1) >> 1)));
+  mo = hmax(mo, hmax(a1 & hprefix((t1 + 1) >> 1), a2 & hprefix(t1 >> 1))) & OM;
   u32x4 o;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
