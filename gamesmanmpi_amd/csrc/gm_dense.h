@@ -1253,10 +1253,18 @@ __device__ __forceinline__ void hex_finish(Hex16& Q, const HexLoads<MAXH>& X) {
 // flight per lane keeps 91 VGPRs (5 waves per SIMD) and measured 3.90 ms per
 // 2^30 backward pass against 4.25 ms for the two-stage pipeline at 166 VGPRs
 // (3 waves per SIMD).
+// six resident 256-thread blocks per CU (6 waves per SIMD: the compiler keeps
+// the kernel at <= 80 VGPRs, no spills): backward 3.17 -> 3.06 ms against the
+// unconstrained 84 VGPRs / 5 waves; prefetching the next unit's list entries
+// measured no gain (tools/ab_dense.sh)
+#ifndef GM_R16_MINB
+#define GM_R16_MINB 6
+#endif
 template <int MAXH>
-__global__ __launch_bounds__(256) void k_dense_resolve16p(Desc d, DenseView v, uint8_t* words, const u64* bits, u64 L,
-                                                          DevState* st, const uint32_t* __restrict__ glist,
-                                                          XcdShares xs, BlockCount* bc) {
+__global__ __launch_bounds__(256, GM_R16_MINB) void k_dense_resolve16p(Desc d, DenseView v, uint8_t* words,
+                                                                       const u64* bits, u64 L, DevState* st,
+                                                                       const uint32_t* __restrict__ glist,
+                                                                       XcdShares xs, BlockCount* bc) {
   Hex16 Q;
   hex_init(Q, d, words, bits, L, v.Wl, v.Wbl);
   const uint32_t lane = __lane_id();
@@ -1264,20 +1272,20 @@ __global__ __launch_bounds__(256) void k_dense_resolve16p(Desc d, DenseView v, u
   const u64 first = (u64)xs.o[x] * 16 + (u64)(blockIdx.x / kXcds) * blockDim.x + threadIdx.x;
   const u64 end = (u64)xs.o[x + 1] * 16, stride = (u64)(gridDim.x / kXcds) * blockDim.x;
   const uint32_t last = xs.o[8] - 1;  // last entry of the level's list (the host launches only non-empty lists)
-  auto issue = [&](u64 iu, HexLoads<MAXH>& X) {
-    const bool on = iu < end;
+  // the wave's four list entries (scalar loads), lane's group = entry lane >> 4
+  auto fetch = [&](u64 iu) -> uint32_t {
     const uint32_t g0 = min(__builtin_amdgcn_readfirstlane((uint32_t)((iu - lane) >> 4)), last);
     const uint32_t e0 = glist[g0], e1 = glist[min(g0 + 1, last)], e2 = glist[min(g0 + 2, last)],
                    e3 = glist[min(g0 + 3, last)];
     const uint32_t k = lane >> 4;
-    const uint32_t e = k == 0 ? e0 : k == 1 ? e1 : k == 2 ? e2 : e3;
-    hex_issue<MAXH>(d, Q, ((u64)e << 8) + 16 * (lane & 15), on, X);
+    return k == 0 ? e0 : k == 1 ? e1 : k == 2 ? e2 : e3;
   };
   for (u64 iu = first; iu < end; iu += stride) {
     HexLoads<MAXH> X;
-    issue(iu, X);
+    hex_issue<MAXH>(d, Q, ((u64)fetch(iu) << 8) + 16 * (lane & 15), iu < end, X);
     hex_finish<MAXH>(Q, X);
   }
+
   block_count(bc, (u64)Q.npos, (u64)Q.edges);
   if (Q.S == 0) block_add(&st->prims, (u64)Q.npos);  // one launch per solve
 }

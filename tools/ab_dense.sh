@@ -1,13 +1,26 @@
 #!/bin/bash
-# A/B of two builds on the bench workload: bash tools/ab_dense.sh LIB_B TAG
+# A/B of library variants (GM_LIBPATH) on the bench workload (dense 2^30):
+# bash tools/ab_dense.sh build/ab_x.so ...  -- a warm-up process first, then the
+# default library and each variant twice, interleaved.
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-for lib in gamesmanmpi_amd/libgamesman_hip.so "$1"; do
-  GM_LIBPATH=$PWD/$lib timeout -k 10 120 python3 tools/solve_once.py sum_four_to_one "heaps=31:31:31:31:31:31" dense 3 \
-    > gpurun_out/${2}_$(basename $lib .so).log 2>&1 || { echo "run $lib failed"; tail gpurun_out/${2}_$(basename $lib .so).log; exit 1; }
-  echo "$lib"; grep wall_ms gpurun_out/${2}_$(basename $lib .so).log | python3 -c "
-import json,sys
-for l in sys.stdin:
-    d=json.loads(l); print('  wall %.2f fwd %.2f bwd %.2f' % (d['wall_ms'], d['ms_forward'], d['ms_backward']), d.get('ms_resolve_kernels',''), d.get('checksum',{}).get('checksum',''))"
+run() {
+  local lib=$1
+  if [ "$lib" = default ]; then unset GM_LIBPATH; else export GM_LIBPATH=$PWD/$lib; fi
+  timeout -k 10 120 python3 tools/solve_once.py sum_four_to_one "heaps=31:31:31:31:31:31" dense ${REPS:-4} \
+    > gpurun_out/ab_dense.jsonl 2>&1 || { echo "run $lib failed"; tail -5 gpurun_out/ab_dense.jsonl; exit 1; }
+  python3 -c "
+import json
+out=[]
+for l in open('gpurun_out/ab_dense.jsonl'):
+    if l.startswith('{'):
+        d=json.loads(l)
+        if 'checksum' not in d: out.append('%.2f/%.2f/%.2f' % (d['ms_total'], d['ms_forward'], d['ms_backward']))
+        else: out.append(d['checksum']['checksum'])
+print('$lib:', ' | '.join(out))"
+}
+REPS=1 run default > /dev/null
+for pass in 1 2; do
+  for lib in default "$@"; do run $lib; done
 done
