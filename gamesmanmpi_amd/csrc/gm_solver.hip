@@ -3340,17 +3340,56 @@ int gm_solver_checksum(gm_solver* s, uint64_t out[6]) {
   return 0;
 }
 
+// gm_solve keeps its solver per game id until the next gm_solve of that game
+// or gm_release(game), so gm_query(game, ...) reads the table it left in the
+// caller's buffers (SURVEY §8b's one-shot pair)
+static std::mutex g_solved_mu;
+static std::map<int, gm_solver*> g_solved;
+
 int gm_solve(int game, uint64_t root, int ngpus, const gm_buffers* buf, gm_result* out) {
   const Desc* d = get_game(game);
   if (!d) return fail(GM_EINVAL, "bad game id %d", game);
   if (ngpus != 1) return fail(GM_EINVAL, "gm_solve drives one GPU; run one process per GPU for sharded solves");
   if (root != d->root) return fail(GM_EINVAL, "root must be the game's initial position");
+  (void)gm_release(game);
   gm_solver* s = nullptr;
   int rc = gm_solver_create(game, buf, &s);
   if (rc) return rc;
   rc = gm_solver_solve(s, out);
+  if (rc) {
+    gm_solver_destroy(s);
+    return rc;
+  }
+  std::lock_guard<std::mutex> lk(g_solved_mu);
+  g_solved[game] = s;
+  return 0;
+}
+
+int gm_query(int game, const uint64_t* keys_dev, size_t n, uint32_t* words_dev) {
+  gm_solver* s = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_solved_mu);
+    auto it = g_solved.find(game);
+    if (it != g_solved.end()) s = it->second;
+  }
+  if (!s) return fail(GM_EINVAL, "game %d has no finished gm_solve to query", game);
+  int rc = gm_solver_query(s, keys_dev, (uint64_t)n, words_dev);
+  if (rc) return rc;
+  HIPCHK(hipStreamSynchronize(s->stream));
+  return 0;
+}
+
+int gm_release(int game) {
+  gm_solver* s = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_solved_mu);
+    auto it = g_solved.find(game);
+    if (it == g_solved.end()) return 0;
+    s = it->second;
+    g_solved.erase(it);
+  }
   gm_solver_destroy(s);
-  return rc;
+  return 0;
 }
 
 int gm_owner(int game, const uint64_t* keys_dev, uint64_t n, int world_size, uint32_t* owners_dev, void* stream) {

@@ -324,10 +324,21 @@ int gm_graph_solve(const uint8_t *prim_dev, const uint64_t *offsets_dev,
                    uint32_t *words_dev, void *scratch_dev, void *stream,
                    gm_result *out);
 
-/* One-shot convenience: create + solve + destroy.  ngpus must
- * be 1; multi-GPU runs are driven one process per GPU by the Python host. */
+/* One-shot pair: gm_solve creates a solver on the caller's
+ * buffers and solves from the game's root; the solver is kept per game id
+ * (the buffers must stay valid) until the next gm_solve of that game or
+ * gm_release(game).  ngpus must be 1; multi-GPU runs are driven one process
+ * per GPU by the Python host.  Replaces solver_launcher.py:68-72 (Process
+ * construction + run). */
 int gm_solve(int game, uint64_t root, int ngpus, const gm_buffers *buf,
              gm_result *out);
+/* words_dev[i] = word of keys_dev[i] in the table of the game's last
+ * gm_solve (GM_NO_WORD if unreachable); device pointers, synchronous.
+ * Replaces the resolved/remote CacheDict lookups (src/cache_dict.py:62-79). */
+int gm_query(int game, const uint64_t *keys_dev, size_t n,
+             uint32_t *words_dev);
+/* drop the solver gm_solve kept for `game` (0 if none) */
+int gm_release(int game);
 
 /* md5(str(pos).encode('utf-8')) mod world_size for n device keys
  * (GameState.get_hash, src/game_state.py:22-30). */

@@ -153,3 +153,44 @@ def test_gpu_full_size_synthetic_properties():
     keys = rng.integers(0, 1 << 30, size=1 << 20, dtype=np.uint64)
     w = s.query(keys)
     _sprague_grundy_check(keys, (w & 3).astype(np.uint8), heaps)
+
+
+@pytest.mark.parametrize("name", ["tic_tac_toe_np", "othello_4x4", "sum_fto_6_6_6_6"])
+def test_gpu_one_shot_solve_and_query(name, golden_summary):
+    """SURVEY §8b's one-shot pair: gm_solve(game, root, 1, buffers) then
+    gm_query(game, keys, n, words) on the table it keeps, every golden
+    position's word bit-exact; gm_release drops it and a query then fails."""
+    import ctypes
+    import torch
+    from gamesmanmpi_amd import _lib
+    from gamesmanmpi_amd.games import GameSpec
+    if name not in CASES:
+        pytest.skip("no golden table %s" % name)
+    stem, params = CASES[name]
+    info = golden_summary[name]
+    spec = GameSpec(stem, params)
+    L = _lib.load()
+    plan = _lib.gm_plan_t()
+    _lib.check(L.gm_plan(spec.id, info["positions"], 0, 0, ctypes.byref(plan)))
+    dev = torch.device("cuda")
+    table = torch.empty(plan.table_bytes, dtype=torch.uint8, device=dev)
+    levels = torch.empty(max(1, plan.level_capacity), dtype=torch.int64, device=dev)
+    scratch = torch.empty(plan.scratch_bytes, dtype=torch.uint8, device=dev)
+    b = _lib.gm_buffers()
+    b.table, b.table_slots = table.data_ptr(), plan.table_slots
+    b.levels, b.level_capacity = levels.data_ptr(), plan.level_capacity
+    b.scratch, b.scratch_bytes = scratch.data_ptr(), plan.scratch_bytes
+    b.stream, b.mode, b.table_bytes = torch.cuda.current_stream().cuda_stream, plan.mode, plan.table_bytes
+    r = _lib.gm_result()
+    _lib.check(L.gm_solve(spec.id, spec.root_key, 1, ctypes.byref(b), ctypes.byref(r)))
+    assert (r.positions, r.edges) == (info["positions"], info["edges"])
+    t = load_table(name)
+    keys = spec.encode_batch(t["canon"], t["clen"])
+    kd = torch.from_numpy(np.ascontiguousarray(keys.astype(np.int64))).to(dev)
+    wd = torch.empty(len(keys), dtype=torch.int32, device=dev)
+    _lib.check(L.gm_query(spec.id, kd.data_ptr(), len(keys), wd.data_ptr()))
+    w = wd.cpu().numpy().astype(np.uint32)
+    np.testing.assert_array_equal(w & 3, t["value"])
+    np.testing.assert_array_equal(w >> 2, t["remoteness"])
+    _lib.check(L.gm_release(spec.id))
+    assert L.gm_query(spec.id, kd.data_ptr(), len(keys), wd.data_ptr()) == _lib.GM_EINVAL
