@@ -1137,14 +1137,8 @@ __device__ __forceinline__ void hex_issue(const Desc& d, const Hex16& Q, u64 q, 
 #pragma unroll
   for (int i = 2; i < MAXH; i++) {
     const bool live = (MAXH <= 8) || i < d.nheaps;
-#ifdef GM_DIAG_NEAR  // diagnostic only (wrong words): heaps >= GM_DIAG_NEAR read the own prefix's lines
-    const u64 off = i >= GM_DIAG_NEAR ? 0 : d.pstride[i];
-    X.C1[i] = Q.n1.at(q - off, any && live && h[i] >= 1);
-    X.C2[i] = Q.n2.at(q - 2 * off, any && live && h[i] >= 2);
-#else
     X.C1[i] = Q.n1.at(q - d.pstride[i], any && live && h[i] >= 1);
     X.C2[i] = Q.n2.at(q - 2 * d.pstride[i], any && live && h[i] >= 2);
-#endif
   }
 }
 // Byte arithmetic on the packed 16-B vectors (SWAR), so a lane keeps 4 VGPRs
