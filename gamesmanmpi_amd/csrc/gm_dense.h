@@ -1290,6 +1290,77 @@ __global__ __launch_bounds__(256, GM_R16_MINB) void k_dense_resolve16p(Desc d, D
   if (Q.S == 0) block_add(&st->prims, (u64)Q.npos);  // one launch per solve
 }
 
+// ---------------------------------------------------------------------------
+// Tail runs (world 1, live-group lists): the narrow ends of the tier sequence
+// hold a few hundred live groups per level, where a launch costs its fixed
+// ~4-6 us (dispatch, list entry, parent / child loads, store drain) for well
+// under a microsecond of work.  One 1024-thread workgroup walks a run of such
+// levels instead, a barrier between levels: its stores reach its own later
+// loads through the CU's L1 / its XCD's L2 (workgroup-scope release/acquire
+// of __syncthreads), so a level costs about one L2 round trip.  Same per-word
+// (pull_issue / pull_finish) and per-unit (hex_issue / hex_finish) bodies as
+// the per-level kernels.
+// ---------------------------------------------------------------------------
+constexpr int kTailMax = 40;       // levels per run
+constexpr int kTailThreads = 1024;
+constexpr uint64_t kTailPullGroups = 512;     // two passes of 1024 bitmap words
+constexpr uint64_t kTailResolveGroups = 128;  // two passes of 1024 sixteen-prefix units
+struct TailRun {
+  uint32_t n;                      // levels in the run
+  uint32_t L[kTailMax];            // the levels, in solve order
+  uint32_t off[kTailMax];          // first list entry of the level (relative to glist)
+  uint32_t cnt[kTailMax];          // live groups of the level
+  u64 phi[kTailMax];               // band end of the level (dense_band p_hi)
+};
+template <int MAXH>
+__global__ __launch_bounds__(kTailThreads) void k_dense_pull_tail(Desc d, DenseView v, u64* bits, u64 root_p,
+                                                                  const u64* __restrict__ masks,
+                                                                  const uint32_t* __restrict__ glist, TailRun R) {
+  __shared__ u64 M[64 * (MAXH + 1)];
+  for (int k = threadIdx.x; k < 64 * (MAXH + 1); k += blockDim.x) M[k] = masks[k];
+  __syncthreads();
+  for (uint32_t i = 0; i < R.n; i++) {
+    const u64 L = R.L[i];
+    const uint32_t nw = R.cnt[i] * 4;  // one thread per 64-prefix bitmap word
+    for (uint32_t w = threadIdx.x; w < nw; w += blockDim.x) {
+      const u64 qi = ((u64)glist[R.off[i] + (w >> 2)] << 8) + ((w & 3) << 6);
+      uint64_t q;
+      bool run;
+      const u64 pg = dense_sweep(v, qi, &q, &run);
+      if (!run) continue;
+      const u64 V0 = qi + 64 > R.phi[i] ? (qi >= R.phi[i] ? 0ull : (1ull << (R.phi[i] - qi)) - 1) : ~0ull;
+      PullLd<MAXH> X;
+      pull_issue<MAXH>(d, v.Wbl, bits, L, q, X);
+      pull_finish<MAXH>(d, v.Wbl, bits, L, root_p, q, pg, V0, M, M, X);
+    }
+    __syncthreads();  // level L's words visible to level L + 1's parents
+  }
+}
+template <int MAXH>
+__global__ __launch_bounds__(kTailThreads) void k_dense_resolve16_tail(Desc d, DenseView v, uint8_t* words,
+                                                                       const u64* bits, DevState* st,
+                                                                       const uint32_t* __restrict__ glist, TailRun R,
+                                                                       BlockCount* bc) {
+  u64 npos = 0, edges = 0, prims = 0;
+  for (uint32_t i = 0; i < R.n; i++) {
+    const u64 L = R.L[i];
+    Hex16 Q;
+    hex_init(Q, d, words, bits, L, v.Wl, v.Wbl);
+    const uint32_t nu = R.cnt[i] * 16;  // sixteen prefixes per unit
+    for (uint32_t u = threadIdx.x; u < nu; u += blockDim.x) {
+      HexLoads<MAXH> X;
+      hex_issue<MAXH>(d, Q, ((u64)glist[R.off[i] + (u >> 4)] << 8) + 16 * (u & 15), true, X);
+      hex_finish<MAXH>(Q, X);
+    }
+    npos += Q.npos;
+    edges += Q.edges;
+    if (Q.S == 0) prims += Q.npos;
+    __syncthreads();  // level L's words visible to levels L - 1 and L - 2
+  }
+  block_count(bc, npos, edges);
+  block_add(&st->prims, prims);
+}
+
 // Column jobs over a 16-bit table (shards): the octet body of
 // k_dense_resolve8p, a wave = two consecutive columns of the jobs'
 // concatenation (lanes 0-31 / 32-63; each half finds its slice by a scalar

@@ -1215,6 +1215,36 @@ static void dense_launch_resolve(gm_solver* s, const DenseView& v, int grid, u64
   else dense_launch_resolve_p<false>(s, v, grid, L);
 }
 
+// Tail runs (world 1, lists; gm_dense.h k_dense_pull_tail /
+// k_dense_resolve16_tail): one workgroup walks the run's levels
+template <int MAXH>
+static void dense_launch_tail_t(gm_solver* s, const TailRun& R, bool pull, u64 root_p) {
+  if (pull) {
+    hipLaunchKernelGGL((k_dense_pull_tail<MAXH>), dim3(1), dim3(kTailThreads), 0, s->stream, s->d, s->view, s->bits,
+                       root_p, s->masks, s->glist, R);
+    return;
+  }
+  if constexpr (MAXH >= 2)
+    hipLaunchKernelGGL((k_dense_resolve16_tail<MAXH>), dim3(1), dim3(kTailThreads), 0, s->stream, s->d, s->view,
+                       (uint8_t*)s->words, s->bits, s->st, s->glist, R, s->bcount);
+  else
+    s->launch_err = true;
+}
+static void dense_launch_tail(gm_solver* s, const TailRun& R, bool pull, u64 root_p) {
+  if (!R.n) return;
+  switch (s->d.nheaps) {
+    case 1: dense_launch_tail_t<1>(s, R, pull, root_p); break;
+    case 2: dense_launch_tail_t<2>(s, R, pull, root_p); break;
+    case 3: dense_launch_tail_t<3>(s, R, pull, root_p); break;
+    case 4: dense_launch_tail_t<4>(s, R, pull, root_p); break;
+    case 5: dense_launch_tail_t<5>(s, R, pull, root_p); break;
+    case 6: dense_launch_tail_t<6>(s, R, pull, root_p); break;
+    case 7: dense_launch_tail_t<7>(s, R, pull, root_p); break;
+    case 8: dense_launch_tail_t<8>(s, R, pull, root_p); break;
+    default: dense_launch_tail_t<16>(s, R, pull, root_p); break;
+  }
+}
+
 static std::string err_text(uint32_t e) {
   std::string s;
   if (e & ERR_TABLE_FULL) s += " table-full";
@@ -2734,11 +2764,39 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
     int rc = check_halo_plan(ss, mode, st);
     if (rc) return rc;
   }
+  // Tail runs (one table, whole solves, live-group lists, 8-bit words): the
+  // levels at both ends whose live groups fit a workgroup in a pass or two
+  // run as one single-workgroup launch each (k_dense_pull_tail,
+  // k_dense_resolve16_tail).  A kernel-timing solve keeps one launch per
+  // level, so per-launch figures (bench roofline, PMC passes of a timed solve)
+  // describe the per-level kernels alone.
+  const bool tails = mode == 0 && !timing && first == 0 && stop == 2 * T && s0->glist && !s0->view.blk &&
+                     s0->pk == PK_WORDS && s0->w8 && d.pow2;
+  int pa = 0, pb = T, ra = T, rb = 0;  // per-level pulls [pa, pb); per-level resolves [rb, ra)
+  TailRun pull_head{}, pull_end{}, res_head{}, res_end{};
+  if (tails) {
+    auto groups = [&](int L) { return s0->goff[(size_t)L + 1] - s0->goff[(size_t)L]; };
+    auto add = [&](TailRun& R, int L) {
+      R.L[R.n] = (uint32_t)L;
+      R.off[R.n] = (uint32_t)s0->goff[(size_t)L];
+      R.cnt[R.n] = (uint32_t)groups(L);
+      R.phi[R.n] = dense_band(d, s0->view, (u64)L).p_hi;
+      R.n++;
+    };
+    while (pa < T && pa < kTailMax && groups(pa) <= kTailPullGroups) add(pull_head, pa++);
+    while (pb > pa && T - pb < kTailMax && groups(pb - 1) <= kTailPullGroups) pb--;
+    for (int L = pb; L < T; L++) add(pull_end, L);
+    while (ra > 0 && T - ra < kTailMax && groups(ra - 1) <= kTailResolveGroups) add(res_head, --ra);
+    while (rb < ra && rb < kTailMax && groups(rb) <= kTailResolveGroups) rb++;
+    for (int L = rb - 1; L >= 0; L--) add(res_end, L);
+  }
   // forward (pull): level 0 .. T-1, each level's bitmap written exactly once.
   // Parents are one or two top values ABOVE: the boundary is the top two
   // slices [b-2, b), whose parents sit in the halo [b, b+2) sent down by the
   // rank above.
+  dense_launch_tail(s0, pull_head, true, root_p);
   for (int L = first; L < T && L < stop; L++) {
+    if (L < pa || L >= pb) continue;  // in a tail run
     if (timing) HIPCHK(hipEventRecord(kx[2 * L], st));
     for (gm_solver* s : ss) {
       const uint32_t B = s->view.B;  // pull: the top two own slices read the upper halo
@@ -2763,6 +2821,7 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
     }
     if (timing) HIPCHK(hipEventRecord(kx[2 * L + 1], st));
   }
+  dense_launch_tail(s0, pull_end, true, root_p);
   HIPCHK(hipGetLastError());
   if (pipe) {  // the backward pass reuses the events: drain the forward exchanges first
     HIPCHK(hipEventRecord(E[0], cs));
@@ -2772,9 +2831,11 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
   // backward (resolve): children are one or two top values BELOW: the
   // boundary is the bottom two slices [a, a+2), whose children sit in the
   // halo [a-2, a) sent up by the rank below.
+  dense_launch_tail(s0, res_head, false, root_p);
   for (int L = T - 1; L >= 0; L--) {
     if (2 * T - 1 - L < first) continue;
     if (2 * T - 1 - L >= stop) break;
+    if (L >= ra || L < rb) continue;  // in a tail run
     if (timing) HIPCHK(hipEventRecord(kr[2 * L], st));
     for (gm_solver* s : ss) {
       const uint32_t B = s->view.B;  // resolve: the bottom two own slices read the lower halo
@@ -2799,6 +2860,7 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
     }
     if (timing) HIPCHK(hipEventRecord(kr[2 * L + 1], st));
   }
+  dense_launch_tail(s0, res_end, false, root_p);
   HIPCHK(hipGetLastError());
   if (pipe) {  // every exchange done before the reduction and the host read-back
     HIPCHK(hipEventRecord(E[0], cs));
