@@ -4,7 +4,7 @@ set -o pipefail
 out=${1:-gpurun_out/pmc_dense}
 export TMPDIR=/tmp
 mkdir -p "$out"
-cmd=(python3 tools/solve_once.py sum_four_to_one "heaps=31:31:31:31:31:31" dense 0)
+cmd=(python3 tools/solve_once.py sum_four_to_one "heaps=31:31:31:31:31:31" dense 0 timing)
 pass() {
   local name=$1; shift
   timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d "$out/$name" -o run -- "${cmd[@]}" > "$out/$name.log" 2>&1 || { echo "pass $name failed"; exit 1; }
