@@ -1876,13 +1876,15 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
     t += 4 * s->Ecap;
     s->REc = (uint16_t*)t;
     t += (2 * s->Ecap + 7) & ~7ull;
+    // staging: [S1k | S1p | S1f] (the count-free expand writes the first 13
+    // Emax bytes of it in its chunked layout, BkChunked) then S2k
     s->S1k = (u64*)t;
-    t += 8 * s->Emax;
-    s->S2k = (u64*)t;
     t += 8 * s->Emax;
     s->S1p = (uint32_t*)t;
     t += 4 * s->Emax;
     s->S1f = (uint8_t*)t;  // (4 Emax bytes of the plan; one is used)
+    t += 4 * s->Emax;
+    s->S2k = (u64*)t;
     const BkScratch x = bk_scratch(d->max_levels);
     char* sc = (char*)buf->scratch;
     s->bkL = (BkLevel*)(sc + x.lv);
@@ -3089,7 +3091,11 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
       // Count-free form first (k_bk_expand<OVER>): children go straight to
       // provisioned partitions; a partition past its share -> the exact
       // form (F0 counts, then k_bk_expand<false>) for this level.
-      const uint32_t cap = (uint32_t)(s->Emax / kBkC);
+      // a partition's provisioned share, whole chunks of the chunked staging
+      uint32_t ck_sh = 14;
+      while (ck_sh > 6 && (s->Emax / kBkC) < (1ull << ck_sh)) ck_sh--;
+      const uint32_t cap = (uint32_t)((s->Emax / kBkC) >> ck_sh << ck_sh);
+      const BkChunked ck{(char*)s->S1k, ck_sh};
       uint32_t incap = 0;
       bool exact = true;
       hipEvent_t* sp = nullptr;
@@ -3105,7 +3111,7 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
           constexpr int K_ = decltype(kind_)::value;
           hipLaunchKernelGGL((k_bk_expand<K_, true>), dim3(nblk), dim3(kBkExpandThreads), 0, st, s->d, s->bkK + P.lb, P.n,
                              chunk, (const uint32_t*)nullptr, (const uint32_t*)nullptr, ppr, s->S1k, s->S1p, s->S1f, cap,
-                             s->bkgc, P.pshift, P.fb, s->bkgc + kBkC, rfo, s->bkgc + 2 * kBkC, s->st);
+                             s->bkgc, P.pshift, P.fb, s->bkgc + kBkC, rfo, s->bkgc + 2 * kBkC, s->st, ck);
         });
         hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, st, rfo, NR + 1, rfo, s->bktotal + 1);
         if ((rc = span_end(sp))) return bail(rc);
@@ -3180,7 +3186,7 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
             hipLaunchKernelGGL((k_bk_expand<K_, false>), dim3(nblk), dim3(kBkExpandThreads), 0, st, s->d, s->bkK + P.lb,
                                P.n, chunk, (const uint32_t*)s->boff, (const uint32_t*)s->cbase, ppr, s->S1k, s->S1p,
                                s->S1f, 0u, (uint32_t*)nullptr, 0u, 0u, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                               (uint32_t*)nullptr, s->st);
+                               (uint32_t*)nullptr, s->st, BkChunked{nullptr, 0});
           });
           nfwd++;
         }
@@ -3188,7 +3194,7 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
         // in-edge parents (REp); F3 adds the child indices (REc)
         hipLaunchKernelGGL(k_bk_fine, dim3(kBkC), dim3(kBkFineThreads), 0, st, (const u64*)s->S1k,
                            (const uint32_t*)s->S1p, (const uint8_t*)s->S1f, (const uint32_t*)s->cbase, 8u - f, F, s->S2k,
-                           s->REp + X.rb, fo, P.pshift, s->bkah + (size_t)L * kBkC * kBkC, incap);
+                           s->REp + X.rb, fo, P.pshift, s->bkah + (size_t)L * kBkC * kBkC, incap, ck);
         // unique keys of bucket b to S1k[fo[b] ..), compacted into the level
         hipLaunchKernelGGL(k_bk_dedup, dim3(gd), dim3(kBkDedupThreads), 0, st, s->S2k, (const uint32_t*)fo, NB, s->S1k,
                            s->ucnt, s->REc + X.rb, s->st);
