@@ -3242,7 +3242,7 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
       const uint32_t* rfo = s->meta + P.rfo_off;
       const uint32_t* pb = s->pbase + (size_t)L * (kBkC + 1);
       uint32_t* Ap = (uint32_t*)s->S1k;
-      constexpr uint32_t K = 4;  // B4 workgroups per range (two resident per CU)
+      constexpr uint32_t K = kBkSplitK;  // B4 workgroups per range
       // B3: one workgroup per children's partition, exact offsets per
       // (partition, parent range) from the counts F2 kept (ah).  (Measured:
       // K = 4 workgroups of 512 threads per partition on device run cursors
