@@ -1077,8 +1077,8 @@ struct WordRow16 {
     r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(uint32_t)nwords, 0x00020000);
   }
   // words [idx, idx + 16), idx 16-aligned; !ok reads zeros with no memory access
-  __device__ __forceinline__ u8x16 at(u64 idx, bool ok) const {
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, ok ? (uint32_t)idx : 0xFFFFFFF0u, 0, 0);
+  __device__ __forceinline__ u8x16 at(uint32_t idx, bool ok) const {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, ok ? idx : 0xFFFFFFF0u, 0, 0);
     return __builtin_bit_cast(u8x16, v);
   }
 };
@@ -1107,14 +1107,16 @@ __device__ __forceinline__ void hex_init(Hex16& Q, const Desc& d, uint8_t* words
   Q.bits = bits;
   Q.Lb = L * Wbl;
 }
+// q: the unit's first prefix in the row (8-bit tables have rows below 2^31
+// words, dense_plan_bits, so prefixes and buffer offsets are 32-bit)
 template <int MAXH>
-__device__ __forceinline__ void hex_issue(const Desc& d, const Hex16& Q, u64 q, bool on, HexLoads<MAXH>& X) {
+__device__ __forceinline__ void hex_issue(const Desc& d, const Hex16& Q, uint32_t q, bool on, HexLoads<MAXH>& X) {
   const uint32_t S = Q.S;
   uint32_t h[MAXH];
   uint32_t s = 0;
 #pragma unroll
   for (int i = 1; i < MAXH; i++) {
-    h[i] = ((MAXH <= 8) || i < d.nheaps) ? (uint32_t)((q >> d.pshift[i]) & (d.base[i] - 1)) : 0u;
+    h[i] = ((MAXH <= 8) || i < d.nheaps) ? (q >> d.pshift[i]) & ((uint32_t)d.base[i] - 1u) : 0u;
     s += h[i];
   }
   // valid e: s + e <= S and S - (s + e) <= H0, i.e. e in [S - s - H0, S - s]
@@ -1137,8 +1139,9 @@ __device__ __forceinline__ void hex_issue(const Desc& d, const Hex16& Q, u64 q, 
 #pragma unroll
   for (int i = 2; i < MAXH; i++) {
     const bool live = (MAXH <= 8) || i < d.nheaps;
-    X.C1[i] = Q.n1.at(q - d.pstride[i], any && live && h[i] >= 1);
-    X.C2[i] = Q.n2.at(q - 2 * d.pstride[i], any && live && h[i] >= 2);
+    const uint32_t ps = (uint32_t)d.pstride[i];
+    X.C1[i] = Q.n1.at(q - ps, any && live && h[i] >= 1);
+    X.C2[i] = Q.n2.at(q - 2 * ps, any && live && h[i] >= 2);
   }
 }
 // Byte arithmetic on the packed 16-B vectors (SWAR), so a lane keeps 4 VGPRs
@@ -1175,15 +1178,13 @@ __device__ __forceinline__ u32x4 hshift(u32x4 v, u32x4 prev) {
   for (int k = 1; k < 4; k++) r[k] = __builtin_amdgcn_alignbit(v[k], v[k - 1], SH);
   return r;
 }
-// 16-bit lanes [0, n) all ones (n clamped to [0, 8])
+// 16-bit lanes [0, n) all ones (n clamped to [0, 8]): two 64-bit halves of
+// (1 << 16 n) - 1 (compares and selects per dword cost 4x the VALU)
 __device__ __forceinline__ u32x4 hprefix(int n) {
-  u32x4 m;
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const int c = min(max(n - 2 * k, 0), 2);
-    m[k] = c == 2 ? ~0u : c == 1 ? 0xFFFFu : 0u;
-  }
-  return m;
+  const uint32_t c = (uint32_t)min(max(n, 0), 8);
+  const u64 lo = c >= 4 ? ~0ull : (1ull << (16 * c)) - 1;
+  const u64 hi = c <= 4 ? 0ull : c >= 8 ? ~0ull : (1ull << (16 * (c - 4))) - 1;
+  return u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
 }
 // dense_parent8 in each 16-bit lane, on the byte at bit B of the lane (B = 0:
 // low byte, B = 8: high byte); never 0x7F: remoteness < 255.  No borrow
@@ -1269,20 +1270,21 @@ __global__ __launch_bounds__(256, GM_R16_MINB) void k_dense_resolve16p(Desc d, D
   hex_init(Q, d, words, bits, L, v.Wl, v.Wbl);
   const uint32_t lane = __lane_id();
   const uint32_t x = blockIdx.x % kXcds;
-  const u64 first = (u64)xs.o[x] * 16 + (u64)(blockIdx.x / kXcds) * blockDim.x + threadIdx.x;
-  const u64 end = (u64)xs.o[x + 1] * 16, stride = (u64)(gridDim.x / kXcds) * blockDim.x;
+  // units (16 prefixes each) of this XCD's share; a level has < 2^28 of them
+  const uint32_t first = xs.o[x] * 16 + (blockIdx.x / kXcds) * blockDim.x + threadIdx.x;
+  const uint32_t end = xs.o[x + 1] * 16, stride = (gridDim.x / kXcds) * blockDim.x;
   const uint32_t last = xs.o[8] - 1;  // last entry of the level's list (the host launches only non-empty lists)
   // the wave's four list entries (scalar loads), lane's group = entry lane >> 4
-  auto fetch = [&](u64 iu) -> uint32_t {
-    const uint32_t g0 = min(__builtin_amdgcn_readfirstlane((uint32_t)((iu - lane) >> 4)), last);
+  auto fetch = [&](uint32_t iu) -> uint32_t {
+    const uint32_t g0 = min(__builtin_amdgcn_readfirstlane((iu - lane) >> 4), last);
     const uint32_t e0 = glist[g0], e1 = glist[min(g0 + 1, last)], e2 = glist[min(g0 + 2, last)],
                    e3 = glist[min(g0 + 3, last)];
     const uint32_t k = lane >> 4;
     return k == 0 ? e0 : k == 1 ? e1 : k == 2 ? e2 : e3;
   };
-  for (u64 iu = first; iu < end; iu += stride) {
+  for (uint32_t iu = first; iu < end; iu += stride) {
     HexLoads<MAXH> X;
-    hex_issue<MAXH>(d, Q, ((u64)fetch(iu) << 8) + 16 * (lane & 15), iu < end, X);
+    hex_issue<MAXH>(d, Q, (fetch(iu) << 8) + 16 * (lane & 15), true, X);
     hex_finish<MAXH>(Q, X);
   }
 
@@ -1349,7 +1351,7 @@ __global__ __launch_bounds__(kTailThreads) void k_dense_resolve16_tail(Desc d, D
     const uint32_t nu = R.cnt[i] * 16;  // sixteen prefixes per unit
     for (uint32_t u = threadIdx.x; u < nu; u += blockDim.x) {
       HexLoads<MAXH> X;
-      hex_issue<MAXH>(d, Q, ((u64)glist[R.off[i] + (u >> 4)] << 8) + 16 * (u & 15), true, X);
+      hex_issue<MAXH>(d, Q, (glist[R.off[i] + (u >> 4)] << 8) + 16 * (u & 15), true, X);
       hex_finish<MAXH>(Q, X);
     }
     npos += Q.npos;
