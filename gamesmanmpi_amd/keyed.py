@@ -36,12 +36,33 @@ from .solver import SolveResult, Solver
 # ---------------------------------------------------------------------------
 # exchanges
 # ---------------------------------------------------------------------------
+# An exchange moves, for every local shard, one flat tensor whose first
+# counts[0] entries go to rank 0, the next counts[1] to rank 1, ... .  The
+# per-destination counts stay on the device until the exchange reads them:
+# ONE host read per exchange (send and receive sizes together); a reply that
+# retraces a previous exchange reuses its sizes and reads nothing.
 class GroupExchange:
     """All shards in this process: recv[dst][src] = send[src][dst]."""
 
-    def all_to_all(self, send):
-        n = len(send)
-        return [[send[src][dst] for src in range(n)] for dst in range(n)]
+    def all_to_all(self, flats, counts_dev):
+        """-> (per shard: list of received tensors by source, sizes) where
+        sizes[g] = (sent per destination, received per source)"""
+        import torch
+        n = len(flats)
+        c = torch.stack(counts_dev).cpu().tolist()  # the one host read
+        parts = [list(torch.split(f, c[g])) for g, f in enumerate(flats)]
+        recv = [[parts[src][dst] for src in range(n)] for dst in range(n)]
+        sizes = [(c[g], [c[src][g] for src in range(n)]) for g in range(n)]
+        return recv, sizes
+
+    def reply(self, flats, sizes):
+        """Send back along a previous exchange: flats[g] holds, by source,
+        the answers to what shard g received (sizes[g][1]); returns per
+        shard the answers by destination of its original send."""
+        import torch
+        n = len(flats)
+        parts = [list(torch.split(f, sizes[g][1])) for g, f in enumerate(flats)]
+        return [[parts[dst][src] for dst in range(n)] for src in range(n)]
 
     def allreduce_sum(self, values):
         return [sum(col) for col in zip(*values)]
@@ -60,18 +81,30 @@ class TorchExchange:
         self.torch, self.dist, self.device = torch, dist, device
         self.stage = torch.device(stage) if stage is not None else device
 
-    def all_to_all(self, send):
+    def all_to_all(self, flats, counts_dev):
         torch, dist = self.torch, self.dist
-        (lists,) = send
-        in_sizes = [int(t.numel()) for t in lists]
-        sizes = torch.tensor(in_sizes, dtype=torch.int64, device=self.stage)
-        got = torch.empty_like(sizes)
-        dist.all_to_all_single(got, sizes)
-        out_sizes = [int(x) for x in got.tolist()]
-        inp = torch.cat(lists).to(self.stage)
+        (flat,), (cnt,) = flats, counts_dev
+        cnt = cnt.to(torch.int64).to(self.stage)
+        got = torch.empty_like(cnt)
+        dist.all_to_all_single(got, cnt)
+        both = torch.cat([cnt, got]).tolist()  # the one host read
+        w = len(both) // 2
+        in_sizes, out_sizes = both[:w], both[w:]
+        out = self._move(flat, in_sizes, out_sizes)
+        return [list(torch.split(out, out_sizes))], [(in_sizes, out_sizes)]
+
+    def reply(self, flats, sizes):
+        torch = self.torch
+        (flat,), ((sent, received),) = flats, sizes
+        out = self._move(flat, received, sent)  # back along the same pairs
+        return [list(torch.split(out, sent))]
+
+    def _move(self, flat, in_sizes, out_sizes):
+        torch, dist = self.torch, self.dist
+        inp = flat.to(self.stage)
         out = torch.empty(sum(out_sizes), dtype=inp.dtype, device=self.stage)
         dist.all_to_all_single(out, inp, out_sizes, in_sizes)
-        return [list(torch.split(out.to(self.device), out_sizes))]
+        return out.to(self.device)
 
     def allreduce_sum(self, values):
         (v,) = values
@@ -211,17 +244,31 @@ class GpuShard:
 # the level loop
 # ---------------------------------------------------------------------------
 def _bucket(torch, keys, owners, world):
-    """keys grouped by owner: (list of `world` tensors, permutation such
-    that cat(list) == keys[perm])."""
+    """keys grouped by owner, on the device: (keys[perm], perm, counts per
+    owner as a device tensor)."""
     perm = torch.argsort(owners, stable=True)
-    counts = torch.bincount(owners.long(), minlength=world).tolist()
-    return list(torch.split(keys[perm], counts)), perm
+    counts = torch.bincount(owners.long(), minlength=world)
+    return keys[perm], perm, counts
+
+
+def _distinct(torch, keys, owners):
+    """distinct keys with their owners, and each original key's index among
+    them (None when there are no keys)"""
+    if not keys.numel():
+        return keys, owners, None
+    ukeys, inv = torch.unique(keys, return_inverse=True)
+    own = torch.empty(ukeys.numel(), dtype=owners.dtype, device=owners.device)
+    own[inv] = owners
+    return ukeys, own, inv
 
 
 def keyed_solve(shards, exchange):
     """Solve the job whose LOCAL shards are `shards` (every rank for a
     group, this rank's one shard under torch.distributed).  Returns the
-    whole job's SolveResult (the same on every rank)."""
+    whole job's SolveResult (the same on every rank).  Per level and shard
+    the host reads sizes three times: the expanded child count
+    (gm_ks_expand), the distinct count (torch.unique) and the exchange
+    sizes; the backward's replies retrace the query exchange and read none."""
     s0 = shards[0]
     torch, spec, world = s0.torch, s0.spec, s0.world
     T = spec.max_levels
@@ -235,43 +282,33 @@ def keyed_solve(shards, exchange):
         for sh in shards:
             sh.begin(sh.rank == root_owner)
         for L in range(T - 1):
-            send = []
+            flats, counts = [], []
             for sh in shards:
                 keys, owners = sh.expand(L)
-                if keys.numel():  # duplicates need not travel
-                    keys, inv = torch.unique(keys, return_inverse=True)
-                    own = torch.empty(keys.numel(), dtype=owners.dtype,
-                                      device=owners.device)
-                    own[inv] = owners
-                    owners = own
-                send.append(_bucket(torch, keys, owners, world)[0])
-            for sh, lists in zip(shards, exchange.all_to_all(send)):
+                keys, owners, _ = _distinct(torch, keys, owners)  # duplicates need not travel
+                flat, _, cnt = _bucket(torch, keys, owners, world)
+                flats.append(flat)
+                counts.append(cnt)
+            recv, _ = exchange.all_to_all(flats, counts)
+            for sh, lists in zip(shards, recv):
                 sh.insert(L, torch.cat(lists))
                 sh.finalize(L)
         t1 = time.perf_counter()
         for L in range(T - 1, -1, -1):
-            queries, state = [], []
+            flats, counts, state = [], [], []
             for g, sh in enumerate(shards):
                 offsets, keys, owners = sh.children(L)
                 widths[g][L] = offsets.numel() - 1
                 # one query per distinct child (a position reached from
                 # several parents of this shard is asked for once)
-                inv = None
-                if keys.numel():
-                    keys, inv = torch.unique(keys, return_inverse=True)
-                    own = torch.empty(keys.numel(), dtype=owners.dtype,
-                                      device=owners.device)
-                    own[inv] = owners
-                    owners = own
-                lists, perm = _bucket(torch, keys, owners, world)
-                queries.append(lists)
+                keys, owners, inv = _distinct(torch, keys, owners)
+                flat, perm, cnt = _bucket(torch, keys, owners, world)
+                flats.append(flat)
+                counts.append(cnt)
                 state.append((offsets, perm, keys.numel(), inv))
-            replies = []
-            for sh, lists in zip(shards, exchange.all_to_all(queries)):
-                sizes = [int(t.numel()) for t in lists]
-                replies.append(list(torch.split(sh.lookup(torch.cat(lists)),
-                                                sizes)))
-            answers = exchange.all_to_all(replies)
+            recv, sizes = exchange.all_to_all(flats, counts)
+            replies = [sh.lookup(torch.cat(lists)) for sh, lists in zip(shards, recv)]
+            answers = exchange.reply(replies, sizes)
             for sh, lists, (offsets, perm, n, inv) in zip(shards, answers,
                                                           state):
                 words = torch.empty(n, dtype=torch.int32, device=sh.device)
