@@ -1305,8 +1305,16 @@ __global__ __launch_bounds__(256, GM_R16_MINB) void k_dense_resolve16p(Desc d, D
 // ---------------------------------------------------------------------------
 constexpr int kTailMax = 40;       // levels per run
 constexpr int kTailThreads = 1024;
-constexpr uint64_t kTailPullGroups = 512;     // two passes of 1024 bitmap words
-constexpr uint64_t kTailResolveGroups = 128;  // two passes of 1024 sixteen-prefix units
+// thresholds measured (tools/ab_dense.sh): 1024 / 256 and 2048 / 512 groups
+// were slower (+0.05, +0.3 ms): past two passes a workgroup's serial passes
+// cost more than the launch they save.  Staging the run's list in LDS saved
+// nothing (a tail level costs ~4 us: its data round, store drain, barrier).
+#ifndef GM_TAIL_PULL_GROUPS
+#define GM_TAIL_PULL_GROUPS 512
+#define GM_TAIL_RESOLVE_GROUPS 128
+#endif
+constexpr uint64_t kTailPullGroups = GM_TAIL_PULL_GROUPS;        // two passes of 1024 bitmap words
+constexpr uint64_t kTailResolveGroups = GM_TAIL_RESOLVE_GROUPS;  // two passes of 1024 sixteen-prefix units
 struct TailRun {
   uint32_t n;                      // levels in the run
   uint32_t L[kTailMax];            // the levels, in solve order
