@@ -221,6 +221,10 @@ def main():
     ap.add_argument("--no-keyed", action="store_true",
                     help="skip the toot 6x4 keyed-table sub-record")
     ap.add_argument("--layout", default="auto", choices=["auto", "dense", "hashed"])
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "host"],
+                    help="N>1 halo exchange: RCCL (one GPU per rank), or host-staged over "
+                         "gloo -- every rank on cuda:0, for rehearsing the N-rank bench on "
+                         "one GPU (not a performance path)")
     args = ap.parse_args()
 
     import torch
@@ -229,11 +233,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("WORLD_SIZE=%d but --gpus %d" % (world, args.gpus))
+    host = args.transport == "host"
+    if host:
+        local = 0  # every rank on the one GPU
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if host:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from gamesmanmpi_amd.games import GameSpec
     from gamesmanmpi_amd.solver import Solver
@@ -243,7 +253,8 @@ def main():
     spec = GameSpec("sum_four_to_one", params)
     if world > 1:
         from gamesmanmpi_amd.dist import ShardedSolver
-        solver = ShardedSolver(spec, rank, world, device="cuda:%d" % local)
+        solver = ShardedSolver(spec, rank, world, device="cuda:%d" % local,
+                               transport="host" if host else "rccl")
     else:
         solver = Solver(spec, device="cuda:%d" % local, layout=args.layout)
 
@@ -262,7 +273,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if host else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     r = results[-1]
@@ -349,7 +360,9 @@ def main():
                    "positions_per_gpu": P // world, "edges_per_gpu": E // world,
                    "levels": r.levels, "root": r.root_line, "root_checked_against": root_src,
                    "layout": layout,
-                   "parallelism": ("round-robin top-heap blocks x%d, RCCL halo exchange" % world
+                   "parallelism": (("round-robin top-heap blocks x%d, %s halo exchange" %
+                                    (world, "host-staged (gloo, all ranks on one GPU: rehearsal, "
+                                            "not a performance figure)" if host else "RCCL"))
                                    if world > 1 else "1 GPU")},
         "roofline": roof,
         "phase_ms": {"forward": r.ms_forward, "backward": r.ms_backward,
