@@ -38,7 +38,11 @@ CASES = {
     "othello_4x4": ("othello_bit_new", "length=4,height=4", "levels"),
     "sum_31x6": ("sum_four_to_one", "heaps=31:31:31:31:31:31", "rows"),
     "sum_15x5": ("sum_four_to_one", "heaps=15:15:15:15:15", "rows"),
+    # the bench's N-rank shapes (31^5 x (32N - 1)): their root lines let the
+    # multi-GPU bench check the root remoteness as well as the closed forms
     "sum_31x5_63": ("sum_four_to_one", "heaps=31:31:31:31:31:63", "rows"),
+    "sum_31x5_127": ("sum_four_to_one", "heaps=31:31:31:31:31:127", "rows"),
+    "sum_31x5_255": ("sum_four_to_one", "heaps=31:31:31:31:31:255", "rows"),
 }
 
 

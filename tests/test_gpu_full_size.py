@@ -87,3 +87,35 @@ def test_gpu_toot_6x4_checksum():
 def test_gpu_sum_31x6_checksum():
     """The bench workload: all 2^30 positions' values and remoteness."""
     _check("sum_31x6", layout="dense")
+
+
+def _check_group(name, world):
+    """The N-GPU bench shape, all `world` shards solved in this process
+    (dist.group_solve: the halo exchange runs device-to-device on one
+    stream): the shards' fingerprints -- each over the slices it owns,
+    halos excluded -- add up to the single-table golden."""
+    from gamesmanmpi_amd.dist import group_solve
+    from gamesmanmpi_amd.games import GameSpec
+    e = _gold(name)
+    r, shards = group_solve(GameSpec(e["game"], e["params"]), world)
+    assert (r.positions, r.edges, r.primitives) == (e["positions"], e["edges"], e["primitives"])
+    assert r.root_line == e["root_line"]
+    tot = {"checksum": 0, "positions": 0, "win": 0, "loss": 0, "tie": 0, "draw": 0}
+    for s in shards:
+        ck = s.checksum()
+        tot["checksum"] = (tot["checksum"] + int(ck["checksum"], 16)) & (2 ** 64 - 1)
+        for k in ("positions", "win", "loss", "tie", "draw"):
+            tot[k] += ck[k]
+    assert tot["positions"] == e["positions"]
+    assert (tot["win"], tot["loss"], tot["tie"], tot["draw"]) == (e["win"], e["loss"], e["tie"], e["draw"])
+    assert "%016x" % tot["checksum"] == e["checksum"]
+
+
+def test_gpu_sum_31x5_63_two_shards_checksum():
+    """bench.py --gpus 2 workload (31^5 x 63 heaps, 2^31 positions)."""
+    _check_group("sum_31x5_63", 2)
+
+
+def test_gpu_sum_31x5_127_four_shards_checksum():
+    """bench.py --gpus 4 workload (31^5 x 127 heaps, 2^32 positions)."""
+    _check_group("sum_31x5_127", 4)
