@@ -25,7 +25,9 @@ GM_F_SHARD_INORDER = 16
 GM_F_HASH_TABLE = 32  # gm_plan, keyed games: open-addressing table, not BUCKETED
 GM_F_WORDS16 = 64  # dense: 16-bit words where 8-bit ones would be chosen
 GM_F_BK_EXACT = 128  # bucketed: count pass + exact partition offsets
-KERNEL_FLAGS = GM_F_WORDS32 | GM_F_RESOLVE_SCALAR | GM_F_SHARD_INORDER | GM_F_WORDS16 | GM_F_BK_EXACT
+GM_F_GRAPH = 256  # dense one-table solves replay captured HIP graphs
+KERNEL_FLAGS = (GM_F_WORDS32 | GM_F_RESOLVE_SCALAR | GM_F_SHARD_INORDER | GM_F_WORDS16 | GM_F_BK_EXACT
+                | GM_F_GRAPH)
 # gm_result.kernels codes (gm_solver.hip DenseResolveKind / DensePullKind)
 RESOLVE_KERNELS = {1: "k_dense_resolve8p", 2: "k_dense_resolve8c", 3: "k_dense_resolve4p",
                    4: "k_dense_resolve4c", 5: "k_dense_resolve4", 6: "k_dense_resolve",

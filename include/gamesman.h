@@ -109,6 +109,10 @@ typedef struct gm_buffers {
 #define GM_F_BK_EXACT 128u     /* BUCKETED: count every level's children first
                                   (exact partition offsets) instead of writing
                                   into provisioned partitions */
+#define GM_F_GRAPH 256u       /* dense one-table full solves: capture the
+                                  forward and backward launches as HIP graphs
+                                  on the first solve, replay them after
+                                  (measured: no faster than plain launches) */
 
 typedef struct gm_result {
   uint32_t root_word;

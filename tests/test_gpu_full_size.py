@@ -119,3 +119,15 @@ def test_gpu_sum_31x5_63_two_shards_checksum():
 def test_gpu_sum_31x5_127_four_shards_checksum():
     """bench.py --gpus 4 workload (31^5 x 127 heaps, 2^32 positions)."""
     _check_group("sum_31x5_127", 4)
+
+
+def test_gpu_sum_31x6_graph_replay():
+    """GM_F_GRAPH: the first solve captures the forward and backward launches
+    as HIP graphs, the later ones replay them -- same table bit for bit."""
+    from gamesmanmpi_amd import _lib
+    s, r = _check("sum_31x6", layout="dense", flags=_lib.GM_F_GRAPH)
+    e = _gold("sum_31x6")
+    for _ in range(2):
+        r2 = s.solve()
+        assert (r2.positions, r2.edges, r2.root_line) == (e["positions"], e["edges"], e["root_line"])
+    assert s.checksum()["checksum"] == e["checksum"]
