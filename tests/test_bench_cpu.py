@@ -31,6 +31,19 @@ def test_closed_forms_match_the_oracle(heaps):
     assert (sol.count, sol.edges, sol.root_line.split()[0]) == (P, E, root)
 
 
+def test_scaling_workloads_have_goldens():
+    """Every bench shape N = 1, 2, 4, 8 has a whole-solve golden (the N > 1
+    steps check their root line against it) whose counts and root value are
+    the closed forms'."""
+    for n in (1, 2, 4, 8):
+        heaps = bench.heaps_for(n)
+        e = bench.golden_for_params("sum_four_to_one", "heaps=" + ":".join(map(str, heaps)))
+        assert e is not None, n
+        P, E, root = bench.expected(heaps)
+        assert (e["positions"], e["edges"], e["root_line"].split()[0]) == (P, E, root)
+        assert e["win"] + e["loss"] == P
+
+
 def test_level_counts_and_compulsory_bytes():
     """Per-level position counts (digit-sum distribution) and the dense
     layout's compulsory byte model."""

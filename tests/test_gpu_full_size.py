@@ -131,3 +131,9 @@ def test_gpu_sum_31x6_graph_replay():
         r2 = s.solve()
         assert (r2.positions, r2.edges, r2.root_line) == (e["positions"], e["edges"], e["root_line"])
     assert s.checksum()["checksum"] == e["checksum"]
+
+
+def test_gpu_sum_31x5_255_eight_shards_checksum():
+    """bench.py --gpus 8 workload (31^5 x 255 heaps, 2^33 positions), its
+    eight shards in one process on one GPU."""
+    _check_group("sum_31x5_255", 8)
