@@ -1,12 +1,14 @@
 #!/usr/bin/env python3
 """Solves of one game (for profiler passes and A/B timing):
     python tools/solve_once.py GAME [PARAMS] [LAYOUT] [REPEATS] [timing]
-e.g. toot_and_otto_bitstring "length=6,height=4" bucketed 3.  The first
+e.g. toot_and_otto_bitstring "length=6,height=4" bucketed 3 (env SOLVE_FLAGS:
+GM_F_* kernel flags of the solver, e.g. 256 = GM_F_GRAPH).  The first
 solve warms up; each later one prints a JSON line (the last with per-kernel
 timing and the whole-solve checksum).  REPEATS 0: one solve, printed; with
 `timing` it runs with per-kernel timing (one launch per dense level, as the
 bench's roofline solve does -- the PMC passes use this form).""" 
 import json
+import os
 import sys
 import time
 
@@ -21,7 +23,7 @@ def main():
     params = sys.argv[2] if len(sys.argv) > 2 else ""
     layout = sys.argv[3] if len(sys.argv) > 3 else "auto"
     reps = int(sys.argv[4]) if len(sys.argv) > 4 else 1
-    s = Solver(GameSpec(name, params), layout=layout)
+    s = Solver(GameSpec(name, params), layout=layout, flags=int(os.environ.get("SOLVE_FLAGS", "0")))
     if reps == 0 and len(sys.argv) > 5 and sys.argv[5] == "timing":
         s.set_kernel_timing(True)
     for i in range(reps + 1):
