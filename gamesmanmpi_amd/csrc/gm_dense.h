@@ -1375,8 +1375,11 @@ __global__ __launch_bounds__(kTailThreads) void k_dense_resolve16_tail(Desc d, D
 // k_dense_resolve8p, a wave = two consecutive columns of the jobs'
 // concatenation (lanes 0-31 / 32-63; each half finds its slice by a scalar
 // search), software-pipelined.
+#ifndef GM_R8C_MINB
+#define GM_R8C_MINB 1
+#endif
 template <int MAXH>
-__global__ __launch_bounds__(256) void k_dense_resolve8c(Desc d, RowGeom g, uint16_t* words, const u64* bits, u64 L,
+__global__ __launch_bounds__(256, GM_R8C_MINB) void k_dense_resolve8c(Desc d, RowGeom g, uint16_t* words, const u64* bits, u64 L,
                                                          DevState* st, const uint32_t* __restrict__ colperm,
                                                          ColJobs J, BlockCount* bc) {
   Oct8 Q;
