@@ -1378,6 +1378,13 @@ __global__ __launch_bounds__(kTailThreads) void k_dense_resolve16_tail(Desc d, D
 #ifndef GM_R8C_MINB
 #define GM_R8C_MINB 1
 #endif
+// One unit in flight per lane (86 VGPRs, 5 waves per SIMD) against the
+// two-stage software pipeline (GM_R8C_PIPE 1: 138 VGPRs, 3 waves): the
+// 2-shard group solve's backward 22.4 -> 20.1 ms (tools/ab_group.sh), the
+// same trade the 8-bit list kernel made
+#ifndef GM_R8C_PIPE
+#define GM_R8C_PIPE 0
+#endif
 template <int MAXH>
 __global__ __launch_bounds__(256, GM_R8C_MINB) void k_dense_resolve8c(Desc d, RowGeom g, uint16_t* words, const u64* bits, u64 L,
                                                          DevState* st, const uint32_t* __restrict__ colperm,
@@ -1408,6 +1415,7 @@ __global__ __launch_bounds__(256, GM_R8C_MINB) void k_dense_resolve8c(Desc d, Ro
     const u64 o = 8 * (lane & 31);
     oct_issue<MAXH>(d, Q, (lane < 32 ? q0 : q1) + o, (lane < 32 ? p0 : p1) + o, on, X);
   };
+#if GM_R8C_PIPE
   if (r.first < r.end) {
     OctLoads<MAXH> X0, X1;
     issue(r.first, X0);
@@ -1419,6 +1427,13 @@ __global__ __launch_bounds__(256, GM_R8C_MINB) void k_dense_resolve8c(Desc d, Ro
       oct_finish<MAXH>(Q, X1);
     }
   }
+#else
+  for (u64 iu = r.first; iu < r.end; iu += r.stride) {
+    OctLoads<MAXH> X;
+    issue(iu, X);
+    oct_finish<MAXH>(Q, X);
+  }
+#endif
   block_count(bc, (u64)Q.npos, (u64)Q.edges);
   if (Q.S == 0) block_add(&st->prims, (u64)Q.npos);  // one launch per solve
 }
