@@ -958,10 +958,16 @@ __device__ __forceinline__ void oct_finish(Oct8& Q, const OctLoads<MAXH>& X) {
   }
   *(u16x8*)(Q.mine + X.q) = o;
 }
-// Live-group list sweep over a 16-bit table, software-pipelined like
-// k_dense_resolve4p.  Units of 8 prefixes, 32 per group; the host starts
+// Live-group list sweep over a 16-bit table (software-pipelined like
+// k_dense_resolve4p when GM_R8P_PIPE).  Units of 8 prefixes, 32 per group; the host starts
 // every XCD share at an even list entry, so a wave's 64 units are two whole
 // groups (lanes 0-31 / 32-63), read with two scalar loads.
+// one unit in flight per lane (88 VGPRs, 5 waves per SIMD) against the
+// two-stage pipeline (GM_R8P_PIPE 1: 3 waves): GM_F_WORDS16 bench backward
+// 5.35 -> 5.08 ms (tools/ab_dense.sh default:64 against a variant)
+#ifndef GM_R8P_PIPE
+#define GM_R8P_PIPE 0
+#endif
 template <int MAXH>
 __device__ __forceinline__ void resolve8p_body(const Desc& d, const DenseView& v, uint16_t* words, const u64* bits,
                                                u64 L, DevState* st, const uint32_t* __restrict__ glist,
@@ -981,6 +987,7 @@ __device__ __forceinline__ void resolve8p_body(const Desc& d, const DenseView& v
     const u64 pg = ((u64)(lane < 32 ? e0 : e1) << 8) + 8 * (lane & 31);
     oct_issue<MAXH>(d, Q, pg, pg, on, X);
   };
+#if GM_R8P_PIPE
   if (first < end) {
     OctLoads<MAXH> X0, X1;
     issue(first, X0);
@@ -992,6 +999,13 @@ __device__ __forceinline__ void resolve8p_body(const Desc& d, const DenseView& v
       oct_finish<MAXH>(Q, X1);
     }
   }
+#else
+  for (u64 iu = first; iu < end; iu += stride) {
+    OctLoads<MAXH> X;
+    issue(iu, X);
+    oct_finish<MAXH>(Q, X);
+  }
+#endif
   block_count(bc, (u64)Q.npos, (u64)Q.edges);
   if (Q.S == 0) block_add(&st->prims, (u64)Q.npos);  // one launch per solve
 }
