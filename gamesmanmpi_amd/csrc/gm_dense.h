@@ -789,6 +789,9 @@ __global__ __launch_bounds__(256) void k_dense_resolve4(Desc d, DenseView v, uin
 }
 
 // Live-group list sweep (world 1), software-pipelined: see quad_issue.
+#ifndef GM_R4P_PIPE
+#define GM_R4P_PIPE 1
+#endif
 template <int MAXH>
 __global__ __launch_bounds__(256) void k_dense_resolve4p(Desc d, DenseView v, uint32_t* words, const u64* bits, u64 L,
                                                          DevState* st, const uint32_t* __restrict__ glist,
@@ -806,6 +809,7 @@ __global__ __launch_bounds__(256) void k_dense_resolve4p(Desc d, DenseView v, ui
     const u64 pw = (u64)glist[gi] << 8;  // world 1: local = global prefix
     quad_issue<MAXH>(d, Q, hl, sl, pw + 4 * (iu & 63), pw, on, X);
   };
+#if GM_R4P_PIPE
   if (first < end) {
     // two register sets, statically named (a dynamically indexed pair
     // would live in scratch)
@@ -819,6 +823,13 @@ __global__ __launch_bounds__(256) void k_dense_resolve4p(Desc d, DenseView v, ui
       quad_finish<MAXH>(Q, X1);
     }
   }
+#else
+  for (u64 iu = first; iu < end; iu += stride) {
+    QuadLoads<MAXH> X;
+    issue(iu, X);
+    quad_finish<MAXH>(Q, X);
+  }
+#endif
   quad_done(Q, st);
 }
 
