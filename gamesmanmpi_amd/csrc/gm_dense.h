@@ -1223,10 +1223,11 @@ __device__ __forceinline__ uint32_t parent8x2(uint32_t m) {
 __device__ __forceinline__ uint32_t bits4_to_bytes(uint32_t b4) {  // 4 bits -> 4 byte masks
   return ((b4 * 0x00204081u) & 0x01010101u) * 0xFFu;
 }
+// the unit's parent words into o (false: no valid slot, nothing to store)
 template <int MAXH>
-__device__ __forceinline__ void hex_finish(Hex16& Q, const HexLoads<MAXH>& X) {
+__device__ __forceinline__ bool hex_reduce(Hex16& Q, const HexLoads<MAXH>& X, u32x4& o) {
   const uint32_t valid = X.valid;
-  if (!valid) return;
+  if (!valid) return false;
   const uint32_t S = Q.S;
   const uint32_t rbits = (uint32_t)(X.bitsw >> ((Q.Lb + X.q) & 63)) & 0xFFFFu;
   const u32x4 EM = splat4(opaque_u32(0x00FF00FFu)), OM = splat4(opaque_u32(0xFF00FF00u));
@@ -1255,7 +1256,6 @@ __device__ __forceinline__ void hex_finish(Hex16& Q, const HexLoads<MAXH>& X) {
   const int t1 = (int)S - (int)X.s - 1;
   me = hmax(me, hmax(a1e & hprefix((t1 + 2) >> 1), a2e & hprefix((t1 + 1) >> 1)));
   mo = hmax(mo, hmax(a1 & hprefix((t1 + 1) >> 1), a2 & hprefix(t1 >> 1))) & OM;
-  u32x4 o;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const uint32_t w = S == 0 ? 0xFFFFFFFFu : parent8x2<0>(me[k]) | parent8x2<8>(mo[k]);  // DENSE_PRIMITIVE8
@@ -1271,7 +1271,12 @@ __device__ __forceinline__ void hex_finish(Hex16& Q, const HexLoads<MAXH>& X) {
     Q.edges += n * X.nch_hi + (uint32_t)__popc(V & pre(t1)) + (uint32_t)__popc(V & pre(t1 - 1)) +
                (X.h1 >= 2 ? 2 * n : (uint32_t)__popc(V & 0xFFFEu) + (uint32_t)__popc(V & 0xFFFCu));
   }
-  *(u32x4*)(Q.mine + X.q) = o;
+  return true;
+}
+template <int MAXH>
+__device__ __forceinline__ void hex_finish(Hex16& Q, const HexLoads<MAXH>& X) {
+  u32x4 o;
+  if (hex_reduce<MAXH>(Q, X, o)) *(u32x4*)(Q.mine + X.q) = o;
 }
 // Live-group list sweep; the host starts every XCD share at an entry
 // divisible by 4, so a wave's 64 units are four whole groups (lanes 16k ..
@@ -1285,6 +1290,9 @@ __device__ __forceinline__ void hex_finish(Hex16& Q, const HexLoads<MAXH>& X) {
 // measured no gain (tools/ab_dense.sh)
 #ifndef GM_R16_MINB
 #define GM_R16_MINB 6
+#endif
+#ifndef GM_R16_DEFER
+#define GM_R16_DEFER 0
 #endif
 template <int MAXH>
 __global__ __launch_bounds__(256, GM_R16_MINB) void k_dense_resolve16p(Desc d, DenseView v, uint8_t* words,
@@ -1307,11 +1315,28 @@ __global__ __launch_bounds__(256, GM_R16_MINB) void k_dense_resolve16p(Desc d, D
     const uint32_t k = lane >> 4;
     return k == 0 ? e0 : k == 1 ? e1 : k == 2 ? e2 : e3;
   };
+#if GM_R16_DEFER
+  // each unit's store is issued after the NEXT unit's loads: gfx9 counts
+  // loads and stores in one in-order vmcnt, so a store issued before the
+  // loads would make their wait cover its write acknowledgement too
+  u32x4 po;
+  uint32_t pq = 0;
+  bool pend = false;
+  for (uint32_t iu = first; iu < end; iu += stride) {
+    HexLoads<MAXH> X;
+    hex_issue<MAXH>(d, Q, (fetch(iu) << 8) + 16 * (lane & 15), true, X);
+    if (pend) *(u32x4*)(Q.mine + pq) = po;
+    pend = hex_reduce<MAXH>(Q, X, po);
+    pq = (uint32_t)X.q;
+  }
+  if (pend) *(u32x4*)(Q.mine + pq) = po;
+#else
   for (uint32_t iu = first; iu < end; iu += stride) {
     HexLoads<MAXH> X;
     hex_issue<MAXH>(d, Q, (fetch(iu) << 8) + 16 * (lane & 15), true, X);
     hex_finish<MAXH>(Q, X);
   }
+#endif
 
   block_count(bc, (u64)Q.npos, (u64)Q.edges);
   if (Q.S == 0) block_add(&st->prims, (u64)Q.npos);  // one launch per solve
