@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # kernel variants, tools/diag_streams.sh)
 LIBPATH = os.environ.get("GM_LIBPATH") or os.path.join(HERE, "libgamesman_hip.so")
 
-GM_EINVAL, GM_EHIP, GM_EFULL, GM_ECORRUPT, GM_ENOGPU = -1, -2, -3, -4, -5
+GM_EINVAL, GM_EHIP, GM_EFULL, GM_ECORRUPT, GM_ENOGPU, GM_ELIMIT = -1, -2, -3, -4, -5, -6
 GM_PARTIAL = 1  # gm_solver_solve stopped at the gm_solver_set_steps bound
 GM_F_KERNEL_TIMING = 1
 GM_F_FORCE_HASHED = 2
@@ -51,7 +51,12 @@ class GmError(RuntimeError):
 
 
 class TableFull(GmError):
-    pass
+    """GM_EFULL: the buffers are too small; re-planning larger fixes it."""
+
+
+class LayoutLimit(GmError):
+    """GM_ELIMIT: a limit of the layout that more memory cannot lift (a
+    bucketed hash bucket over capacity, a level too wide); never retried."""
 
 
 class gm_plan_t(ctypes.Structure):
@@ -207,4 +212,6 @@ def check(rc):
     msg = load().gm_last_error().decode(errors="replace")
     if rc == GM_EFULL:
         raise TableFull(rc, msg)
+    if rc == GM_ELIMIT:
+        raise LayoutLimit(rc, msg)
     raise GmError(rc, msg)

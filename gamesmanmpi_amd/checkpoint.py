@@ -79,6 +79,21 @@ def check_target(directory):
                              "checkpoint; refusing to overwrite it" % directory)
 
 
+def check_scratch_dir(directory):
+    """Refuse a save()'s own scratch directory (`directory`.tmp / .old) if
+    it holds anything but checkpoint files.  Unlike check_target it needs no
+    meta.json: save() writes meta.json last, so a crash while the .bin
+    files stream out leaves a .tmp without one, and the next save() must
+    be able to reuse it."""
+    if not os.path.exists(directory):
+        return
+    if not os.path.isdir(directory):
+        raise NotACheckpoint("%s exists and is not a directory" % directory)
+    if not set(os.listdir(directory)) <= _OURS:
+        raise NotACheckpoint("%s holds files that are not a gamesmanmpi_amd checkpoint's; "
+                             "refusing to overwrite it" % directory)
+
+
 def _remove_ours(directory):
     """Delete only the files a checkpoint consists of, then the directory if
     that left it empty."""
@@ -132,8 +147,8 @@ def save(solver, directory, step):
     torch = solver.torch
     torch.cuda.synchronize(solver.device)
     tmp, old = directory + ".tmp", directory + ".old"
-    check_target(tmp)
-    check_target(old)
+    check_scratch_dir(tmp)
+    check_scratch_dir(old)
     _remove_ours(tmp)
     os.makedirs(tmp)
     for name, t in zip(_NAMES, solver.buffers):
@@ -203,8 +218,11 @@ def solve_checkpointed(solver, directory, every, first=0, keep=False, max_regrow
     `directory` every `every` steps; removes the checkpoint's files when the
     solve completes unless keep=True.  A keyed table that fills during the
     forward pass (positions_hint too small) is regrown and the solve
-    restarted from step 0, as Solver.solve() does; a resumed solve
-    (first > 0) cannot regrow and raises TableFull."""
+    restarted from step 0, as Solver.solve() does.  That includes a resumed
+    solve (first > 0) whose checkpoint was taken with a plan that is too
+    small: the stale checkpoint is dropped as soon as the buffers regrow
+    (a later restore would otherwise rebuild the small plan and fail at the
+    same level on every resume), and the solve restarts from the root."""
     if every < 1:
         raise ValueError("every must be >= 1")
     check_target(directory)
@@ -215,11 +233,13 @@ def solve_checkpointed(solver, directory, every, first=0, keep=False, max_regrow
         try:
             r = solver.solve_steps(step, stop if stop < total else 0)
         except _lib.TableFull:
-            if first > 0 or grown >= max_regrow:
+            if grown >= max_regrow:
                 raise
             grown += 1
             solver.positions_hint *= 2
             solver._alloc(solver.positions_hint)
+            _remove_ours(directory.rstrip("/"))
+            _remove_ours(directory.rstrip("/") + ".old")
             step = 0
             continue
         if r is not None:

@@ -899,6 +899,7 @@ struct gm_solver {
   int rank, world;
   u64 nblocks;  // blocks of the top digit over all ranks (view.B values each)
   ncclComm_t comm;  // RCCL communicator (world > 1), or null
+  u64* errg = nullptr;  // RCCL: every rank's error mask, all-gathered (world u64, device)
   gm_xfer_fn xfer = nullptr;  // host-staged transport (gm_solver_set_transport), replaces comm
   void* xfer_ctx = nullptr;
   bool halo_ok = false;       // the exchange plan was checked against the other ranks'
@@ -1591,12 +1592,17 @@ int gm_plan(int game, uint64_t positions, uint32_t flags, uint64_t max_table_byt
     // partition buffers of the widest level's in-edges (table buffer)
     const u64 P = positions + 64, E = bk_edges_bound(d, positions), Em = bk_emax_bound(E);
     if (Em >= 0xFFFFFFF0ull) return fail(GM_EINVAL, "a level of more than 2^32 edges: not supported");
-    out->mode = GM_MODE_BUCKETED;
-    out->level_capacity = P;
-    out->table_slots = E;
-    out->table_bytes = 4 * P + 6 * E + 24 * Em;  // words, in-edges (u32 parent + u16 child), staging
-    out->scratch_bytes = bk_scratch(d->max_levels).end;
-    return 0;
+    const u64 bytes = 4 * P + 6 * E + 24 * Em;  // words, in-edges (u32 parent + u16 child), staging
+    // over the caller's byte budget: the keyed hash table instead (as a
+    // dense table over budget falls back above)
+    if (max_table_bytes == 0 || bytes <= max_table_bytes) {
+      out->mode = GM_MODE_BUCKETED;
+      out->level_capacity = P;
+      out->table_slots = E;
+      out->table_bytes = bytes;
+      out->scratch_bytes = bk_scratch(d->max_levels).end;
+      return 0;
+    }
   }
   uint64_t slots = 1024;
   while (slots < 2 * positions) slots <<= 1;  // load factor <= 0.5
@@ -1938,6 +1944,8 @@ int gm_solver_comm_init(gm_solver* s, const void* id) {
   ncclResult_t r = ncclCommInitRank(&c, s->world, uid, s->rank);
   if (r != ncclSuccess) return fail(GM_EHIP, "ncclCommInitRank: %s", ncclGetErrorString(r));
   s->comm = c;
+  if (!s->errg && hipMalloc((void**)&s->errg, (size_t)s->world * sizeof(u64)) != hipSuccess)
+    return fail(GM_EHIP, "error-mask gather buffer");
   return 0;
 }
 
@@ -2019,6 +2027,7 @@ void gm_solver_destroy(gm_solver* s) {
   if (s->gbwd) (void)hipGraphExecDestroy(s->gbwd);
   if (s->cstream) (void)hipStreamDestroy(s->cstream);
   if (s->comm) (void)ncclCommDestroy(s->comm);
+  if (s->errg) (void)hipFree(s->errg);
   if (s->own_stream) (void)hipStreamDestroy(s->stream);
   delete s;
 }
@@ -2941,10 +2950,10 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
     hipLaunchKernelGGL(k_dense_root, dim3(1), dim3(64), 0, st, s->view, s->words, s->bits, root_q, s->st, s->wbits());
     hipLaunchKernelGGL(k_fill_red, dim3(1), dim3(1024), 0, st, s->st, s->bcount);
   }
-  if (mode == 1) {  // counts and root word summed; the error masks max-reduced (a sum would carry)
+  if (mode == 1) {  // counts and root word summed; every rank's error mask gathered, OR-ed on the host
     ncclGroupStart();
     ncclResult_t r = ncclAllReduce(s0->st->red, s0->st->red, 4, ncclUint64, ncclSum, s0->comm, st);
-    ncclResult_t r2 = ncclAllReduce(s0->st->red + 4, s0->st->red + 4, 1, ncclUint64, ncclMax, s0->comm, st);
+    ncclResult_t r2 = ncclAllGather(s0->st->red + 4, s0->errg, 1, ncclUint64, s0->comm, st);
     ncclResult_t r3 = ncclGroupEnd();
     if (r != ncclSuccess || r2 != ncclSuccess || r3 != ncclSuccess)
       return fail(GM_EHIP, "RCCL allreduce: %s", ncclGetErrorString(r != ncclSuccess ? r : r2 != ncclSuccess ? r2 : r3));
@@ -2963,6 +2972,12 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
       for (int g = 0; g < s->world; g++)
         for (int i = 0; i < 5; i++) red[i] = (i == 4) ? (red[i] | all[(size_t)g * 5 + i]) : red[i] + all[(size_t)g * 5 + i];
       continue;
+    }
+    if (mode == 1) {
+      std::vector<u64> e((size_t)s->world);
+      HIPCHK(hipMemcpy(e.data(), s->errg, e.size() * sizeof(u64), hipMemcpyDeviceToHost));
+      r[4] = 0;
+      for (u64 x : e) r[4] |= x;
     }
     for (int i = 0; i < 5; i++) red[i] = (i == 4) ? (red[i] | r[i]) : red[i] + r[i];
   }
@@ -3133,7 +3148,7 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
     X.lb = P.lb + P.n;
     X.rb = re_used;
     if (!bk_ranges(P.n, &P.pshift, &P.fb))
-      return bail(fail(GM_EFULL, "level %d holds %llu positions: more than the 2^29 a bucketed level supports", L,
+      return bail(fail(GM_ELIMIT, "level %d holds %llu positions: more than the 2^29 a bucketed level supports", L,
                        (unsigned long long)P.n));
     P.eout = 0;
     if (P.n) {
@@ -3266,8 +3281,10 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
         HIPCHK(hipMemcpyAsync(&herr, &s->st->err, 4, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         if (herr) {
-          const bool full = herr & ERR_BUCKET_FULL;
-          return bail(fail(full ? GM_EFULL : GM_ECORRUPT, "level %d:%s", L + 1, err_text(herr).c_str()));
+          // a fine bucket over kBkMaxUnique keys follows from the level's
+          // real edges, not from the buffers: more memory cannot fix it
+          const bool lim = herr & ERR_BUCKET_FULL;
+          return bail(fail(lim ? GM_ELIMIT : GM_ECORRUPT, "level %d:%s", L + 1, err_text(herr).c_str()));
         }
         if (X.lb + n1 > s->Pcap) return bail(fail(GM_EFULL, "positions exceed the plan's %llu", (unsigned long long)s->Pcap));
         X.n = n1;
@@ -3289,7 +3306,7 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
     if (k >= stop) break;
     BkLevel& P = lv[(size_t)L];
     if (!P.n) continue;
-    if (!bk_ranges(P.n, &P.pshift, &P.fb)) return bail(fail(GM_EFULL, "level %d too wide", L));
+    if (!bk_ranges(P.n, &P.pshift, &P.fb)) return bail(fail(GM_ELIMIT, "level %d too wide for bucketed levels", L));
     const uint32_t NR = (uint32_t)((P.n + (1ull << P.fb) - 1) >> P.fb);
     const int gr = (int)std::min<uint32_t>(NR, 512);
     hipEvent_t* sp = span(false);
@@ -3379,8 +3396,9 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
   out->max_level_width = (uint32_t)std::min<u64>(wmax, 0xFFFFFFFFull);
   out->root_word = root_word;
   if (hs->err) {
-    const bool full = hs->err & (ERR_TABLE_FULL | ERR_LEVELS_FULL | ERR_BUCKET_FULL);
-    return fail(full ? GM_EFULL : GM_ECORRUPT, "solve failed:%s", err_text(hs->err).c_str());
+    const bool full = hs->err & (ERR_TABLE_FULL | ERR_LEVELS_FULL);
+    const bool lim = hs->err & ERR_BUCKET_FULL;
+    return fail(lim ? GM_ELIMIT : full ? GM_EFULL : GM_ECORRUPT, "solve failed:%s", err_text(hs->err).c_str());
   }
   if (root_word == NO_WORD) return fail(GM_ECORRUPT, "root unresolved");
   out->root_value = (int32_t)(root_word & 3u);

@@ -41,6 +41,10 @@ extern "C" {
 #define GM_EFULL (-3)     /* table or level storage too small: re-plan larger */
 #define GM_ECORRUPT (-4)  /* internal consistency check failed (bug) */
 #define GM_ENOGPU (-5)    /* no usable gfx950 device */
+#define GM_ELIMIT (-6)    /* a layout limit more memory cannot lift (a BUCKETED
+                             hash bucket over capacity, a level wider than
+                             the layout supports): re-planning larger does
+                             not help, use another layout */
 #define GM_PARTIAL 1      /* gm_solver_solve stopped at the step set by gm_solver_set_steps (not an error) */
 
 /* layout of one hash-table slot (16 B): key, word, spare */

@@ -222,3 +222,31 @@ def test_checkpoint_helpers_only_touch_their_own_files(tmp_path):
     extra.write_text("k")
     ck._remove_ours(str(d) + ".old")
     assert os.listdir(tmp_path / "ck.old") == ["keep.txt"]
+
+
+def test_checkpoint_save_reuses_a_crashed_tmp(tmp_path, monkeypatch):
+    """a save() that crashed while its .bin files streamed out
+    leaves DIR.tmp holding our .bin files and no meta.json; the next save()
+    must reuse it (not raise NotACheckpoint), while a .tmp holding foreign
+    files is still refused.  Host-only: the device streaming is stubbed."""
+    import types
+    from gamesmanmpi_amd import checkpoint as ck
+    d = str(tmp_path / "ck")
+    tmp = tmp_path / "ck.tmp"
+    tmp.mkdir()
+    (tmp / "table.bin").write_bytes(b"\1" * 16)  # the crash left this
+    monkeypatch.setattr(ck, "_stream_out", lambda t, path, torch: open(path, "wb").write(b"\0" * 8))
+    monkeypatch.setattr(ck, "_plan_dict", lambda s: {"mode": 0})
+    fake_torch = types.SimpleNamespace(cuda=types.SimpleNamespace(synchronize=lambda dev=None: None))
+    solver = types.SimpleNamespace(world=1, torch=fake_torch, device="cpu", buffers=(0, 0, 0),
+                                   spec=types.SimpleNamespace(name="g", params=""), layout="auto",
+                                   positions_hint=1, max_table_bytes=0, flags=0, steps=4)
+    ck.save(solver, d, 2)
+    assert ck.read_meta(d)["step"] == 2
+    assert not os.path.exists(str(tmp))
+    # a foreign file in the scratch directory is still refused
+    tmp.mkdir()
+    (tmp / "notes.txt").write_text("mine")
+    with pytest.raises(ck.NotACheckpoint):
+        ck.save(solver, d, 3)
+    assert (tmp / "notes.txt").read_text() == "mine"

@@ -1,3 +1,7 @@
+"""Allocation-order probe: toot 6x4 solve times after a dense
+solve or cold.  A script, not a test: run as
+    python tools/order_probe.py dense_first|cold
+"""
 import sys, time, json
 sys.path.insert(0, ".")
 import torch
@@ -11,9 +15,14 @@ def toot(tag):
         out.append(round((time.perf_counter() - t0) * 1e3, 1))
     print(tag, out, r.extra["layout"], flush=True)
     del s; torch.cuda.empty_cache()
-if sys.argv[1] == "dense_first":
-    d = Solver(GameSpec("sum_four_to_one", "heaps=31:31:31:31:31:31"))
-    for i in range(5): d.solve()
-    del d; torch.cuda.empty_cache()
-toot(sys.argv[1])
-toot(sys.argv[1] + "_again")
+def main():
+    if sys.argv[1] == "dense_first":
+        d = Solver(GameSpec("sum_four_to_one", "heaps=31:31:31:31:31:31"))
+        for i in range(5): d.solve()
+        del d; torch.cuda.empty_cache()
+    toot(sys.argv[1])
+    toot(sys.argv[1] + "_again")
+
+
+if __name__ == "__main__":
+    main()
