@@ -1,0 +1,325 @@
+// gm_plane.h -- PLANES layout of the dense (rank-indexable) sum games:
+// natural rank order, 1 or 2 bytes per position, no holes.  Kernels for
+// gfx950 (MI355X).
+//
+// Replaces, for sum_four_to_one with heaps 0 and 1 of 32 values, the
+// reference's per-position job loop (src/process.py:109-267: lookup ->
+// distribute -> resolve with _res_red/_remote_red) by a sweep over PLANES:
+//
+//   position (h0, h1, P), P = mixed-radix index of the outer heaps
+//   h2..h(K-1) ("plane"), stored at
+//       word[P * 1024 + h1 * 32 + ((h0 + h1) & 31)]
+//   i.e. planes of 32 x 32 positions, rows of 32, each row ROTATED left by
+//   its row number.  A plane is 1 KiB (8-bit words) or 2 KiB (16-bit).
+//
+// One move lowers ONE heap by 1 or 2 (test_games/four_to_one.py:7-22), so a
+// position's children lie in its own plane (h0 / h1 lowered) or at the same
+// (h0, h1) of one of 2 (K - 2) neighbour planes P - k * stride_j (k = 1, 2).
+// Planes of equal outer digit sum s are independent of each other; plane
+// level s needs levels s - 1 and s - 2 only.  The backward pass is one launch
+// per plane level (outer digit sums 0 .. sum of outer heaps; 125 launches
+// for 31^6 instead of 187 levels of the level-major DENSE layout).
+//
+// k_plane_resolve: one wave = two planes (lanes 0-31 and 32-63, lane = row
+// h1).  Each lane loads its row of the neighbour planes (16-B loads, a
+// wave's load = 1 KiB of contiguous rows), folds them into E, the per-
+// position max of the external children, with packed 16-bit maxes, and then
+// resolves its row by a 63-step skewed wavefront: at step t lane h1 handles
+// h0 = t - h1, whose children (h0-1, h1), (h0-2, h1) are the lane's last two
+// results and (h0, h1-1), (h0, h1-2) the last results of lanes h1-1 / h1-2
+// one and two steps ago (DPP wave_shr:1).  Because every row is rotated by
+// its row number, the byte a lane needs at step t sits at register byte
+// t & 31 in EVERY lane: all extracts and inserts are static.
+//
+// Order-form words (the unsigned max over the children is the reduction of
+// _res_red/_remote_red; absent children read 0, neutral):
+//   8-bit (every value WIN/LOSS, remoteness < 255, value = parity of the
+//          remoteness): WIN r -> (r - 1) / 2, LOSS r -> 0x80 | (0x7F - r / 2);
+//          parent of max m: h(m) = 0xFE - m + (m >> 7)
+//   16-bit: WIN r -> r, LOSS r -> 0x8000 | (0x7FFF - r);
+//          parent of max m: h(m) = 0xFFFE - m + 2 (m >> 15)
+// The only primitive (every heap 0, a LOSS) is LOSS 0 = 0xFF / 0xFFFF.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gm {
+
+constexpr int kPlaneMaxOuter = 6;  // K <= 8 heaps
+
+// Geometry of one PLANES table (a whole game, or one shard of it).  A shard
+// (world > 1) owns blocks of B consecutive values of the TOP outer digit
+// (heap K-1), block g owned by rank g mod world (round robin, as the
+// level-major shards: DESIGN.md §6); its table holds only its own slices,
+// block after block: local plane = (j * B + o) * Z + lower, where j is the
+// rank's block number, o the value's offset in the block, Z = planes per top
+// value and lower = the index of the digits below the top.  Neighbours along
+// the top digit that belong to the previous block come from a halo buffer
+// (PlaneEntry).
+struct PlaneGeom {
+  uint32_t no;     // outer digits (heaps 2 .. K-1)
+  uint32_t pow2;   // every outer base a power of two
+  uint32_t nplanes;  // planes of this table (local)
+  uint32_t world, rank, B, Z;  // shards (world 1: B = Z = 0)
+  uint32_t base[kPlaneMaxOuter];
+  uint32_t shift[kPlaneMaxOuter];   // log2(stride[j]) when pow2
+  uint32_t stride[kPlaneMaxOuter];  // global plane-index stride of outer digit j
+  uint32_t rlim[kPlaneMaxOuter + 2];  // reach: heap i reachable up to rlim[i] (heaps 0, 1, then outer)
+};
+
+// Sharded level lists: per plane, where its top-digit neighbours are and
+// where its words go besides the table.
+constexpr uint32_t kPlaneAbsent = 0xFFFFFFFFu;  // no such neighbour (top value < k): reads 0
+constexpr uint32_t kPlaneLocal = 0xFFFFFFFEu;   // the neighbour is local: plane - k * Z
+struct PlaneEntry {
+  uint32_t p;      // local plane
+  uint32_t top1;   // neighbour at top value - 1: kPlaneAbsent / kPlaneLocal / halo plane index
+  uint32_t top2;   // neighbour at top value - 2: the same
+  uint32_t send;   // halo plane index in the send buffer (boundary slices), or kPlaneAbsent
+};
+
+template <int WB>
+struct PlaneWord;
+template <>
+struct PlaneWord<1> {
+  typedef uint8_t T;
+  static constexpr int DW = 8;  // dwords of one 32-position row
+  static constexpr uint32_t kPrim = 0xFFu;
+  __device__ static __forceinline__ uint32_t parent(uint32_t m) { return 0xFEu - m + (m >> 7); }
+};
+template <>
+struct PlaneWord<2> {
+  typedef uint16_t T;
+  static constexpr int DW = 16;
+  static constexpr uint32_t kPrim = 0xFFFFu;
+  __device__ static __forceinline__ uint32_t parent(uint32_t m) { return 0xFFFEu - m + ((m >> 15) << 1); }
+};
+
+// host + device: the order-form word of a value/remoteness and back
+__host__ __device__ inline uint32_t plane_word_to_vr(uint32_t w, int wb) {
+  // -> value | remoteness << 2 (GM_WIN 0 / GM_LOSS 1)
+  if (wb == 1) {
+    if (w & 0x80u) return 1u | ((2u * (0x7Fu - (w & 0x7Fu))) << 2);
+    return 0u | ((2u * w + 1u) << 2);
+  }
+  if (w & 0x8000u) return 1u | ((0x7FFFu - (w & 0x7FFFu)) << 2);
+  return 0u | (w << 2);
+}
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t pk_max16(uint32_t a, uint32_t b) {
+  u16x2 x = __builtin_bit_cast(u16x2, a), y = __builtin_bit_cast(u16x2, b);
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(x, y));
+}
+__device__ __forceinline__ uint32_t pk_shl8(uint32_t a) {
+  u16x2 x = __builtin_bit_cast(u16x2, a);
+  return __builtin_bit_cast(uint32_t, (u16x2)(x << (unsigned short)8));
+}
+// v = lanes set in the 64-bit constant m ? v : 0 (one v_cndmask, SGPR mask)
+__device__ __forceinline__ uint32_t keep_lanes(uint64_t m, uint32_t v) {
+  uint32_t r;
+  asm("v_cndmask_b32 %0, 0, %1, %2" : "=v"(r) : "v"(v), "s"(m));
+  return r;
+}
+// value of lane - 1 (lane 0: 0)
+__device__ __forceinline__ uint32_t from_lane_below(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138 /* wave_shr:1 */, 0xF, 0xF, true);
+}
+
+// lanes whose row is active at skew step t: h1 in [t - 31, t], both halves
+__host__ __device__ constexpr uint64_t plane_step_mask(int t) {
+  const int lo = t - 31 < 0 ? 0 : t - 31, hi = t > 31 ? 31 : t;
+  const uint64_t m = ((hi >= 31 ? 0xFFFFFFFFull : ((1ull << (hi + 1)) - 1)) & ~((1ull << lo) - 1)) & 0xFFFFFFFFull;
+  return m | (m << 32);
+}
+
+template <int NO>
+__device__ __forceinline__ void plane_digits(const PlaneGeom& g, uint32_t P, uint32_t* dig) {
+  if (g.pow2) {
+#pragma unroll
+    for (int j = 0; j < NO; j++) dig[j] = (P >> g.shift[j]) & (g.base[j] - 1u);
+  } else {
+    uint32_t x = P;
+#pragma unroll
+    for (int j = 0; j < NO; j++) {
+      dig[j] = x % g.base[j];
+      x /= g.base[j];
+    }
+  }
+}
+
+// XCD-chunked share of n items for this wave (blocks b -> XCD b % 8):
+// the wave handles items [first, end) with the given stride
+struct PlaneShare {
+  uint32_t first, end, stride;
+};
+__device__ __forceinline__ PlaneShare plane_share(uint32_t n, uint32_t per_wave) {
+  const uint32_t G = gridDim.x, waves = blockDim.x >> 6;
+  const uint32_t nx = (G >= 8 && G % 8 == 0) ? 8u : 1u;
+  const uint32_t x = blockIdx.x % nx, lb = blockIdx.x / nx;
+  const uint32_t chunk = ((n + nx - 1) / nx + per_wave - 1) / per_wave * per_wave;
+  const uint32_t b = min(n, x * chunk);
+  PlaneShare s;
+  s.end = min(n, b + chunk);
+  s.first = b + (lb * waves + (threadIdx.x >> 6)) * per_wave;
+  s.stride = (G / nx) * waves * per_wave;
+  return s;
+}
+
+// One plane level: list[0 .. n) are the level's planes (uint32 plane index,
+// or PlaneEntry for shards).  tab: the table (plane P at tab + P * 1024
+// words); zero: >= 64 zero bytes; recv / send: the shard's halo buffers.
+template <int WB, int NO, bool SH>
+__global__ __launch_bounds__(256) void k_plane_resolve(typename PlaneWord<WB>::T* __restrict__ tab,
+                                                       const void* __restrict__ list, uint32_t n, PlaneGeom g,
+                                                       const uint4* __restrict__ zero,
+                                                       const typename PlaneWord<WB>::T* __restrict__ recv,
+                                                       typename PlaneWord<WB>::T* __restrict__ send) {
+  typedef PlaneWord<WB> W;
+  constexpr int DW = W::DW, NQ = DW / 4;  // dwords / 16-B loads per row
+  const uint32_t lane = threadIdx.x & 63, L = lane & 31;
+  const uint32_t lm = lane == 32 ? 0u : ~0u;  // row 0 of the upper plane has no row below
+  const PlaneShare sh = plane_share(n, 2);
+  for (uint32_t i0 = sh.first; i0 < sh.end; i0 += sh.stride) {
+    const uint32_t idx = i0 + (lane >> 5);
+    const bool live = idx < sh.end;
+    PlaneEntry e;
+    if (SH) {
+      e = ((const PlaneEntry*)list)[live ? idx : i0];
+    } else {
+      e.p = ((const uint32_t*)list)[live ? idx : i0];
+    }
+    const uint32_t P = e.p;
+    uint32_t dig[NO > 0 ? NO : 1];
+    plane_digits<NO>(g, P, dig);
+    const size_t rowoff = (size_t)P * 1024u + L * 32u;  // in words
+    // external children: rows of the neighbour planes, folded into E
+    uint32_t Ehi[DW], Elo[WB == 1 ? DW : 1];
+#pragma unroll
+    for (int d = 0; d < DW; d++) {
+      Ehi[d] = 0;
+      if (WB == 1) Elo[d] = 0;
+    }
+#pragma unroll
+    for (int j = 0; j < NO; j++) {
+#pragma unroll
+      for (int k = 1; k <= 2; k++) {
+        const uint4* src;
+        if (SH && j == NO - 1) {  // the sharded top digit: local, halo or absent
+          const uint32_t w = k == 1 ? e.top1 : e.top2;
+          src = w == kPlaneAbsent ? zero
+                : w == kPlaneLocal ? (const uint4*)(tab + rowoff - (size_t)k * g.Z * 1024u)
+                                   : (const uint4*)(recv + (size_t)w * 1024u + L * 32u);
+        } else {
+          src = dig[j] >= (uint32_t)k ? (const uint4*)(tab + rowoff - (size_t)k * g.stride[j] * 1024u) : zero;
+        }
+        uint4 v[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; q++) v[q] = src[q];
+#pragma unroll
+        for (int q = 0; q < NQ; q++) {
+          const uint32_t x[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+          for (int c = 0; c < 4; c++) {
+            Ehi[4 * q + c] = pk_max16(Ehi[4 * q + c], x[c]);  // 8-bit: odd bytes exact in the high halves
+            if (WB == 1) Elo[4 * q + c] = pk_max16(Elo[4 * q + c], pk_shl8(x[c]));  // even bytes
+          }
+        }
+      }
+    }
+    // the skewed wavefront over the plane: step t = 32 ph + q handles
+    // h0 = t - h1; lanes outside [t - 31, t] are idle and produce 0.  The
+    // idle-lane mask is formed in SALU per step (a hoisted table of 63
+    // 64-bit constants spilled SGPRs).
+    const bool prim = g.rank == 0 && P == 0 && L == 0;  // every heap 0: the primitive LOSS
+    uint32_t cur = 0, prev = 0, u1p = 0;
+    uint32_t out[DW];
+#pragma unroll
+    for (int d = 0; d < DW; d++) out[d] = 0;
+#pragma unroll 1
+    for (uint32_t ph = 0; ph < 2; ph++) {
+      const uint32_t flip = ph ? 0xFFFFFFFFu : 0u;  // phase 1: the lanes past their row's start
+#pragma unroll
+      for (int q = 0; q < 32; q++) {
+        uint32_t a;
+        if (WB == 1) {
+          const int d = q >> 2, b = q & 3;
+          a = (b & 1) ? __builtin_amdgcn_ubfe(Ehi[d], 8 * b, 8) : __builtin_amdgcn_ubfe(Elo[d], 8 * b + 8, 8);
+        } else {
+          a = __builtin_amdgcn_ubfe(Ehi[q >> 1], 16 * (q & 1), 16);
+        }
+        const uint32_t u1 = from_lane_below(cur) & lm;
+        const uint32_t u2 = from_lane_below(u1p) & lm;
+        uint32_t m = max(max(a, cur), prev);
+        m = max(max(m, u1), u2);
+        // active lanes: phase 0 rows 0..q, phase 1 rows q+1..31 (both halves)
+        const uint32_t am = (uint32_t)(q == 31 ? 0xFFFFFFFFull : ((2ull << q) - 1)) ^ flip;
+        uint32_t f = keep_lanes(((uint64_t)am << 32) | am, W::parent(m));
+        if (q == 0) f = (prim && ph == 0) ? W::kPrim : f;
+        if (WB == 1)
+          out[q >> 2] |= f << (8 * (q & 3));
+        else
+          out[q >> 1] |= f << (16 * (q & 1));
+        prev = cur;
+        cur = f;
+        u1p = u1;
+      }
+    }
+    if (live) {
+      uint4* dst = (uint4*)(tab + rowoff);
+#pragma unroll
+      for (int q = 0; q < NQ; q++) dst[q] = make_uint4(out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]);
+      if (SH && e.send != kPlaneAbsent) {  // a boundary slice: also into the send buffer
+        uint4* sd = (uint4*)(send + (size_t)e.send * 1024u + L * 32u);
+#pragma unroll
+        for (int q = 0; q < NQ; q++) sd[q] = make_uint4(out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]);
+      }
+    }
+  }
+}
+
+// global digits of a local plane: outer digits j < NO - 1 from the lower
+// index, the top one from the shard's block layout (world 1: plain digits)
+template <int NO>
+__device__ __forceinline__ void plane_global_digits(const PlaneGeom& g, uint32_t P, uint32_t* dig) {
+  plane_digits<NO>(g, P, dig);
+  if (g.world > 1 && NO > 0) {
+    const uint32_t u = P / g.Z, j = u / g.B, o = u - j * g.B;
+    dig[NO - 1] = (g.rank + j * g.world) * g.B + o;
+  }
+}
+
+// Forward pass: the reach bitmap (one bit per position, plane P's row h1 is
+// the 32-bit word bits[P * 32 + h1], bit h0) and the counts.  Moves act on
+// one heap at a time and the only primitive (every heap 0) has no moves, so
+// the positions reachable from the root are the product of each heap's
+// values reachable by its own moves (x -> x-1 for x >= 1, x -> x-2 for
+// x >= 2: every value up to the start, rlim[i]).  One thread per row word;
+// counts per block into its BlockCount slot (block_count), summed once per
+// solve (k_fill_red).
+template <int NO, class CountFn>
+__device__ __forceinline__ void plane_reach_body(uint32_t* __restrict__ bits, const PlaneGeom& g, CountFn count) {
+  const uint64_t nw = (uint64_t)g.nplanes * 32u;
+  uint64_t npos = 0, edges = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t P = (uint32_t)(i >> 5), h1 = (uint32_t)i & 31u;
+    uint32_t dig[NO > 0 ? NO : 1];
+    plane_global_digits<NO>(g, P, dig);
+    bool in = h1 <= g.rlim[1];
+    uint32_t ext = h1 < 2 ? h1 : 2u;  // moves of the heaps other than heap 0
+#pragma unroll
+    for (int j = 0; j < NO; j++) {
+      in = in && dig[j] <= g.rlim[2 + j];
+      ext += dig[j] < 2 ? dig[j] : 2u;
+    }
+    const uint32_t w = in ? (g.rlim[0] >= 31 ? 0xFFFFFFFFu : ((2u << g.rlim[0]) - 1u)) : 0u;
+    bits[i] = w;
+    const uint32_t c = __builtin_popcount(w);
+    npos += c;
+    edges += (uint64_t)c * ext + __builtin_popcount(w >> 1) + __builtin_popcount(w >> 2);
+  }
+  count(npos, edges);
+}
+
+}  // namespace gm

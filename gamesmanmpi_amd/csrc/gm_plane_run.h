@@ -1,0 +1,741 @@
+// gm_plane_run.h -- host side of the PLANES layout (gm_plane.h): planning,
+// level lists, the solve loop (one table, an in-process shard group, or one
+// shard per process over RCCL / a host-staged transport), and the table
+// readers (query, positions, checksum).  Included by gm_solver.hip after the
+// solver object and the dense helpers it shares (BlockCount slots,
+// k_fill_red, the transport helpers).
+//
+// Reference path replaced: src/process.py:37-267 (the per-state job loop)
+// and src/game_state.py:22-30 (which rank owns a state): a shard owns
+// round-robin blocks of the last heap's values; the per-edge LOOK_UP /
+// RESOLVE messages become, per plane level, ONE send of the rank's boundary
+// slices to the next rank (the planes its first two slices need).
+
+// (gm_solver.hip includes this inside its extern "C" block: templates need
+// C++ linkage)
+extern "C++" {
+// ---------------------------------------------------------------------------
+// kernels (need DevState / BlockCount / Desc from gm_solver.hip)
+// ---------------------------------------------------------------------------
+template <int NO>
+__global__ __launch_bounds__(256) void k_plane_reach(uint32_t* bits, PlaneGeom g, BlockCount* bc, DevState* st) {
+  plane_reach_body<NO>(bits, g, [&](u64 npos, u64 edges) { block_count(bc, npos, edges); });
+  // the only primitive, every heap 0: global plane 0 of rank 0, row 0, bit 0
+  if (blockIdx.x == 0 && threadIdx.x == 0 && g.rank == 0) atomicAdd(&st->prims, 1ull);
+}
+
+// word of local position (h0, h1, P) in value | remoteness << 2 form
+template <int WB>
+__device__ __forceinline__ uint32_t plane_vr(const void* tab, u64 P, uint32_t h0, uint32_t h1) {
+  const u64 i = P * 1024u + h1 * 32u + ((h0 + h1) & 31u);
+  const uint32_t w = WB == 1 ? ((const uint8_t*)tab)[i] : ((const uint16_t*)tab)[i];
+  return plane_word_to_vr(w, WB);
+}
+
+// rank (key) -> local plane, h0, h1; false if another shard owns it or the
+// key lies outside the heaps
+__device__ __forceinline__ bool plane_locate(const Desc& d, const PlaneGeom& g, u64 key, u64* P, uint32_t* h0,
+                                             uint32_t* h1) {
+  u64 x = key;
+  uint32_t dig[16];
+  for (int i = 0; i < d.nheaps; i++) {
+    dig[i] = (uint32_t)(x % d.base[i]);
+    x /= d.base[i];
+  }
+  if (x) return false;
+  *h0 = dig[0];
+  *h1 = dig[1];
+  u64 p = 0;
+  const int no = d.nheaps - 2;
+  if (g.world > 1) {
+    const uint32_t t = dig[d.nheaps - 1], blk = t / g.B, o = t - blk * g.B;
+    if (blk % g.world != g.rank) return false;
+    for (int j = 0; j + 1 < no; j++) p += (u64)dig[2 + j] * g.stride[j];
+    p += ((u64)(blk / g.world) * g.B + o) * g.Z;
+  } else {
+    for (int j = 0; j < no; j++) p += (u64)dig[2 + j] * g.stride[j];
+  }
+  *P = p;
+  return true;
+}
+
+template <int WB>
+__global__ void k_plane_query(Desc d, PlaneGeom g, const void* tab, const uint32_t* bits, const u64* keys, u64 n,
+                              uint32_t* out) {
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+    u64 P;
+    uint32_t h0, h1, w = NO_WORD;
+    if (plane_locate(d, g, keys[i], &P, &h0, &h1) && ((bits[P * 32u + h1] >> h0) & 1u)) w = plane_vr<WB>(tab, P, h0, h1);
+    out[i] = w;
+  }
+}
+
+// the root's word (only the shard that owns it): DevState::root_word
+template <int WB>
+__global__ void k_plane_root(Desc d, PlaneGeom g, const void* tab, const uint32_t* bits, DevState* st) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    u64 P;
+    uint32_t h0, h1, w = NO_WORD;
+    if (plane_locate(d, g, d.root, &P, &h0, &h1) && ((bits[P * 32u + h1] >> h0) & 1u)) w = plane_vr<WB>(tab, P, h0, h1);
+    st->root_word = w;
+  }
+}
+
+// global rank of local position (h0, h1, P)
+template <int NO>
+__device__ __forceinline__ u64 plane_key(const Desc& d, const PlaneGeom& g, uint32_t P, uint32_t h0, uint32_t h1) {
+  uint32_t dig[NO > 0 ? NO : 1];
+  plane_global_digits<NO>(g, P, dig);
+  u64 k = (u64)h0 + (u64)h1 * d.stride[1];
+#pragma unroll
+  for (int j = 0; j < NO; j++) k += (u64)dig[j] * d.stride[2 + j];
+  return k;
+}
+
+template <int NO>
+__global__ void k_plane_positions(Desc d, PlaneGeom g, const uint32_t* bits, u64* out, u64 cap, u64* count) {
+  const u64 nw = (u64)g.nplanes * 32u;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += (u64)gridDim.x * blockDim.x) {
+    uint32_t w = bits[i];
+    if (!w) continue;
+    u64 k = atomicAdd(count, (u64)__builtin_popcount(w));
+    const u64 base = plane_key<NO>(d, g, (uint32_t)(i >> 5), 0, (uint32_t)i & 31u);
+    for (; w; w &= w - 1, k++)
+      if (k < cap) out[k] = base + (u64)__builtin_ctz(w);
+  }
+}
+
+template <int NO, int WB>
+__global__ __launch_bounds__(256) void k_plane_checksum(Desc d, PlaneGeom g, const void* tab, const uint32_t* bits,
+                                                        u64* acc) {
+  u64 a[6] = {0, 0, 0, 0, 0, 0};
+  const u64 nw = (u64)g.nplanes * 32u;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += (u64)gridDim.x * blockDim.x) {
+    const uint32_t P = (uint32_t)(i >> 5), h1 = (uint32_t)i & 31u;
+    uint32_t w = bits[i];
+    if (!w) continue;
+    const u64 base = plane_key<NO>(d, g, P, 0, h1);
+    for (; w; w &= w - 1) {
+      const uint32_t h0 = (uint32_t)__builtin_ctz(w);
+      ck_add(d, base + h0, plane_vr<WB>(tab, P, h0, h1), a);
+    }
+  }
+  ck_block_add(acc, a);
+}
+
+// ---------------------------------------------------------------------------
+// host: shape, plan, lists
+// ---------------------------------------------------------------------------
+// PLANES applies to sum_four_to_one whose heaps 0 and 1 hold 32 values (a
+// plane is 32 x 32), with at most kPlaneMaxOuter further heaps and every
+// remoteness below 2^15 (16-bit order forms).
+static bool plane_ok(const Desc* d) {
+  if (d->kind != K_SUM || d->variant != 0 || d->nheaps < 2 || d->nheaps - 2 > kPlaneMaxOuter) return false;
+  if (d->heap[0] != 31 || d->heap[1] != 31 || d->root_sum >= 0x7FFF) return false;
+  u64 np = 1;
+  for (int i = 2; i < d->nheaps; i++) np *= d->base[i];
+  return np <= 0xFFFFFFF0ull;
+}
+// 8-bit order forms when every remoteness < 255 (they carry the value in the
+// remoteness parity: every K_SUM position is WIN or LOSS), else 16-bit
+static uint32_t plane_wb(const Desc* d, uint32_t flags) {
+  return (d->root_sum <= 253 && !(flags & GM_F_WORDS16)) ? 1u : 2u;
+}
+static bool plane_wanted(const Desc* d, uint32_t flags) {
+  return plane_ok(d) && !(flags & (GM_F_LEVEL_MAJOR | GM_F_FORCE_HASHED | GM_F_WORDS32 | GM_F_RESOLVE_SCALAR));
+}
+
+struct PlaneShape {
+  PlaneGeom g;
+  uint32_t wb;
+  uint32_t S;            // largest plane level (sum of the outer heaps)
+  uint32_t nblocks, nb;  // shards: blocks of the top digit over all ranks / of this rank
+  u64 nlocal;            // planes of this table
+  u64 nrecv, nsend;      // halo planes of this shard (all levels)
+  u64 words_off, bits_off, recv_off, send_off, table_bytes;  // table buffer layout
+  u64 zero_off, list_off, scratch_bytes;                      // scratch layout
+};
+
+static u64 rup256(u64 x) { return (x + 255) & ~255ull; }
+
+static int plane_shape(const Desc* d, int rank, int world, uint32_t flags, PlaneShape* ps) {
+  memset(ps, 0, sizeof *ps);
+  PlaneGeom& g = ps->g;
+  g.no = (uint32_t)(d->nheaps - 2);
+  g.pow2 = 1;
+  g.world = (uint32_t)std::max(world, 1);
+  g.rank = (uint32_t)rank;
+  u64 np = 1;
+  for (uint32_t j = 0; j < g.no; j++) {
+    g.base[j] = d->base[2 + j];
+    g.stride[j] = (uint32_t)np;
+    g.shift[j] = (uint32_t)__builtin_ctzll(np);
+    if (g.base[j] & (g.base[j] - 1)) g.pow2 = 0;
+    np *= g.base[j];
+  }
+  // reach: the values each heap reaches by its own moves from its start
+  // (four_to_one.py:10-15: x -> x-1 for x >= 1, x -> x-2 for x >= 2), a 1-D
+  // closure; the layout needs it to be [0, r] (it is: [0, start])
+  for (int i = 0; i < d->nheaps; i++) {
+    std::vector<uint8_t> seen((size_t)d->heap[i] + 1, 0);
+    std::vector<uint32_t> todo{d->heap[i]};
+    seen[d->heap[i]] = 1;
+    while (!todo.empty()) {
+      const uint32_t x = todo.back();
+      todo.pop_back();
+      for (uint32_t k = 1; k <= 2 && k <= x; k++)
+        if (!seen[x - k]) {
+          seen[x - k] = 1;
+          todo.push_back(x - k);
+        }
+    }
+    uint32_t r = 0;
+    while (r + 1 < seen.size() && seen[r + 1]) r++;
+    for (size_t v = 0; v < seen.size(); v++)
+      if (seen[v] != (v <= r)) return fail(GM_EINVAL, "heap %d: reachable values are not a prefix", i);
+    g.rlim[i] = r;
+  }
+  ps->wb = plane_wb(d, flags);
+  ps->S = 0;
+  for (int i = 2; i < d->nheaps; i++) ps->S += d->heap[i];
+  if (world <= 1) {
+    g.nplanes = (uint32_t)np;
+    ps->nlocal = np;
+  } else {
+    if (g.no < 1) return fail(GM_EINVAL, "sharded planes need at least 3 heaps");
+    if (rank < 0 || rank >= world) return fail(GM_EINVAL, "bad shard %d/%d", rank, world);
+    const u64 E = d->base[d->nheaps - 1], Z = g.stride[g.no - 1];
+    const u64 B = E >= 16 * (u64)world ? 8 : (E + world - 1) / world;
+    if (B < 2 || E % B || E / B < (u64)world)
+      return fail(GM_EINVAL, "last heap of %llu values cannot give %d ranks whole blocks of >= 2", (unsigned long long)E,
+                  world);
+    ps->nblocks = (uint32_t)(E / B);
+    ps->nb = (uint32_t)((ps->nblocks - (u64)rank + world - 1) / world);
+    g.B = (uint32_t)B;
+    g.Z = (uint32_t)Z;
+    ps->nlocal = (u64)ps->nb * B * Z;
+    g.nplanes = (uint32_t)ps->nlocal;
+    for (uint32_t j = 0; j < ps->nb; j++) {
+      const u64 gb = (u64)rank + (u64)j * world;
+      if (gb >= 1) ps->nrecv += 2 * Z;
+      if (gb + 1 < ps->nblocks) ps->nsend += 2 * Z;
+    }
+  }
+  const u64 pb = 1024ull * ps->wb;
+  ps->words_off = 0;
+  ps->bits_off = rup256(ps->nlocal * pb);
+  ps->recv_off = ps->bits_off + rup256(ps->nlocal * 128);
+  ps->send_off = ps->recv_off + rup256(ps->nrecv * pb);
+  ps->table_bytes = ps->send_off + rup256(ps->nsend * pb);
+  ps->zero_off = rup256(scratch_bytes_for(d->max_levels));
+  ps->list_off = ps->zero_off + 4096;
+  ps->scratch_bytes = ps->list_off + rup256(ps->nlocal * (world > 1 ? sizeof(PlaneEntry) : 4));
+  return 0;
+}
+
+static int plan_planes(const Desc* d, int rank, int world, uint32_t flags, uint64_t max_table_bytes, gm_plan_t* out,
+                       bool* fits) {
+  PlaneShape ps;
+  int rc = plane_shape(d, rank, world, flags, &ps);
+  if (rc) return rc;
+  *fits = max_table_bytes == 0 || ps.table_bytes <= max_table_bytes;
+  out->mode = GM_MODE_PLANES;
+  out->table_slots = ps.nlocal * 1024;
+  out->table_bytes = ps.table_bytes;
+  out->level_capacity = 1;
+  out->scratch_bytes = ps.scratch_bytes;
+  out->max_levels = (uint32_t)d->max_levels;
+  return 0;
+}
+
+// Level lists (host, once per solver).  World 1: the planes of each level
+// (outer digit sum s) in index order.  Shards: PlaneEntry per own plane,
+// level by level, and within a level block by block, slice by slice, lower
+// index ascending -- the canonical order in which the boundary slices travel:
+// the sender's level-s segment lists, for each of its blocks with a
+// successor, slices B-2 and B-1; the receiver's, for each of its blocks with
+// a predecessor, the two slices below it.  A halo plane's index is its
+// group's start plus the rank of its lower digits within their digit-sum
+// class, which is also the rank of the receiving plane in its own group.
+static int plane_lists(gm_solver* s, const PlaneShape& ps, std::vector<uint8_t>& bytes) {
+  const PlaneGeom& g = ps.g;
+  const uint32_t S = ps.S;
+  auto digsum = [&](u64 P, uint32_t ndig) {
+    uint32_t t = 0;
+    for (uint32_t j = 0; j < ndig; j++) {
+      t += (uint32_t)(P % g.base[j]);
+      P /= g.base[j];
+    }
+    return t;
+  };
+  s->ploff.assign((size_t)S + 2, 0);
+  if (g.world <= 1) {
+    std::vector<uint32_t> lev(ps.nlocal);
+    for (u64 P = 0; P < ps.nlocal; P++) {
+      lev[P] = digsum(P, g.no);
+      s->ploff[lev[P] + 1]++;
+    }
+    for (uint32_t l = 0; l <= S; l++) s->ploff[l + 1] += s->ploff[l];
+    bytes.resize(ps.nlocal * 4);
+    uint32_t* L = (uint32_t*)bytes.data();
+    std::vector<u64> pos(s->ploff.begin(), s->ploff.end());
+    for (u64 P = 0; P < ps.nlocal; P++) L[pos[lev[P]]++] = (uint32_t)P;
+    return 0;
+  }
+  const u64 Z = g.Z, B = g.B;
+  const uint32_t nlow = g.no - 1;  // digits below the top
+  std::vector<uint32_t> sig(Z), rk(Z);
+  uint32_t smax = 0;
+  for (u64 l = 0; l < Z; l++) smax = std::max(smax, sig[l] = digsum(l, nlow));
+  std::vector<u64> ncl(smax + 1, 0);
+  for (u64 l = 0; l < Z; l++) rk[l] = (uint32_t)ncl[sig[l]]++;
+  auto cls = [&](int64_t c) -> u64 { return c < 0 || c > (int64_t)smax ? 0 : ncl[(size_t)c]; };
+  const u64 nb = ps.nb, world = g.world, rank = g.rank;
+  auto gblk = [&](u64 j) { return rank + j * world; };
+  // halo groups per level: recv (j, h) = top value gB - 2 + h; send (j, h) =
+  // top value gB + B - 2 + h
+  std::vector<u64> rgb(((size_t)S + 1) * nb * 2, ~0ull), sgb(((size_t)S + 1) * nb * 2, ~0ull);
+  s->prcv_off.assign((size_t)S + 2, 0);
+  s->psnd_off.assign((size_t)S + 2, 0);
+  u64 ra = 0, sa = 0;
+  for (uint32_t l = 0; l <= S; l++) {
+    s->prcv_off[l] = ra;
+    s->psnd_off[l] = sa;
+    for (u64 j = 0; j < nb; j++) {
+      const u64 gb = gblk(j);
+      for (u64 h = 0; h < 2; h++) {
+        if (gb >= 1) {
+          rgb[((size_t)l * nb + j) * 2 + h] = ra;
+          ra += cls((int64_t)l - (int64_t)(gb * B - 2 + h));
+        }
+        if (gb + 1 < ps.nblocks) {
+          sgb[((size_t)l * nb + j) * 2 + h] = sa;
+          sa += cls((int64_t)l - (int64_t)(gb * B + B - 2 + h));
+        }
+      }
+    }
+  }
+  s->prcv_off[S + 1] = ra;
+  s->psnd_off[S + 1] = sa;
+  if (ra != ps.nrecv || sa != ps.nsend) return fail(GM_ECORRUPT, "halo plan: %llu / %llu planes, sized %llu / %llu",
+                                                   (unsigned long long)ra, (unsigned long long)sa,
+                                                   (unsigned long long)ps.nrecv, (unsigned long long)ps.nsend);
+  // entries by level
+  for (u64 j = 0; j < nb; j++)
+    for (u64 o = 0; o < B; o++) {
+      const u64 t = gblk(j) * B + o;
+      for (uint32_t c = 0; c <= smax; c++)
+        if (t + c <= S) s->ploff[t + c + 1] += ncl[c];
+    }
+  for (uint32_t l = 0; l <= S; l++) s->ploff[l + 1] += s->ploff[l];
+  if (s->ploff[S + 1] != ps.nlocal) return fail(GM_ECORRUPT, "plane lists: %llu entries for %llu planes",
+                                               (unsigned long long)s->ploff[S + 1], (unsigned long long)ps.nlocal);
+  bytes.resize(ps.nlocal * sizeof(PlaneEntry));
+  PlaneEntry* E = (PlaneEntry*)bytes.data();
+  std::vector<u64> pos(s->ploff.begin(), s->ploff.end());
+  for (u64 j = 0; j < nb; j++) {
+    const u64 gb = gblk(j);
+    for (u64 o = 0; o < B; o++) {
+      const u64 t = gb * B + o;
+      for (u64 l = 0; l < Z; l++) {
+        const u64 lev = t + sig[l];
+        PlaneEntry e;
+        e.p = (uint32_t)((j * B + o) * Z + l);
+        auto halo = [&](u64 k) -> uint32_t {  // neighbour at top value t - k
+          if (t < k) return kPlaneAbsent;
+          if (o >= k) return kPlaneLocal;
+          const u64 h = o + 2 - k;  // halo slice: top value gB - 2 + h
+          return (uint32_t)(rgb[((size_t)(lev - k) * nb + j) * 2 + h] + rk[l]);
+        };
+        e.top1 = halo(1);
+        e.top2 = halo(2);
+        e.send = (o + 2 >= B && gb + 1 < ps.nblocks) ? (uint32_t)(sgb[((size_t)lev * nb + j) * 2 + (o + 2 - B)] + rk[l])
+                                                     : kPlaneAbsent;
+        E[pos[lev]++] = e;
+      }
+    }
+  }
+  return 0;
+}
+
+// solver set-up for PLANES buffers (gm_solver_create_shard)
+static int plane_setup(gm_solver* s, const gm_buffers* buf) {
+  PlaneShape ps;
+  int rc = plane_shape(&s->d, s->rank, s->world, buf->flags, &ps);
+  if (rc) return rc;
+  if (buf->table_bytes < ps.table_bytes || buf->scratch_bytes < ps.scratch_bytes)
+    return fail(GM_EINVAL, "planes table / scratch of %llu / %llu bytes, the plan needs %llu / %llu (plan with the same "
+                           "flags)", (unsigned long long)buf->table_bytes, (unsigned long long)buf->scratch_bytes,
+                (unsigned long long)ps.table_bytes, (unsigned long long)ps.scratch_bytes);
+  s->pg = ps.g;
+  s->pwb = ps.wb;
+  s->pS = ps.S;
+  char* t = (char*)buf->table;
+  s->ptab = t + ps.words_off;
+  s->pbits = (uint32_t*)(t + ps.bits_off);
+  s->precv = t + ps.recv_off;
+  s->psend = t + ps.send_off;
+  char* sc = (char*)buf->scratch;
+  s->pzero = (const uint4*)(sc + ps.zero_off);
+  s->plist = sc + ps.list_off;
+  s->pnrecv = ps.nrecv;
+  s->pnsend = ps.nsend;
+  std::vector<uint8_t> lb;
+  rc = plane_lists(s, ps, lb);
+  if (rc) return rc;
+  HIPCHK(hipMemset((void*)s->pzero, 0, 4096));
+  HIPCHK(hipMemcpy((void*)s->plist, lb.data(), lb.size(), hipMemcpyHostToDevice));
+  s->w8 = ps.wb == 1;
+  s->w16 = ps.wb == 2;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// host: launches
+// ---------------------------------------------------------------------------
+template <int WB, int NO, bool SH>
+static void plane_launch_t(gm_solver* s, uint32_t l) {
+  const u64 a = s->ploff[l], n = s->ploff[l + 1] - a;
+  if (!n) return;
+  const u64 waves = (n + 1) / 2;
+  u64 blocks = (waves + 3) / 4;
+  blocks = std::min<u64>((blocks + 7) & ~7ull, (u64)s->grid * 4);  // plane_share loops past the grid
+  typedef typename PlaneWord<WB>::T T;
+  const void* list = (const char*)s->plist + a * (SH ? sizeof(PlaneEntry) : 4);
+  hipLaunchKernelGGL((k_plane_resolve<WB, NO, SH>), dim3((uint32_t)blocks), dim3(256), 0, s->stream, (T*)s->ptab, list,
+                     (uint32_t)n, s->pg, s->pzero, (const T*)s->precv, (T*)s->psend);
+}
+template <int WB, bool SH>
+static void plane_launch_w(gm_solver* s, uint32_t l) {
+  switch (s->pg.no) {
+    case 0: if (!SH) plane_launch_t<WB, 0, false>(s, l); break;
+    case 1: plane_launch_t<WB, 1, SH>(s, l); break;
+    case 2: plane_launch_t<WB, 2, SH>(s, l); break;
+    case 3: plane_launch_t<WB, 3, SH>(s, l); break;
+    case 4: plane_launch_t<WB, 4, SH>(s, l); break;
+    case 5: plane_launch_t<WB, 5, SH>(s, l); break;
+    default: plane_launch_t<WB, 6, SH>(s, l); break;
+  }
+}
+static void plane_launch(gm_solver* s, uint32_t l) {
+  const bool sh = s->world > 1;
+  if (s->pwb == 1) {
+    if (sh) plane_launch_w<1, true>(s, l);
+    else plane_launch_w<1, false>(s, l);
+  } else {
+    if (sh) plane_launch_w<2, true>(s, l);
+    else plane_launch_w<2, false>(s, l);
+  }
+}
+template <class F>
+static void plane_no_dispatch(uint32_t no, F&& f) {
+  switch (no) {
+    case 0: f(std::integral_constant<int, 0>()); break;
+    case 1: f(std::integral_constant<int, 1>()); break;
+    case 2: f(std::integral_constant<int, 2>()); break;
+    case 3: f(std::integral_constant<int, 3>()); break;
+    case 4: f(std::integral_constant<int, 4>()); break;
+    case 5: f(std::integral_constant<int, 5>()); break;
+    default: f(std::integral_constant<int, 6>()); break;
+  }
+}
+static void plane_reach_launch(gm_solver* s) {
+  const u64 nw = (u64)s->pg.nplanes * 32u;
+  const int grid = (int)std::min<u64>((nw + 255) / 256, (u64)std::min(s->grid, kCountSlots));
+  plane_no_dispatch(s->pg.no, [&](auto NO) {
+    hipLaunchKernelGGL((k_plane_reach<decltype(NO)::value>), dim3(grid), dim3(256), 0, s->stream, s->pbits, s->pg,
+                       s->bcount, s->st);
+  });
+}
+
+// per-level send / receive plane counts of a shard, as a fingerprint pair
+// (checked against the neighbours' before the first exchange: a mismatched
+// receive would wait forever)
+static void plane_sigs(const gm_solver* s, u64 out[2]) {
+  u64 a = 0xcbf29ce484222325ull, b = a;
+  for (size_t l = 0; l + 1 < s->psnd_off.size(); l++) {
+    a = (a ^ (s->psnd_off[l + 1] - s->psnd_off[l])) * 0x100000001b3ull;
+    b = (b ^ (s->prcv_off[l + 1] - s->prcv_off[l])) * 0x100000001b3ull;
+  }
+  out[0] = a;
+  out[1] = b;
+}
+
+// exchange the boundary planes of level l: every shard sends its send-
+// buffer segment of level l to rank + 1 and receives rank - 1's into its
+// receive buffer (mode 1 RCCL, 2 in-process copies, 3 host-staged)
+static int plane_exchange(std::vector<gm_solver*>& ss, uint32_t l, int mode, hipStream_t cs) {
+  const u64 pb = 1024ull * ss[0]->pwb;
+  if (mode == 2) {
+    const int n = (int)ss.size();
+    for (int r = 0; r < n; r++) {
+      gm_solver* a = ss[(size_t)r];
+      gm_solver* b = ss[(size_t)((r + 1) % n)];
+      const u64 ns = a->psnd_off[l + 1] - a->psnd_off[l], nr = b->prcv_off[l + 1] - b->prcv_off[l];
+      if (ns != nr) return fail(GM_ECORRUPT, "level %u: shard %d sends %llu planes, shard %d expects %llu", l, r,
+                                (unsigned long long)ns, (r + 1) % n, (unsigned long long)nr);
+      if (ns)
+        HIPCHK(hipMemcpyAsync((char*)b->precv + b->prcv_off[l] * pb, (const char*)a->psend + a->psnd_off[l] * pb,
+                              ns * pb, hipMemcpyDeviceToDevice, cs));
+    }
+    return 0;
+  }
+  gm_solver* s = ss[0];
+  const int up = (s->rank + 1) % s->world, down = (s->rank + s->world - 1) % s->world;
+  const u64 ns = s->psnd_off[l + 1] - s->psnd_off[l], nr = s->prcv_off[l + 1] - s->prcv_off[l];
+  void* sb = (char*)s->psend + s->psnd_off[l] * pb;
+  void* rb = (char*)s->precv + s->prcv_off[l] * pb;
+  if (mode == 1) {
+    ncclGroupStart();
+    ncclResult_t r1 = ns ? ncclSend(sb, ns * pb, ncclUint8, up, s->comm, cs) : ncclSuccess;
+    ncclResult_t r2 = nr ? ncclRecv(rb, nr * pb, ncclUint8, down, s->comm, cs) : ncclSuccess;
+    ncclResult_t r3 = ncclGroupEnd();
+    if (r1 != ncclSuccess || r2 != ncclSuccess || r3 != ncclSuccess)
+      return fail(GM_EHIP, "RCCL halo exchange: %s",
+                  ncclGetErrorString(r1 != ncclSuccess ? r1 : r2 != ncclSuccess ? r2 : r3));
+    return 0;
+  }
+  std::vector<HostRange> out, in;
+  if (ns) out.push_back({sb, ns * pb});
+  if (nr) in.push_back({rb, nr * pb});
+  return xfer_ranges(s, out, up, in, down, cs);
+}
+
+// before the first sharded solve: every shard's send plan must match its
+// successor's receive plan (fingerprints all-gathered)
+static int plane_check_plan(std::vector<gm_solver*>& ss, int mode, hipStream_t st) {
+  const int W = ss[0]->world;
+  std::vector<u64> all((size_t)2 * W);
+  if (mode == 2) {
+    for (gm_solver* s : ss) plane_sigs(s, &all[(size_t)2 * s->rank]);
+  } else {
+    u64 mine[2];
+    plane_sigs(ss[0], mine);
+    if (mode == 3) {
+      int rc = xfer_call(ss[0], GM_XFER_ALLGATHER, mine, sizeof mine, -1, all.data(), all.size() * 8, -1);
+      if (rc) return rc;
+    } else {
+      u64* dev = nullptr;
+      HIPCHK(hipMalloc((void**)&dev, (size_t)(2 + 2 * W) * 8));
+      HIPCHK(hipMemcpyAsync(dev, mine, sizeof mine, hipMemcpyHostToDevice, st));
+      ncclResult_t r = ncclAllGather(dev, dev + 2, 2, ncclUint64, ss[0]->comm, st);
+      hipError_t e = hipMemcpyAsync(all.data(), dev + 2, all.size() * 8, hipMemcpyDeviceToHost, st);
+      if (e == hipSuccess) e = hipStreamSynchronize(st);
+      (void)hipFree(dev);
+      if (r != ncclSuccess) return fail(GM_EHIP, "RCCL plan check: %s", ncclGetErrorString(r));
+      if (e != hipSuccess) return fail(GM_EHIP, "plan check: %s", hipGetErrorString(e));
+    }
+  }
+  for (int r = 0; r < W; r++)
+    if (all[(size_t)2 * r] != all[(size_t)2 * ((r + 1) % W) + 1])
+      return fail(GM_ECORRUPT, "halo plan mismatch: shard %d's sends vs shard %d's receives", r, (r + 1) % W);
+  for (gm_solver* s : ss) s->halo_ok = true;
+  return 0;
+}
+
+// The PLANES solve.  Steps (gm_solver_set_steps, one table only): 2T like
+// the other layouts; step 0 is the forward pass (reach map + counts), steps
+// 1..T-1 are empty, step T + l is plane level l (l <= S), later steps empty.
+static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
+  gm_solver* s0 = ss[0];
+  const Desc& d = s0->d;
+  const int T = d.max_levels;
+  const uint32_t S = s0->pS;
+  const int mode = s0->world <= 1 ? 0 : ss.size() != 1 ? 2 : s0->xfer ? 3 : 1;
+  if (mode == 1 && !s0->comm) return fail(GM_EINVAL, "shard %d/%d has no communicator (gm_solver_comm_init)", s0->rank, s0->world);
+  if (mode == 2) {
+    if ((int)ss.size() != s0->world) return fail(GM_EINVAL, "group solve needs all %d shards", s0->world);
+    for (size_t g = 0; g < ss.size(); g++)
+      if (ss[g]->rank != (int)g || ss[g]->stream != s0->stream || ss[g]->mode != GM_MODE_PLANES)
+        return fail(GM_EINVAL, "group shards must be ranks 0..n-1 on one stream");
+  }
+  const int first = mode == 0 ? (int)s0->step_first : 0;
+  const int stop = mode == 0 && s0->step_stop ? (int)s0->step_stop : 2 * T;
+  s0->step_first = s0->step_stop = 0;
+  const bool timing = (s0->flags & GM_F_KERNEL_TIMING) && first == 0 && stop == 2 * T;
+  hipStream_t st = s0->stream;
+  if (first > 0) {
+    uint32_t wb = 0;
+    HIPCHK(hipMemcpy(&wb, &s0->st->word_bits, sizeof wb, hipMemcpyDeviceToHost));
+    if (wb != 8 * s0->pwb) return fail(GM_EINVAL, "resume: the scratch holds no %u-bit planes solve", 8 * s0->pwb);
+  }
+  if (mode != 0 && !s0->halo_ok) {
+    int rc = plane_check_plan(ss, mode, st);
+    if (rc) return rc;
+  }
+  std::vector<hipEvent_t> ev;
+  auto new_event = [&](hipEvent_t* e) -> int {
+    HIPCHK(hipEventCreate(e));
+    ev.push_back(*e);
+    return 0;
+  };
+  auto cleanup = [&]() {
+    for (auto e : ev) (void)hipEventDestroy(e);
+  };
+  hipEvent_t e0, e1, e2;
+  if (new_event(&e0) || new_event(&e1) || new_event(&e2)) return GM_EHIP;
+  std::vector<hipEvent_t> kr;  // per-level start/stop (shard 0's launches)
+  hipEvent_t kx[2];
+  if (timing) {
+    kr.resize(2 * ((size_t)S + 1));
+    for (auto& e : kr)
+      if (new_event(&e)) return GM_EHIP;
+    if (new_event(&kx[0]) || new_event(&kx[1])) return GM_EHIP;
+  }
+  auto t0 = std::chrono::steady_clock::now();
+  HIPCHK(hipEventRecord(e0, st));
+  if (first == 0) {
+    for (gm_solver* s : ss) {
+      HIPCHK(hipMemsetAsync(s->st, 0, devstate_bytes(T), st));
+      HIPCHK(hipMemsetAsync(s->bcount, 0, kCountSlots * sizeof(BlockCount), st));
+      const uint32_t wb = 8 * s->pwb;
+      HIPCHK(hipMemcpyAsync(&s->st->word_bits, &wb, sizeof wb, hipMemcpyHostToDevice, st));
+    }
+    if (stop > 0) {
+      if (timing) HIPCHK(hipEventRecord(kx[0], st));
+      for (gm_solver* s : ss) plane_reach_launch(s);
+      if (timing) HIPCHK(hipEventRecord(kx[1], st));
+    }
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(e1, st));
+  for (uint32_t l = 0; l <= S; l++) {
+    const int k = T + (int)l;
+    if (k < first) continue;
+    if (k >= stop) break;
+    if (timing) HIPCHK(hipEventRecord(kr[2 * l], st));
+    for (gm_solver* s : ss) plane_launch(s, l);
+    if (timing) HIPCHK(hipEventRecord(kr[2 * l + 1], st));
+    if (mode != 0) {
+      int rc = plane_exchange(ss, l, mode, st);
+      if (rc) {
+        cleanup();
+        return rc;
+      }
+    }
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(e2, st));
+  if (stop < 2 * T) {
+    HIPCHK(hipStreamSynchronize(st));
+    cleanup();
+    out->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    out->word_bits = 8 * s0->pwb;
+    return GM_PARTIAL;
+  }
+  for (gm_solver* s : ss) {
+    if (s->pwb == 1)
+      hipLaunchKernelGGL(k_plane_root<1>, dim3(1), dim3(64), 0, st, s->d, s->pg, (const void*)s->ptab, s->pbits, s->st);
+    else
+      hipLaunchKernelGGL(k_plane_root<2>, dim3(1), dim3(64), 0, st, s->d, s->pg, (const void*)s->ptab, s->pbits, s->st);
+    hipLaunchKernelGGL(k_fill_red, dim3(1), dim3(1024), 0, st, s->st, s->bcount);
+  }
+  HIPCHK(hipGetLastError());
+  if (mode == 1) {
+    ncclGroupStart();
+    ncclResult_t r = ncclAllReduce(s0->st->red, s0->st->red, 4, ncclUint64, ncclSum, s0->comm, st);
+    ncclResult_t r2 = ncclAllGather(s0->st->red + 4, s0->errg, 1, ncclUint64, s0->comm, st);
+    ncclResult_t r3 = ncclGroupEnd();
+    if (r != ncclSuccess || r2 != ncclSuccess || r3 != ncclSuccess)
+      return fail(GM_EHIP, "RCCL allreduce: %s", ncclGetErrorString(r != ncclSuccess ? r : r2 != ncclSuccess ? r2 : r3));
+  }
+  u64 red[5] = {0, 0, 0, 0, 0};
+  for (gm_solver* s : ss) {
+    u64 r[5];
+    HIPCHK(hipMemcpyAsync(r, s->st->red, sizeof r, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (mode == 3) {
+      std::vector<u64> all((size_t)5 * s->world);
+      int rc = xfer_call(s, GM_XFER_ALLGATHER, r, sizeof r, -1, all.data(), all.size() * 8, -1);
+      if (rc) return rc;
+      for (int g = 0; g < s->world; g++)
+        for (int i = 0; i < 5; i++) red[i] = (i == 4) ? (red[i] | all[(size_t)g * 5 + i]) : red[i] + all[(size_t)g * 5 + i];
+      continue;
+    }
+    if (mode == 1) {
+      std::vector<u64> e((size_t)s->world);
+      HIPCHK(hipMemcpy(e.data(), s->errg, e.size() * sizeof(u64), hipMemcpyDeviceToHost));
+      r[4] = 0;
+      for (u64 x : e) r[4] |= x;
+    }
+    for (int i = 0; i < 5; i++) red[i] = (i == 4) ? (red[i] | r[i]) : red[i] + r[i];
+  }
+  auto t1 = std::chrono::steady_clock::now();
+  float f = 0, b = 0;
+  HIPCHK(hipEventElapsedTime(&f, e0, e1));
+  HIPCHK(hipEventElapsedTime(&b, e1, e2));
+  out->ms_forward = f;
+  out->ms_backward = b;
+  out->ms_total = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  if (timing) {
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, kx[0], kx[1]));
+    out->ms_expand_kernels = ms;
+    out->n_expand_launches = 1;
+    double sr = 0;
+    for (uint32_t l = 0; l <= S; l++) {
+      HIPCHK(hipEventElapsedTime(&ms, kr[2 * l], kr[2 * l + 1]));
+      sr += ms;
+    }
+    out->ms_resolve_kernels = sr;
+    out->n_resolve_launches = (uint64_t)S + 1;
+  }
+  cleanup();
+  out->positions = red[0];
+  out->edges = red[1];
+  out->primitives = red[2];
+  out->levels = (uint32_t)T;
+  out->max_level_width = 0;
+  out->word_bits = 8 * s0->pwb;
+  out->kernels = RK_PLANE | (PK_PLANE << 16);
+  const uint32_t word = red[3] ? (uint32_t)(red[3] - 1) : NO_WORD;
+  out->root_word = word;
+  if (red[4]) return fail(GM_ECORRUPT, "solve failed:%s", err_text((uint32_t)red[4]).c_str());
+  if (word == NO_WORD) return fail(GM_ECORRUPT, "root unresolved");
+  out->root_value = (int32_t)(word & 3u);
+  out->root_remoteness = word >> 2;
+  return 0;
+}
+
+static int plane_query(gm_solver* s, const uint64_t* keys_dev, uint64_t n, uint32_t* words_dev) {
+  const int grid = (int)std::min<u64>((n + kBlock - 1) / kBlock, (u64)s->grid);
+  if (s->pwb == 1)
+    hipLaunchKernelGGL(k_plane_query<1>, dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->pg, (const void*)s->ptab,
+                       s->pbits, (const u64*)keys_dev, n, words_dev);
+  else
+    hipLaunchKernelGGL(k_plane_query<2>, dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->pg, (const void*)s->ptab,
+                       s->pbits, (const u64*)keys_dev, n, words_dev);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s->stream));
+  return 0;
+}
+
+static int plane_positions(gm_solver* s, uint64_t* keys_dev, uint64_t cap, uint64_t* n) {
+  u64 cnt = 0;
+  HIPCHK(hipStreamSynchronize(s->stream));
+  HIPCHK(hipMemcpy(&cnt, &s->st->cursor_front, sizeof cnt, hipMemcpyDeviceToHost));
+  *n = cnt;
+  if (cnt > cap || !keys_dev) return cap < cnt ? fail(GM_EFULL, "need %llu slots", (unsigned long long)cnt) : 0;
+  HIPCHK(hipMemsetAsync(&s->st->cursor_back, 0, sizeof(u64), s->stream));
+  plane_no_dispatch(s->pg.no, [&](auto NO) {
+    hipLaunchKernelGGL((k_plane_positions<decltype(NO)::value>), dim3(s->grid), dim3(kBlock), 0, s->stream, s->d,
+                       s->pg, (const uint32_t*)s->pbits, (u64*)keys_dev, cap, &s->st->cursor_back);
+  });
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s->stream));
+  return 0;
+}
+
+static void plane_checksum_launch(gm_solver* s, u64* acc) {
+  plane_no_dispatch(s->pg.no, [&](auto NO) {
+    constexpr int N = decltype(NO)::value;
+    if (s->pwb == 1)
+      hipLaunchKernelGGL((k_plane_checksum<N, 1>), dim3(s->grid), dim3(kBlock), 0, s->stream, s->d, s->pg,
+                         (const void*)s->ptab, (const uint32_t*)s->pbits, acc);
+    else
+      hipLaunchKernelGGL((k_plane_checksum<N, 2>), dim3(s->grid), dim3(kBlock), 0, s->stream, s->d, s->pg,
+                         (const void*)s->ptab, (const uint32_t*)s->pbits, acc);
+  });
+}
+
+}  // extern "C++"

@@ -51,6 +51,7 @@
 #include "gm_codec.h"
 #include "gm_games.h"
 #include "gm_md5.h"
+#include "gm_plane.h"
 
 using namespace gm;
 typedef unsigned long long u64;
@@ -293,6 +294,18 @@ static u64 dense_words_bytes(const Desc* d, const DenseGeom& g, uint32_t wbits) 
 static u64 dense_bits_bytes(const Desc* d, const DenseGeom& g) {
   return (u64)d->max_levels * g.v.Wbl / 8;
 }
+
+struct gm_solver;
+struct PlaneShape;
+static bool plane_ok(const Desc* d);
+static bool plane_wanted(const Desc* d, uint32_t flags);
+static int plan_planes(const Desc* d, int rank, int world, uint32_t flags, uint64_t max_table_bytes, gm_plan_t* out,
+                       bool* fits);
+static int plane_setup(gm_solver* s, const gm_buffers* buf);
+static int run_planes(std::vector<gm_solver*> ss, gm_result* out);
+static int plane_query(gm_solver* s, const uint64_t* keys_dev, uint64_t n, uint32_t* words_dev);
+static int plane_positions(gm_solver* s, uint64_t* keys_dev, uint64_t cap, uint64_t* n);
+static void plane_checksum_launch(gm_solver* s, u64* acc);
 
 static const Desc* get_game(int id) {
   std::lock_guard<std::mutex> lk(g_mu);
@@ -885,8 +898,9 @@ enum DenseResolveKind : uint32_t {
   RK_QUAD_BAND = 5,  // k_dense_resolve4: 32-bit band sweeps (no list)
   RK_SCALAR = 6,     // k_dense_resolve: one prefix per lane (any bases; GM_F_RESOLVE_SCALAR)
   RK_HEX_LIST = 7,   // k_dense_resolve16p: world 1, 8-bit table, live-group lists
+  RK_PLANE = 8,      // k_plane_resolve: PLANES layout (gm_plane.h)
 };
-enum DensePullKind : uint32_t { PK_NONE = 0, PK_WORDS = 1, PK_LANE = 2 };
+enum DensePullKind : uint32_t { PK_NONE = 0, PK_WORDS = 1, PK_LANE = 2, PK_PLANE = 3 };
 
 struct gm_solver {
   Desc d;
@@ -962,6 +976,19 @@ struct gm_solver {
   u64* bktotal = nullptr;
   u64 meta_cap = 0;
   std::vector<BkLevel> lvh;  // host copy of the level table
+  // PLANES (gm_plane.h, gm_plane_run.h)
+  PlaneGeom pg{};
+  uint32_t pwb = 1;     // word bytes
+  uint32_t pS = 0;      // last plane level
+  void* ptab = nullptr;  // words
+  uint32_t* pbits = nullptr;  // reach map, 32 bits per plane row
+  void* precv = nullptr;  // shard halo planes received / sent (all levels)
+  void* psend = nullptr;
+  u64 pnrecv = 0, pnsend = 0;
+  const uint4* pzero = nullptr;  // 4 KB of zeros (absent neighbours)
+  const void* plist = nullptr;   // level lists (uint32 planes, or PlaneEntry for shards)
+  std::vector<u64> ploff;        // per level: first list entry
+  std::vector<u64> prcv_off, psnd_off;  // shards, per level: first halo plane received / sent
 };
 
 static const int kBlock = 256;
@@ -1502,6 +1529,13 @@ int gm_plan_shard(int game, int rank, int world, uint32_t flags, uint64_t max_ta
   out->scratch_bytes = scratch_bytes_for(d->max_levels);
   if (!d->dense_ok || (flags & GM_F_FORCE_HASHED))
     return fail(GM_EINVAL, "only DENSE layouts shard by prefix blocks; keyed tables shard by md5 owner");
+  if (plane_wanted(d, flags)) {
+    bool fits = false;
+    int rc = plan_planes(d, rank, world, flags, max_table_bytes, out, &fits);
+    if (rc) return rc;
+    if (!fits) return fail(GM_EFULL, "planes shard needs %llu bytes", (unsigned long long)out->table_bytes);
+    return 0;
+  }
   DenseGeom g;
   int grc = dense_geom(d, rank, world, &g);
   if (grc) return grc;
@@ -1573,6 +1607,15 @@ int gm_plan(int game, uint64_t positions, uint32_t flags, uint64_t max_table_byt
   memset(out, 0, sizeof *out);
   out->max_levels = (uint32_t)d->max_levels;
   out->scratch_bytes = scratch_bytes_for(d->max_levels);
+  if (d->dense_ok && plane_wanted(d, flags)) {
+    bool fits = false;
+    int rc = plan_planes(d, 0, 1, flags, max_table_bytes, out, &fits);
+    if (rc) return rc;
+    if (fits) return 0;
+    memset(out, 0, sizeof *out);
+    out->max_levels = (uint32_t)d->max_levels;
+    out->scratch_bytes = scratch_bytes_for(d->max_levels);
+  }
   if (d->dense_ok && !(flags & GM_F_FORCE_HASHED)) {
     bool fits = false;
     int rc = plan_dense(d, 0, 1, flags, max_table_bytes, out, &fits);
@@ -1722,6 +1765,9 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
     if (buf->table_bytes < need)
       return fail(GM_EINVAL, "dense table of %llu bytes, these flags need %llu (plan with the flags the solver is "
                              "created with)", (unsigned long long)buf->table_bytes, (unsigned long long)need);
+  } else if (buf->mode == GM_MODE_PLANES) {
+    if (!d->dense_ok || !plane_ok(d)) return fail(GM_EINVAL, "game has no planes layout");
+    if (world > 1 && (rank < 0 || rank >= world)) return fail(GM_EINVAL, "bad shard %d/%d", rank, world);
   } else if (buf->mode == GM_MODE_BUCKETED) {
     if (world != 1 || rank != 0) return fail(GM_EINVAL, "bucketed levels solve on one GPU (md5 shards use keyed tables)");
     if (!bk_ok(d)) return fail(GM_EINVAL, "bucketed levels need every move to advance one level");
@@ -1918,6 +1964,13 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
       return rc;
     }
   }
+  if (s->mode == GM_MODE_PLANES) {
+    int rc = plane_setup(s, buf);
+    if (rc) {
+      gm_solver_destroy(s);
+      return rc;
+    }
+  }
   *out = s;
   return 0;
 }
@@ -2039,6 +2092,7 @@ int gm_solver_solve(gm_solver* s, gm_result* out) {
   if (!s || !out) return fail(GM_EINVAL, "bad argument");
   memset(out, 0, sizeof *out);
   if (s->mode == GM_MODE_DENSE) return solve_dense(s, out);
+  if (s->mode == GM_MODE_PLANES) return run_planes({s}, out);
   if (s->mode == GM_MODE_BUCKETED) return solve_bucketed(s, out);
   if (s->world > 1) return fail(GM_EINVAL, "keyed-table shard %d/%d: drive it with gm_ks_* (md5 exchange)", s->rank, s->world);
   const int T = s->d.max_levels;
@@ -2290,6 +2344,8 @@ static int xfer_ranges(gm_solver* s, const std::vector<HostRange>& out, int sp, 
   if (rc) return rc;
   return stage_in(s, in, ns, cs);
 }
+
+#include "gm_plane_run.h"
 
 // after pull(L): bits of every block's bottom two own slices go down
 static int exchange_bits(std::vector<gm_solver*>& ss, u64 L, int mode, hipStream_t cs) {
@@ -3412,12 +3468,14 @@ int gm_solve_group(gm_solver** shards, int n, gm_result* out) {
   std::vector<gm_solver*> ss(shards, shards + n);
   for (gm_solver* s : ss)
     if (!s) return fail(GM_EINVAL, "null shard");
+  if (ss[0]->mode == GM_MODE_PLANES) return run_planes(ss, out);
   return run_dense(ss, out);
 }
 
 int gm_solver_query(gm_solver* s, const uint64_t* keys_dev, uint64_t n, uint32_t* words_dev) {
   if (!s || (n && (!keys_dev || !words_dev))) return fail(GM_EINVAL, "bad argument");
   if (!n) return 0;
+  if (s->mode == GM_MODE_PLANES) return plane_query(s, keys_dev, n, words_dev);
   int grid = (int)std::min<u64>((n + kBlock - 1) / kBlock, (u64)s->grid);
   if (s->mode == GM_MODE_DENSE)
     hipLaunchKernelGGL(k_dense_query, dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->view, s->words, s->bits,
@@ -3435,6 +3493,7 @@ int gm_solver_query(gm_solver* s, const uint64_t* keys_dev, uint64_t n, uint32_t
 
 int gm_solver_positions(gm_solver* s, uint64_t* keys_dev, uint64_t cap, uint64_t* n) {
   if (!s || !n) return fail(GM_EINVAL, "bad argument");
+  if (s->mode == GM_MODE_PLANES) return plane_positions(s, keys_dev, cap, n);
   if (s->mode == GM_MODE_BUCKETED) {  // every level's keys, contiguous
     u64 tot = 0;
     for (const BkLevel& x : s->lvh) tot += x.n;
@@ -3469,7 +3528,9 @@ int gm_solver_checksum(gm_solver* s, uint64_t out[6]) {
   if (!s || !out) return fail(GM_EINVAL, "bad argument");
   u64* acc = s->st->ck;
   HIPCHK(hipMemsetAsync(acc, 0, 6 * sizeof(u64), s->stream));
-  if (s->mode == GM_MODE_DENSE)
+  if (s->mode == GM_MODE_PLANES)
+    plane_checksum_launch(s, acc);
+  else if (s->mode == GM_MODE_DENSE)
     hipLaunchKernelGGL(k_checksum_dense, dim3(s->grid), dim3(kBlock), 0, s->stream, s->d, s->view, s->words, s->bits,
                        (u64)s->d.max_levels, s->wbits(), acc);
   else if (s->mode == GM_MODE_BUCKETED) {

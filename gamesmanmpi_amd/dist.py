@@ -1,4 +1,4 @@
-"""Multi-GPU drivers for DENSE solves.
+"""Multi-GPU drivers for PLANES and DENSE solves.
 
 The reference spreads a solve over MPI ranks by md5 ownership and one
 pickled message per tree edge (src/game_state.py:22-30,
@@ -26,9 +26,9 @@ class ShardedSolver(Solver):
     """Shard `rank` of `world` of a dense solve; needs an initialised
     torch.distributed default group (any backend) for the bootstrap."""
 
-    def __init__(self, spec, rank, world, device=None, transport="rccl", **kw):
+    def __init__(self, spec, rank, world, device=None, transport="rccl", layout="auto", **kw):
         super().__init__(spec, device=device, rank=rank, world=world,
-                         layout="dense", **kw)
+                         layout=layout, **kw)
         self._xfer = None
         if world > 1:
             if transport == "host":
@@ -108,7 +108,7 @@ def halo_sigs(spec, rank, world, flags=0):
     return out
 
 
-def group_solve(spec, world, device=None, kernel_timing=False, flags=0):
+def group_solve(spec, world, device=None, kernel_timing=False, flags=0, layout="auto"):
     """Solve all `world` shards in this process (one GPU, one stream).
     Returns (SolveResult of the whole job, [shard Solvers])."""
     import torch
@@ -117,7 +117,7 @@ def group_solve(spec, world, device=None, kernel_timing=False, flags=0):
     # one explicit stream for every shard (torch's default stream has handle
     # 0, which the ABI reads as "library-owned stream per solver")
     stream = torch.cuda.Stream(device=dev)
-    shards = [Solver(spec, device=dev, rank=g, world=world, layout="dense",
+    shards = [Solver(spec, device=dev, rank=g, world=world, layout=layout,
                      kernel_timing=kernel_timing, stream=stream, flags=flags)
               for g in range(world)]
     arr = (ctypes.c_void_p * world)(*[s.handle.value for s in shards])

@@ -49,10 +49,13 @@ class Solver:
     def __init__(self, spec, positions=0, device=None, kernel_timing=False,
                  layout="auto", max_table_bytes=0, rank=0, world=1,
                  stream=None, flags=0):
-        """layout: "auto" (dense when the descriptor supports it and the
-        table fits max_table_bytes; else bucketed levels when every move
-        advances one level; else the keyed hash table), "dense", "bucketed"
-        or "hashed" (the open-addressing hash table).
+        """layout: "auto" (planes, else the level-major dense table, when
+        the descriptor supports it and the table fits max_table_bytes; else
+        bucketed levels when every move advances one level; else the keyed
+        hash table), "planes" (sum games whose first two heaps hold 32
+        values: natural rank order, gm_plane.h), "dense" (the level-major
+        dense table), "bucketed" or "hashed" (the open-addressing hash
+        table).
         flags: kernel-family flags (_lib.GM_F_WORDS32 / GM_F_RESOLVE_SCALAR /
         GM_F_SHARD_INORDER, A/B runs), fixed for this solver's lifetime.
         rank/world > 1: this object is one shard of a dense multi-GPU solve
@@ -67,8 +70,8 @@ class Solver:
         self.spec = spec if isinstance(spec, GameSpec) else GameSpec(*spec)
         self.device = torch.device(device if device is not None else "cuda")
         self.kernel_timing = kernel_timing
-        if layout not in ("auto", "dense", "hashed", "bucketed"):
-            raise ValueError("layout must be auto, dense, bucketed or hashed")
+        if layout not in ("auto", "planes", "dense", "hashed", "bucketed"):
+            raise ValueError("layout must be auto, planes, dense, bucketed or hashed")
         self.layout = layout
         self.max_table_bytes = int(max_table_bytes)
         self.rank, self.world = int(rank), int(world)
@@ -87,7 +90,8 @@ class Solver:
         self._free()
         plan = _lib.gm_plan_t()
         flags = self.flags | {"hashed": _lib.GM_F_FORCE_HASHED | _lib.GM_F_HASH_TABLE,
-                              "bucketed": _lib.GM_F_FORCE_HASHED}.get(self.layout, 0)
+                              "bucketed": _lib.GM_F_FORCE_HASHED,
+                              "dense": _lib.GM_F_LEVEL_MAJOR}.get(self.layout, 0)
         if self.world > 1 and self.layout != "hashed":
             _lib.check(L.gm_plan_shard(self.spec.id, self.rank, self.world,
                                        flags, self.max_table_bytes,
@@ -98,6 +102,9 @@ class Solver:
         if self.layout == "dense" and plan.mode != _lib.GM_MODE_DENSE:
             raise ValueError("%r has no dense layout (or it does not fit)"
                              % (self.spec,))
+        if self.layout == "planes" and plan.mode != _lib.GM_MODE_PLANES:
+            raise ValueError("%r has no planes layout (heaps 0 and 1 of 32 "
+                             "values), or it does not fit" % (self.spec,))
         if self.layout == "bucketed" and plan.mode != _lib.GM_MODE_BUCKETED:
             raise ValueError("%r: bucketed levels need every move to advance "
                              "one level" % (self.spec,))
@@ -118,7 +125,7 @@ class Solver:
         b.scratch = scratch.data_ptr()
         b.scratch_bytes = plan.scratch_bytes
         b.stream = stream.cuda_stream
-        b.flags = self.flags | (_lib.GM_F_KERNEL_TIMING if self.kernel_timing else 0)
+        b.flags = flags | (_lib.GM_F_KERNEL_TIMING if self.kernel_timing else 0)
         b.mode = plan.mode
         b.table_bytes = plan.table_bytes
         self._bufs = b

@@ -67,6 +67,15 @@ typedef struct gm_slot {
  * (table_slots = edge capacity); dedup and lookups happen in LDS
  * (gamesmanmpi_amd/csrc/gm_bucketed.h). */
 #define GM_MODE_BUCKETED 2u
+/* PLANES (sum_four_to_one with heaps 0 and 1 of 32 values; the default for
+ * those): no levels at all in the layout -- every position's 8- or 16-bit
+ * order-form word in natural rank order, planes of 32 x 32 positions (heaps
+ * 0 and 1) with each row rotated by its row number, plus a 1-bit reach map;
+ * table_slots = positions.  The backward pass runs once per sum of the outer
+ * heaps (gamesmanmpi_amd/csrc/gm_plane.h).  Shards own round-robin blocks
+ * of the last heap's values and exchange two boundary slices per plane
+ * level; their table buffer also holds the halo send / receive areas. */
+#define GM_MODE_PLANES 3u
 
 /* Sizes the caller must allocate for a solve (see gm_plan). */
 typedef struct gm_plan_t {
@@ -113,6 +122,8 @@ typedef struct gm_buffers {
 #define GM_F_BK_EXACT 128u     /* BUCKETED: count every level's children first
                                   (exact partition offsets) instead of writing
                                   into provisioned partitions */
+#define GM_F_LEVEL_MAJOR 512u /* gm_plan / gm_plan_shard: the level-major DENSE
+                                  layout even where PLANES applies (A/B runs) */
 #define GM_F_GRAPH 256u       /* dense one-table full solves: capture the
                                   forward and backward launches as HIP graphs
                                   on the first solve, replay them after

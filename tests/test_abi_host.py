@@ -128,21 +128,30 @@ def test_plan_sizes():
     assert p.mode == _lib.GM_MODE_HASHED
     assert p.table_slots == 1 << 31 and p.level_capacity >= 1 << 30
     assert p.table_bytes == 16 << 31
+    # default: PLANES, one 8-bit word per position (natural rank order, no
+    # holes) + a 1-bit reach map
     _lib.check(_lib.load().gm_plan(s.id, 0, 0, 0, ctypes.byref(p)))
+    assert p.mode == _lib.GM_MODE_PLANES
+    assert p.table_slots == 1 << 30
+    assert p.table_bytes == (1 << 30) + (1 << 30) // 8
+    _lib.check(_lib.load().gm_plan(s.id, 0, _lib.GM_F_WORDS16, 0, ctypes.byref(p)))
+    assert p.mode == _lib.GM_MODE_PLANES and p.table_bytes == (2 << 30) + (1 << 30) // 8
+    # the level-major DENSE table on request
+    _lib.check(_lib.load().gm_plan(s.id, 0, _lib.GM_F_LEVEL_MAJOR, 0, ctypes.byref(p)))
     assert p.mode == _lib.GM_MODE_DENSE
     assert p.table_slots == 187 * 32 ** 5
     # 8-bit order-form words (one-GPU, remoteness < 255) + reach bitmap
     assert p.table_bytes == 1 * 187 * 32 ** 5 + 187 * 32 ** 5 // 8
     # the kernel-family flags plan 16- or 32-bit words (and the environment
     # does not: no knob is read from it)
-    _lib.check(_lib.load().gm_plan(s.id, 0, _lib.GM_F_WORDS16, 0, ctypes.byref(p)))
+    _lib.check(_lib.load().gm_plan(s.id, 0, _lib.GM_F_WORDS16 | _lib.GM_F_LEVEL_MAJOR, 0, ctypes.byref(p)))
     assert p.table_bytes == 2 * 187 * 32 ** 5 + 187 * 32 ** 5 // 8
     for f in (_lib.GM_F_WORDS32, _lib.GM_F_RESOLVE_SCALAR):
         _lib.check(_lib.load().gm_plan(s.id, 0, f, 0, ctypes.byref(p)))
         assert p.table_bytes == 4 * 187 * 32 ** 5 + 187 * 32 ** 5 // 8
     os.environ["GM_WORDS32"] = "1"
     try:
-        _lib.check(_lib.load().gm_plan(s.id, 0, 0, 0, ctypes.byref(p)))
+        _lib.check(_lib.load().gm_plan(s.id, 0, _lib.GM_F_LEVEL_MAJOR, 0, ctypes.byref(p)))
         assert p.table_bytes == 1 * 187 * 32 ** 5 + 187 * 32 ** 5 // 8
     finally:
         del os.environ["GM_WORDS32"]

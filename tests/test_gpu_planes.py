@@ -1,0 +1,202 @@
+"""PLANES layout (gamesmanmpi_amd/csrc/gm_plane.h): sum_four_to_one with heaps
+0 and 1 of 32 values, every position's order-form word in natural rank
+order, resolved plane level by plane level.
+
+Checked against the CPU oracle (oracle/oracle.c, pinned to the reference's
+own game modules by tests/test_oracle.py) position by position on small
+shapes, against the level-major DENSE layout word for word, and at full size
+(2^30, and the 2-, 4- and 8-GPU bench shapes 2^31..2^33 as in-process shard
+groups) by whole-solve fingerprints against tests/golden/checksums.json
+(oracle/oracle_mt.c)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def _planes(params, **kw):
+    from gamesmanmpi_amd.games import GameSpec
+    from gamesmanmpi_amd.solver import Solver
+    s = Solver(GameSpec("sum_four_to_one", params), layout="planes", **kw)
+    return s, s.solve()
+
+
+def _oracle(params):
+    """The CPU restatement's row solver (oracle/oracle_mt.c, pinned to the
+    DFS oracle and the reference-generated tables by tests/test_oracle.py):
+    stats + the word (value | remoteness << 2) of every rank."""
+    from oracle.oracle import Game
+    sol = Game("sum_four_to_one", params).solve_rows()
+    sol.refresh(True)
+    return sol
+
+
+def _oracle_words(sol, n):
+    return np.array([sol.word(k) for k in range(n)], np.uint32)
+
+
+@pytest.mark.parametrize("params", ["heaps=31:31", "heaps=31:31:1", "heaps=31:31:3", "heaps=31:31:2:5",
+                                    "heaps=31:31:4:0:2", "heaps=31:31:7:7"])
+def test_planes_match_oracle(params):
+    """Every position's value and remoteness (and the counts / root line)
+    equal the oracle's, including non-power-of-two and zero-height outer
+    heaps and the plane-less K = 2 shape."""
+    s, r = _planes(params)
+    sol = _oracle(params)
+    assert r.extra["layout"] == "planes" and r.extra["resolve_kernel"] == "k_plane_resolve"
+    assert (r.positions, r.edges, r.primitives, r.root_line) == (sol.count, sol.edges, sol.stats["primitives"],
+                                                                  sol.root_line)
+    keys, val, rem = s.dump()
+    assert len(keys) == sol.count
+    np.testing.assert_array_equal(np.sort(keys), np.arange(sol.count, dtype=np.uint64))
+    want = _oracle_words(sol, sol.count)[keys.astype(np.int64)]
+    np.testing.assert_array_equal(val, want & 3)
+    np.testing.assert_array_equal(rem, want >> 2)
+    ck = s.checksum()
+    assert (ck["checksum"], ck["win"], ck["loss"]) == ("%016x" % sol.stats["checksum"], sol.stats["win"],
+                                                       sol.stats["loss"])
+
+
+def test_planes_words16_equal_words8():
+    """16-bit order forms (GM_F_WORDS16) give the same words as 8-bit."""
+    from gamesmanmpi_amd import _lib
+    params = "heaps=31:31:15:15"
+    s8, r8 = _planes(params)
+    s16, r16 = _planes(params, flags=_lib.GM_F_WORDS16)
+    assert (r8.extra["word_bits"], r16.extra["word_bits"]) == (8, 16)
+    assert r8.root_line == r16.root_line
+    keys = np.arange(32 * 32 * 16 * 16, dtype=np.uint64)
+    np.testing.assert_array_equal(s8.query(keys), s16.query(keys))
+
+
+def test_planes_equal_level_major():
+    """PLANES and the level-major DENSE table agree word for word (and on
+    keys outside the state space: GM_NO_WORD)."""
+    from gamesmanmpi_amd.games import GameSpec
+    from gamesmanmpi_amd.solver import Solver
+    params = "heaps=31:31:31:7"
+    s, r = _planes(params)
+    d = Solver(GameSpec("sum_four_to_one", params), layout="dense")
+    rd = d.solve()
+    assert (r.positions, r.edges, r.primitives, r.root_line) == (rd.positions, rd.edges, rd.primitives, rd.root_line)
+    keys = np.arange(32 * 32 * 32 * 8 + 5, dtype=np.uint64)
+    w = s.query(keys)
+    np.testing.assert_array_equal(w, d.query(keys))
+    assert (w[-5:] == 0xFFFFFFFF).all()
+
+
+def test_planes_positions_and_checksum_match_level_major():
+    from gamesmanmpi_amd.games import GameSpec
+    from gamesmanmpi_amd.solver import Solver
+    params = "heaps=31:31:6:9"
+    s, _ = _planes(params)
+    d = Solver(GameSpec("sum_four_to_one", params), layout="dense")
+    d.solve()
+    np.testing.assert_array_equal(np.sort(s.positions()), np.sort(d.positions()))
+    assert s.checksum() == d.checksum()
+
+
+def _gold(name):
+    with open(os.path.join(GOLDEN, "checksums.json")) as f:
+        return json.load(f)[name]
+
+
+def _check_gold(e, r, cks):
+    assert (r.positions, r.edges, r.primitives, r.root_line) == (e["positions"], e["edges"], e["primitives"],
+                                                                  e["root_line"])
+    tot = sum(int(c["checksum"], 16) for c in cks) % (1 << 64)
+    assert "%016x" % tot == e["checksum"]
+    assert sum(c["positions"] for c in cks) == e["positions"]
+    assert (sum(c["win"] for c in cks), sum(c["loss"] for c in cks)) == (e["win"], e["loss"])
+
+
+def test_planes_sum_31x6_checksum():
+    """BASELINE config 4, the bench shape (2^30 positions): every position's
+    value and remoteness by fingerprint against the CPU restatement."""
+    e = _gold("sum_31x6")
+    s, r = _planes(e["params"])
+    assert r.extra["word_bits"] == 8
+    _check_gold(e, r, [s.checksum()])
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+def test_planes_group_matches_single(world):
+    """Shards of the PLANES layout (round-robin blocks of the last heap,
+    boundary slices exchanged per plane level) solved as an in-process
+    group: every position answered by exactly one shard, word-equal to the
+    one-table solve."""
+    from gamesmanmpi_amd.dist import group_solve
+    from gamesmanmpi_amd.games import GameSpec
+    params = "heaps=31:31:3:23" if world == 3 else "heaps=31:31:3:15"
+    s1, r1 = _planes(params)
+    rg, shards = group_solve(GameSpec("sum_four_to_one", params), world)
+    assert rg.extra["layout"] == "planes"
+    assert (rg.positions, rg.edges, rg.primitives, rg.root_line) == (r1.positions, r1.edges, r1.primitives,
+                                                                      r1.root_line)
+    keys = s1.positions()
+    want = s1.query(keys)
+    out = np.full(len(keys), 0xFFFFFFFF, np.uint32)
+    hits = np.zeros(len(keys), np.int64)
+    for sh in shards:
+        w = sh.query(keys)
+        own = w != 0xFFFFFFFF
+        out[own] = w[own]
+        hits += own
+    assert (hits == 1).all()
+    np.testing.assert_array_equal(out, want)
+    assert sum(len(sh.positions()) for sh in shards) == len(keys)
+
+
+def test_planes_group_matches_oracle():
+    from gamesmanmpi_amd.dist import group_solve
+    from gamesmanmpi_amd.games import GameSpec
+    params = "heaps=31:31:2:7"
+    rg, shards = group_solve(GameSpec("sum_four_to_one", params), 2)
+    sol = _oracle(params)
+    assert (rg.positions, rg.edges, rg.root_line) == (sol.count, sol.edges, sol.root_line)
+    keys = np.arange(sol.count, dtype=np.uint64)
+    want = _oracle_words(sol, sol.count)
+    got = np.full(sol.count, 0xFFFFFFFF, np.uint32)
+    for sh in shards:
+        w = sh.query(keys)
+        own = w != 0xFFFFFFFF
+        assert (got[own] == 0xFFFFFFFF).all()
+        got[own] = w[own]
+    np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("world,name", [(2, "sum_31x5_63"), (4, "sum_31x5_127"), (8, "sum_31x5_255")])
+def test_planes_bench_shapes_as_groups(world, name):
+    """The N = 2 / 4 / 8 bench workloads (31^5 x (32N - 1): 2^31 / 2^32 /
+    2^33 positions, blocks of 8 top values, four per rank) solved as
+    in-process shard groups on one GPU, checked by the sum of the shards'
+    fingerprints against the CPU restatement's golden."""
+    import torch
+    from gamesmanmpi_amd.dist import group_solve
+    from gamesmanmpi_amd.games import GameSpec
+    e = _gold(name)
+    rg, shards = group_solve(GameSpec("sum_four_to_one", e["params"]), world)
+    assert rg.extra["layout"] == "planes"
+    _check_gold(e, rg, [sh.checksum() for sh in shards])
+    del shards
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("cut", [1, 187, 187 + 40, 187 + 124])
+def test_planes_stop_resume(cut):
+    """Stop after step `cut` (forward; mid-backward; the last plane level)
+    and resume in the same solver: identical words and counts."""
+    params = "heaps=31:31:31:31:31:31"
+    e = _gold("sum_31x6")
+    from gamesmanmpi_amd.games import GameSpec
+    from gamesmanmpi_amd.solver import Solver
+    s = Solver(GameSpec("sum_four_to_one", e["params"]), layout="planes")
+    assert s.solve_steps(0, cut) is None
+    r = s.solve_steps(cut, 0)
+    _check_gold(e, r, [s.checksum()])
+    del params
