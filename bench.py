@@ -101,6 +101,37 @@ def dense_bytes(heaps, word_bytes):
             "pull_per_edge": (E + P) / 8.0}
 
 
+def plane_bytes(heaps, word_bytes):
+    """Per-solve byte models of the PLANES layout (planes of
+    32 x 32 positions, plane level l = sum of the outer heaps 2..K-1).
+    compulsory -- what any schedule of this layout must move from HBM:
+      resolve(l): the level's own planes written + the planes of levels l-1
+                  and l-2 (its children's planes) read once
+                  = w KiB x (n(l) + n(l-1) + n(l-2));
+      reach:      one bit per position written.
+    requested -- what the kernel asks of the memory system: own plane
+      written + every neighbour plane row read (one per outer heap and move
+      that exists), L2 / Infinity-Cache hits included."""
+    outer = heaps[2:]
+    n = [1]
+    for h in outer:
+        m = [0] * (len(n) + h)
+        for i, v in enumerate(n):
+            for j in range(h + 1):
+                m[i + j] += v
+        n = m
+    pb = 1024 * word_bytes
+    nx = lambda k: n[k] if 0 <= k < len(n) else 0  # noqa: E731
+    comp = sum(pb * (n[l] + nx(l - 1) + nx(l - 2)) for l in range(len(n)))
+    planes = 1
+    for h in outer:
+        planes *= h + 1
+    nbr = sum(planes * sum(min(v, 2) for v in range(h + 1)) // (h + 1) for h in outer)
+    P = planes * 1024
+    return {"resolve_compulsory": comp, "resolve_requested": pb * (planes + nbr),
+            "pull_compulsory": P / 8.0, "pull_requested": P / 8.0, "launches": len(n)}
+
+
 def keyed_bytes(positions, edges):
     """SURVEY §8d algorithmic bytes of the keyed table: expand 24 B/position
     + 8 B/edge, resolve 12 B/position + 12 B/edge (8-B keys, 4-B words)."""
@@ -152,11 +183,20 @@ def cpu_baseline(params):
     t0 = time.perf_counter()
     sol = g.solve_rows()
     dt = time.perf_counter() - t0
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        allowed = os.cpu_count() or 0
+    omp = os.environ.get("OMP_NUM_THREADS")
+    why = ("OMP_NUM_THREADS=%s, set by the GPU box's environment as this job's CPU share "
+           "(the harness asks that it be left as is)" % omp) if omp else "every CPU the process may run on"
     out = {"value": sol.count / dt, "unit": "positions/s", "cores": threads(),
            "kind": "port",
-           "sample": "full workload: oracle/oracle_mt.c row solver (OpenMP, %d threads; "
-                     "host nproc %d), sum_four_to_one %s: %d positions, %d edges, root %s, %.2f s"
-                     % (threads(), os.cpu_count() or 0, params, sol.count, sol.edges,
+           "sample": "full workload: oracle/oracle_mt.c row solver (OpenMP, %d threads = %s; host nproc %d, "
+                     "CPUs in this process's affinity mask %d), sum_four_to_one %s: %d positions, %d edges, "
+                     "root %s, %.2f s.  For scale: the reference's own Python job loop solves mttt (5,478 "
+                     "positions) at ~84 positions/s on one core (SURVEY.md section 6)"
+                     % (threads(), why, os.cpu_count() or 0, allowed, params, sol.count, sol.edges,
                         sol.root_line, dt)}
     return out, sol.root_line
 
@@ -220,7 +260,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-keyed", action="store_true",
                     help="skip the toot 6x4 keyed-table sub-record")
-    ap.add_argument("--layout", default="auto", choices=["auto", "dense", "hashed"])
+    ap.add_argument("--layout", default="auto", choices=["auto", "planes", "dense", "hashed"])
     ap.add_argument("--transport", default="rccl", choices=["rccl", "host"],
                     help="N>1 halo exchange: RCCL (one GPU per rank), or host-staged over "
                          "gloo -- every rank on cuda:0, for rehearsing the N-rank bench on "
@@ -291,7 +331,14 @@ def main():
     solver.set_kernel_timing(False)
     word_bits = tr.extra.get("word_bits", 32) or 32
     workload = "sum_four_to_one heaps=%s" % ":".join(map(str, heaps))
-    if layout == "dense":
+    if layout == "planes":
+        m = plane_bytes(heaps, word_bits // 8)
+        model = {"resolve_compulsory": m["resolve_compulsory"] / world,
+                 "pull_compulsory": m["pull_compulsory"] / world,
+                 "resolve_per_edge": m["resolve_requested"] / world,
+                 "pull_per_edge": m["pull_requested"] / world}
+        resolve_k, pull_k = tr.extra.get("resolve_kernel", "?"), tr.extra.get("pull_kernel", "?")
+    elif layout == "dense":
         model = dense_bytes(heaps if world == 1 else heaps[:-1] + [(heaps[-1] + 1) // world - 1],
                             word_bits // 8)
         resolve_k, pull_k = tr.extra.get("resolve_kernel", "?"), tr.extra.get("pull_kernel", "?")
@@ -318,10 +365,15 @@ def main():
             "frac_per_edge_model": (ke / kn) / t_launch / 1e9 / HBM_PEAK_GBS,
             "algorithmic_bytes_per_launch": kb / kn,
             "per_edge_model_bytes_per_launch": ke / kn,
-            "model": ("compulsory bytes of the dense layout: resolve (3w + 1/8) B per position "
-                      "(own %d-bit word written, live words of rows L+1 and L+2 read once, reach "
-                      "bit); pull 3/8 B per position" % word_bits if layout == "dense" else
-                      "SURVEY 8d keyed: expand 24 B/position + 8 B/edge, resolve 12 B/position + 12 B/edge"),
+            "model": ({"planes": "compulsory bytes of the PLANES layout: per plane level, the level's own "
+                                 "%d-bit words written + the planes of the two child levels read once "
+                                 "(w KiB x (n(l) + n(l-1) + n(l-2)) per launch); frac_per_edge_model = every "
+                                 "neighbour-plane row the kernel requests (L2/MALL hits included)" % word_bits,
+                       "dense": "compulsory bytes of the dense layout: resolve (3w + 1/8) B per position "
+                                "(own %d-bit word written, live words of rows L+1 and L+2 read once, reach "
+                                "bit); pull 3/8 B per position" % word_bits}.get(
+                          layout, "SURVEY 8d keyed: expand 24 B/position + 8 B/edge, resolve 12 B/position + "
+                                  "12 B/edge")),
             "launches": kn, "ms_kernel_total": kms, "ms_per_launch": kms / kn,
             "algorithmic_bytes_total": kb}
 
@@ -353,8 +405,8 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": ("u%d order-form words, integer (dense table: keys implicit in the slot)" % word_bits
-                  if layout == "dense" else "u64 keys / u32 words, integer"),
+        "dtype": ("u%d order-form words, integer (%s table: keys implicit in the slot)" % (word_bits, layout)
+                  if layout in ("dense", "planes") else "u64 keys / u32 words, integer"),
         "data": "synthetic: sum of Four-To-One heaps, fully determined state space",
         "config": {"workload": workload,
                    "positions_per_gpu": P // world, "edges_per_gpu": E // world,

@@ -27,12 +27,13 @@ GM_F_WORDS16 = 64  # dense: 16-bit words where 8-bit ones would be chosen
 GM_F_BK_EXACT = 128  # bucketed: count pass + exact partition offsets
 GM_F_GRAPH = 256  # dense one-table solves replay captured HIP graphs
 GM_F_LEVEL_MAJOR = 512  # the level-major DENSE layout where PLANES would apply
+GM_F_PLANE_X1 = 1024  # PLANES A/B: one plane per half-wave (k_plane_resolve)
 KERNEL_FLAGS = (GM_F_WORDS32 | GM_F_RESOLVE_SCALAR | GM_F_SHARD_INORDER | GM_F_WORDS16 | GM_F_BK_EXACT
-                | GM_F_GRAPH | GM_F_LEVEL_MAJOR)
+                | GM_F_GRAPH | GM_F_LEVEL_MAJOR | GM_F_PLANE_X1)
 # gm_result.kernels codes (gm_solver.hip DenseResolveKind / DensePullKind)
 RESOLVE_KERNELS = {1: "k_dense_resolve8p", 2: "k_dense_resolve8c", 3: "k_dense_resolve4p",
                    4: "k_dense_resolve4c", 5: "k_dense_resolve4", 6: "k_dense_resolve",
-                   7: "k_dense_resolve16p", 8: "k_plane_resolve"}
+                   7: "k_dense_resolve16p", 8: "k_plane_resolve", 9: "k_plane_resolve_x2"}
 PULL_KERNELS = {1: "k_dense_pull_words", 2: "k_dense_pull", 3: "k_plane_reach"}
 GM_MODE_HASHED, GM_MODE_DENSE, GM_MODE_BUCKETED, GM_MODE_PLANES = 0, 1, 2, 3
 # host-staged transport (include/gamesman.h gm_xfer_fn)

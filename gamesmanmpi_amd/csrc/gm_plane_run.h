@@ -393,17 +393,29 @@ static int plane_setup(gm_solver* s, const gm_buffers* buf) {
 // ---------------------------------------------------------------------------
 // host: launches
 // ---------------------------------------------------------------------------
+// kernel family: two planes per half-wave in packed 16-bit lanes for 8-bit
+// words (1.65 vs 1.87 ms per 2^30 backward); one plane per half-wave for
+// 16-bit words, where the packed form's register and byte footprint made it
+// slower (3.80 vs 2.77 ms; profiles/r03b_plane_proto.txt); GM_F_PLANE_X1
+// forces the one-plane form (A/B)
+static bool plane_x1(const gm_solver* s) { return s->pwb == 2 || (s->flags & GM_F_PLANE_X1); }
+
 template <int WB, int NO, bool SH>
 static void plane_launch_t(gm_solver* s, uint32_t l) {
   const u64 a = s->ploff[l], n = s->ploff[l + 1] - a;
   if (!n) return;
-  const u64 waves = (n + 1) / 2;
+  const bool x1 = plane_x1(s);
+  const u64 waves = x1 ? (n + 1) / 2 : (n + 3) / 4;
   u64 blocks = (waves + 3) / 4;
   blocks = std::min<u64>((blocks + 7) & ~7ull, (u64)s->grid * 4);  // plane_share loops past the grid
   typedef typename PlaneWord<WB>::T T;
   const void* list = (const char*)s->plist + a * (SH ? sizeof(PlaneEntry) : 4);
-  hipLaunchKernelGGL((k_plane_resolve<WB, NO, SH>), dim3((uint32_t)blocks), dim3(256), 0, s->stream, (T*)s->ptab, list,
-                     (uint32_t)n, s->pg, s->pzero, (const T*)s->precv, (T*)s->psend);
+  if (x1)
+    hipLaunchKernelGGL((k_plane_resolve<WB, NO, SH>), dim3((uint32_t)blocks), dim3(256), 0, s->stream, (T*)s->ptab,
+                       list, (uint32_t)n, s->pg, s->pzero, (const T*)s->precv, (T*)s->psend);
+  else
+    hipLaunchKernelGGL((k_plane_resolve_x2<WB, NO, SH>), dim3((uint32_t)blocks), dim3(256), 0, s->stream,
+                       (T*)s->ptab, list, (uint32_t)n, s->pg, s->pzero, (const T*)s->precv, (T*)s->psend);
 }
 template <int WB, bool SH>
 static void plane_launch_w(gm_solver* s, uint32_t l) {
@@ -687,7 +699,7 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
   out->levels = (uint32_t)T;
   out->max_level_width = 0;
   out->word_bits = 8 * s0->pwb;
-  out->kernels = RK_PLANE | (PK_PLANE << 16);
+  out->kernels = (plane_x1(s0) ? RK_PLANE : RK_PLANE_X2) | (PK_PLANE << 16);
   const uint32_t word = red[3] ? (uint32_t)(red[3] - 1) : NO_WORD;
   out->root_word = word;
   if (red[4]) return fail(GM_ECORRUPT, "solve failed:%s", err_text((uint32_t)red[4]).c_str());

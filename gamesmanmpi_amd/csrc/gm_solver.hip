@@ -898,7 +898,8 @@ enum DenseResolveKind : uint32_t {
   RK_QUAD_BAND = 5,  // k_dense_resolve4: 32-bit band sweeps (no list)
   RK_SCALAR = 6,     // k_dense_resolve: one prefix per lane (any bases; GM_F_RESOLVE_SCALAR)
   RK_HEX_LIST = 7,   // k_dense_resolve16p: world 1, 8-bit table, live-group lists
-  RK_PLANE = 8,      // k_plane_resolve: PLANES layout (gm_plane.h)
+  RK_PLANE = 8,      // k_plane_resolve: PLANES layout (gm_plane.h), one plane per half-wave
+  RK_PLANE_X2 = 9,   // k_plane_resolve_x2: two planes per half-wave, packed 16-bit lanes
 };
 enum DensePullKind : uint32_t { PK_NONE = 0, PK_WORDS = 1, PK_LANE = 2, PK_PLANE = 3 };
 

@@ -124,6 +124,9 @@ typedef struct gm_buffers {
                                   into provisioned partitions */
 #define GM_F_LEVEL_MAJOR 512u /* gm_plan / gm_plan_shard: the level-major DENSE
                                   layout even where PLANES applies (A/B runs) */
+#define GM_F_PLANE_X1 1024u   /* PLANES: one plane per half-wave in 32-bit lanes
+                                  (k_plane_resolve) instead of two per half-wave
+                                  in packed 16-bit lanes (A/B runs) */
 #define GM_F_GRAPH 256u       /* dense one-table full solves: capture the
                                   forward and backward launches as HIP graphs
                                   on the first solve, replay them after

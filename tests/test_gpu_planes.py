@@ -48,7 +48,7 @@ def test_planes_match_oracle(params):
     heaps and the plane-less K = 2 shape."""
     s, r = _planes(params)
     sol = _oracle(params)
-    assert r.extra["layout"] == "planes" and r.extra["resolve_kernel"] == "k_plane_resolve"
+    assert r.extra["layout"] == "planes" and r.extra["resolve_kernel"] == "k_plane_resolve_x2"  # 8-bit words
     assert (r.positions, r.edges, r.primitives, r.root_line) == (sol.count, sol.edges, sol.stats["primitives"],
                                                                   sol.root_line)
     keys, val, rem = s.dump()
@@ -62,16 +62,23 @@ def test_planes_match_oracle(params):
                                                        sol.stats["loss"])
 
 
-def test_planes_words16_equal_words8():
-    """16-bit order forms (GM_F_WORDS16) give the same words as 8-bit."""
+def test_planes_kernel_families_agree():
+    """16-bit order forms (GM_F_WORDS16, k_plane_resolve) and the one-plane
+    kernel on 8-bit words (GM_F_PLANE_X1) give the same words as the
+    default packed 8-bit kernel."""
     from gamesmanmpi_amd import _lib
     params = "heaps=31:31:15:15"
     s8, r8 = _planes(params)
     s16, r16 = _planes(params, flags=_lib.GM_F_WORDS16)
-    assert (r8.extra["word_bits"], r16.extra["word_bits"]) == (8, 16)
-    assert r8.root_line == r16.root_line
+    s1, r1 = _planes(params, flags=_lib.GM_F_PLANE_X1)
+    assert (r8.extra["word_bits"], r16.extra["word_bits"], r1.extra["word_bits"]) == (8, 16, 8)
+    assert (r8.extra["resolve_kernel"], r16.extra["resolve_kernel"], r1.extra["resolve_kernel"]) == (
+        "k_plane_resolve_x2", "k_plane_resolve", "k_plane_resolve")
+    assert r8.root_line == r16.root_line == r1.root_line
     keys = np.arange(32 * 32 * 16 * 16, dtype=np.uint64)
-    np.testing.assert_array_equal(s8.query(keys), s16.query(keys))
+    w = s8.query(keys)
+    np.testing.assert_array_equal(w, s16.query(keys))
+    np.testing.assert_array_equal(w, s1.query(keys))
 
 
 def test_planes_equal_level_major():

@@ -25,14 +25,20 @@ using namespace gm;
     }                                                                                  \
   } while (0)
 
+static int g_x2 = 1;
 template <int WB, int NO>
 static void launch(void* tab, const uint32_t* list, uint32_t n, const PlaneGeom& g, const uint4* zero,
                    hipStream_t st) {
-  const uint32_t waves = (n + 1) / 2;
+  typedef typename PlaneWord<WB>::T T;
+  const uint32_t waves = g_x2 ? (n + 3) / 4 : (n + 1) / 2;
   uint32_t blocks = (waves + 3) / 4;
   blocks = (blocks + 7) / 8 * 8;
-  hipLaunchKernelGGL((k_plane_resolve<WB, NO>), dim3(blocks), dim3(256), 0, st, (typename PlaneWord<WB>::T*)tab,
-                     list, n, g, zero);
+  if (g_x2)
+    hipLaunchKernelGGL((k_plane_resolve_x2<WB, NO, false>), dim3(blocks), dim3(256), 0, st, (T*)tab, list, n, g, zero,
+                       (const T*)nullptr, (T*)nullptr);
+  else
+    hipLaunchKernelGGL((k_plane_resolve<WB, NO, false>), dim3(blocks), dim3(256), 0, st, (T*)tab, list, n, g, zero,
+                       (const T*)nullptr, (T*)nullptr);
 }
 
 int main(int argc, char** argv) {
@@ -40,11 +46,13 @@ int main(int argc, char** argv) {
   const int top = argc > 2 ? atoi(argv[2]) : 31;
   const int WB = argc > 3 ? atoi(argv[3]) : 1;
   const int reps = argc > 4 ? atoi(argv[4]) : 10;
+  g_x2 = argc > 5 ? atoi(argv[5]) : 1;
   std::vector<int> heaps(K, 31);
   heaps[K - 1] = top;
   PlaneGeom g{};
   g.no = K - 2;
   g.pow2 = 1;
+  g.world = 1;
   uint64_t np = 1;
   int root_sum = 0;
   for (int h : heaps) root_sum += h;
@@ -127,8 +135,8 @@ int main(int argc, char** argv) {
     sum += t;
   }
   const double P = (double)np * 1024;
-  printf("K=%d top=%d wb=%d planes=%llu levels=%d positions=%.0f backward best %.3f ms mean %.3f ms (%.3g pos/s)\n",
-         K, top, WB, (unsigned long long)np, S + 1, P, best, sum / reps, P / (best * 1e-3));
+  printf("x%d K=%d top=%d wb=%d planes=%llu levels=%d positions=%.0f backward best %.3f ms mean %.3f ms (%.3g pos/s)\n",
+         g_x2 ? 2 : 1, K, top, WB, (unsigned long long)np, S + 1, P, best, sum / reps, P / (best * 1e-3));
   // root
   std::vector<uint8_t> host(tbytes);
   CK(hipMemcpy(host.data(), tab, tbytes, hipMemcpyDeviceToHost));
