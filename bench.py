@@ -374,6 +374,10 @@ def main():
                                 "bit); pull 3/8 B per position" % word_bits}.get(
                           layout, "SURVEY 8d keyed: expand 24 B/position + 8 B/edge, resolve 12 B/position + "
                                   "12 B/edge")),
+            "timing": ("HIP events on the solve stream in an extra solve of the same launch schedule: "
+                       + ("one event pair around the whole backward (nothing but the %d resolve launches), "
+                          "average = span / launches" % kn if layout == "planes" and world == 1 else
+                          "an event pair around each launch, summed")),
             "launches": kn, "ms_kernel_total": kms, "ms_per_launch": kms / kn,
             "algorithmic_bytes_total": kb}
 

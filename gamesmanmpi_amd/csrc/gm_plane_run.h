@@ -611,13 +611,18 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(e1, st));
+  // kernel timing: one table -- the backward is nothing but the resolve
+  // launches, so one event pair around all of them (no events between
+  // launches: they would add their own gaps to what they time); shards --
+  // a pair around each level's launches (exchanges sit between them)
+  const bool per_level = timing && mode != 0;
   for (uint32_t l = 0; l <= S; l++) {
     const int k = T + (int)l;
     if (k < first) continue;
     if (k >= stop) break;
-    if (timing) HIPCHK(hipEventRecord(kr[2 * l], st));
+    if (per_level || (timing && l == 0)) HIPCHK(hipEventRecord(kr[2 * l], st));
     for (gm_solver* s : ss) plane_launch(s, l);
-    if (timing) HIPCHK(hipEventRecord(kr[2 * l + 1], st));
+    if (per_level || (timing && l == S)) HIPCHK(hipEventRecord(kr[2 * l + 1], st));
     if (mode != 0) {
       int rc = plane_exchange(ss, l, mode, st);
       if (rc) {
@@ -685,9 +690,14 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
     out->ms_expand_kernels = ms;
     out->n_expand_launches = 1;
     double sr = 0;
-    for (uint32_t l = 0; l <= S; l++) {
-      HIPCHK(hipEventElapsedTime(&ms, kr[2 * l], kr[2 * l + 1]));
-      sr += ms;
+    if (per_level) {
+      for (uint32_t l = 0; l <= S; l++) {
+        HIPCHK(hipEventElapsedTime(&ms, kr[2 * l], kr[2 * l + 1]));
+        sr += ms;
+      }
+    } else {
+      HIPCHK(hipEventElapsedTime(&ms, kr[0], kr[2 * (size_t)S + 1]));
+      sr = ms;
     }
     out->ms_resolve_kernels = sr;
     out->n_resolve_launches = (uint64_t)S + 1;

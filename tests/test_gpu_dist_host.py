@@ -1,9 +1,14 @@
-"""Sharded dense solves, one process per rank, over the host-staged
+"""Sharded sum-game solves, one process per rank, over the host-staged
 transport (gamesmanmpi_amd.dist.HostTransport over torch.distributed gloo):
 the RCCL path's geometry, halo plan check and reductions with the transfers
-carried through host memory, so two ranks can share one GPU.  Every
-position's word equals the single-table solve's; totals equal on every
-rank."""
+carried through host memory, so two or three ranks can share one GPU.
+
+Checked against the CPU oracle (oracle/oracle_mt.c's row solver, pinned to
+the DFS oracle and the reference-generated tables by tests/test_oracle.py):
+every position answered by exactly one rank, with the oracle's value and
+remoteness; counts and root line equal on every rank.  Both sharded
+layouts: PLANES (heaps 0 and 1 of 32 values -- the bench's layout) and the
+level-major DENSE table."""
 import os
 import socket
 
@@ -12,56 +17,62 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-PARAMS = "heaps=15:15:15:15:31"
+CASES = {  # (params, layout) per world size
+    ("planes", 2): "heaps=31:31:3:15",
+    ("planes", 3): "heaps=31:31:3:23",
+    ("dense", 2): "heaps=15:15:15:15:31",
+    ("dense", 3): "heaps=15:15:15:15:31",
+}
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, params, layout):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from gamesmanmpi_amd.dist import ShardedSolver
         from gamesmanmpi_amd.games import GameSpec
-        spec = GameSpec("sum_four_to_one", PARAMS)
-        s = ShardedSolver(spec, rank, world, device="cuda:0", transport="host")
+        spec = GameSpec("sum_four_to_one", params)
+        s = ShardedSolver(spec, rank, world, device="cuda:0", transport="host", layout=layout)
         r = s.solve()
-        from gamesmanmpi_amd.solver import Solver
-        s1 = Solver(spec, device="cuda:0", layout="dense")
-        keys, val, rem = s1.dump()
-        w = s.query(keys)
-        q.put((rank, (r.positions, r.edges, r.primitives, r.root_line), keys, val, rem, w))
+        n = 1
+        for h in params.split("=")[1].split(":"):
+            n *= int(h) + 1
+        w = s.query(np.arange(n, dtype=np.uint64))
+        q.put((rank, r.extra["layout"], (r.positions, r.edges, r.primitives, r.root_line), w))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_host_transport_matches_single_table(world):
+@pytest.mark.parametrize("layout,world", sorted(CASES))
+def test_host_transport_matches_oracle(layout, world):
     import torch.multiprocessing as mp
+    from oracle.oracle import Game  # checker only
+    params = CASES[(layout, world)]
     sk = socket.socket()
     sk.bind(("127.0.0.1", 0))
     port = sk.getsockname()[1]
     sk.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, params, layout)) for r in range(world)]
     for p in procs:
         p.start()
     out = sorted((q.get(timeout=200) for _ in range(world)), key=lambda t: t[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    from gamesmanmpi_amd.games import GameSpec
-    from gamesmanmpi_amd.solver import Solver
-    r1 = Solver(GameSpec("sum_four_to_one", PARAMS), layout="dense").solve()
+    sol = Game("sum_four_to_one", params).solve_rows()
+    sol.refresh(True)
     for o in out:
-        assert o[1] == (r1.positions, r1.edges, r1.primitives, r1.root_line)
-    keys, val, rem = out[0][2], out[0][3], out[0][4]
-    words = np.full(len(keys), 0xFFFFFFFF, np.uint64)
-    hits = np.zeros(len(keys), np.int64)
+        assert o[1] == layout
+        assert o[2] == (sol.count, sol.edges, sol.stats["primitives"], sol.root_line)
+    want = np.array([sol.word(k) for k in range(sol.count)], np.uint32)
+    got = np.full(sol.count, 0xFFFFFFFF, np.uint32)
+    hits = np.zeros(sol.count, np.int64)
     for o in out:
-        own = o[5] != 0xFFFFFFFF
-        words[own] = o[5][own]
+        own = o[3] != 0xFFFFFFFF
+        got[own] = o[3][own]
         hits += own
     assert (hits == 1).all()
-    np.testing.assert_array_equal(words & 3, val)
-    np.testing.assert_array_equal(words >> 2, rem)
+    np.testing.assert_array_equal(got, want)

@@ -90,7 +90,8 @@ def test_gpu_sum_31x6_checksum():
 
 
 def _check_group(name, world):
-    """The N-GPU bench shape, all `world` shards solved in this process
+    """The N-GPU bench shape (PLANES shards: round-robin blocks of 8 values of
+    the last heap), all `world` shards solved in this process
     (dist.group_solve: the halo exchange runs device-to-device on one
     stream): the shards' fingerprints -- each over the slices it owns,
     halos excluded -- add up to the single-table golden."""
@@ -98,6 +99,7 @@ def _check_group(name, world):
     from gamesmanmpi_amd.games import GameSpec
     e = _gold(name)
     r, shards = group_solve(GameSpec(e["game"], e["params"]), world)
+    assert r.extra["layout"] == "planes"
     assert (r.positions, r.edges, r.primitives) == (e["positions"], e["edges"], e["primitives"])
     assert r.root_line == e["root_line"]
     tot = {"checksum": 0, "positions": 0, "win": 0, "loss": 0, "tie": 0, "draw": 0}
@@ -132,7 +134,10 @@ def test_gpu_sum_31x6_graph_replay():
         assert (r2.positions, r2.edges, r2.root_line) == (e["positions"], e["edges"], e["root_line"])
     assert s.checksum()["checksum"] == e["checksum"]
 
-# The 8-GPU shape (31^5 x 255, golden sum_31x5_255) plans ~80 GB of table and
-# scratch per shard: its eight shards do not fit one GPU together, so it is
-# checked by its root line inside bench.py --gpus 8 (golden_for_params), and
-# world-8 sharding at small sizes by tests/test_gpu_sharded.py.
+def test_gpu_sum_31x5_255_eight_shards_checksum():
+    """bench.py --gpus 8 workload (31^5 x 255 heaps, 2^33 positions): the
+    eight PLANES shards (2^30 positions, ~1.2 GB each) solved as one
+    in-process group, fingerprints summed against the golden."""
+    import torch
+    _check_group("sum_31x5_255", 8)
+    torch.cuda.empty_cache()

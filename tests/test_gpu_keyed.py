@@ -52,7 +52,7 @@ def test_gpu_keyed_shard_refuses_whole_solve():
         sh.solver.solve()
 
 
-def _dist_worker(rank, world, port, q):
+def _dist_worker(rank, world, port, q, name):
     import os
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
@@ -60,7 +60,7 @@ def _dist_worker(rank, world, port, q):
     try:
         from gamesmanmpi_amd.games import GameSpec
         from gamesmanmpi_amd.keyed import dist_keyed_solve
-        spec = GameSpec(*CASES["othello_4x4"])
+        spec = GameSpec(*CASES[name])
         r, shard = dist_keyed_solve(spec, device="cuda:0", stage="cpu")
         keys, val, rem = shard.dump()
         q.put((rank, (r.positions, r.edges, r.primitives, r.root_line),
@@ -69,11 +69,13 @@ def _dist_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_gpu_keyed_two_processes_torch_exchange(golden_summary):
+@pytest.mark.parametrize("name", ["othello_4x4", "toot_4x3"])
+def test_gpu_keyed_two_processes_torch_exchange(name, golden_summary):
     """The one-process-per-rank path (TorchExchange over torch.distributed,
     the code the launcher runs under torchrun) with two ranks sharing one
     GPU: gloo carries the all-to-alls through host memory here, RCCL does on
-    an 8-GPU node.  othello 4x4 bit-exact, positions on their md5 owners."""
+    an 8-GPU node.  othello 4x4 and toot 4x3 bit-exact against the reference-
+    generated tables, positions on their md5 owners."""
     import socket
     import torch.multiprocessing as mp
     s = socket.socket()
@@ -82,24 +84,24 @@ def test_gpu_keyed_two_processes_torch_exchange(golden_summary):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_dist_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_dist_worker, args=(r, 2, port, q, name)) for r in range(2)]
     for p in procs:
         p.start()
     out = sorted((q.get(timeout=100) for _ in range(2)), key=lambda t: t[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    info = golden_summary["othello_4x4"]
+    info = golden_summary[name]
     for _, tot, _, _, _ in out:
         assert tot == (info["positions"], info["edges"], info["primitives"], info["root_line"])
     from gamesmanmpi_amd.games import GameSpec
-    spec = GameSpec(*CASES["othello_4x4"])
+    spec = GameSpec(*CASES[name])
     keys = np.concatenate([o[2] for o in out])
     val = np.concatenate([o[3] for o in out])
     rem = np.concatenate([o[4] for o in out])
     for rank, o in enumerate(out):
         assert (spec.owners_host(o[2], 2) == rank).all()
-    t = load_table("othello_4x4")
+    t = load_table(name)
     canon, clen = spec.decode_batch(keys, stride=t["canon"].shape[1])
     order = np.array(sorted(range(len(keys)), key=lambda i: bytes(canon[i, :clen[i]])), np.int64)
     np.testing.assert_array_equal(canon[order], t["canon"])

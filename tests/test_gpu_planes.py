@@ -5,8 +5,8 @@ order, resolved plane level by plane level.
 Checked against the CPU oracle (oracle/oracle.c, pinned to the reference's
 own game modules by tests/test_oracle.py) position by position on small
 shapes, against the level-major DENSE layout word for word, and at full size
-(2^30, and the 2-, 4- and 8-GPU bench shapes 2^31..2^33 as in-process shard
-groups) by whole-solve fingerprints against tests/golden/checksums.json
+(2^30; the 2-, 4- and 8-GPU bench shapes 2^31..2^33 as in-process shard
+groups are in tests/test_gpu_full_size.py) by whole-solve fingerprints against tests/golden/checksums.json
 (oracle/oracle_mt.c)."""
 import json
 import os
@@ -175,23 +175,6 @@ def test_planes_group_matches_oracle():
         assert (got[own] == 0xFFFFFFFF).all()
         got[own] = w[own]
     np.testing.assert_array_equal(got, want)
-
-
-@pytest.mark.parametrize("world,name", [(2, "sum_31x5_63"), (4, "sum_31x5_127"), (8, "sum_31x5_255")])
-def test_planes_bench_shapes_as_groups(world, name):
-    """The N = 2 / 4 / 8 bench workloads (31^5 x (32N - 1): 2^31 / 2^32 /
-    2^33 positions, blocks of 8 top values, four per rank) solved as
-    in-process shard groups on one GPU, checked by the sum of the shards'
-    fingerprints against the CPU restatement's golden."""
-    import torch
-    from gamesmanmpi_amd.dist import group_solve
-    from gamesmanmpi_amd.games import GameSpec
-    e = _gold(name)
-    rg, shards = group_solve(GameSpec("sum_four_to_one", e["params"]), world)
-    assert rg.extra["layout"] == "planes"
-    _check_gold(e, rg, [sh.checksum() for sh in shards])
-    del shards
-    torch.cuda.empty_cache()
 
 
 @pytest.mark.parametrize("cut", [1, 187, 187 + 40, 187 + 124])

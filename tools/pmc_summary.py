@@ -38,7 +38,7 @@ def traffic(workload, out_path, root):
     for name, ctr in per.items():
         if "FETCH_SIZE" not in ctr or "WRITE_SIZE" not in ctr:
             continue
-        short = name.split("(")[0].replace("void ", "").split("<")[0]
+        short = name.split("(")[0].replace("void ", "").split("<")[0].split("::")[-1]
         n = len(launches[name]) / max(1, len({p for p, _ in launches[name]}))
         f = ctr["FETCH_SIZE"] * 1024 * 2 / n
         w = ctr["WRITE_SIZE"] * 1024 / n
