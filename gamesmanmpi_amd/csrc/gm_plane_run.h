@@ -355,6 +355,16 @@ static int plane_lists(gm_solver* s, const PlaneShape& ps, std::vector<uint8_t>&
       }
     }
   }
+  // per level, the planes that read a halo plane (top values gB, gB + 1 of
+  // blocks with a predecessor) last: the launch can be split into an own
+  // part and a boundary part that waits for the exchange (run_planes)
+  s->pbnd.assign((size_t)S + 1, 0);
+  auto reads_halo = [](const PlaneEntry& e) { return e.top1 < kPlaneLocal || e.top2 < kPlaneLocal; };
+  for (uint32_t l = 0; l <= S; l++) {
+    PlaneEntry* a = E + s->ploff[l];
+    PlaneEntry* b = E + s->ploff[l + 1];
+    s->pbnd[l] = s->ploff[l] + (u64)(std::stable_partition(a, b, [&](const PlaneEntry& e) { return !reads_halo(e); }) - a);
+  }
   return 0;
 }
 
@@ -401,8 +411,7 @@ static int plane_setup(gm_solver* s, const gm_buffers* buf) {
 static bool plane_x1(const gm_solver* s) { return s->pwb == 2 || (s->flags & GM_F_PLANE_X1); }
 
 template <int WB, int NO, bool SH>
-static void plane_launch_t(gm_solver* s, uint32_t l) {
-  const u64 a = s->ploff[l], n = s->ploff[l + 1] - a;
+static void plane_launch_t(gm_solver* s, u64 a, u64 n) {
   if (!n) return;
   const bool x1 = plane_x1(s);
   const u64 waves = x1 ? (n + 1) / 2 : (n + 3) / 4;
@@ -418,26 +427,36 @@ static void plane_launch_t(gm_solver* s, uint32_t l) {
                        (T*)s->ptab, list, (uint32_t)n, s->pg, s->pzero, (const T*)s->precv, (T*)s->psend);
 }
 template <int WB, bool SH>
-static void plane_launch_w(gm_solver* s, uint32_t l) {
+static void plane_launch_w(gm_solver* s, u64 a, u64 n) {
   switch (s->pg.no) {
-    case 0: if (!SH) plane_launch_t<WB, 0, false>(s, l); break;
-    case 1: plane_launch_t<WB, 1, SH>(s, l); break;
-    case 2: plane_launch_t<WB, 2, SH>(s, l); break;
-    case 3: plane_launch_t<WB, 3, SH>(s, l); break;
-    case 4: plane_launch_t<WB, 4, SH>(s, l); break;
-    case 5: plane_launch_t<WB, 5, SH>(s, l); break;
-    default: plane_launch_t<WB, 6, SH>(s, l); break;
+    case 0: if (!SH) plane_launch_t<WB, 0, false>(s, a, n); break;
+    case 1: plane_launch_t<WB, 1, SH>(s, a, n); break;
+    case 2: plane_launch_t<WB, 2, SH>(s, a, n); break;
+    case 3: plane_launch_t<WB, 3, SH>(s, a, n); break;
+    case 4: plane_launch_t<WB, 4, SH>(s, a, n); break;
+    case 5: plane_launch_t<WB, 5, SH>(s, a, n); break;
+    default: plane_launch_t<WB, 6, SH>(s, a, n); break;
   }
 }
-static void plane_launch(gm_solver* s, uint32_t l) {
+// list entries [a, a + n) of the solver's level lists
+static void plane_launch_range(gm_solver* s, u64 a, u64 n) {
   const bool sh = s->world > 1;
   if (s->pwb == 1) {
-    if (sh) plane_launch_w<1, true>(s, l);
-    else plane_launch_w<1, false>(s, l);
+    if (sh) plane_launch_w<1, true>(s, a, n);
+    else plane_launch_w<1, false>(s, a, n);
   } else {
-    if (sh) plane_launch_w<2, true>(s, l);
-    else plane_launch_w<2, false>(s, l);
+    if (sh) plane_launch_w<2, true>(s, a, n);
+    else plane_launch_w<2, false>(s, a, n);
   }
+}
+// plane level l; part 0: all of it, 1: the planes that read no halo plane,
+// 2: the ones that do
+static void plane_launch(gm_solver* s, uint32_t l, int part = 0) {
+  const u64 a = s->ploff[l], b = s->ploff[(size_t)l + 1];
+  const u64 m = s->world > 1 ? s->pbnd[l] : b;
+  if (part == 0) plane_launch_range(s, a, b - a);
+  else if (part == 1) plane_launch_range(s, a, m - a);
+  else plane_launch_range(s, m, b - m);
 }
 template <class F>
 static void plane_no_dispatch(uint32_t no, F&& f) {
@@ -616,21 +635,58 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
   // launches: they would add their own gaps to what they time); shards --
   // a pair around each level's launches (exchanges sit between them)
   const bool per_level = timing && mode != 0;
+  // Shards (RCCL or in-process copies): each level's launch is split into
+  // the planes that read no halo plane -- the boundary slices the exchange
+  // sends are among them when blocks hold >= 4 top values -- and the ones
+  // that do.  Own part -> event -> exchange on the comm stream -> event;
+  // the boundary part of the NEXT level waits for it, so the exchange of
+  // level l overlaps the boundary part of l and the own part of l + 1.  The
+  // host-staged transport (mode 3) and blocks of < 4 values exchange in
+  // order.
+  bool pipe = mode == 1 || mode == 2;
+  if (s0->pg.B < 4 || (s0->flags & GM_F_SHARD_INORDER)) pipe = false;
+  hipStream_t cs = st;
+  hipEvent_t* PE = nullptr;  // [0, S]: own part of level l done; [S+1, 2S+2): exchange of l done
+  if (pipe) {
+    if (!s0->cstream) HIPCHK(hipStreamCreateWithFlags(&s0->cstream, hipStreamNonBlocking));
+    while (s0->pev.size() < 2 * ((size_t)S + 1)) {
+      hipEvent_t e;
+      HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      s0->pev.push_back(e);
+    }
+    cs = s0->cstream;
+    PE = s0->pev.data();
+  }
+  int last_x = -1;  // last level exchanged on the comm stream
   for (uint32_t l = 0; l <= S; l++) {
     const int k = T + (int)l;
     if (k < first) continue;
     if (k >= stop) break;
     if (per_level || (timing && l == 0)) HIPCHK(hipEventRecord(kr[2 * l], st));
-    for (gm_solver* s : ss) plane_launch(s, l);
-    if (per_level || (timing && l == S)) HIPCHK(hipEventRecord(kr[2 * l + 1], st));
+    if (!pipe) {
+      for (gm_solver* s : ss) plane_launch(s, l);
+    } else {
+      for (gm_solver* s : ss) plane_launch(s, l, 1);
+      HIPCHK(hipEventRecord(PE[l], st));
+      HIPCHK(hipStreamWaitEvent(cs, PE[l], 0));
+    }
     if (mode != 0) {
-      int rc = plane_exchange(ss, l, mode, st);
+      int rc = plane_exchange(ss, l, mode, cs);
       if (rc) {
         cleanup();
         return rc;
       }
     }
+    if (pipe) {
+      HIPCHK(hipEventRecord(PE[S + 1 + l], cs));
+      last_x = (int)l;
+      // the boundary planes read the halos of levels l - 1 and l - 2
+      if (l >= 1) HIPCHK(hipStreamWaitEvent(st, PE[S + l], 0));
+      for (gm_solver* s : ss) plane_launch(s, l, 2);
+    }
+    if (per_level || (timing && l == S)) HIPCHK(hipEventRecord(kr[2 * l + 1], st));
   }
+  if (last_x >= 0) HIPCHK(hipStreamWaitEvent(st, PE[S + 1 + last_x], 0));  // join the comm stream
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(e2, st));
   if (stop < 2 * T) {

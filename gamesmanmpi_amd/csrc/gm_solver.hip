@@ -989,6 +989,7 @@ struct gm_solver {
   const uint4* pzero = nullptr;  // 4 KB of zeros (absent neighbours)
   const void* plist = nullptr;   // level lists (uint32 planes, or PlaneEntry for shards)
   std::vector<u64> ploff;        // per level: first list entry
+  std::vector<u64> pbnd;         // shards, per level: first entry that reads a halo plane (they come last)
   std::vector<u64> prcv_off, psnd_off;  // shards, per level: first halo plane received / sent
 };
 
@@ -2049,7 +2050,8 @@ int gm_shard_halo_sigs(int game, int rank, int world, uint32_t flags, uint64_t* 
 
 int gm_solver_set_transport(gm_solver* s, gm_xfer_fn fn, void* ctx) {
   if (!s) return fail(GM_EINVAL, "bad argument");
-  if (s->mode != GM_MODE_DENSE || s->world <= 1) return fail(GM_EINVAL, "a transport serves dense shards of a world > 1");
+  if ((s->mode != GM_MODE_DENSE && s->mode != GM_MODE_PLANES) || s->world <= 1)
+    return fail(GM_EINVAL, "a transport serves dense / planes shards of a world > 1");
   s->xfer = fn;
   s->xfer_ctx = ctx;
   return 0;

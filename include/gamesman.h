@@ -113,8 +113,8 @@ typedef struct gm_buffers {
  * refuses a table sized for other flags with GM_EINVAL. */
 #define GM_F_WORDS32 4u        /* dense: 32-bit table words (quad kernels) */
 #define GM_F_RESOLVE_SCALAR 8u /* dense: one-prefix-per-lane resolve, 32-bit */
-#define GM_F_SHARD_INORDER 16u /* dense shards: exchange each level's halo in
-                                  order instead of overlapping it */
+#define GM_F_SHARD_INORDER 16u /* dense / planes shards: exchange each level's
+                                  halo in order instead of overlapping it */
 #define GM_F_HASH_TABLE 32u    /* gm_plan, keyed games: the open-addressing
                                   hash table (HASHED) instead of BUCKETED */
 #define GM_F_WORDS16 64u       /* dense: 16-bit table words (octet kernels)

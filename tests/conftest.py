@@ -53,3 +53,24 @@ def load_table(name):
         return None
     z = np.load(path)  # allow_pickle=False (default)
     return {k: z[k] for k in z.files}
+
+
+def collect_workers(q, procs, world, limit=200):
+    """The workers' results; fails at once when a worker dies (its peers
+    would wait in a collective until the limit)."""
+    import queue
+    import time
+    out, t0 = [], time.time()
+    while len(out) < world:
+        try:
+            out.append(q.get(timeout=2))
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            if dead or time.time() - t0 > limit:
+                for p in procs:
+                    p.kill()
+                pytest.fail("worker exit codes %s after %.0f s" % ([p.exitcode for p in procs], time.time() - t0))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return sorted(out, key=lambda t: t[0])

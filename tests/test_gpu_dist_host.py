@@ -15,6 +15,8 @@ import socket
 import numpy as np
 import pytest
 
+from conftest import collect_workers
+
 pytestmark = pytest.mark.gpu
 
 CASES = {  # (params, layout) per world size
@@ -58,10 +60,7 @@ def test_host_transport_matches_oracle(layout, world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, q, params, layout)) for r in range(world)]
     for p in procs:
         p.start()
-    out = sorted((q.get(timeout=200) for _ in range(world)), key=lambda t: t[0])
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    out = collect_workers(q, procs, world)
     sol = Game("sum_four_to_one", params).solve_rows()
     sol.refresh(True)
     for o in out:

@@ -6,7 +6,7 @@ BASELINE config 5 is othello 4x4 over 8 ranks."""
 import numpy as np
 import pytest
 
-from conftest import CASES, load_table
+from conftest import CASES, collect_workers, load_table
 
 pytestmark = pytest.mark.gpu
 
@@ -87,10 +87,7 @@ def test_gpu_keyed_two_processes_torch_exchange(name, golden_summary):
     procs = [ctx.Process(target=_dist_worker, args=(r, 2, port, q, name)) for r in range(2)]
     for p in procs:
         p.start()
-    out = sorted((q.get(timeout=100) for _ in range(2)), key=lambda t: t[0])
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    out = collect_workers(q, procs, 2, limit=150)
     info = golden_summary[name]
     for _, tot, _, _, _ in out:
         assert tot == (info["positions"], info["edges"], info["primitives"], info["root_line"])

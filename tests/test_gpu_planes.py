@@ -190,3 +190,21 @@ def test_planes_stop_resume(cut):
     r = s.solve_steps(cut, 0)
     _check_gold(e, r, [s.checksum()])
     del params
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_planes_group_pipelined_equals_in_order(world):
+    """Shards exchange each level's boundary planes on a comm stream while
+    the next launches run (own part / boundary part split, the RCCL path's
+    schedule); GM_F_SHARD_INORDER exchanges after each whole level.  Same
+    words either way."""
+    from gamesmanmpi_amd import _lib
+    from gamesmanmpi_amd.dist import group_solve
+    from gamesmanmpi_amd.games import GameSpec
+    spec = GameSpec("sum_four_to_one", "heaps=31:31:7:7:15")
+    rp, sp = group_solve(spec, world)
+    ri, si = group_solve(spec, world, flags=_lib.GM_F_SHARD_INORDER)
+    assert (rp.positions, rp.edges, rp.root_line) == (ri.positions, ri.edges, ri.root_line)
+    keys = np.arange(32 * 32 * 8 * 8 * 16, dtype=np.uint64)
+    for a, b in zip(sp, si):
+        np.testing.assert_array_equal(a.query(keys), b.query(keys))

@@ -33,7 +33,19 @@ static void launch(void* tab, const uint32_t* list, uint32_t n, const PlaneGeom&
   const uint32_t waves = g_x2 ? (n + 3) / 4 : (n + 1) / 2;
   uint32_t blocks = (waves + 3) / 4;
   blocks = (blocks + 7) / 8 * 8;
-  if (g_x2)
+  if (g_x2 == 4 && WB == 1)  // diagnostic: no neighbour loads
+    hipLaunchKernelGGL((k_plane_resolve_x2h<NO, false, 1>), dim3(blocks), dim3(256), 0, st, (uint8_t*)tab, list, n, g,
+                       zero, (const uint8_t*)nullptr, (uint8_t*)nullptr);
+  else if (g_x2 == 5 && WB == 1)  // diagnostic: no wavefront
+    hipLaunchKernelGGL((k_plane_resolve_x2h<NO, false, 2>), dim3(blocks), dim3(256), 0, st, (uint8_t*)tab, list, n, g,
+                       zero, (const uint8_t*)nullptr, (uint8_t*)nullptr);
+  else if (g_x2 == 3 && WB == 1)
+    hipLaunchKernelGGL((k_plane_resolve_x2h<NO, false>), dim3(blocks), dim3(256), 0, st, (uint8_t*)tab, list, n, g,
+                       zero, (const uint8_t*)nullptr, (uint8_t*)nullptr);
+  else if (g_x2 == 2 && WB == 1)
+    hipLaunchKernelGGL((k_plane_resolve_x2l<NO, false>), dim3(blocks), dim3(256), 0, st, (uint8_t*)tab, list, n, g,
+                       zero, (const uint8_t*)nullptr, (uint8_t*)nullptr);
+  else if (g_x2)
     hipLaunchKernelGGL((k_plane_resolve_x2<WB, NO, false>), dim3(blocks), dim3(256), 0, st, (T*)tab, list, n, g, zero,
                        (const T*)nullptr, (T*)nullptr);
   else
@@ -99,8 +111,11 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
+  std::vector<hipEvent_t> lev_ev;
+  bool lev_timing = false;
   auto run = [&]() {
     for (int s = 0; s <= S; s++) {
+      if (lev_timing) CK(hipEventRecord(lev_ev[s], st));
       const uint32_t n = cnt[s];
       const uint32_t* l = dlist + off[s];
       switch (WB * 10 + (K - 2)) {
@@ -115,6 +130,7 @@ int main(int argc, char** argv) {
           exit(1);
       }
     }
+    if (lev_timing) CK(hipEventRecord(lev_ev[S + 1], st));
   };
   run();
   CK(hipStreamSynchronize(st));
@@ -129,14 +145,29 @@ int main(int argc, char** argv) {
     CK(hipEventElapsedTime(&ms, e0, e1));
     ts.push_back(ms);
   }
+  if (getenv("LEVEL_TIMES")) {  // per-level times of one more solve (an event between launches)
+    lev_ev.resize(S + 2);
+    for (auto& ev : lev_ev) CK(hipEventCreate(&ev));
+    lev_timing = true;
+    run();
+    CK(hipStreamSynchronize(st));
+    lev_timing = false;
+    printf("level_us");
+    for (int s = 0; s <= S; s++) {
+      float ms;
+      CK(hipEventElapsedTime(&ms, lev_ev[s], lev_ev[s + 1]));
+      printf(" %.1f", ms * 1e3);
+    }
+    printf("\n");
+  }
   float best = 1e9, sum = 0;
   for (float t : ts) {
     best = t < best ? t : best;
     sum += t;
   }
   const double P = (double)np * 1024;
-  printf("x%d K=%d top=%d wb=%d planes=%llu levels=%d positions=%.0f backward best %.3f ms mean %.3f ms (%.3g pos/s)\n",
-         g_x2 ? 2 : 1, K, top, WB, (unsigned long long)np, S + 1, P, best, sum / reps, P / (best * 1e-3));
+  printf("v%d K=%d top=%d wb=%d planes=%llu levels=%d positions=%.0f backward best %.3f ms mean %.3f ms (%.3g pos/s)\n",
+         g_x2, K, top, WB, (unsigned long long)np, S + 1, P, best, sum / reps, P / (best * 1e-3));
   // root
   std::vector<uint8_t> host(tbytes);
   CK(hipMemcpy(host.data(), tab, tbytes, hipMemcpyDeviceToHost));
