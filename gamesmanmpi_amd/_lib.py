@@ -110,7 +110,7 @@ EXPORTS = (
     "gm_solver_solve", "gm_solver_query", "gm_solver_positions",
     "gm_solver_checksum",
     "gm_solver_destroy", "gm_solve", "gm_query", "gm_release", "gm_owner", "gm_owner_host",
-    "gm_plan_shard", "gm_solver_create_shard", "gm_comm_unique_id",
+    "gm_plan_shard", "gm_plan_keyed_shard", "gm_solver_create_shard", "gm_comm_unique_id",
     "gm_solver_comm_init", "gm_solve_group", "gm_solver_set_flags", "gm_solver_set_steps",
     "gm_shard_info", "gm_solver_set_transport", "gm_shard_halo_sigs",
     "gm_ks_begin", "gm_ks_level_size", "gm_ks_expand", "gm_ks_insert",
@@ -171,6 +171,8 @@ def load():
                           c.c_void_p],
         "gm_plan_shard": [c.c_int, c.c_int, c.c_int, c.c_uint32, c.c_uint64,
                           P(gm_plan_t)],
+        "gm_plan_keyed_shard": [c.c_int, c.c_int, c.c_int, c.c_uint64, c.c_uint32,
+                                c.c_uint64, P(gm_plan_t)],
         "gm_solver_create_shard": [c.c_int, c.c_int, c.c_int, P(gm_buffers),
                                    P(c.c_void_p)],
         "gm_comm_unique_id": [c.c_void_p],

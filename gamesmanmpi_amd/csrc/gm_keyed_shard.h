@@ -28,6 +28,11 @@ __device__ __forceinline__ uint32_t owner_of(const Desc& d, u64 key, uint32_t P)
   return md5_mod(dig, P);
 }
 
+// the same as a call: the bucketed kernels ask for owners inside the
+// unrolled move generators, where an inlined MD5 per move site multiplies the
+// code (and the compile time) by the number of sites
+__device__ __noinline__ uint32_t owner_of_call(const Desc& d, u64 key, uint32_t P) { return owner_of(d, key, P); }
+
 // rank owning the root seeds its table and level 0; every rank zeroes state
 __global__ void k_ks_seed(gm_slot* tab, u64 mask, u64* lv, DevState* st, u64 root, int owned) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {

@@ -969,6 +969,9 @@ struct gm_solver {
   uint32_t* S1p = nullptr;
   u64* S2k = nullptr;
   uint8_t* S1f = nullptr;  // per staged child: the byte under mix64's top byte (fine bucket bits)
+  u64 *XSk = nullptr, *XRk = nullptr;  // md5-sharded bucketed levels: exchange buffers
+  uint32_t *XSr = nullptr, *XRr = nullptr;
+  std::vector<std::vector<u64>> bks_sc, bks_rc;  // per forward level: records sent to / received from each rank
   u64 Pcap = 0, Ecap = 0, Emax = 0;
   BkLevel* bkL = nullptr;  // device level table (scratch)
   uint32_t *pbase = nullptr, *bh = nullptr, *ph = nullptr, *boff = nullptr, *tot = nullptr, *cbase = nullptr;
@@ -1658,6 +1661,32 @@ int gm_plan(int game, uint64_t positions, uint32_t flags, uint64_t max_table_byt
   return 0;
 }
 
+int gm_plan_keyed_shard(int game, int rank, int world, uint64_t positions, uint32_t flags, uint64_t max_table_bytes,
+                        gm_plan_t* out) {
+  const Desc* d = get_game(game);
+  if (!d || !out) return fail(GM_EINVAL, "bad argument");
+  if (world < 2 || world > 8 || rank < 0 || rank >= world) return fail(GM_EINVAL, "bad shard %d/%d (2..8 ranks)", rank, world);
+  if (!bk_ok(d) || (flags & GM_F_HASH_TABLE))
+    return fail(GM_EINVAL, "md5-sharded bucketed levels need every move to advance one level");
+  memset(out, 0, sizeof *out);
+  out->max_levels = (uint32_t)d->max_levels;
+  if (positions == 0) {
+    gm_game_info(game, &positions, nullptr, nullptr);
+    if (positions == 0) return fail(GM_EINVAL, "no known position bound for this board; pass an estimate");
+  }
+  const u64 P = positions + 64, E = bk_edges_bound(d, positions), Em = bk_emax_bound(E);
+  if (Em >= 0xFFFFFFF0ull) return fail(GM_EINVAL, "a level of more than 2^32 edges: not supported");
+  const u64 bytes = 4 * P + 6 * E + 48 * Em;  // the one-GPU layout + the exchange buffers
+  if (max_table_bytes && bytes > max_table_bytes)
+    return fail(GM_EFULL, "bucketed shard needs %llu bytes", (unsigned long long)bytes);
+  out->mode = GM_MODE_BUCKETED;
+  out->level_capacity = P;
+  out->table_slots = E;
+  out->table_bytes = bytes;
+  out->scratch_bytes = bk_scratch(d->max_levels).end;
+  return 0;
+}
+
 // Per-lane condition masks of a 64-prefix group for power-of-two layouts
 // (k_dense_pull_words): with j the lane's offset in the group,
 //   M[t]              = { j : sum_i digit_i(j) <= t }   (TS)
@@ -1771,12 +1800,14 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
     if (!d->dense_ok || !plane_ok(d)) return fail(GM_EINVAL, "game has no planes layout");
     if (world > 1 && (rank < 0 || rank >= world)) return fail(GM_EINVAL, "bad shard %d/%d", rank, world);
   } else if (buf->mode == GM_MODE_BUCKETED) {
-    if (world != 1 || rank != 0) return fail(GM_EINVAL, "bucketed levels solve on one GPU (md5 shards use keyed tables)");
+    if (world < 1 || rank < 0 || rank >= world) return fail(GM_EINVAL, "bad shard %d/%d", rank, world);
+    if (world > 8) return fail(GM_EINVAL, "md5-sharded bucketed levels support up to 8 ranks");
     if (!bk_ok(d)) return fail(GM_EINVAL, "bucketed levels need every move to advance one level");
     if (!buf->levels || buf->level_capacity < 2) return fail(GM_EINVAL, "null level store");
     if (buf->scratch_bytes < bk_scratch(d->max_levels).end) return fail(GM_EINVAL, "scratch too small (use gm_plan)");
     const u64 fixed = 4 * buf->level_capacity + 6 * buf->table_slots;
-    if (buf->table_bytes < fixed + 24 * 1024ull) return fail(GM_EINVAL, "bucketed table too small (use gm_plan)");
+    if (buf->table_bytes < fixed + (world > 1 ? 48 : 24) * 1024ull)
+      return fail(GM_EINVAL, "bucketed table too small (use gm_plan / gm_plan_keyed_shard)");
   } else if (buf->mode == GM_MODE_HASHED) {
     if (world < 1 || rank < 0 || rank >= world) return fail(GM_EINVAL, "bad shard %d/%d", rank, world);
     if (!buf->levels || buf->level_capacity < 1) return fail(GM_EINVAL, "null level store");
@@ -1925,7 +1956,8 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
     char* t = (char*)buf->table;
     s->Pcap = buf->level_capacity;
     s->Ecap = buf->table_slots;
-    s->Emax = std::min<u64>((buf->table_bytes - 4 * s->Pcap - 6 * s->Ecap) / 24, 0xFFFFFFF0ull);
+    // a shard of a world > 1 job also holds the md5 exchange buffers (24 B per staged record)
+    s->Emax = std::min<u64>((buf->table_bytes - 4 * s->Pcap - 6 * s->Ecap) / (world > 1 ? 48 : 24), 0xFFFFFFF0ull);
     s->bkK = (u64*)buf->levels;
     s->bkW = (uint32_t*)t;
     t += (4 * s->Pcap + 7) & ~7ull;
@@ -1942,6 +1974,16 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
     s->S1f = (uint8_t*)t;  // (4 Emax bytes of the plan; one is used)
     t += 4 * s->Emax;
     s->S2k = (u64*)t;
+    t += 8 * s->Emax;
+    if (world > 1) {  // md5 exchange: records sent / received (keys, refs; answers reuse the key arrays)
+      s->XSk = (u64*)t;
+      t += 8 * s->Emax;
+      s->XSr = (uint32_t*)t;
+      t += 4 * s->Emax;
+      s->XRk = (u64*)t;
+      t += 8 * s->Emax;
+      s->XRr = (uint32_t*)t;
+    }
     const BkScratch x = bk_scratch(d->max_levels);
     char* sc = (char*)buf->scratch;
     s->bkL = (BkLevel*)(sc + x.lv);
@@ -2050,8 +2092,8 @@ int gm_shard_halo_sigs(int game, int rank, int world, uint32_t flags, uint64_t* 
 
 int gm_solver_set_transport(gm_solver* s, gm_xfer_fn fn, void* ctx) {
   if (!s) return fail(GM_EINVAL, "bad argument");
-  if ((s->mode != GM_MODE_DENSE && s->mode != GM_MODE_PLANES) || s->world <= 1)
-    return fail(GM_EINVAL, "a transport serves dense / planes shards of a world > 1");
+  if ((s->mode != GM_MODE_DENSE && s->mode != GM_MODE_PLANES && s->mode != GM_MODE_BUCKETED) || s->world <= 1)
+    return fail(GM_EINVAL, "a transport serves dense / planes / bucketed shards of a world > 1");
   s->xfer = fn;
   s->xfer_ctx = ctx;
   return 0;
@@ -2090,13 +2132,14 @@ void gm_solver_destroy(gm_solver* s) {
 
 static int solve_dense(gm_solver* s, gm_result* out);
 static int solve_bucketed(gm_solver* s, gm_result* out);
+static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out);
 
 int gm_solver_solve(gm_solver* s, gm_result* out) {
   if (!s || !out) return fail(GM_EINVAL, "bad argument");
   memset(out, 0, sizeof *out);
   if (s->mode == GM_MODE_DENSE) return solve_dense(s, out);
   if (s->mode == GM_MODE_PLANES) return run_planes({s}, out);
-  if (s->mode == GM_MODE_BUCKETED) return solve_bucketed(s, out);
+  if (s->mode == GM_MODE_BUCKETED) return s->world > 1 ? run_bucketed_shards({s}, out) : solve_bucketed(s, out);
   if (s->world > 1) return fail(GM_EINVAL, "keyed-table shard %d/%d: drive it with gm_ks_* (md5 exchange)", s->rank, s->world);
   const int T = s->d.max_levels;
   // steps [first, stop) of the 2T (gm_solver_set_steps); forward level L is
@@ -3465,6 +3508,8 @@ static int solve_bucketed(gm_solver* s, gm_result* out) {
   return 0;
 }
 
+#include "gm_bucketed_shard.h"
+
 int gm_solve_group(gm_solver** shards, int n, gm_result* out) {
   if (!shards || n < 1 || !out) return fail(GM_EINVAL, "bad argument");
   memset(out, 0, sizeof *out);
@@ -3472,6 +3517,7 @@ int gm_solve_group(gm_solver** shards, int n, gm_result* out) {
   for (gm_solver* s : ss)
     if (!s) return fail(GM_EINVAL, "null shard");
   if (ss[0]->mode == GM_MODE_PLANES) return run_planes(ss, out);
+  if (ss[0]->mode == GM_MODE_BUCKETED) return run_bucketed_shards(ss, out);
   return run_dense(ss, out);
 }
 

@@ -1,4 +1,10 @@
-"""md5-sharded solve of keyed (HASHED) tables (keyed).
+"""md5-sharded solves of keyed games (keyed).
+
+Games whose every move advances one level (tic-tac-toe, toot-and-otto,
+othello) run as md5-sharded BUCKETED levels inside the library
+(gm_bucketed_shard.h: the level loop, both all-to-alls and the size reads
+are native; group_keyed_solve / dist_keyed_solve pick it).  Every other
+keyed game runs on HASHED shards driven by the loop below.
 
 The reference partitions positions over MPI ranks by
 owner(pos) = md5(str(pos)) % world (GameState.get_hash,
@@ -338,24 +344,81 @@ def keyed_solve(shards, exchange):
                "root_owner": root_owner})
 
 
-def group_keyed_solve(spec, world, device=None):
+def bucketed_shards_apply(spec, world):
+    """True when the md5-sharded BUCKETED levels serve this game (every move
+    advances one level: tic-tac-toe, toot-and-otto, othello), i.e. the
+    library plans a bucketed shard for it."""
+    plan = _lib.gm_plan_t()
+    return _lib.load().gm_plan_keyed_shard(
+        spec.id, 0, int(world), _shard_bound(spec, world, 0), 0, 0,
+        ctypes.byref(plan)) == 0
+
+
+def _shard_bound(spec, world, positions):
+    """positions bound of one md5 shard (2x its share of the job's bound)"""
+    return 2 * int(positions or spec.positions_bound) // int(world) + 4096
+
+
+def _pick(spec, world, layout):
+    if layout not in ("auto", "bucketed", "hashed"):
+        raise ValueError("layout: auto, bucketed or hashed")
+    if layout == "hashed":
+        return "hashed"
+    if bucketed_shards_apply(spec, world):
+        return "bucketed"
+    if layout == "bucketed":
+        raise ValueError("%r: md5-sharded bucketed levels need every move to "
+                         "advance one level" % (spec,))
+    return "hashed"
+
+
+def group_keyed_solve(spec, world, device=None, layout="auto"):
     """Every md5 shard of a `world`-rank job in this process, on one GPU
-    and one stream.  Returns (SolveResult, [GpuShard])."""
+    and one stream.  layout "auto": md5-sharded BUCKETED levels where they
+    apply (the library's all-to-all level loop, gm_bucketed_shard.h), else
+    HASHED shards driven by keyed_solve.  Returns (SolveResult, shards):
+    Solvers (bucketed) or GpuShards (hashed), both with dump()."""
     import torch
     spec = spec if isinstance(spec, GameSpec) else GameSpec(*spec)
     dev = torch.device(device if device is not None else "cuda")
     stream = torch.cuda.Stream(device=dev)
+    if _pick(spec, world, layout) == "bucketed":
+        per = _shard_bound(spec, world, 0)
+        shards = [Solver(spec, positions=per, device=dev, layout="bucketed",
+                         rank=g, world=world, stream=stream)
+                  for g in range(world)]
+        arr = (ctypes.c_void_p * world)(*[s.handle.value for s in shards])
+        r = _lib.gm_result()
+        torch.cuda.synchronize(dev)
+        with torch.cuda.device(dev):
+            _lib.check(_lib.load().gm_solve_group(arr, world, ctypes.byref(r)))
+        res = shards[0]._result(r)
+        res.extra.update({"partition": "md5", "world": world})
+        return res, shards
     shards = [GpuShard(spec, g, world, device=dev, stream=stream)
               for g in range(world)]
     return keyed_solve(shards, GroupExchange()), shards
 
 
-def dist_keyed_solve(spec, device=None, positions=0, stage=None):
+def dist_keyed_solve(spec, device=None, positions=0, stage=None,
+                     layout="auto"):
     """This process's shard of an md5-sharded job over the initialised
     torch.distributed default group; `positions`: bound for the whole job
-    (0: the game's own).  Returns (SolveResult, GpuShard)."""
+    (0: the game's own); stage="cpu": collectives through host memory
+    (several ranks sharing one GPU in tests).  Returns (SolveResult,
+    shard)."""
     import torch.distributed as dist
+    spec = spec if isinstance(spec, GameSpec) else GameSpec(*spec)
     world = dist.get_world_size()
+    if _pick(spec, world, layout) == "bucketed":
+        from .dist import ShardedSolver
+        shard = ShardedSolver(spec, dist.get_rank(), world, device=device,
+                              transport="host" if stage == "cpu" else "rccl",
+                              layout="bucketed",
+                              positions=_shard_bound(spec, world, positions))
+        res = shard.solve()
+        res.extra.update({"partition": "md5", "world": world})
+        return res, shard
     per_shard = 2 * int(positions) // world + 4096 if positions else 0
     shard = GpuShard(spec, dist.get_rank(), world, device=device,
                      positions=per_shard)

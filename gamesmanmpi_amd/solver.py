@@ -58,10 +58,11 @@ class Solver:
         table).
         flags: kernel-family flags (_lib.GM_F_WORDS32 / GM_F_RESOLVE_SCALAR /
         GM_F_SHARD_INORDER, A/B runs), fixed for this solver's lifetime.
-        rank/world > 1: this object is one shard of a dense multi-GPU solve
-        (gamesmanmpi_amd.dist), or with layout="hashed" one md5 shard of a
-        keyed solve (gamesmanmpi_amd.keyed; `positions` is then this
-        shard's bound); stream: a torch stream to run on."""
+        rank/world > 1: this object is one shard of a dense / planes multi-
+        GPU solve (gamesmanmpi_amd.dist), or with layout="bucketed" /
+        "hashed" one md5 shard of a keyed solve (gamesmanmpi_amd.keyed;
+        `positions` is then this shard's bound); stream: a torch stream to
+        run on."""
         import torch
         if not torch.cuda.is_available():
             raise RuntimeError("gamesmanmpi_amd needs a ROCm GPU (gfx950); "
@@ -92,7 +93,13 @@ class Solver:
         flags = self.flags | {"hashed": _lib.GM_F_FORCE_HASHED | _lib.GM_F_HASH_TABLE,
                               "bucketed": _lib.GM_F_FORCE_HASHED,
                               "dense": _lib.GM_F_LEVEL_MAJOR}.get(self.layout, 0)
-        if self.world > 1 and self.layout != "hashed":
+        if self.world > 1 and self.layout == "bucketed":
+            # an md5 shard of bucketed levels: `positions` bounds this shard
+            _lib.check(L.gm_plan_keyed_shard(self.spec.id, self.rank,
+                                             self.world, int(positions), flags,
+                                             self.max_table_bytes,
+                                             ctypes.byref(plan)))
+        elif self.world > 1 and self.layout != "hashed":
             _lib.check(L.gm_plan_shard(self.spec.id, self.rank, self.world,
                                        flags, self.max_table_bytes,
                                        ctypes.byref(plan)))

@@ -262,6 +262,18 @@ int gm_plan_shard(int game, int rank, int world, uint32_t flags,
                   uint64_t max_table_bytes, gm_plan_t *out);
 int gm_solver_create_shard(int game, int rank, int world,
                            const gm_buffers *buf, gm_solver **out);
+/* Keyed games whose every move advances one level (tic-tac-toe, toot-and-
+ * otto, othello): one shard of an md5-partitioned BUCKETED solve -- the
+ * positions with md5(str(pos)) % world == rank (GameState.get_hash,
+ * src/game_state.py:22-30; the routing of src/process.py:157-160), each
+ * level's child occurrences moved to their owners and the answers back in
+ * two all-to-alls per level (gm_solve_group for every shard in one process;
+ * gm_solver_solve per process over RCCL or a transport).  `positions`:
+ * bound on this shard's positions (0: the game's own).  Replaces the
+ * per-edge LOOK_UP / RESOLVE messages of src/process.py:146-185. */
+int gm_plan_keyed_shard(int game, int rank, int world, uint64_t positions,
+                        uint32_t flags, uint64_t max_table_bytes,
+                        gm_plan_t *out);
 /* host-only: geometry of shard `rank` -- out[0..7] = block width B (values
  * of the top digit per block), blocks over all ranks, blocks of this rank
  * (global blocks rank, rank + world, ...), rank, slice size Z (prefixes

@@ -1,8 +1,11 @@
-"""GPU: md5-sharded keyed solves through the gm_ks_* ABI, every shard of a
-job in one process on one MI355X (GroupExchange; the RCCL variant differs
-only in the exchange object).  Bit-exact against the reference's golden
-tables; every position must sit on its md5 owner (src/game_state.py:22-30).
-BASELINE config 5 is othello 4x4 over 8 ranks."""
+"""GPU: md5-sharded keyed solves, every shard of a job in one process on one
+MI355X -- BUCKETED shards (gm_bucketed_shard.h, gm_solve_group: the
+all-to-alls as device copies) for games whose every move advances one
+level, HASHED shards through the gm_ks_* ABI (GroupExchange) otherwise --
+and two processes over torch.distributed.  Bit-exact against the
+reference's golden tables; every position must sit on its md5 owner
+(src/game_state.py:22-30).  BASELINE config 5 is othello 4x4 over 8
+ranks."""
 import numpy as np
 import pytest
 
@@ -21,6 +24,9 @@ def test_gpu_group_keyed_matches_golden(name, world, golden_summary):
     from gamesmanmpi_amd.keyed import group_keyed_solve
     spec = GameSpec(*CASES[name])
     r, shards = group_keyed_solve(spec, world)
+    # games whose every move advances one level run as md5-sharded BUCKETED
+    # levels (gm_bucketed_shard.h), the others on HASHED shards
+    assert r.extra["layout"] == ("hashed" if name.startswith(("four_to_one", "sum_")) else "bucketed")
     info = golden_summary[name]
     assert (r.positions, r.edges, r.primitives) == (
         info["positions"], info["edges"], info["primitives"])
@@ -40,6 +46,64 @@ def test_gpu_group_keyed_matches_golden(name, world, golden_summary):
     np.testing.assert_array_equal(canon[order], t["canon"])
     np.testing.assert_array_equal(val[order], t["value"])
     np.testing.assert_array_equal(rem[order], t["remoteness"])
+
+
+def _check_golden_shards(name, r, shards, world, golden_summary):
+    from gamesmanmpi_amd.games import GameSpec
+    spec = GameSpec(*CASES[name])
+    info = golden_summary[name]
+    assert (r.positions, r.edges, r.primitives, r.root_line) == (
+        info["positions"], info["edges"], info["primitives"], info["root_line"])
+    dumps = [s.dump() for s in shards]
+    for rank, d in enumerate(dumps):
+        if len(d[0]):
+            assert (spec.owners_host(d[0], world) == rank).all()
+    keys = np.concatenate([d[0] for d in dumps])
+    val = np.concatenate([d[1] for d in dumps])
+    rem = np.concatenate([d[2] for d in dumps])
+    t = load_table(name)
+    canon, clen = spec.decode_batch(keys, stride=t["canon"].shape[1])
+    order = np.array(sorted(range(len(keys)), key=lambda i: bytes(canon[i, :clen[i]])), np.int64)
+    np.testing.assert_array_equal(canon[order], t["canon"])
+    np.testing.assert_array_equal(val[order], t["value"])
+    np.testing.assert_array_equal(rem[order], t["remoteness"])
+
+
+@pytest.mark.parametrize("name,world", [("othello_4x4", 8), ("toot_4x3", 3), ("tic_tac_toe_np", 2)])
+def test_gpu_group_keyed_hashed_shards_still_golden(name, world, golden_summary):
+    """The HASHED md5 shards (the path of games the bucketed levels do not
+    serve) on games both layouts serve."""
+    from gamesmanmpi_amd.games import GameSpec
+    from gamesmanmpi_amd.keyed import group_keyed_solve
+    r, shards = group_keyed_solve(GameSpec(*CASES[name]), world, layout="hashed")
+    assert r.extra["layout"] == "hashed"
+    _check_golden_shards(name, r, shards, world, golden_summary)
+
+
+@pytest.mark.parametrize("world", [2, 4, 7])
+def test_gpu_bucketed_shards_toot_5x4_checksum(world):
+    """toot 5x4 (70,184,763 positions) on 2 / 4 / 7 md5 BUCKETED shards: the
+    shards' fingerprints (each over the positions it owns) add up to the CPU
+    restatement's golden (oracle/oracle_mt.c; beyond 4x4 no reference
+    fixture exists -- parity against the restatement, as on one GPU)."""
+    import json
+    import os
+    import torch
+    from conftest import GOLDEN
+    from gamesmanmpi_amd.games import GameSpec
+    from gamesmanmpi_amd.keyed import group_keyed_solve
+    e = json.load(open(os.path.join(GOLDEN, "checksums.json")))["toot_5x4"]
+    r, shards = group_keyed_solve(GameSpec(e["game"], e["params"]), world)
+    assert r.extra["layout"] == "bucketed"
+    assert (r.positions, r.edges, r.primitives, r.root_line) == (e["positions"], e["edges"], e["primitives"],
+                                                                  e["root_line"])
+    cks = [s.checksum() for s in shards]
+    assert "%016x" % (sum(int(c["checksum"], 16) for c in cks) % (1 << 64)) == e["checksum"]
+    assert sum(c["positions"] for c in cks) == e["positions"]
+    assert (sum(c["win"] for c in cks), sum(c["loss"] for c in cks), sum(c["tie"] for c in cks)) == (
+        e["win"], e["loss"], e["tie"])
+    del shards
+    torch.cuda.empty_cache()
 
 
 def test_gpu_keyed_shard_refuses_whole_solve():
@@ -71,10 +135,10 @@ def _dist_worker(rank, world, port, q, name):
 
 @pytest.mark.parametrize("name", ["othello_4x4", "toot_4x3"])
 def test_gpu_keyed_two_processes_torch_exchange(name, golden_summary):
-    """The one-process-per-rank path (TorchExchange over torch.distributed,
-    the code the launcher runs under torchrun) with two ranks sharing one
-    GPU: gloo carries the all-to-alls through host memory here, RCCL does on
-    an 8-GPU node.  othello 4x4 and toot 4x3 bit-exact against the reference-
+    """The one-process-per-rank path (the code the launcher runs under
+    torchrun): md5-sharded BUCKETED shards (ShardedSolver; the library's
+    level loop with the host-staged transport over gloo here, RCCL send /
+    recv on an 8-GPU node) with two ranks sharing one GPU.  othello 4x4 and toot 4x3 bit-exact against the reference-
     generated tables, positions on their md5 owners."""
     import socket
     import torch.multiprocessing as mp
