@@ -303,6 +303,7 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
     // (a) per shard: children per owner and per parent range
     std::vector<std::vector<u64>> sendc(ss.size());
     std::vector<u64> meta_at(ss.size(), 0), ptot_all(ss.size() * kBkC, 0);
+    std::vector<char> over(ss.size(), 0);  // the count-free expand already filled the send regions
     for (size_t g = 0; g < ss.size(); g++) {
       gm_solver* s = ss[g];
       std::vector<BkLevel>& lv = s->lvh;
@@ -330,21 +331,48 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
         P.rfo_off = (uint32_t)meta_used;
         meta_used += NR + 1;
         uint32_t* rfo = s->meta + P.rfo_off;
-        if (!prc) HIPCHK(hipMemsetAsync(rfo, 0, (NR + 1) * 4, st));
-        bk_dispatch(s->d, [&](auto kind_) {
-          constexpr int K_ = decltype(kind_)::value;
-          hipLaunchKernelGGL((k_bk_count<K_, true>), dim3(nblk), dim3(kBkStreamThreads), 0, st, s->d, s->bkK + P.lb, P.n,
-                             chunk, P.pshift, P.fb, s->bh, s->ph, rfo, s->st, (uint32_t)W);
-        });
-        hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, st, s->bh, (uint32_t)nblk, s->boff, s->tot);
-        hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, st, s->ph, (uint32_t)nblk, s->ph, s->tot + kBkC);
-        hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, st, rfo, NR + 1, rfo, s->bktotal + 1);
-        HIPCHK(hipGetLastError());
-        std::vector<uint32_t> htot(2 * kBkC);
+        // Count-free form first: the children go straight to per-owner
+        // regions of the send buffer (one MD5 per child); an owner past its
+        // region (Emax / W records) -> count, then the exact form in (c).
+        bool exact = (s->flags & GM_F_BK_EXACT) != 0 || prc;
+        std::vector<uint32_t> htot(2 * kBkC + 1, 0);
         uint32_t herr = 0;
-        HIPCHK(hipMemcpyAsync(htot.data(), s->tot, 2 * kBkC * 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipMemcpyAsync(&herr, &s->st->err, 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
+        if (!exact) {
+          HIPCHK(hipMemsetAsync(rfo, 0, (NR + 1) * 4, st));
+          HIPCHK(hipMemsetAsync(s->bkgc, 0, (2 * kBkC + 4) * 4, st));
+          const double avg = (L > 0 && s->lvh[(size_t)L - 1].n) ? std::max(1.0, (double)P.ein / (double)s->lvh[(size_t)L - 1].n)
+                                                                 : 4.0;
+          const uint32_t capd = (uint32_t)(s->Emax / (u64)W);
+          bk_dispatch(s->d, [&](auto kind_) {
+            constexpr int K_ = decltype(kind_)::value;
+            hipLaunchKernelGGL((k_bk_expand<K_, true, true>), dim3(nblk), dim3(kBkExpandThreads), 0, st, s->d,
+                               s->bkK + P.lb, P.n, chunk, (const uint32_t*)nullptr, (const uint32_t*)nullptr, bk_ppr(avg),
+                               s->XSk, s->XSr, (uint8_t*)nullptr, capd, s->bkgc, P.pshift, P.fb, s->bkgc + kBkC, rfo,
+                               s->bkgc + 2 * kBkC, s->st, BkChunked{nullptr, 0}, (uint32_t)W, (uint32_t)s->rank << 29);
+          });
+          hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, st, rfo, NR + 1, rfo, s->bktotal + 1);
+          HIPCHK(hipGetLastError());
+          HIPCHK(hipMemcpyAsync(htot.data(), s->bkgc, htot.size() * 4, hipMemcpyDeviceToHost, st));
+          HIPCHK(hipMemcpyAsync(&herr, &s->st->err, 4, hipMemcpyDeviceToHost, st));
+          HIPCHK(hipStreamSynchronize(st));
+          if (htot[2 * kBkC]) exact = true;  // an owner region overflowed: redo the level counted
+          else over[g] = 1;
+        }
+        if (exact && !prc && !herr) {
+          HIPCHK(hipMemsetAsync(rfo, 0, (NR + 1) * 4, st));
+          bk_dispatch(s->d, [&](auto kind_) {
+            constexpr int K_ = decltype(kind_)::value;
+            hipLaunchKernelGGL((k_bk_count<K_, true>), dim3(nblk), dim3(kBkStreamThreads), 0, st, s->d, s->bkK + P.lb,
+                               P.n, chunk, P.pshift, P.fb, s->bh, s->ph, rfo, s->st, (uint32_t)W);
+          });
+          hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, st, s->bh, (uint32_t)nblk, s->boff, s->tot);
+          hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, st, s->ph, (uint32_t)nblk, s->ph, s->tot + kBkC);
+          hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, st, rfo, NR + 1, rfo, s->bktotal + 1);
+          HIPCHK(hipGetLastError());
+          HIPCHK(hipMemcpyAsync(htot.data(), s->tot, 2 * kBkC * 4, hipMemcpyDeviceToHost, st));
+          HIPCHK(hipMemcpyAsync(&herr, &s->st->err, 4, hipMemcpyDeviceToHost, st));
+          HIPCHK(hipStreamSynchronize(st));
+        }
         if (herr) defer(fail(GM_ECORRUPT, "shard %d level %d:%s", s->rank, L, err_text(herr).c_str()));
         for (int p = 0; p < W; p++) sendc[g][(size_t)p] = htot[(size_t)p];
         for (int j = 0; j < kBkC; j++) ptot_all[g * kBkC + (size_t)j] = htot[(size_t)kBkC + j];
@@ -388,8 +416,11 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
         sc[(size_t)p] = M[(size_t)r * W + p];
         rcv[(size_t)p] = M[(size_t)p * W + r];
       }
-      const std::vector<u64> so = bks_prefix(sc), ro = bks_prefix(rcv);
+      std::vector<u64> so = bks_prefix(sc);
+      const std::vector<u64> ro = bks_prefix(rcv);
       const u64 Eout = so[(size_t)W], Ein = ro[(size_t)W];
+      if (over[g])  // owner p's records sit at [p cap, ...) of the send buffer
+        for (int p = 0; p < W; p++) so[(size_t)p] = (u64)p * (s->Emax / (u64)W);
       u64 Ep = 0;
       for (int j = 0; j < kBkC; j++) Ep += ptot_all[g * kBkC + (size_t)j];
       if (Eout != Ep)  // an internal inconsistency of this rank's own counts: recorded, reported at the end
@@ -411,7 +442,7 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
       HIPCHK(hipMemcpyAsync(s->cbase, hb.data(), (kBkC + 1) * 4, hipMemcpyHostToDevice, st));
       HIPCHK(hipMemcpyAsync(s->pbase + (size_t)L * (kBkC + 1), hb.data() + kBkC + 1, (kBkC + 1) * 4,
                             hipMemcpyHostToDevice, st));
-      if (P.n && Eout) {
+      if (P.n && Eout && !over[g]) {
         const u64 nblk = std::min<u64>(kBkExpandBlocks, (P.n + kBkExpandThreads - 1) / kBkExpandThreads),
                   chunk = (P.n + nblk - 1) / nblk;
         const uint32_t ppr = bk_ppr((double)Eout / (double)P.n);

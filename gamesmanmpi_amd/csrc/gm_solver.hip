@@ -808,17 +808,16 @@ __global__ void k_gather_positions(const u64* lv, u64 lcap, const DevState* st, 
     out[i] = i < nf ? lv[i] : lv[lcap - 1 - (i - nf)];
 }
 
-__global__ void k_owner(Desc d, const u64* keys, u64 n, uint32_t P, uint32_t* owners) {
-  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
-    uint8_t s[56], dig[16];
-    int len = str_utf8_from_key(d, keys[i], s);
-    md5_block(s, len, dig);
-    owners[i] = md5_mod(dig, P);
-  }
-}
 
 #include "gm_dense.h"
 #include "gm_keyed_shard.h"
+
+// K4 owner kernel: md5(str(pos)) % P per key (GameState.get_hash,
+// src/game_state.py:22-30), the register-resident form where it applies
+__global__ void k_owner(Desc d, const u64* keys, u64 n, uint32_t P, uint32_t* owners) {
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x)
+    owners[i] = owner_dev(d, keys[i], P);
+}
 #include "gm_bucketed.h"
 
 // ---------------------------------------------------------------------------

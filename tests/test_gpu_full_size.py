@@ -141,3 +141,26 @@ def test_gpu_sum_31x5_255_eight_shards_checksum():
     import torch
     _check_group("sum_31x5_255", 8)
     torch.cuda.empty_cache()
+
+
+def test_gpu_toot_6x4_two_md5_shards_checksum():
+    """BASELINE config 3's board (toot 6x4, 1,187,212,827 positions) as two
+    md5 shards of BUCKETED levels (gm_bucketed_shard.h) solved as an
+    in-process group: the shards' fingerprints, each over the positions it
+    owns, add up to the CPU restatement's golden (parity unpinned by
+    reference fixtures beyond 4x4, as on one GPU)."""
+    import torch
+    from gamesmanmpi_amd.games import GameSpec
+    from gamesmanmpi_amd.keyed import group_keyed_solve
+    e = _gold("toot_6x4")
+    r, shards = group_keyed_solve(GameSpec(e["game"], e["params"]), 2)
+    assert r.extra["layout"] == "bucketed"
+    assert (r.positions, r.edges, r.primitives, r.root_line) == (e["positions"], e["edges"], e["primitives"],
+                                                                  e["root_line"])
+    cks = [s.checksum() for s in shards]
+    assert "%016x" % (sum(int(c["checksum"], 16) for c in cks) % (1 << 64)) == e["checksum"]
+    assert sum(c["positions"] for c in cks) == e["positions"]
+    assert (sum(c["win"] for c in cks), sum(c["loss"] for c in cks), sum(c["tie"] for c in cks)) == (
+        e["win"], e["loss"], e["tie"])
+    del shards
+    torch.cuda.empty_cache()
