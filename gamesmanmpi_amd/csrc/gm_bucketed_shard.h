@@ -214,13 +214,18 @@ static int bks_allgather(std::vector<gm_solver*>& ss, int mode, hipStream_t st, 
   }
   gm_solver* s = ss[0];
   if (mode == 3) return xfer_call(s, GM_XFER_ALLGATHER, mine[0].data(), m * 8, -1, out.data(), out.size() * 8, -1);
-  u64* dev = nullptr;
-  HIPCHK(hipMalloc((void**)&dev, (m + out.size()) * 8));
+  if (s->xdev_n < m + out.size()) {  // kept across levels and solves (freed with the solver)
+    if (s->xdev) (void)hipFree(s->xdev);
+    s->xdev = nullptr;
+    s->xdev_n = 0;
+    HIPCHK(hipMalloc((void**)&s->xdev, (m + out.size()) * 8));
+    s->xdev_n = m + out.size();
+  }
+  u64* dev = s->xdev;
   HIPCHK(hipMemcpyAsync(dev, mine[0].data(), m * 8, hipMemcpyHostToDevice, st));
   const ncclResult_t r = ncclAllGather(dev, dev + m, m, ncclUint64, s->comm, st);
   hipError_t e = hipMemcpyAsync(out.data(), dev + m, out.size() * 8, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
-  (void)hipFree(dev);
   if (r != ncclSuccess) return fail(GM_EHIP, "RCCL all-gather: %s", ncclGetErrorString(r));
   if (e != hipSuccess) return fail(GM_EHIP, "all-gather: %s", hipGetErrorString(e));
   return 0;
@@ -304,6 +309,16 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
     std::vector<std::vector<u64>> sendc(ss.size());
     std::vector<u64> meta_at(ss.size(), 0), ptot_all(ss.size() * kBkC, 0);
     std::vector<char> over(ss.size(), 0);  // the count-free expand already filled the send regions
+    // every shard's launches first, then ONE host sync for all of them (and
+    // a second only when some owner region overflowed)
+    struct Pending {
+      std::vector<uint32_t> htot;
+      uint32_t herr = 0;
+      bool active = false, exact = false;
+      u64 nblk = 0, chunk = 0;
+      uint32_t NR = 0;
+    };
+    std::vector<Pending> pd(ss.size());
     for (size_t g = 0; g < ss.size(); g++) {
       gm_solver* s = ss[g];
       std::vector<BkLevel>& lv = s->lvh;
@@ -320,67 +335,83 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
       X.rb = P.rb + P.ein;
       P.eout = 0;
       sendc[g].assign((size_t)W + 3, 0);
+      Pending& q = pd[g];
+      q.htot.assign(2 * kBkC + 1, 0);
       if (!bk_ranges(P.n, &P.pshift, &P.fb))
         defer(fail(GM_ELIMIT, "level %d holds %llu positions: more than a bucketed level supports", L,
                    (unsigned long long)P.n));
       if (P.n && !prc) {
-        const u64 nblk = std::min<u64>(kBkExpandBlocks, (P.n + kBkExpandThreads - 1) / kBkExpandThreads),
-                  chunk = (P.n + nblk - 1) / nblk;
-        const uint32_t NR = (uint32_t)((P.n + (1ull << P.fb) - 1) >> P.fb);
-        if (meta_used + NR + 1 > s->meta_cap) defer(fail(GM_ECORRUPT, "bucket tables exceed the scratch"));
+        q.nblk = std::min<u64>(kBkExpandBlocks, (P.n + kBkExpandThreads - 1) / kBkExpandThreads);
+        q.chunk = (P.n + q.nblk - 1) / q.nblk;
+        q.NR = (uint32_t)((P.n + (1ull << P.fb) - 1) >> P.fb);
+        if (meta_used + q.NR + 1 > s->meta_cap) defer(fail(GM_ECORRUPT, "bucket tables exceed the scratch"));
         P.rfo_off = (uint32_t)meta_used;
-        meta_used += NR + 1;
-        uint32_t* rfo = s->meta + P.rfo_off;
-        // Count-free form first: the children go straight to per-owner
-        // regions of the send buffer (one MD5 per child); an owner past its
-        // region (Emax / W records) -> count, then the exact form in (c).
-        bool exact = (s->flags & GM_F_BK_EXACT) != 0 || prc;
-        std::vector<uint32_t> htot(2 * kBkC + 1, 0);
-        uint32_t herr = 0;
-        if (!exact) {
-          HIPCHK(hipMemsetAsync(rfo, 0, (NR + 1) * 4, st));
-          HIPCHK(hipMemsetAsync(s->bkgc, 0, (2 * kBkC + 4) * 4, st));
-          const double avg = (L > 0 && s->lvh[(size_t)L - 1].n) ? std::max(1.0, (double)P.ein / (double)s->lvh[(size_t)L - 1].n)
-                                                                 : 4.0;
-          const uint32_t capd = (uint32_t)(s->Emax / (u64)W);
-          bk_dispatch(s->d, [&](auto kind_) {
-            constexpr int K_ = decltype(kind_)::value;
-            hipLaunchKernelGGL((k_bk_expand<K_, true, true>), dim3(nblk), dim3(kBkExpandThreads), 0, st, s->d,
-                               s->bkK + P.lb, P.n, chunk, (const uint32_t*)nullptr, (const uint32_t*)nullptr, bk_ppr(avg),
-                               s->XSk, s->XSr, (uint8_t*)nullptr, capd, s->bkgc, P.pshift, P.fb, s->bkgc + kBkC, rfo,
-                               s->bkgc + 2 * kBkC, s->st, BkChunked{nullptr, 0}, (uint32_t)W, (uint32_t)s->rank << 29);
-          });
-          hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, st, rfo, NR + 1, rfo, s->bktotal + 1);
-          HIPCHK(hipGetLastError());
-          HIPCHK(hipMemcpyAsync(htot.data(), s->bkgc, htot.size() * 4, hipMemcpyDeviceToHost, st));
-          HIPCHK(hipMemcpyAsync(&herr, &s->st->err, 4, hipMemcpyDeviceToHost, st));
-          HIPCHK(hipStreamSynchronize(st));
-          if (htot[2 * kBkC]) exact = true;  // an owner region overflowed: redo the level counted
-          else over[g] = 1;
-        }
-        if (exact && !prc && !herr) {
-          HIPCHK(hipMemsetAsync(rfo, 0, (NR + 1) * 4, st));
-          bk_dispatch(s->d, [&](auto kind_) {
-            constexpr int K_ = decltype(kind_)::value;
-            hipLaunchKernelGGL((k_bk_count<K_, true>), dim3(nblk), dim3(kBkStreamThreads), 0, st, s->d, s->bkK + P.lb,
-                               P.n, chunk, P.pshift, P.fb, s->bh, s->ph, rfo, s->st, (uint32_t)W);
-          });
-          hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, st, s->bh, (uint32_t)nblk, s->boff, s->tot);
-          hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, st, s->ph, (uint32_t)nblk, s->ph, s->tot + kBkC);
-          hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, st, rfo, NR + 1, rfo, s->bktotal + 1);
-          HIPCHK(hipGetLastError());
-          HIPCHK(hipMemcpyAsync(htot.data(), s->tot, 2 * kBkC * 4, hipMemcpyDeviceToHost, st));
-          HIPCHK(hipMemcpyAsync(&herr, &s->st->err, 4, hipMemcpyDeviceToHost, st));
-          HIPCHK(hipStreamSynchronize(st));
-        }
-        if (herr) defer(fail(GM_ECORRUPT, "shard %d level %d:%s", s->rank, L, err_text(herr).c_str()));
-        for (int p = 0; p < W; p++) sendc[g][(size_t)p] = htot[(size_t)p];
-        for (int j = 0; j < kBkC; j++) ptot_all[g * kBkC + (size_t)j] = htot[(size_t)kBkC + j];
+        meta_used += q.NR + 1;
+        q.active = !prc;
+        q.exact = (s->flags & GM_F_BK_EXACT) != 0;
       }
       meta_at[g] = meta_used;
+      if (!q.active || q.exact) continue;
+      // Count-free form first: the children go straight to per-owner
+      // regions of the send buffer (one MD5 per child); an owner past its
+      // region (Emax / W records) -> count, then the exact form in (c).
+      uint32_t* rfo = s->meta + P.rfo_off;
+      HIPCHK(hipMemsetAsync(rfo, 0, (q.NR + 1) * 4, st));
+      HIPCHK(hipMemsetAsync(s->bkgc, 0, (2 * kBkC + 4) * 4, st));
+      const double avg =
+          (L > 0 && s->lvh[(size_t)L - 1].n) ? std::max(1.0, (double)P.ein / (double)s->lvh[(size_t)L - 1].n) : 4.0;
+      const uint32_t capd = (uint32_t)(s->Emax / (u64)W);
+      bk_dispatch(s->d, [&](auto kind_) {
+        constexpr int K_ = decltype(kind_)::value;
+        hipLaunchKernelGGL((k_bk_expand<K_, true, true>), dim3(q.nblk), dim3(kBkExpandThreads), 0, st, s->d,
+                           s->bkK + P.lb, P.n, q.chunk, (const uint32_t*)nullptr, (const uint32_t*)nullptr, bk_ppr(avg),
+                           s->XSk, s->XSr, (uint8_t*)nullptr, capd, s->bkgc, P.pshift, P.fb, s->bkgc + kBkC, rfo,
+                           s->bkgc + 2 * kBkC, s->st, BkChunked{nullptr, 0}, (uint32_t)W, (uint32_t)s->rank << 29);
+      });
+      hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, st, rfo, q.NR + 1, rfo, s->bktotal + 1);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipMemcpyAsync(q.htot.data(), s->bkgc, q.htot.size() * 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(&q.herr, &s->st->err, 4, hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    bool any_exact = false;
+    for (size_t g = 0; g < ss.size(); g++) {
+      gm_solver* s = ss[g];
+      Pending& q = pd[g];
+      if (!q.active) continue;
+      if (!q.exact) {
+        if (q.htot[2 * kBkC] && !q.herr) q.exact = true;  // an owner region overflowed: redo the level counted
+        else over[g] = 1;
+      }
+      if (!q.exact || q.herr) continue;
+      any_exact = true;
+      BkLevel& P = s->lvh[(size_t)L];
+      uint32_t* rfo = s->meta + P.rfo_off;
+      HIPCHK(hipMemsetAsync(rfo, 0, (q.NR + 1) * 4, st));
+      bk_dispatch(s->d, [&](auto kind_) {
+        constexpr int K_ = decltype(kind_)::value;
+        hipLaunchKernelGGL((k_bk_count<K_, true>), dim3(q.nblk), dim3(kBkStreamThreads), 0, st, s->d, s->bkK + P.lb,
+                           P.n, q.chunk, P.pshift, P.fb, s->bh, s->ph, rfo, s->st, (uint32_t)W);
+      });
+      hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, st, s->bh, (uint32_t)q.nblk, s->boff, s->tot);
+      hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, st, s->ph, (uint32_t)q.nblk, s->ph, s->tot + kBkC);
+      hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, st, rfo, q.NR + 1, rfo, s->bktotal + 1);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipMemcpyAsync(q.htot.data(), s->tot, 2 * kBkC * 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(&q.herr, &s->st->err, 4, hipMemcpyDeviceToHost, st));
+    }
+    if (any_exact) HIPCHK(hipStreamSynchronize(st));
+    for (size_t g = 0; g < ss.size(); g++) {
+      gm_solver* s = ss[g];
+      Pending& q = pd[g];
+      if (q.active) {
+        if (q.herr) defer(fail(GM_ECORRUPT, "shard %d level %d:%s", s->rank, L, err_text(q.herr).c_str()));
+        for (int p = 0; p < W; p++) sendc[g][(size_t)p] = q.htot[(size_t)p];
+        for (int j = 0; j < kBkC; j++) ptot_all[g * kBkC + (size_t)j] = q.htot[(size_t)kBkC + j];
+      }
       sendc[g][(size_t)W] = (u64)(int64_t)prc;
       sendc[g][(size_t)W + 1] = s->Emax;
-      sendc[g][(size_t)W + 2] = s->Ecap - std::min(s->Ecap, X.rb);
+      sendc[g][(size_t)W + 2] = s->Ecap - std::min(s->Ecap, s->lvh[(size_t)L + 1].rb);
     }
     // (b) the size matrix (with every rank's status and room)
     std::vector<u64> MA;
@@ -506,14 +537,19 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
       HIPCHK(hipGetLastError());
       (void)P;
     }
+    std::vector<uint32_t> derr(ss.size(), 0);
+    for (size_t g = 0; g < ss.size(); g++) {
+      gm_solver* s = ss[g];
+      if (!s->lvh[(size_t)L + 1].ein) continue;
+      HIPCHK(hipMemcpyAsync(&ncnt[g], s->bktotal, 8, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(&derr[g], &s->st->err, 4, hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(hipStreamSynchronize(st));  // one host sync for every shard's level size
     for (size_t g = 0; g < ss.size(); g++) {
       gm_solver* s = ss[g];
       BkLevel& X = s->lvh[(size_t)L + 1];
       if (!X.ein) continue;
-      uint32_t herr = 0;
-      HIPCHK(hipMemcpyAsync(&ncnt[g], s->bktotal, 8, hipMemcpyDeviceToHost, st));
-      HIPCHK(hipMemcpyAsync(&herr, &s->st->err, 4, hipMemcpyDeviceToHost, st));
-      HIPCHK(hipStreamSynchronize(st));
+      const uint32_t herr = derr[g];
       if (herr) {
         const bool lim = herr & ERR_BUCKET_FULL;
         defer(fail(lim ? GM_ELIMIT : GM_ECORRUPT, "shard %d level %d:%s", s->rank, L + 1, err_text(herr).c_str()));

@@ -971,6 +971,8 @@ struct gm_solver {
   u64 *XSk = nullptr, *XRk = nullptr;  // md5-sharded bucketed levels: exchange buffers
   uint32_t *XSr = nullptr, *XRr = nullptr;
   std::vector<std::vector<u64>> bks_sc, bks_rc;  // per forward level: records sent to / received from each rank
+  u64* xdev = nullptr;  // RCCL all-gather staging of the sharded bucketed loop
+  size_t xdev_n = 0;
   u64 Pcap = 0, Ecap = 0, Emax = 0;
   BkLevel* bkL = nullptr;  // device level table (scratch)
   uint32_t *pbase = nullptr, *bh = nullptr, *ph = nullptr, *boff = nullptr, *tot = nullptr, *cbase = nullptr;
@@ -2125,6 +2127,7 @@ void gm_solver_destroy(gm_solver* s) {
   if (s->cstream) (void)hipStreamDestroy(s->cstream);
   if (s->comm) (void)ncclCommDestroy(s->comm);
   if (s->errg) (void)hipFree(s->errg);
+  if (s->xdev) (void)hipFree(s->xdev);
   if (s->own_stream) (void)hipStreamDestroy(s->stream);
   delete s;
 }
