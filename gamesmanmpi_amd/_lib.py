@@ -28,8 +28,9 @@ GM_F_BK_EXACT = 128  # bucketed: count pass + exact partition offsets
 GM_F_GRAPH = 256  # dense one-table solves replay captured HIP graphs
 GM_F_LEVEL_MAJOR = 512  # the level-major DENSE layout where PLANES would apply
 GM_F_PLANE_X1 = 1024  # PLANES A/B: one plane per half-wave (k_plane_resolve)
+GM_F_PLANE_ROUND_ROBIN = 2048  # PLANES shards A/B: round-robin blocks (one halo link)
 KERNEL_FLAGS = (GM_F_WORDS32 | GM_F_RESOLVE_SCALAR | GM_F_SHARD_INORDER | GM_F_WORDS16 | GM_F_BK_EXACT
-                | GM_F_GRAPH | GM_F_LEVEL_MAJOR | GM_F_PLANE_X1)
+                | GM_F_GRAPH | GM_F_LEVEL_MAJOR | GM_F_PLANE_X1 | GM_F_PLANE_ROUND_ROBIN)
 # gm_result.kernels codes (gm_solver.hip DenseResolveKind / DensePullKind)
 RESOLVE_KERNELS = {1: "k_dense_resolve8p", 2: "k_dense_resolve8c", 3: "k_dense_resolve4p",
                    4: "k_dense_resolve4c", 5: "k_dense_resolve4", 6: "k_dense_resolve",
@@ -112,7 +113,7 @@ EXPORTS = (
     "gm_solver_destroy", "gm_solve", "gm_query", "gm_release", "gm_owner", "gm_owner_host",
     "gm_plan_shard", "gm_plan_keyed_shard", "gm_solver_create_shard", "gm_comm_unique_id",
     "gm_solver_comm_init", "gm_solve_group", "gm_solver_set_flags", "gm_solver_set_steps",
-    "gm_shard_info", "gm_solver_set_transport", "gm_shard_halo_sigs",
+    "gm_shard_info", "gm_solver_set_transport", "gm_shard_halo_sigs", "gm_plane_halo_plan",
     "gm_ks_begin", "gm_ks_level_size", "gm_ks_expand", "gm_ks_insert",
     "gm_ks_finalize", "gm_ks_counts", "gm_ks_children", "gm_ks_reduce",
     "gm_ks_end", "gm_graph_solve",
@@ -183,6 +184,7 @@ def load():
         "gm_shard_info": [c.c_int, c.c_int, c.c_int, P(c.c_uint64)],
         "gm_solver_set_transport": [c.c_void_p, XFER_FN, c.c_void_p],
         "gm_shard_halo_sigs": [c.c_int, c.c_int, c.c_int, c.c_uint32, c.c_void_p, c.c_uint32],
+        "gm_plane_halo_plan": [c.c_int, c.c_int, c.c_int, c.c_uint32, c.c_void_p, c.c_uint32],
         "gm_ks_begin": [c.c_void_p, c.c_int],
         "gm_ks_level_size": [c.c_void_p, c.c_int, P(c.c_uint64)],
         "gm_ks_expand": [c.c_void_p, c.c_int, c.c_void_p, c.c_void_p,

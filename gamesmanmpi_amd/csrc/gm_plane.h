@@ -49,23 +49,44 @@ constexpr int kPlaneMaxOuter = 6;  // K <= 8 heaps
 
 // Geometry of one PLANES table (a whole game, or one shard of it).  A shard
 // (world > 1) owns blocks of B consecutive values of the TOP outer digit
-// (heap K-1), block g owned by rank g mod world (round robin, as the
-// level-major shards: DESIGN.md §6); its table holds only its own slices,
-// block after block: local plane = (j * B + o) * Z + lower, where j is the
-// rank's block number, o the value's offset in the block, Z = planes per top
-// value and lower = the index of the digits below the top.  Neighbours along
-// the top digit that belong to the previous block come from a halo buffer
-// (PlaneEntry).
+// (heap K-1), dealt in rounds of `world` blocks: round j = blocks
+// [j * world, (j + 1) * world) gives each rank one block (plane_owner); its
+// table holds only its own slices, block after block: local plane =
+// (j * B + o) * Z + lower, where j is the rank's block number (= the round),
+// o the value's offset in the block, Z = planes per top value and lower =
+// the index of the digits below the top.  Neighbours along the top digit
+// that belong to the previous block come from a halo buffer (PlaneEntry).
 struct PlaneGeom {
   uint32_t no;     // outer digits (heaps 2 .. K-1)
   uint32_t pow2;   // every outer base a power of two
   uint32_t nplanes;  // planes of this table (local)
   uint32_t world, rank, B, Z;  // shards (world 1: B = Z = 0)
+  uint32_t spread;  // shards: the link-spreading deal (plane_owner), else round robin
   uint32_t base[kPlaneMaxOuter];
   uint32_t shift[kPlaneMaxOuter];   // log2(stride[j]) when pow2
   uint32_t stride[kPlaneMaxOuter];  // global plane-index stride of outer digit j
   uint32_t rlim[kPlaneMaxOuter + 2];  // reach: heap i reachable up to rlim[i] (heaps 0, 1, then outer)
 };
+
+// Which rank owns global block b, and which global block is a rank's local
+// block j.  Round robin: block c of a round goes to rank c, so every block's
+// successor lives on rank + 1 and a shard's whole halo crosses ONE xGMI link.
+// The spreading deal (world a power of two >= 4, whole rounds): round j
+// gives block c to rank c * (2j + 1) mod world -- an odd multiplier, so a
+// permutation -- and the successor of a rank's round-j block sits 2j + 1
+// ranks further on: the rounds' halos leave on up to world / 2 different
+// links.  Block 0 stays rank 0's local block 0 (the primitive plane).
+__host__ __device__ inline uint32_t plane_owner(const PlaneGeom& g, uint32_t b) {
+  const uint32_t c = b % g.world;
+  return g.spread ? (c * (2u * (b / g.world) + 1u)) & (g.world - 1u) : c;
+}
+__host__ __device__ inline uint32_t plane_gblock(const PlaneGeom& g, uint32_t j) {
+  if (!g.spread) return g.rank + j * g.world;
+  const uint32_t m = 2u * j + 1u;
+  uint32_t inv = m;  // m^-1 mod 2^32 by Newton steps (each doubles the good bits)
+  for (int i = 0; i < 5; i++) inv *= 2u - m * inv;
+  return j * g.world + ((g.rank * inv) & (g.world - 1u));
+}
 
 // Sharded level lists: per plane, where its top-digit neighbours are and
 // where its words go besides the table.
@@ -452,7 +473,7 @@ __device__ __forceinline__ void plane_global_digits(const PlaneGeom& g, uint32_t
   plane_digits<NO>(g, P, dig);
   if (g.world > 1 && NO > 0) {
     const uint32_t u = P / g.Z, j = u / g.B, o = u - j * g.B;
-    dig[NO - 1] = (g.rank + j * g.world) * g.B + o;
+    dig[NO - 1] = plane_gblock(g, j) * g.B + o;
   }
 }
 

@@ -7,9 +7,10 @@
 //
 // Reference path replaced: src/process.py:37-267 (the per-state job loop)
 // and src/game_state.py:22-30 (which rank owns a state): a shard owns
-// round-robin blocks of the last heap's values; the per-edge LOOK_UP /
-// RESOLVE messages become, per plane level, ONE send of the rank's boundary
-// slices to the next rank (the planes its first two slices need).
+// blocks of the last heap's values (plane_owner); the per-edge LOOK_UP /
+// RESOLVE messages become, per plane level, one grouped send of the rank's
+// boundary slices to the ranks owning its blocks' successors (the planes
+// their first two slices need).
 
 // (gm_solver.hip includes this inside its extern "C" block: templates need
 // C++ linkage)
@@ -49,7 +50,7 @@ __device__ __forceinline__ bool plane_locate(const Desc& d, const PlaneGeom& g, 
   const int no = d.nheaps - 2;
   if (g.world > 1) {
     const uint32_t t = dig[d.nheaps - 1], blk = t / g.B, o = t - blk * g.B;
-    if (blk % g.world != g.rank) return false;
+    if (plane_owner(g, blk) != g.rank) return false;
     for (int j = 0; j + 1 < no; j++) p += (u64)dig[2 + j] * g.stride[j];
     p += ((u64)(blk / g.world) * g.B + o) * g.Z;
   } else {
@@ -213,10 +214,12 @@ static int plane_shape(const Desc* d, int rank, int world, uint32_t flags, Plane
     ps->nb = (uint32_t)((ps->nblocks - (u64)rank + world - 1) / world);
     g.B = (uint32_t)B;
     g.Z = (uint32_t)Z;
+    g.spread = world >= 4 && !(world & (world - 1)) && ps->nblocks % world == 0 && ps->nblocks > (u64)world &&
+               !(flags & GM_F_PLANE_ROUND_ROBIN);
     ps->nlocal = (u64)ps->nb * B * Z;
     g.nplanes = (uint32_t)ps->nlocal;
     for (uint32_t j = 0; j < ps->nb; j++) {
-      const u64 gb = (u64)rank + (u64)j * world;
+      const u64 gb = plane_gblock(g, j);
       if (gb >= 1) ps->nrecv += 2 * Z;
       if (gb + 1 < ps->nblocks) ps->nsend += 2 * Z;
     }
@@ -252,9 +255,11 @@ static int plan_planes(const Desc* d, int rank, int world, uint32_t flags, uint6
 // (outer digit sum s) in index order.  Shards: PlaneEntry per own plane,
 // level by level, and within a level block by block, slice by slice, lower
 // index ascending -- the canonical order in which the boundary slices travel:
-// the sender's level-s segment lists, for each of its blocks with a
-// successor, slices B-2 and B-1; the receiver's, for each of its blocks with
-// a predecessor, the two slices below it.  A halo plane's index is its
+// the sender's (level s, peer p) segment lists, for each of its blocks whose
+// successor p owns, slices B-2 and B-1; the receiver's (s, q), for each of
+// its blocks whose predecessor q owns, the two slices below it (local block
+// order is global block order, so both walk the same blocks in the same
+// order).  Segments are level-major, peer-minor.  A halo plane's index is its
 // group's start plus the rank of its lower digits within their digit-sum
 // class, which is also the rank of the receiving plane in its own group.
 static int plane_lists(gm_solver* s, const PlaneShape& ps, std::vector<uint8_t>& bytes) {
@@ -290,33 +295,36 @@ static int plane_lists(gm_solver* s, const PlaneShape& ps, std::vector<uint8_t>&
   std::vector<u64> ncl(smax + 1, 0);
   for (u64 l = 0; l < Z; l++) rk[l] = (uint32_t)ncl[sig[l]]++;
   auto cls = [&](int64_t c) -> u64 { return c < 0 || c > (int64_t)smax ? 0 : ncl[(size_t)c]; };
-  const u64 nb = ps.nb, world = g.world, rank = g.rank;
-  auto gblk = [&](u64 j) { return rank + j * world; };
-  // halo groups per level: recv (j, h) = top value gB - 2 + h; send (j, h) =
-  // top value gB + B - 2 + h
+  const u64 nb = ps.nb, W = g.world;
+  auto gblk = [&](u64 j) { return (u64)plane_gblock(g, (uint32_t)j); };
+  // halo groups per level and peer (the rank the slices come from / go to):
+  // recv (j, h) = top value gB - 2 + h; send (j, h) = top value gB + B - 2 + h
   std::vector<u64> rgb(((size_t)S + 1) * nb * 2, ~0ull), sgb(((size_t)S + 1) * nb * 2, ~0ull);
-  s->prcv_off.assign((size_t)S + 2, 0);
-  s->psnd_off.assign((size_t)S + 2, 0);
+  s->prcv_off.assign(((size_t)S + 1) * W + 1, 0);
+  s->psnd_off.assign(((size_t)S + 1) * W + 1, 0);
   u64 ra = 0, sa = 0;
-  for (uint32_t l = 0; l <= S; l++) {
-    s->prcv_off[l] = ra;
-    s->psnd_off[l] = sa;
-    for (u64 j = 0; j < nb; j++) {
-      const u64 gb = gblk(j);
-      for (u64 h = 0; h < 2; h++) {
-        if (gb >= 1) {
-          rgb[((size_t)l * nb + j) * 2 + h] = ra;
-          ra += cls((int64_t)l - (int64_t)(gb * B - 2 + h));
-        }
-        if (gb + 1 < ps.nblocks) {
-          sgb[((size_t)l * nb + j) * 2 + h] = sa;
-          sa += cls((int64_t)l - (int64_t)(gb * B + B - 2 + h));
+  for (uint32_t l = 0; l <= S; l++)
+    for (u64 p = 0; p < W; p++) {
+      s->prcv_off[(size_t)l * W + p] = ra;
+      s->psnd_off[(size_t)l * W + p] = sa;
+      for (u64 j = 0; j < nb; j++) {
+        const u64 gb = gblk(j);
+        const bool rx = gb >= 1 && plane_owner(g, (uint32_t)(gb - 1)) == p;
+        const bool tx = gb + 1 < ps.nblocks && plane_owner(g, (uint32_t)(gb + 1)) == p;
+        for (u64 h = 0; h < 2; h++) {
+          if (rx) {
+            rgb[((size_t)l * nb + j) * 2 + h] = ra;
+            ra += cls((int64_t)l - (int64_t)(gb * B - 2 + h));
+          }
+          if (tx) {
+            sgb[((size_t)l * nb + j) * 2 + h] = sa;
+            sa += cls((int64_t)l - (int64_t)(gb * B + B - 2 + h));
+          }
         }
       }
     }
-  }
-  s->prcv_off[S + 1] = ra;
-  s->psnd_off[S + 1] = sa;
+  s->prcv_off[((size_t)S + 1) * W] = ra;
+  s->psnd_off[((size_t)S + 1) * W] = sa;
   if (ra != ps.nrecv || sa != ps.nsend) return fail(GM_ECORRUPT, "halo plan: %llu / %llu planes, sized %llu / %llu",
                                                    (unsigned long long)ra, (unsigned long long)sa,
                                                    (unsigned long long)ps.nrecv, (unsigned long long)ps.nsend);
@@ -479,78 +487,107 @@ static void plane_reach_launch(gm_solver* s) {
   });
 }
 
-// per-level send / receive plane counts of a shard, as a fingerprint pair
-// (checked against the neighbours' before the first exchange: a mismatched
-// receive would wait forever)
-static void plane_sigs(const gm_solver* s, u64 out[2]) {
-  u64 a = 0xcbf29ce484222325ull, b = a;
-  for (size_t l = 0; l + 1 < s->psnd_off.size(); l++) {
-    a = (a ^ (s->psnd_off[l + 1] - s->psnd_off[l])) * 0x100000001b3ull;
-    b = (b ^ (s->prcv_off[l + 1] - s->prcv_off[l])) * 0x100000001b3ull;
-  }
-  out[0] = a;
-  out[1] = b;
+// halo segment (level l, peer p) of a shard's send / receive plan: first
+// plane and plane count
+static u64 plane_seg(const std::vector<u64>& off, uint32_t l, int W, int p, u64* n) {
+  const size_t i = (size_t)l * W + p;
+  *n = off[i + 1] - off[i];
+  return off[i];
 }
 
-// exchange the boundary planes of level l: every shard sends its send-
-// buffer segment of level l to rank + 1 and receives rank - 1's into its
-// receive buffer (mode 1 RCCL, 2 in-process copies, 3 host-staged)
+// per-peer send / receive plane counts of a shard over all levels, as
+// fingerprints out[2p] (sends to p), out[2p + 1] (receives from p) --
+// checked against the peers' before the first exchange: a mismatched
+// receive would wait forever
+static void plane_sigs(const gm_solver* s, u64* out) {
+  const int W = s->world;
+  const uint32_t nl = (uint32_t)((s->psnd_off.size() - 1) / W);
+  for (int p = 0; p < W; p++) {
+    u64 a = 0xcbf29ce484222325ull, b = a, n;
+    for (uint32_t l = 0; l < nl; l++) {
+      plane_seg(s->psnd_off, l, W, p, &n);
+      a = (a ^ n) * 0x100000001b3ull;
+      plane_seg(s->prcv_off, l, W, p, &n);
+      b = (b ^ n) * 0x100000001b3ull;
+    }
+    out[2 * p] = a;
+    out[2 * p + 1] = b;
+  }
+}
+
+// exchange the boundary planes of level l: every shard sends its (l, p)
+// send segment to each peer p and receives each peer q's into its (l, q)
+// receive segment (mode 1 RCCL, one grouped send/recv set; 2 in-process
+// copies; 3 host-staged, world - 1 shifted pairwise rounds)
 static int plane_exchange(std::vector<gm_solver*>& ss, uint32_t l, int mode, hipStream_t cs) {
   const u64 pb = 1024ull * ss[0]->pwb;
+  const int W = ss[0]->world;
   if (mode == 2) {
-    const int n = (int)ss.size();
-    for (int r = 0; r < n; r++) {
-      gm_solver* a = ss[(size_t)r];
-      gm_solver* b = ss[(size_t)((r + 1) % n)];
-      const u64 ns = a->psnd_off[l + 1] - a->psnd_off[l], nr = b->prcv_off[l + 1] - b->prcv_off[l];
-      if (ns != nr) return fail(GM_ECORRUPT, "level %u: shard %d sends %llu planes, shard %d expects %llu", l, r,
-                                (unsigned long long)ns, (r + 1) % n, (unsigned long long)nr);
-      if (ns)
-        HIPCHK(hipMemcpyAsync((char*)b->precv + b->prcv_off[l] * pb, (const char*)a->psend + a->psnd_off[l] * pb,
-                              ns * pb, hipMemcpyDeviceToDevice, cs));
-    }
+    for (int r = 0; r < W; r++)
+      for (int p = 0; p < W; p++) {
+        gm_solver* a = ss[(size_t)r];
+        gm_solver* b = ss[(size_t)p];
+        u64 ns, nr;
+        const u64 so = plane_seg(a->psnd_off, l, W, p, &ns), ro = plane_seg(b->prcv_off, l, W, r, &nr);
+        if (ns != nr) return fail(GM_ECORRUPT, "level %u: shard %d sends %llu planes, shard %d expects %llu", l, r,
+                                  (unsigned long long)ns, p, (unsigned long long)nr);
+        if (ns)
+          HIPCHK(hipMemcpyAsync((char*)b->precv + ro * pb, (const char*)a->psend + so * pb, ns * pb,
+                                hipMemcpyDeviceToDevice, cs));
+      }
     return 0;
   }
   gm_solver* s = ss[0];
-  const int up = (s->rank + 1) % s->world, down = (s->rank + s->world - 1) % s->world;
-  const u64 ns = s->psnd_off[l + 1] - s->psnd_off[l], nr = s->prcv_off[l + 1] - s->prcv_off[l];
-  void* sb = (char*)s->psend + s->psnd_off[l] * pb;
-  void* rb = (char*)s->precv + s->prcv_off[l] * pb;
+  auto sbuf = [&](int p, u64* n) { return (void*)((char*)s->psend + plane_seg(s->psnd_off, l, W, p, n) * pb); };
+  auto rbuf = [&](int p, u64* n) { return (void*)((char*)s->precv + plane_seg(s->prcv_off, l, W, p, n) * pb); };
   if (mode == 1) {
-    ncclGroupStart();
-    ncclResult_t r1 = ns ? ncclSend(sb, ns * pb, ncclUint8, up, s->comm, cs) : ncclSuccess;
-    ncclResult_t r2 = nr ? ncclRecv(rb, nr * pb, ncclUint8, down, s->comm, cs) : ncclSuccess;
-    ncclResult_t r3 = ncclGroupEnd();
-    if (r1 != ncclSuccess || r2 != ncclSuccess || r3 != ncclSuccess)
-      return fail(GM_EHIP, "RCCL halo exchange: %s",
-                  ncclGetErrorString(r1 != ncclSuccess ? r1 : r2 != ncclSuccess ? r2 : r3));
+    ncclResult_t r = ncclGroupStart();
+    for (int p = 0; p < W && r == ncclSuccess; p++) {
+      u64 ns, nr;
+      void* sb = sbuf(p, &ns);
+      void* rb = rbuf(p, &nr);
+      if (ns) r = ncclSend(sb, ns * pb, ncclUint8, p, s->comm, cs);
+      if (nr && r == ncclSuccess) r = ncclRecv(rb, nr * pb, ncclUint8, p, s->comm, cs);
+    }
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess || r2 != ncclSuccess)
+      return fail(GM_EHIP, "RCCL halo exchange: %s", ncclGetErrorString(r != ncclSuccess ? r : r2));
     return 0;
   }
-  std::vector<HostRange> out, in;
-  if (ns) out.push_back({sb, ns * pb});
-  if (nr) in.push_back({rb, nr * pb});
-  return xfer_ranges(s, out, up, in, down, cs);
+  for (int k = 1; k < W; k++) {
+    const int to = (s->rank + k) % W, from = (s->rank + W - k) % W;
+    u64 ns, nr;
+    void* sb = sbuf(to, &ns);
+    void* rb = rbuf(from, &nr);
+    std::vector<HostRange> out, in;
+    if (ns) out.push_back({sb, ns * pb});
+    if (nr) in.push_back({rb, nr * pb});
+    int rc = xfer_ranges(s, out, to, in, from, cs);
+    if (rc) return rc;
+  }
+  return 0;
 }
 
-// before the first sharded solve: every shard's send plan must match its
-// successor's receive plan (fingerprints all-gathered)
+// before the first sharded solve: every shard's sends to each peer must
+// match that peer's receives from it (fingerprints all-gathered)
 static int plane_check_plan(std::vector<gm_solver*>& ss, int mode, hipStream_t st) {
   const int W = ss[0]->world;
-  std::vector<u64> all((size_t)2 * W);
+  const size_t m = (size_t)2 * W;  // fingerprints per shard
+  std::vector<u64> all(m * W);
   if (mode == 2) {
-    for (gm_solver* s : ss) plane_sigs(s, &all[(size_t)2 * s->rank]);
+    for (gm_solver* s : ss) plane_sigs(s, &all[m * s->rank]);
   } else {
-    u64 mine[2];
-    plane_sigs(ss[0], mine);
+    std::vector<u64> mine(m);
+    plane_sigs(ss[0], mine.data());
     if (mode == 3) {
-      int rc = xfer_call(ss[0], GM_XFER_ALLGATHER, mine, sizeof mine, -1, all.data(), all.size() * 8, -1);
+      int rc = xfer_call(ss[0], GM_XFER_ALLGATHER, mine.data(), m * 8, -1, all.data(), all.size() * 8, -1);
       if (rc) return rc;
     } else {
       u64* dev = nullptr;
-      HIPCHK(hipMalloc((void**)&dev, (size_t)(2 + 2 * W) * 8));
-      HIPCHK(hipMemcpyAsync(dev, mine, sizeof mine, hipMemcpyHostToDevice, st));
-      ncclResult_t r = ncclAllGather(dev, dev + 2, 2, ncclUint64, ss[0]->comm, st);
-      hipError_t e = hipMemcpyAsync(all.data(), dev + 2, all.size() * 8, hipMemcpyDeviceToHost, st);
+      HIPCHK(hipMalloc((void**)&dev, (m + all.size()) * 8));
+      HIPCHK(hipMemcpyAsync(dev, mine.data(), m * 8, hipMemcpyHostToDevice, st));
+      ncclResult_t r = ncclAllGather(dev, dev + m, m, ncclUint64, ss[0]->comm, st);
+      hipError_t e = hipMemcpyAsync(all.data(), dev + m, all.size() * 8, hipMemcpyDeviceToHost, st);
       if (e == hipSuccess) e = hipStreamSynchronize(st);
       (void)hipFree(dev);
       if (r != ncclSuccess) return fail(GM_EHIP, "RCCL plan check: %s", ncclGetErrorString(r));
@@ -558,8 +595,9 @@ static int plane_check_plan(std::vector<gm_solver*>& ss, int mode, hipStream_t s
     }
   }
   for (int r = 0; r < W; r++)
-    if (all[(size_t)2 * r] != all[(size_t)2 * ((r + 1) % W) + 1])
-      return fail(GM_ECORRUPT, "halo plan mismatch: shard %d's sends vs shard %d's receives", r, (r + 1) % W);
+    for (int p = 0; p < W; p++)
+      if (all[m * r + 2 * p] != all[m * p + 2 * r + 1])
+        return fail(GM_ECORRUPT, "halo plan mismatch: shard %d's sends vs shard %d's receives", r, p);
   for (gm_solver* s : ss) s->halo_ok = true;
   return 0;
 }

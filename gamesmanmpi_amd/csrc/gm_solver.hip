@@ -2395,6 +2395,31 @@ static int xfer_ranges(gm_solver* s, const std::vector<HostRange>& out, int sp, 
 
 #include "gm_plane_run.h"
 
+int gm_plane_halo_plan(int game, int rank, int world, uint32_t flags, uint64_t* out, uint32_t levels) {
+  const Desc* d = get_game(game);
+  if (!d || !out || world < 2 || rank < 0 || rank >= world) return fail(GM_EINVAL, "bad argument");
+  if (!plane_ok(d)) return fail(GM_EINVAL, "game has no planes layout");
+  PlaneShape ps;
+  int rc = plane_shape(d, rank, world, flags, &ps);
+  if (rc) return rc;
+  if (levels < ps.S + 1) return fail(GM_EINVAL, "out holds %u levels, the game has %u plane levels", levels, ps.S + 1);
+  std::unique_ptr<gm_solver> s(new gm_solver());
+  s->world = world;
+  s->rank = rank;
+  std::vector<uint8_t> lb;
+  rc = plane_lists(s.get(), ps, lb);
+  if (rc) return rc;
+  for (uint32_t l = 0; l <= ps.S; l++)
+    for (int p = 0; p < world; p++) {
+      u64 n;
+      plane_seg(s->psnd_off, l, world, p, &n);
+      out[((size_t)l * world + p) * 2] = n;
+      plane_seg(s->prcv_off, l, world, p, &n);
+      out[((size_t)l * world + p) * 2 + 1] = n;
+    }
+  return 0;
+}
+
 // after pull(L): bits of every block's bottom two own slices go down
 static int exchange_bits(std::vector<gm_solver*>& ss, u64 L, int mode, hipStream_t cs) {
   auto bits_at = [&](gm_solver* s, u64 j, u64 o, u64 off) {

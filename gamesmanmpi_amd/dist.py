@@ -108,6 +108,18 @@ def halo_sigs(spec, rank, world, flags=0):
     return out
 
 
+def plane_halo_plan(spec, rank, world, flags=0):
+    """PLANES shards: shard `rank`'s halo plan (host only): uint64
+    [levels, world, 2] = boundary planes sent to / received from each peer
+    after each plane level (rows past the last plane level are 0)."""
+    import numpy as np
+    spec = spec if isinstance(spec, GameSpec) else GameSpec(*spec)
+    T = int(spec.max_levels)
+    out = np.zeros((T, world, 2), np.uint64)
+    _lib.check(_lib.load().gm_plane_halo_plan(spec.id, rank, world, flags, out.ctypes.data, T))
+    return out
+
+
 def group_solve(spec, world, device=None, kernel_timing=False, flags=0, layout="auto"):
     """Solve all `world` shards in this process (one GPU, one stream).
     Returns (SolveResult of the whole job, [shard Solvers])."""

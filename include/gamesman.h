@@ -127,7 +127,11 @@ typedef struct gm_buffers {
 #define GM_F_PLANE_X1 1024u   /* PLANES: one plane per half-wave in 32-bit lanes
                                   (k_plane_resolve) instead of two per half-wave
                                   in packed 16-bit lanes (A/B runs) */
-#define GM_F_GRAPH 256u       /* dense one-table full solves: capture the
+#define GM_F_PLANE_ROUND_ROBIN 2048u /* PLANES shards: deal the top-digit blocks
+                                  round robin (every halo to rank + 1, one link)
+                                  instead of the link-spreading deal used for
+                                  power-of-two worlds >= 4 (A/B runs) */
+#define GM_F_GRAPH 256u      /* dense one-table full solves: capture the
                                   forward and backward launches as HIP graphs
                                   on the first solve, replay them after
                                   (measured: no faster than plain launches) */
@@ -304,6 +308,13 @@ int gm_solver_set_transport(gm_solver *s, gm_xfer_fn fn, void *ctx);
  * bits received from above, words sent up, words received from below.
  * Host only: no device memory, no GPU needed. */
 int gm_shard_halo_sigs(int game, int rank, int world, uint32_t flags, uint64_t *out, uint32_t levels);
+/* PLANES shards: the halo plan of shard `rank` (gm_plane_run.h
+ * plane_lists), host only.  out[(l * world + p) * 2 + 0] = boundary planes
+ * the shard sends to rank p after plane level l, [.. + 1] = planes it
+ * receives from p; `levels` >= the game's plane levels (sum of the outer
+ * heaps + 1), else GM_EINVAL.  Replaces the same per-edge message fan-out as
+ * gm_solver_solve on shards (src/process.py:37-267). */
+int gm_plane_halo_plan(int game, int rank, int world, uint32_t flags, uint64_t *out, uint32_t levels);
 /* All `n` shards of one job in ONE process on one stream, halos moved by
  * device-to-device copies: the same kernels and halo geometry as the RCCL
  * path, runnable on a single GPU (parity tests). */
