@@ -375,9 +375,12 @@ def main():
                           layout, "SURVEY 8d keyed: expand 24 B/position + 8 B/edge, resolve 12 B/position + "
                                   "12 B/edge")),
             "timing": ("HIP events on the solve stream in an extra solve of the same launch schedule: "
-                       + ("one event pair around the whole backward (nothing but the %d resolve launches), "
-                          "average = span / launches" % kn if layout == "planes" and world == 1 else
-                          "an event pair around each launch, summed")),
+                       + ("one event pair around the whole backward (nothing but its %d resolve launches: "
+                          "grid-wide k_plane_resolve* for wide plane levels, one-workgroup k_plane_run for runs "
+                          "of narrow ones), average = span / launches" % kn if layout == "planes" and world == 1
+                          else "one event pair around this rank's whole staged backward (%d launches over its "
+                          "keys, halo waits included), average = span / launches" % kn if layout == "planes"
+                          else "an event pair around each launch, summed")),
             "launches": kn, "ms_kernel_total": kms, "ms_per_launch": kms / kn,
             "algorithmic_bytes_total": kb}
 

@@ -185,17 +185,19 @@ __device__ __forceinline__ PlaneShare plane_share(uint32_t n, uint32_t per_wave)
 // One plane level: list[0 .. n) are the level's planes (uint32 plane index,
 // or PlaneEntry for shards).  tab: the table (plane P at tab + P * 1024
 // words); zero: >= 64 zero bytes; recv / send: the shard's halo buffers.
+// the wave's share of list entries [first, end), two planes per wave
+// visit, `stride` apart (k_plane_resolve: plane_share; k_plane_run: the
+// workgroup's waves)
 template <int WB, int NO, bool SH>
-__global__ __launch_bounds__(256) void k_plane_resolve(typename PlaneWord<WB>::T* __restrict__ tab,
-                                                       const void* __restrict__ list, uint32_t n, PlaneGeom g,
-                                                       const uint4* __restrict__ zero,
-                                                       const typename PlaneWord<WB>::T* __restrict__ recv,
-                                                       typename PlaneWord<WB>::T* __restrict__ send) {
+__device__ __forceinline__ void plane_x1_range(typename PlaneWord<WB>::T* __restrict__ tab,
+                                               const void* __restrict__ list, const PlaneShare sh,
+                                               const PlaneGeom& g, const uint4* __restrict__ zero,
+                                               const typename PlaneWord<WB>::T* __restrict__ recv,
+                                               typename PlaneWord<WB>::T* __restrict__ send) {
   typedef PlaneWord<WB> W;
   constexpr int DW = W::DW, NQ = DW / 4;  // dwords / 16-B loads per row
   const uint32_t lane = threadIdx.x & 63, L = lane & 31;
   const uint32_t lm = lane == 32 ? 0u : ~0u;  // row 0 of the upper plane has no row below
-  const PlaneShare sh = plane_share(n, 2);
   for (uint32_t i0 = sh.first; i0 < sh.end; i0 += sh.stride) {
     const uint32_t idx = i0 + (lane >> 5);
     const bool live = idx < sh.end;
@@ -294,6 +296,30 @@ __global__ __launch_bounds__(256) void k_plane_resolve(typename PlaneWord<WB>::T
   }
 }
 
+// Warm the caches with the NEXT launch's list entries: one 128-B line per
+// thread, issued before this wave's own loads so its wait overlaps theirs;
+// the value is kept live to the end of the kernel (a dead load is dropped).
+// The line lands in this XCD's L2 and the memory-side Infinity Cache, so
+// the next level's first, dependent load (list entry -> neighbour rows)
+// does not go to HBM.
+__device__ __forceinline__ uint32_t plane_prefetch(const uint32_t* __restrict__ pf, uint32_t lines) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  return t < lines ? pf[(size_t)t * 32u] : 0u;
+}
+__device__ __forceinline__ void plane_keep(uint32_t v) { asm volatile("; keep %0" ::"v"(v)); }
+
+template <int WB, int NO, bool SH>
+__global__ __launch_bounds__(256) void k_plane_resolve(typename PlaneWord<WB>::T* __restrict__ tab,
+                                                       const void* __restrict__ list, uint32_t n, PlaneGeom g,
+                                                       const uint4* __restrict__ zero,
+                                                       const typename PlaneWord<WB>::T* __restrict__ recv,
+                                                       typename PlaneWord<WB>::T* __restrict__ send,
+                                                       const uint32_t* __restrict__ pf, uint32_t pflines) {
+  const uint32_t v = plane_prefetch(pf, pflines);
+  plane_x1_range<WB, NO, SH>(tab, list, plane_share(n, 2), g, zero, recv, send);
+  plane_keep(v);
+}
+
 // Packed form: a wave resolves FOUR planes -- each lane carries two planes'
 // rows in the 16-bit halves of its registers (X low, Y high; lanes 0-31 one
 // pair, 32-63 another), so every step of the skewed wavefront advances two
@@ -323,17 +349,16 @@ __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
 }
 
 template <int WB, int NO, bool SH>
-__global__ __launch_bounds__(256) void k_plane_resolve_x2(typename PlaneWord<WB>::T* __restrict__ tab,
-                                                          const void* __restrict__ list, uint32_t n, PlaneGeom g,
-                                                          const uint4* __restrict__ zero,
-                                                          const typename PlaneWord<WB>::T* __restrict__ recv,
-                                                          typename PlaneWord<WB>::T* __restrict__ send) {
+__device__ __forceinline__ void plane_x2_range(typename PlaneWord<WB>::T* __restrict__ tab,
+                                               const void* __restrict__ list, const PlaneShare sh,
+                                               const PlaneGeom& g, const uint4* __restrict__ zero,
+                                               const typename PlaneWord<WB>::T* __restrict__ recv,
+                                               typename PlaneWord<WB>::T* __restrict__ send) {
   typedef PlaneWord<WB> W;
   typedef typename W::T T;
   constexpr int DW = W::DW, NQ = DW / 4;
   const uint32_t lane = threadIdx.x & 63, L = lane & 31;
   const bool l32 = lane == 32;
-  const PlaneShare sh = plane_share(n, 4);
   for (uint32_t i0 = sh.first; i0 < sh.end; i0 += sh.stride) {
     const uint32_t ix = i0 + 2 * (lane >> 5), iy = ix + 1;
     const bool livex = ix < sh.end, livey = iy < sh.end;
@@ -463,6 +488,51 @@ __global__ __launch_bounds__(256) void k_plane_resolve_x2(typename PlaneWord<WB>
       store(tab + oy, oy_);
       if (SH && ey.send != kPlaneAbsent) store(send + (size_t)ey.send * 1024u + L * 32u, oy_);
     }
+  }
+}
+
+template <int WB, int NO, bool SH>
+__global__ __launch_bounds__(256) void k_plane_resolve_x2(typename PlaneWord<WB>::T* __restrict__ tab,
+                                                          const void* __restrict__ list, uint32_t n, PlaneGeom g,
+                                                          const uint4* __restrict__ zero,
+                                                          const typename PlaneWord<WB>::T* __restrict__ recv,
+                                                          typename PlaneWord<WB>::T* __restrict__ send,
+                                                          const uint32_t* __restrict__ pf, uint32_t pflines) {
+  const uint32_t v = plane_prefetch(pf, pflines);
+  plane_x2_range<WB, NO, SH>(tab, list, plane_share(n, 4), g, zero, recv, send);
+  plane_keep(v);
+}
+
+// A run of narrow plane levels (or staged keys) in ONE workgroup: the
+// groups [off[i], off[i + 1]) one after another, a workgroup barrier
+// between them.  One CU suffices for a group of a few dozen planes, and the
+// run pays one launch instead of one per group (a narrow launch costs
+// ~5 us of kernel plus ~2-3 us of boundary: profiles/r03c_trace_levels.txt).
+// Coherence: the waves share the CU's L1 and write through to its XCD's L2;
+// a plane's lines are first loaded by this CU only after the group that
+// writes them (neighbours lie in earlier groups), so the barrier's
+// workgroup-scope release / acquire is all a later group needs.
+constexpr int kPlaneRunMax = 32;      // groups per run
+constexpr int kPlaneRunThreads = 512;  // 8 waves: <= 256 VGPRs, every kernel variant fits
+struct PlaneRun {
+  uint32_t n;
+  uint32_t off[kPlaneRunMax + 1];  // list entries, absolute
+};
+template <int WB, int NO, bool SH, bool X1>
+__global__ __launch_bounds__(kPlaneRunThreads) void k_plane_run(typename PlaneWord<WB>::T* __restrict__ tab,
+                                                                const void* __restrict__ list, PlaneRun run,
+                                                                PlaneGeom g, const uint4* __restrict__ zero,
+                                                                const typename PlaneWord<WB>::T* __restrict__ recv,
+                                                                typename PlaneWord<WB>::T* __restrict__ send) {
+  constexpr uint32_t per = X1 ? 2u : 4u;  // planes per wave visit
+  const uint32_t w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (uint32_t i = 0; i < run.n; i++) {
+    const PlaneShare sh{run.off[i] + w * per, run.off[i + 1], nw * per};
+    if (X1)
+      plane_x1_range<WB, NO, SH>(tab, list, sh, g, zero, recv, send);
+    else
+      plane_x2_range<WB, NO, SH>(tab, list, sh, g, zero, recv, send);
+    __syncthreads();
   }
 }
 

@@ -155,9 +155,36 @@ struct PlaneShape {
   u64 nrecv, nsend;      // halo planes of this shard (all levels)
   u64 words_off, bits_off, recv_off, send_off, table_bytes;  // table buffer layout
   u64 zero_off, list_off, scratch_bytes;                      // scratch layout
+  // the staged deal (shards; 0: level-synchronous): key skew k, keys, rows
+  uint32_t stage_k, nkeys, nrows;
 };
 
+// Staged PLANES shards.  Rank r owns ONE block: the top
+// values [r B, (r + 1) B), B = E / world.  A plane (top offset o, lower
+// digits of sum s) depends only on planes at o - 1, o - 2 (same lower digits)
+// and at lower sums s - 1, s - 2 (same o); so key(o, s) = o + k s, k >= 1,
+// orders every plane after its children and a rank resolves its planes key
+// by key with NO level barrier across ranks.  The only cross-rank edge: the
+// planes of top offsets 0, 1 read the previous rank's last two slices at the
+// same lower digits.  Those leave rank r - 1 row by row -- row s (slices
+// B - 2, B - 1 at lower sum s) is final after key B - 1 + k s -- and rank r
+// first needs row s at key k s: the ranks form a pipeline in which rank r
+// trails rank r - 1 by about B keys, and the transfers hide under B - 1 keys
+// of compute.  Larger k shortens the trail (fewer planes per key) but adds
+// launches (each >= ~9 us: profiles/r03l_group*.jsonl); k by world from the
+// pipeline model with that floor (tools/stage_model.py --floor 9e-6).
+static uint32_t plane_stage_k(int world) { return world <= 2 ? 2u : world <= 4 ? 4u : 5u; }
+
 static u64 rup256(u64 x) { return (x + 255) & ~255ull; }
+// A/B switches read once from the environment ("0" turns the feature off)
+static bool getenv_flag_off(const char* name) {
+  const char* v = getenv(name);
+  return v && v[0] == '0';
+}
+static bool plane_prefetch_on() {
+  static const bool on = !getenv_flag_off("GM_PLANE_PREFETCH");
+  return on;
+}
 
 static int plane_shape(const Desc* d, int rank, int world, uint32_t flags, PlaneShape* ps) {
   memset(ps, 0, sizeof *ps);
@@ -206,7 +233,8 @@ static int plane_shape(const Desc* d, int rank, int world, uint32_t flags, Plane
     if (g.no < 1) return fail(GM_EINVAL, "sharded planes need at least 3 heaps");
     if (rank < 0 || rank >= world) return fail(GM_EINVAL, "bad shard %d/%d", rank, world);
     const u64 E = d->base[d->nheaps - 1], Z = g.stride[g.no - 1];
-    const u64 B = E >= 16 * (u64)world ? 8 : (E + world - 1) / world;
+    const bool staged = !(flags & GM_F_PLANE_LEVEL_SYNC) && E % (u64)world == 0 && E / (u64)world >= 2;
+    const u64 B = staged ? E / world : E >= 16 * (u64)world ? 8 : (E + world - 1) / world;
     if (B < 2 || E % B || E / B < (u64)world)
       return fail(GM_EINVAL, "last heap of %llu values cannot give %d ranks whole blocks of >= 2", (unsigned long long)E,
                   world);
@@ -214,8 +242,15 @@ static int plane_shape(const Desc* d, int rank, int world, uint32_t flags, Plane
     ps->nb = (uint32_t)((ps->nblocks - (u64)rank + world - 1) / world);
     g.B = (uint32_t)B;
     g.Z = (uint32_t)Z;
-    g.spread = world >= 4 && !(world & (world - 1)) && ps->nblocks % world == 0 && ps->nblocks > (u64)world &&
-               !(flags & GM_F_PLANE_ROUND_ROBIN);
+    g.spread = !staged && world >= 4 && !(world & (world - 1)) && ps->nblocks % world == 0 &&
+               ps->nblocks > (u64)world && !(flags & GM_F_PLANE_ROUND_ROBIN);
+    if (staged) {
+      uint32_t smax = 0;  // largest digit sum below the top
+      for (uint32_t j = 0; j + 1 < g.no; j++) smax += g.base[j] - 1;
+      ps->stage_k = plane_stage_k(world);
+      ps->nrows = smax + 1;
+      ps->nkeys = (uint32_t)(B - 1) + ps->stage_k * smax + 1;
+    }
     ps->nlocal = (u64)ps->nb * B * Z;
     g.nplanes = (uint32_t)ps->nlocal;
     for (uint32_t j = 0; j < ps->nb; j++) {
@@ -262,6 +297,59 @@ static int plan_planes(const Desc* d, int rank, int world, uint32_t flags, uint6
 // order).  Segments are level-major, peer-minor.  A halo plane's index is its
 // group's start plus the rank of its lower digits within their digit-sum
 // class, which is also the rank of the receiving plane in its own group.
+// Staged lists: PlaneEntry per own plane, key by key (key = o + k s, s the
+// lower digit sum).  Halo buffers (send and receive alike) are row-major:
+// row s = [2 R(s), 2 R(s + 1)) with R the prefix of the lower-digit class
+// sizes, slice h (top value rB - 2 + h / the sender's B - 2 + h) at
+// 2 R(s) + h ncl(s) + the lower digits' rank in their class -- so a row is one
+// contiguous message.  ploff: per key; prcv_off / psnd_off: per row.
+static int plane_lists_staged(gm_solver* s, const PlaneShape& ps, const std::vector<uint32_t>& sig,
+                              const std::vector<uint32_t>& rk, const std::vector<u64>& ncl,
+                              std::vector<uint8_t>& bytes) {
+  const PlaneGeom& g = ps.g;
+  const u64 Z = g.Z, B = g.B, k = ps.stage_k, K = ps.nkeys, R = ps.nrows;
+  if (ncl.size() != R) return fail(GM_ECORRUPT, "staged lists: %zu digit-sum classes, %llu rows", ncl.size(),
+                                   (unsigned long long)R);
+  const bool rx = g.rank > 0, tx = g.rank + 1 < g.world;
+  std::vector<u64> row(R + 1, 0);
+  for (u64 r = 0; r < R; r++) row[r + 1] = row[r] + 2 * ncl[r];
+  s->prcv_off.assign(R + 1, 0);
+  s->psnd_off.assign(R + 1, 0);
+  if (rx) s->prcv_off = row;
+  if (tx) s->psnd_off = row;
+  if (s->prcv_off[R] != ps.nrecv || s->psnd_off[R] != ps.nsend)
+    return fail(GM_ECORRUPT, "staged halo plan: %llu / %llu planes, sized %llu / %llu",
+                (unsigned long long)s->prcv_off[R], (unsigned long long)s->psnd_off[R],
+                (unsigned long long)ps.nrecv, (unsigned long long)ps.nsend);
+  s->ploff.assign(K + 1, 0);
+  for (u64 o = 0; o < B; o++)
+    for (u64 l = 0; l < Z; l++) s->ploff[o + k * sig[l] + 1]++;
+  for (u64 q = 0; q < K; q++) s->ploff[q + 1] += s->ploff[q];
+  if (s->ploff[K] != ps.nlocal) return fail(GM_ECORRUPT, "staged lists: %llu entries for %llu planes",
+                                            (unsigned long long)s->ploff[K], (unsigned long long)ps.nlocal);
+  bytes.resize(ps.nlocal * sizeof(PlaneEntry));
+  PlaneEntry* E = (PlaneEntry*)bytes.data();
+  std::vector<u64> pos(s->ploff.begin(), s->ploff.end());
+  const u64 t0 = (u64)g.rank * B;
+  for (u64 o = 0; o < B; o++)
+    for (u64 l = 0; l < Z; l++) {
+      const uint32_t c = sig[l];
+      PlaneEntry e;
+      e.p = (uint32_t)(o * Z + l);
+      auto halo = [&](u64 kk) -> uint32_t {  // neighbour at top value t0 + o - kk
+        if (t0 + o < kk) return kPlaneAbsent;
+        if (o >= kk) return kPlaneLocal;
+        return (uint32_t)(row[c] + (o + 2 - kk) * ncl[c] + rk[l]);
+      };
+      e.top1 = halo(1);
+      e.top2 = halo(2);
+      e.send = (tx && o + 2 >= B) ? (uint32_t)(row[c] + (o + 2 - B) * ncl[c] + rk[l]) : kPlaneAbsent;
+      E[pos[o + k * c]++] = e;
+    }
+  s->pbnd.clear();
+  return 0;
+}
+
 static int plane_lists(gm_solver* s, const PlaneShape& ps, std::vector<uint8_t>& bytes) {
   const PlaneGeom& g = ps.g;
   const uint32_t S = ps.S;
@@ -295,6 +383,7 @@ static int plane_lists(gm_solver* s, const PlaneShape& ps, std::vector<uint8_t>&
   std::vector<u64> ncl(smax + 1, 0);
   for (u64 l = 0; l < Z; l++) rk[l] = (uint32_t)ncl[sig[l]]++;
   auto cls = [&](int64_t c) -> u64 { return c < 0 || c > (int64_t)smax ? 0 : ncl[(size_t)c]; };
+  if (ps.stage_k) return plane_lists_staged(s, ps, sig, rk, ncl, bytes);
   const u64 nb = ps.nb, W = g.world;
   auto gblk = [&](u64 j) { return (u64)plane_gblock(g, (uint32_t)j); };
   // halo groups per level and peer (the rank the slices come from / go to):
@@ -398,6 +487,9 @@ static int plane_setup(gm_solver* s, const gm_buffers* buf) {
   s->plist = sc + ps.list_off;
   s->pnrecv = ps.nrecv;
   s->pnsend = ps.nsend;
+  s->pstage_k = ps.stage_k;
+  s->pkeys = ps.nkeys;
+  s->prows = ps.nrows;
   std::vector<uint8_t> lb;
   rc = plane_lists(s, ps, lb);
   if (rc) return rc;
@@ -419,8 +511,12 @@ static int plane_setup(gm_solver* s, const gm_buffers* buf) {
 static bool plane_x1(const gm_solver* s) { return s->pwb == 2 || (s->flags & GM_F_PLANE_X1); }
 
 template <int WB, int NO, bool SH>
-static void plane_launch_t(gm_solver* s, u64 a, u64 n) {
+static void plane_launch_t(gm_solver* s, u64 a, u64 n, u64 pa, u64 pn) {
   if (!n) return;
+  // next launch's entries [pa, pa + pn): lines to prefetch (none: pn = 0)
+  const size_t esz = SH ? sizeof(PlaneEntry) : 4;
+  const uint32_t* pf = (const uint32_t*)((const char*)s->plist + ((pa * esz) & ~(size_t)127));
+  const uint32_t pfl = pn ? (uint32_t)(((pa + pn) * esz - ((pa * esz) & ~(size_t)127) + 127) / 128) : 0u;
   const bool x1 = plane_x1(s);
   const u64 waves = x1 ? (n + 1) / 2 : (n + 3) / 4;
   u64 blocks = (waves + 3) / 4;
@@ -429,34 +525,102 @@ static void plane_launch_t(gm_solver* s, u64 a, u64 n) {
   const void* list = (const char*)s->plist + a * (SH ? sizeof(PlaneEntry) : 4);
   if (x1)
     hipLaunchKernelGGL((k_plane_resolve<WB, NO, SH>), dim3((uint32_t)blocks), dim3(256), 0, s->stream, (T*)s->ptab,
-                       list, (uint32_t)n, s->pg, s->pzero, (const T*)s->precv, (T*)s->psend);
+                       list, (uint32_t)n, s->pg, s->pzero, (const T*)s->precv, (T*)s->psend, pf, pfl);
   else
     hipLaunchKernelGGL((k_plane_resolve_x2<WB, NO, SH>), dim3((uint32_t)blocks), dim3(256), 0, s->stream,
-                       (T*)s->ptab, list, (uint32_t)n, s->pg, s->pzero, (const T*)s->precv, (T*)s->psend);
+                       (T*)s->ptab, list, (uint32_t)n, s->pg, s->pzero, (const T*)s->precv, (T*)s->psend, pf, pfl);
 }
 template <int WB, bool SH>
-static void plane_launch_w(gm_solver* s, u64 a, u64 n) {
+static void plane_launch_w(gm_solver* s, u64 a, u64 n, u64 pa, u64 pn) {
   switch (s->pg.no) {
-    case 0: if (!SH) plane_launch_t<WB, 0, false>(s, a, n); break;
-    case 1: plane_launch_t<WB, 1, SH>(s, a, n); break;
-    case 2: plane_launch_t<WB, 2, SH>(s, a, n); break;
-    case 3: plane_launch_t<WB, 3, SH>(s, a, n); break;
-    case 4: plane_launch_t<WB, 4, SH>(s, a, n); break;
-    case 5: plane_launch_t<WB, 5, SH>(s, a, n); break;
-    default: plane_launch_t<WB, 6, SH>(s, a, n); break;
+    case 0: if (!SH) plane_launch_t<WB, 0, false>(s, a, n, pa, pn); break;
+    case 1: plane_launch_t<WB, 1, SH>(s, a, n, pa, pn); break;
+    case 2: plane_launch_t<WB, 2, SH>(s, a, n, pa, pn); break;
+    case 3: plane_launch_t<WB, 3, SH>(s, a, n, pa, pn); break;
+    case 4: plane_launch_t<WB, 4, SH>(s, a, n, pa, pn); break;
+    case 5: plane_launch_t<WB, 5, SH>(s, a, n, pa, pn); break;
+    default: plane_launch_t<WB, 6, SH>(s, a, n, pa, pn); break;
   }
 }
-// list entries [a, a + n) of the solver's level lists
-static void plane_launch_range(gm_solver* s, u64 a, u64 n) {
+// list entries [a, a + n) of the solver's level lists; [pa, pa + pn): the
+// entries the next launch starts with, prefetched (pn = 0: none)
+static void plane_launch_range(gm_solver* s, u64 a, u64 n, u64 pa = 0, u64 pn = 0) {
   const bool sh = s->world > 1;
+  if (!plane_prefetch_on()) pn = 0;
   if (s->pwb == 1) {
-    if (sh) plane_launch_w<1, true>(s, a, n);
-    else plane_launch_w<1, false>(s, a, n);
+    if (sh) plane_launch_w<1, true>(s, a, n, pa, pn);
+    else plane_launch_w<1, false>(s, a, n, pa, pn);
   } else {
-    if (sh) plane_launch_w<2, true>(s, a, n);
-    else plane_launch_w<2, false>(s, a, n);
+    if (sh) plane_launch_w<2, true>(s, a, n, pa, pn);
+    else plane_launch_w<2, false>(s, a, n, pa, pn);
   }
 }
+template <int WB, int NO, bool SH>
+static void plane_run_t(gm_solver* s, const PlaneRun& run) {
+  typedef typename PlaneWord<WB>::T T;
+  if (plane_x1(s))
+    hipLaunchKernelGGL((k_plane_run<WB, NO, SH, true>), dim3(1), dim3(kPlaneRunThreads), 0, s->stream, (T*)s->ptab,
+                       s->plist, run, s->pg, s->pzero, (const T*)s->precv, (T*)s->psend);
+  else
+    hipLaunchKernelGGL((k_plane_run<WB, NO, SH, false>), dim3(1), dim3(kPlaneRunThreads), 0, s->stream, (T*)s->ptab,
+                       s->plist, run, s->pg, s->pzero, (const T*)s->precv, (T*)s->psend);
+}
+template <int WB, bool SH>
+static void plane_run_w(gm_solver* s, const PlaneRun& run) {
+  switch (s->pg.no) {
+    case 0: if (!SH) plane_run_t<WB, 0, false>(s, run); break;
+    case 1: plane_run_t<WB, 1, SH>(s, run); break;
+    case 2: plane_run_t<WB, 2, SH>(s, run); break;
+    case 3: plane_run_t<WB, 3, SH>(s, run); break;
+    case 4: plane_run_t<WB, 4, SH>(s, run); break;
+    case 5: plane_run_t<WB, 5, SH>(s, run); break;
+    default: plane_run_t<WB, 6, SH>(s, run); break;
+  }
+}
+// Batches consecutive groups of list entries (plane levels, staged keys)
+// into launches: a group of at most `narrow` planes joins the open run
+// (k_plane_run, one workgroup), a wider one flushes the run and gets its own
+// grid-wide launch.  flush() before anything that must see the groups so
+// far done on the stream (an event, an exchange).
+struct PlaneBatcher {
+  gm_solver* s;
+  PlaneRun run{};
+  u64 narrow;
+  u64 launches = 0;  // grid launches + runs issued
+  explicit PlaneBatcher(gm_solver* sv) : s(sv) {
+    // two passes of the run's waves: one CU beats a launch up to about there
+    narrow = (s->flags & GM_F_PLANE_NO_RUNS) ? 0 : (u64)(kPlaneRunThreads / 64) * (plane_x1(s) ? 2 : 4) * 2;
+    run.n = 0;
+  }
+  void flush() {
+    launches += run.n ? 1 : 0;
+    if (run.n == 1) plane_launch_range(s, run.off[0], run.off[1] - run.off[0]);
+    else if (run.n > 1) {
+      const bool sh = s->world > 1;
+      if (s->pwb == 1) {
+        if (sh) plane_run_w<1, true>(s, run);
+        else plane_run_w<1, false>(s, run);
+      } else {
+        if (sh) plane_run_w<2, true>(s, run);
+        else plane_run_w<2, false>(s, run);
+      }
+    }
+    run.n = 0;
+  }
+  void add(u64 a, u64 b, u64 next = 0) {  // list entries [a, b); the next group's size (prefetch)
+    if (b == a) return;
+    if (b - a > narrow) {
+      flush();
+      plane_launch_range(s, a, b - a, b, next);
+      launches++;
+      return;
+    }
+    if (run.n == (uint32_t)kPlaneRunMax || (run.n && run.off[run.n] != a)) flush();
+    if (run.n == 0) run.off[0] = (uint32_t)a;
+    run.off[++run.n] = (uint32_t)b;
+  }
+};
+
 // plane level l; part 0: all of it, 1: the planes that read no halo plane,
 // 2: the ones that do
 static void plane_launch(gm_solver* s, uint32_t l, int part = 0) {
@@ -602,6 +766,208 @@ static int plane_check_plan(std::vector<gm_solver*>& ss, int mode, hipStream_t s
   return 0;
 }
 
+// Staged shards: every rank's geometry must be the same staged deal (the
+// row messages pair by construction then: both sides size row s from the
+// lower digits alone)
+static u64 plane_stage_sig(const gm_solver* s) {
+  u64 h = 0xcbf29ce484222325ull;
+  auto mix = [&](u64 v) { h = (h ^ v) * 0x100000001b3ull; };
+  mix(s->pstage_k);
+  mix(s->pkeys);
+  mix(s->prows);
+  mix(s->pg.B);
+  mix(s->pg.Z);
+  mix(s->world);
+  const std::vector<u64>& rows = s->rank > 0 ? s->prcv_off : s->psnd_off;
+  for (u64 v : rows) mix(v);
+  return h;
+}
+static int plane_check_stage(std::vector<gm_solver*>& ss, int mode, hipStream_t st) {
+  const int W = ss[0]->world;
+  std::vector<u64> all((size_t)W);
+  if (mode == 2) {
+    for (gm_solver* s : ss) all[(size_t)s->rank] = plane_stage_sig(s);
+  } else {
+    u64 mine = plane_stage_sig(ss[0]);
+    if (mode == 3) {
+      int rc = xfer_call(ss[0], GM_XFER_ALLGATHER, &mine, 8, -1, all.data(), all.size() * 8, -1);
+      if (rc) return rc;
+    } else {
+      u64* dev = nullptr;
+      HIPCHK(hipMalloc((void**)&dev, (size_t)(1 + W) * 8));
+      HIPCHK(hipMemcpyAsync(dev, &mine, 8, hipMemcpyHostToDevice, st));
+      ncclResult_t r = ncclAllGather(dev, dev + 1, 1, ncclUint64, ss[0]->comm, st);
+      hipError_t e = hipMemcpyAsync(all.data(), dev + 1, all.size() * 8, hipMemcpyDeviceToHost, st);
+      if (e == hipSuccess) e = hipStreamSynchronize(st);
+      (void)hipFree(dev);
+      if (r != ncclSuccess) return fail(GM_EHIP, "RCCL plan check: %s", ncclGetErrorString(r));
+      if (e != hipSuccess) return fail(GM_EHIP, "plan check: %s", hipGetErrorString(e));
+    }
+  }
+  for (int r = 1; r < W; r++)
+    if (all[(size_t)r] != all[0])
+      return fail(GM_ECORRUPT, "staged plan mismatch: shard %d's geometry differs from shard 0's", r);
+  for (gm_solver* s : ss) s->halo_ok = true;
+  return 0;
+}
+
+// The staged backward (see plane_stage_k): every rank walks its keys; row s
+// of the halo is waited for before key k s and sent after key B - 1 + k s.
+//  mode 2 (in-process group, one stream): shard after shard, rows copied to
+//    the next shard as they complete (the next shard runs after this one).
+//  mode 1 (RCCL): transfers r -> r + 1 travel on comm when r is even and on
+//    comm2 (ncclCommSplit, made on first use) when odd, so on every rank one
+//    communicator carries only its receives and the other only its sends:
+//    receives are posted ahead (a window of rows) on the receive stream and
+//    can never hold up the sends, which follow the rank's own keys on the
+//    send stream.
+//  mode 3 (host-staged transport): blocking row transfers in key order.
+static int plane_backward_staged(std::vector<gm_solver*>& ss, int mode, hipStream_t st, u64* nlaunch) {
+  gm_solver* s0 = ss[0];
+  const uint32_t k = s0->pstage_k, K = s0->pkeys, R = s0->prows, B = s0->pg.B;
+  const int W = s0->world;
+  const u64 pb = 1024ull * s0->pwb;
+  auto row_done = [&](uint32_t key, uint32_t* r) {  // key completes row *r (its last slice)
+    if (key + 1 < B || (key - (B - 1)) % k) return false;
+    *r = (key - (B - 1)) / k;
+    return *r < R;
+  };
+  auto row_need = [&](uint32_t key, uint32_t* r) {  // key is the first to read row *r
+    if (key % k) return false;
+    *r = key / k;
+    return *r < R;
+  };
+  auto seg = [](const std::vector<u64>& off, uint32_t r, u64* n) {
+    *n = off[r + 1] - off[r];
+    return off[r];
+  };
+  auto launch_key = [K](PlaneBatcher& pb_, uint32_t key) {
+    const std::vector<u64>& o = pb_.s->ploff;
+    pb_.add(o[key], o[(size_t)key + 1], key + 1 < K ? o[(size_t)key + 2] - o[(size_t)key + 1] : 0);
+  };
+  if (mode == 2) {
+    for (int c = 0; c < W; c++) {
+      gm_solver* s = ss[(size_t)c];
+      PlaneBatcher bat(s);
+      for (uint32_t key = 0; key < K; key++) {
+        launch_key(bat, key);
+        uint32_t r;
+        if (c + 1 < W && row_done(key, &r)) {
+          bat.flush();
+          gm_solver* t = ss[(size_t)c + 1];
+          u64 ns, nr;
+          const u64 so = seg(s->psnd_off, r, &ns), ro = seg(t->prcv_off, r, &nr);
+          if (ns != nr) return fail(GM_ECORRUPT, "row %u: shard %d sends %llu planes, shard %d expects %llu", r, c,
+                                    (unsigned long long)ns, c + 1, (unsigned long long)nr);
+          if (ns)
+            HIPCHK(hipMemcpyAsync((char*)t->precv + ro * pb, (const char*)s->psend + so * pb, ns * pb,
+                                  hipMemcpyDeviceToDevice, st));
+        }
+      }
+      bat.flush();
+      if (c == 0) *nlaunch = bat.launches;
+    }
+    return 0;
+  }
+  gm_solver* s = s0;
+  PlaneBatcher bat(s);
+  const int rank = s->rank;
+  const bool rx = rank > 0, tx = rank + 1 < W;
+  auto rbuf = [&](uint32_t r, u64* n) { return (void*)((char*)s->precv + seg(s->prcv_off, r, n) * pb); };
+  auto sbuf = [&](uint32_t r, u64* n) { return (void*)((char*)s->psend + seg(s->psnd_off, r, n) * pb); };
+  if (mode == 3) {
+    for (uint32_t key = 0; key < K; key++) {
+      uint32_t r;
+      if (rx && row_need(key, &r)) {
+        bat.flush();
+        u64 n;
+        void* b = rbuf(r, &n);
+        std::vector<HostRange> out, in;
+        if (n) in.push_back({b, n * pb});
+        int rc = xfer_ranges(s, out, -1, in, rank - 1, st);
+        if (rc) return rc;
+      }
+      launch_key(bat, key);
+      if (tx && row_done(key, &r)) {
+        bat.flush();
+        u64 n;
+        void* b = sbuf(r, &n);
+        std::vector<HostRange> out, in;
+        if (n) out.push_back({b, n * pb});
+        int rc = xfer_ranges(s, out, rank + 1, in, -1, st);
+        if (rc) return rc;
+      }
+    }
+    bat.flush();
+    *nlaunch = bat.launches;
+    return 0;
+  }
+  // mode 1
+  if (!s->comm2) {
+    ncclResult_t e = ncclCommSplit(s->comm, 0, rank, &s->comm2, nullptr);
+    if (e != ncclSuccess) return fail(GM_EHIP, "ncclCommSplit: %s", ncclGetErrorString(e));
+  }
+  if (!s->cstream) HIPCHK(hipStreamCreateWithFlags(&s->cstream, hipStreamNonBlocking));
+  if (!s->cstream2) HIPCHK(hipStreamCreateWithFlags(&s->cstream2, hipStreamNonBlocking));
+  while (s->pev.size() < 2 * (size_t)R + 3) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    s->pev.push_back(e);
+  }
+  hipEvent_t* RE = s->pev.data();      // row r received
+  hipEvent_t* SE = RE + R;             // row r final on this rank
+  hipEvent_t* XE = SE + R;             // [0] start, [1] sends done, [2] receives done
+  ncclComm_t csend = (rank % 2 == 0) ? s->comm : s->comm2, crecv = (rank % 2 == 1) ? s->comm : s->comm2;
+  hipStream_t ts = s->cstream, rs = s->cstream2;
+  HIPCHK(hipEventRecord(XE[0], st));
+  HIPCHK(hipStreamWaitEvent(ts, XE[0], 0));
+  HIPCHK(hipStreamWaitEvent(rs, XE[0], 0));
+  constexpr uint32_t kAhead = 8;  // rows whose receives are posted ahead of the key that reads them
+  uint32_t posted = 0;            // rows [0, posted) have their receive posted
+  auto post_to = [&](uint32_t lim) -> int {
+    for (; rx && posted < std::min(lim, R); posted++) {
+      u64 n;
+      void* b = rbuf(posted, &n);
+      if (n) {
+        const ncclResult_t e = ncclRecv(b, n * pb, ncclUint8, rank - 1, crecv, rs);
+        if (e != ncclSuccess) return fail(GM_EHIP, "RCCL halo receive: %s", ncclGetErrorString(e));
+      }
+      HIPCHK(hipEventRecord(RE[posted], rs));
+    }
+    return 0;
+  };
+  for (uint32_t key = 0; key < K; key++) {
+    uint32_t r;
+    if (rx && row_need(key, &r)) {
+      bat.flush();
+      int rc = post_to(r + 1 + kAhead);
+      if (rc) return rc;
+      HIPCHK(hipStreamWaitEvent(st, RE[r], 0));
+    }
+    launch_key(bat, key);
+    if (tx && row_done(key, &r)) {
+      bat.flush();
+      HIPCHK(hipEventRecord(SE[r], st));
+      HIPCHK(hipStreamWaitEvent(ts, SE[r], 0));
+      u64 n;
+      void* b = sbuf(r, &n);
+      if (n) {
+        const ncclResult_t e = ncclSend(b, n * pb, ncclUint8, rank + 1, csend, ts);
+        if (e != ncclSuccess) return fail(GM_EHIP, "RCCL halo send: %s", ncclGetErrorString(e));
+      }
+    }
+  }
+  bat.flush();
+  *nlaunch = bat.launches;
+  int rc = post_to(R);
+  if (rc) return rc;
+  HIPCHK(hipEventRecord(XE[1], ts));
+  HIPCHK(hipEventRecord(XE[2], rs));
+  HIPCHK(hipStreamWaitEvent(st, XE[1], 0));
+  HIPCHK(hipStreamWaitEvent(st, XE[2], 0));
+  return 0;
+}
+
 // The PLANES solve.  Steps (gm_solver_set_steps, one table only): 2T like
 // the other layouts; step 0 is the forward pass (reach map + counts), steps
 // 1..T-1 are empty, step T + l is plane level l (l <= S), later steps empty.
@@ -628,8 +994,9 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
     HIPCHK(hipMemcpy(&wb, &s0->st->word_bits, sizeof wb, hipMemcpyDeviceToHost));
     if (wb != 8 * s0->pwb) return fail(GM_EINVAL, "resume: the scratch holds no %u-bit planes solve", 8 * s0->pwb);
   }
+  const bool staged = mode != 0 && s0->pstage_k;
   if (mode != 0 && !s0->halo_ok) {
-    int rc = plane_check_plan(ss, mode, st);
+    int rc = staged ? plane_check_stage(ss, mode, st) : plane_check_plan(ss, mode, st);
     if (rc) return rc;
   }
   std::vector<hipEvent_t> ev;
@@ -672,7 +1039,7 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
   // launches, so one event pair around all of them (no events between
   // launches: they would add their own gaps to what they time); shards --
   // a pair around each level's launches (exchanges sit between them)
-  const bool per_level = timing && mode != 0;
+  const bool per_level = timing && mode != 0 && !staged;
   // Shards (RCCL or in-process copies): each level's launch is split into
   // the planes that read no halo plane -- the boundary slices the exchange
   // sends are among them when blocks hold >= 4 top values -- and the ones
@@ -681,7 +1048,7 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
   // level l overlaps the boundary part of l and the own part of l + 1.  The
   // host-staged transport (mode 3) and blocks of < 4 values exchange in
   // order.
-  bool pipe = mode == 1 || mode == 2;
+  bool pipe = (mode == 1 || mode == 2) && !staged;
   if (s0->pg.B < 4 || (s0->flags & GM_F_SHARD_INORDER)) pipe = false;
   hipStream_t cs = st;
   hipEvent_t* PE = nullptr;  // [0, S]: own part of level l done; [S+1, 2S+2): exchange of l done
@@ -696,12 +1063,26 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
     PE = s0->pev.data();
   }
   int last_x = -1;  // last level exchanged on the comm stream
-  for (uint32_t l = 0; l <= S; l++) {
+  PlaneBatcher bat0(s0);  // one table: narrow levels in one-workgroup runs
+  u64 nlaunch = 0;        // resolve launches of this solve (shard 0's)
+  if (staged && stop == 2 * T) {
+    if (timing) HIPCHK(hipEventRecord(kr[0], st));
+    int rc = plane_backward_staged(ss, mode, st, &nlaunch);
+    if (rc) {
+      cleanup();
+      return rc;
+    }
+    if (timing) HIPCHK(hipEventRecord(kr[2 * (size_t)S + 1], st));
+  }
+  for (uint32_t l = 0; l <= S && !staged; l++) {
     const int k = T + (int)l;
     if (k < first) continue;
     if (k >= stop) break;
     if (per_level || (timing && l == 0)) HIPCHK(hipEventRecord(kr[2 * l], st));
-    if (!pipe) {
+    if (mode == 0 && !per_level) {
+      bat0.add(s0->ploff[l], s0->ploff[(size_t)l + 1], l < S ? s0->ploff[(size_t)l + 2] - s0->ploff[(size_t)l + 1] : 0);
+      if (l == S) bat0.flush();
+    } else if (!pipe) {
       for (gm_solver* s : ss) plane_launch(s, l);
     } else {
       for (gm_solver* s : ss) plane_launch(s, l, 1);
@@ -724,6 +1105,8 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
     }
     if (per_level || (timing && l == S)) HIPCHK(hipEventRecord(kr[2 * l + 1], st));
   }
+  bat0.flush();  // a stop inside a run
+  if (!staged) nlaunch = mode == 0 && !per_level ? bat0.launches : (u64)(S + 1) * (pipe ? 2 : 1);
   if (last_x >= 0) HIPCHK(hipStreamWaitEvent(st, PE[S + 1 + last_x], 0));  // join the comm stream
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(e2, st));
@@ -794,7 +1177,7 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
       sr = ms;
     }
     out->ms_resolve_kernels = sr;
-    out->n_resolve_launches = (uint64_t)S + 1;
+    out->n_resolve_launches = nlaunch;
   }
   cleanup();
   out->positions = red[0];

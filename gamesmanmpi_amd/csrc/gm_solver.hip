@@ -995,6 +995,11 @@ struct gm_solver {
   std::vector<u64> ploff;        // per level: first list entry
   std::vector<u64> pbnd;         // shards, per level: first entry that reads a halo plane (they come last)
   std::vector<u64> prcv_off, psnd_off;  // shards, per level: first halo plane received / sent
+  // staged PLANES shards (run_planes_staged): ploff / prcv_off / psnd_off are
+  // per key / per row; k = key skew, K keys, rows 0..smax
+  uint32_t pstage_k = 0, pkeys = 0, prows = 0;
+  ncclComm_t comm2 = nullptr;        // second communicator (ncclCommSplit): the other halo direction
+  hipStream_t cstream2 = nullptr;    // receive stream of the staged exchange
 };
 
 static const int kBlock = 256;
@@ -2125,6 +2130,8 @@ void gm_solver_destroy(gm_solver* s) {
   if (s->gfwd) (void)hipGraphExecDestroy(s->gfwd);
   if (s->gbwd) (void)hipGraphExecDestroy(s->gbwd);
   if (s->cstream) (void)hipStreamDestroy(s->cstream);
+  if (s->cstream2) (void)hipStreamDestroy(s->cstream2);
+  if (s->comm2) (void)ncclCommDestroy(s->comm2);
   if (s->comm) (void)ncclCommDestroy(s->comm);
   if (s->errg) (void)hipFree(s->errg);
   if (s->xdev) (void)hipFree(s->xdev);
@@ -2402,13 +2409,22 @@ int gm_plane_halo_plan(int game, int rank, int world, uint32_t flags, uint64_t* 
   PlaneShape ps;
   int rc = plane_shape(d, rank, world, flags, &ps);
   if (rc) return rc;
-  if (levels < ps.S + 1) return fail(GM_EINVAL, "out holds %u levels, the game has %u plane levels", levels, ps.S + 1);
+  const uint32_t steps = ps.stage_k ? ps.nrows : ps.S + 1;
+  if (levels < steps) return fail(GM_EINVAL, "out holds %u steps, the plan has %u", levels, steps);
+  memset(out, 0, (size_t)levels * world * 2 * sizeof(uint64_t));
   std::unique_ptr<gm_solver> s(new gm_solver());
   s->world = world;
   s->rank = rank;
   std::vector<uint8_t> lb;
   rc = plane_lists(s.get(), ps, lb);
   if (rc) return rc;
+  if (ps.stage_k) {  // staged: step = halo row, to rank + 1 / from rank - 1
+    for (uint32_t r = 0; r < ps.nrows; r++) {
+      if (rank + 1 < world) out[((size_t)r * world + rank + 1) * 2] = s->psnd_off[r + 1] - s->psnd_off[r];
+      if (rank > 0) out[((size_t)r * world + rank - 1) * 2 + 1] = s->prcv_off[r + 1] - s->prcv_off[r];
+    }
+    return 0;
+  }
   for (uint32_t l = 0; l <= ps.S; l++)
     for (int p = 0; p < world; p++) {
       u64 n;

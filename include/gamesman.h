@@ -131,6 +131,13 @@ typedef struct gm_buffers {
                                   round robin (every halo to rank + 1, one link)
                                   instead of the link-spreading deal used for
                                   power-of-two worlds >= 4 (A/B runs) */
+#define GM_F_PLANE_LEVEL_SYNC 4096u /* PLANES shards: the level-synchronous deal
+                                  (blocks of 8 top values, one halo exchange
+                                  per plane level) even where the staged
+                                  pipeline applies (A/B runs) */
+#define GM_F_PLANE_NO_RUNS 8192u /* PLANES: one launch per narrow plane level /
+                                  staged key instead of one-workgroup runs of
+                                  them (A/B runs) */
 #define GM_F_GRAPH 256u      /* dense one-table full solves: capture the
                                   forward and backward launches as HIP graphs
                                   on the first solve, replay them after
@@ -309,11 +316,14 @@ int gm_solver_set_transport(gm_solver *s, gm_xfer_fn fn, void *ctx);
  * Host only: no device memory, no GPU needed. */
 int gm_shard_halo_sigs(int game, int rank, int world, uint32_t flags, uint64_t *out, uint32_t levels);
 /* PLANES shards: the halo plan of shard `rank` (gm_plane_run.h
- * plane_lists), host only.  out[(l * world + p) * 2 + 0] = boundary planes
- * the shard sends to rank p after plane level l, [.. + 1] = planes it
- * receives from p; `levels` >= the game's plane levels (sum of the outer
- * heaps + 1), else GM_EINVAL.  Replaces the same per-edge message fan-out as
- * gm_solver_solve on shards (src/process.py:37-267). */
+ * plane_lists), host only.  out[(step * world + p) * 2 + 0] = boundary planes
+ * the shard sends to rank p at that step, [.. + 1] = planes it receives from
+ * p (the rest of out[levels][world][2] zeroed).  A step is a plane level for
+ * the level-synchronous deal (GM_F_PLANE_LEVEL_SYNC, or shapes the staged
+ * deal does not fit) and a halo row -- the boundary planes of one lower-digit
+ * sum, sent to rank + 1 -- for the staged pipeline.  `levels` >= the steps
+ * (the game's levels always suffice), else GM_EINVAL.  Replaces the per-edge
+ * message fan-out of the reference's shards (src/process.py:37-267). */
 int gm_plane_halo_plan(int game, int rank, int world, uint32_t flags, uint64_t *out, uint32_t levels);
 /* All `n` shards of one job in ONE process on one stream, halos moved by
  * device-to-device copies: the same kernels and halo geometry as the RCCL

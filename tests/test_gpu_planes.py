@@ -131,17 +131,31 @@ def test_planes_sum_31x6_checksum():
     _check_gold(e, r, [s.checksum()])
 
 
-@pytest.mark.parametrize("world", [2, 3, 4, 8])
-def test_planes_group_matches_single(world):
-    """Shards of the PLANES layout (round-robin blocks of the last heap,
-    boundary slices exchanged per plane level) solved as an in-process
-    group: every position answered by exactly one shard, word-equal to the
-    one-table solve."""
+LS, RR = 4096, 2048  # GM_F_PLANE_LEVEL_SYNC, GM_F_PLANE_ROUND_ROBIN
+GROUP_CASES = [  # world, params, flags: the deal each exercises
+    (2, "heaps=31:31:3:15", 0),         # staged, blocks of 8
+    (3, "heaps=31:31:3:23", 0),         # staged, blocks of 8
+    (4, "heaps=31:31:3:15", 0),         # staged, blocks of 4
+    (8, "heaps=31:31:3:15", 0),         # staged, blocks of 2 (the halo is a whole block)
+    (3, "heaps=31:31:3:63", 0),         # 64 values / 3 ranks: level-synchronous, round robin
+    (2, "heaps=31:31:3:15", LS),        # level-synchronous
+    (4, "heaps=31:31:3:63", LS),        # level-synchronous, link-spreading deal (two rounds)
+    (8, "heaps=31:31:1:127", LS),       # level-synchronous, link-spreading deal
+    (4, "heaps=31:31:3:63", LS | RR),   # level-synchronous, round robin
+]
+
+
+@pytest.mark.parametrize("world,params,flags", GROUP_CASES)
+def test_planes_group_matches_single(world, params, flags):
+    """Shards of the PLANES layout solved as an in-process group, for every
+    deal (the staged pipeline: one block per rank, halo rows copied as they
+    complete; the level-synchronous deals: boundary slices exchanged per
+    plane level): every position answered by exactly one shard, word-equal
+    to the one-table solve."""
     from gamesmanmpi_amd.dist import group_solve
     from gamesmanmpi_amd.games import GameSpec
-    params = "heaps=31:31:3:23" if world == 3 else "heaps=31:31:3:15"
     s1, r1 = _planes(params)
-    rg, shards = group_solve(GameSpec("sum_four_to_one", params), world)
+    rg, shards = group_solve(GameSpec("sum_four_to_one", params), world, flags=flags)
     assert rg.extra["layout"] == "planes"
     assert (rg.positions, rg.edges, rg.primitives, rg.root_line) == (r1.positions, r1.edges, r1.primitives,
                                                                       r1.root_line)
@@ -159,11 +173,12 @@ def test_planes_group_matches_single(world):
     assert sum(len(sh.positions()) for sh in shards) == len(keys)
 
 
-def test_planes_group_matches_oracle():
+@pytest.mark.parametrize("world", [2, 4])
+def test_planes_group_matches_oracle(world):
     from gamesmanmpi_amd.dist import group_solve
     from gamesmanmpi_amd.games import GameSpec
     params = "heaps=31:31:2:7"
-    rg, shards = group_solve(GameSpec("sum_four_to_one", params), 2)
+    rg, shards = group_solve(GameSpec("sum_four_to_one", params), world)
     sol = _oracle(params)
     assert (rg.positions, rg.edges, rg.root_line) == (sol.count, sol.edges, sol.root_line)
     keys = np.arange(sol.count, dtype=np.uint64)
@@ -194,17 +209,33 @@ def test_planes_stop_resume(cut):
 
 @pytest.mark.parametrize("world", [2, 4])
 def test_planes_group_pipelined_equals_in_order(world):
-    """Shards exchange each level's boundary planes on a comm stream while
-    the next launches run (own part / boundary part split, the RCCL path's
+    """Level-synchronous shards exchange each level's boundary planes on a
+    comm stream while the next launches run (own part / boundary part split, the RCCL path's
     schedule); GM_F_SHARD_INORDER exchanges after each whole level.  Same
     words either way."""
     from gamesmanmpi_amd import _lib
     from gamesmanmpi_amd.dist import group_solve
     from gamesmanmpi_amd.games import GameSpec
     spec = GameSpec("sum_four_to_one", "heaps=31:31:7:7:15")
-    rp, sp = group_solve(spec, world)
-    ri, si = group_solve(spec, world, flags=_lib.GM_F_SHARD_INORDER)
+    ls = _lib.GM_F_PLANE_LEVEL_SYNC
+    rp, sp = group_solve(spec, world, flags=ls)
+    ri, si = group_solve(spec, world, flags=ls | _lib.GM_F_SHARD_INORDER)
     assert (rp.positions, rp.edges, rp.root_line) == (ri.positions, ri.edges, ri.root_line)
     keys = np.arange(32 * 32 * 8 * 8 * 16, dtype=np.uint64)
     for a, b in zip(sp, si):
         np.testing.assert_array_equal(a.query(keys), b.query(keys))
+
+
+@pytest.mark.parametrize("flags", [0, 64, 1024])  # 8-bit packed, 16-bit, one plane per half-wave
+def test_planes_runs_equal_single_launches(flags):
+    """Narrow plane levels run as one-workgroup runs (k_plane_run, a
+    barrier between levels) give the words of one grid launch per level
+    (GM_F_PLANE_NO_RUNS), for every kernel family."""
+    from gamesmanmpi_amd import _lib
+    params = "heaps=31:31:7:7:15"
+    sa, ra = _planes(params, flags=flags)
+    sb, rb = _planes(params, flags=flags | _lib.GM_F_PLANE_NO_RUNS)
+    assert (ra.positions, ra.edges, ra.root_line) == (rb.positions, rb.edges, rb.root_line)
+    keys = np.arange(32 * 32 * 8 * 8 * 16, dtype=np.uint64)
+    np.testing.assert_array_equal(sa.query(keys), sb.query(keys))
+    assert sa.checksum() == sb.checksum()

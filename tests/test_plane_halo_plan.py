@@ -1,13 +1,14 @@
 """Halo plans of PLANES shards (gm_plane_halo_plan, host only): what every
-shard sends to each peer after each plane level is exactly what that peer
-posts to receive from it, for the round-robin deal and for the link-
-spreading deal -- the pairing the RCCL exchange relies on.
-The spreading deal must put a shard's halo on world / 2 links at N = 4 and 8
-(bench shapes) while moving the same planes in total."""
+shard sends to each peer at each step is exactly what that peer posts to
+receive from it -- the pairing the RCCL exchange relies on -- for the staged
+pipeline (steps = halo rows, one block per rank, sends to rank + 1 only) and
+the level-synchronous deals (steps = plane levels; round robin, and the
+link-spreading deal that must put a shard's halo on world / 2 links at N = 4
+and 8 while moving the same planes in total).  DESIGN.md §6a."""
 import numpy as np
 import pytest
 
-from gamesmanmpi_amd._lib import GM_F_PLANE_ROUND_ROBIN
+from gamesmanmpi_amd._lib import GM_F_PLANE_LEVEL_SYNC, GM_F_PLANE_ROUND_ROBIN
 from gamesmanmpi_amd.dist import plane_halo_plan
 from gamesmanmpi_amd.games import GameSpec
 
@@ -30,8 +31,8 @@ def _peers(plan):
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_bench_shape_spreads_links(world):
     params = "heaps=31:31:31:31:31:%d" % (32 * world - 1)
-    spread = _plans(params, world)
-    rr = _plans(params, world, GM_F_PLANE_ROUND_ROBIN)
+    spread = _plans(params, world, GM_F_PLANE_LEVEL_SYNC)
+    rr = _plans(params, world, GM_F_PLANE_LEVEL_SYNC | GM_F_PLANE_ROUND_ROBIN)
     total = lambda ps: sum(int(p[:, :, 0].sum()) for p in ps)
     assert total(spread) == total(rr) > 0
     for r in range(world):
@@ -52,12 +53,43 @@ def test_bench_shape_spreads_links(world):
                                           ("heaps=31:31:3:3:47", 3), ("heaps=31:31:7:7", 4)])
 def test_test_shape_plans_pair(params, world):
     _plans(params, world)
-    _plans(params, world, GM_F_PLANE_ROUND_ROBIN)
+    _plans(params, world, GM_F_PLANE_LEVEL_SYNC)
+    _plans(params, world, GM_F_PLANE_LEVEL_SYNC | GM_F_PLANE_ROUND_ROBIN)
 
 
 def test_spreading_deal_only_where_it_applies():
     """Non-power-of-two worlds and partial rounds keep the round-robin deal:
     every shard's halo goes to rank + 1."""
     for params, world in (("heaps=31:31:3:47", 3), ("heaps=31:31:3:15", 4)):
-        for r, plan in enumerate(_plans(params, world)):
+        for r, plan in enumerate(_plans(params, world, GM_F_PLANE_LEVEL_SYNC)):
             assert _peers(plan) in ([(r + 1) % world], [])
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_staged_bench_shape_rows(world):
+    """The staged pipeline on the bench shapes: one block of 32 top values
+    per rank, the halo = the last two slices, sent to rank + 1 row by row
+    (one row per lower-digit sum 0..93), 2 x 32^3 planes per step in all."""
+    params = "heaps=31:31:31:31:31:%d" % (32 * world - 1)
+    plans = _plans(params, world)
+    Z = 32 ** 3
+    cls = np.convolve(np.convolve(np.ones(32), np.ones(32)), np.ones(32)).astype(np.int64)
+    for r, plan in enumerate(plans):
+        sent = plan[:, :, 0].sum(axis=1).astype(np.int64)
+        assert _peers(plan) == ([r + 1] if r + 1 < world else [])
+        if r + 1 < world:
+            assert sent.sum() == 2 * Z
+            np.testing.assert_array_equal(sent[:94], 2 * cls)
+            assert not sent[94:].any()
+        got = plan[:, :, 1].sum(axis=1).astype(np.int64)
+        assert got.sum() == (2 * Z if r else 0)
+
+
+def test_staged_only_where_blocks_divide():
+    """A last heap whose values do not split evenly over the ranks keeps the
+    level-synchronous deal (steps = plane levels, more of them than rows)."""
+    spec_params, world = "heaps=31:31:3:23", 3  # 24 values / 3 ranks: staged, rows 0..3
+    plans = _plans(spec_params, world)
+    assert all(not p[4:].any() for p in plans)
+    plans = _plans("heaps=31:31:3:63", 3)  # 64 values: not divisible by 3
+    assert any(p[4:].any() for p in plans)

@@ -6,7 +6,11 @@ shards re-solved REPS times; prints one JSON line per solve.  On one GPU the
 shards' launches run back to back on one stream, so ms_backward / N is a
 shard's device time per level sweep -- what each GPU of an N-GPU run spends
 in kernels, before the exchange.
-    python tools/group_planes.py WORLD [REPS]"""
+In the staged deal (the default where the last heap splits evenly) the
+shards run one after another, so ms_backward / N is one rank's key sweep
+with its launch floor; FLAGS 4096 (GM_F_PLANE_LEVEL_SYNC) times the
+level-synchronous deal instead.
+    python tools/group_planes.py WORLD [REPS] [FLAGS]"""
 import ctypes
 import json
 import sys
@@ -23,10 +27,11 @@ def main():
     from gamesmanmpi_amd.solver import Solver
     world = int(sys.argv[1])
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+    flags = int(sys.argv[3]) if len(sys.argv) > 3 else 0
     heaps = bench.heaps_for(world)
     spec = GameSpec("sum_four_to_one", "heaps=" + ":".join(map(str, heaps)))
     stream = torch.cuda.Stream()
-    shards = [Solver(spec, rank=g, world=world, stream=stream) for g in range(world)]
+    shards = [Solver(spec, rank=g, world=world, stream=stream, flags=flags) for g in range(world)]
     arr = (ctypes.c_void_p * world)(*[s.handle.value for s in shards])
     L = _lib.load()
     for i in range(reps + 1):
@@ -39,7 +44,7 @@ def main():
         res = shards[0]._result(r)
         if i == 0:
             continue  # warm-up
-        print(json.dumps({"world": world, "heaps": heaps, "positions": res.positions, "root": res.root_line,
+        print(json.dumps({"world": world, "heaps": heaps, "flags": flags, "positions": res.positions, "root": res.root_line,
                           "layout": res.extra.get("layout"), "wall_ms": wall, "ms_forward": res.ms_forward,
                           "ms_backward": res.ms_backward, "ms_backward_per_shard": res.ms_backward / world,
                           "word_bits": res.extra.get("word_bits")}), flush=True)
