@@ -72,9 +72,12 @@ typedef struct gm_slot {
  * order-form word in natural rank order, planes of 32 x 32 positions (heaps
  * 0 and 1) with each row rotated by its row number, plus a 1-bit reach map;
  * table_slots = positions.  The backward pass runs once per sum of the outer
- * heaps (gamesmanmpi_amd/csrc/gm_plane.h).  Shards own round-robin blocks
- * of the last heap's values and exchange two boundary slices per plane
- * level; their table buffer also holds the halo send / receive areas. */
+ * heaps (gamesmanmpi_amd/csrc/gm_plane.h).  Shards own blocks of the last
+ * heap's values -- one block per rank, resolved as a pipeline with the
+ * boundary slices streamed to the next rank row by row (the staged deal), or
+ * round-robin blocks with one exchange per plane level (GM_F_PLANE_LEVEL_SYNC
+ * or uneven splits); their table buffer also holds the halo send / receive
+ * areas. */
 #define GM_MODE_PLANES 3u
 
 /* Sizes the caller must allocate for a solve (see gm_plan). */
