@@ -136,6 +136,7 @@ class Solver:
         b.mode = plan.mode
         b.table_bytes = plan.table_bytes
         self._bufs = b
+        self._cflags = flags  # the flags the solver was created with (layout bits included)
         self.plan = plan
         h = ctypes.c_void_p()
         _lib.check(L.gm_solver_create_shard(self.spec.id, self.rank,
@@ -163,7 +164,7 @@ class Solver:
         """Time every kernel launch with HIP events (on the solve stream)."""
         self.kernel_timing = bool(on)
         _lib.check(_lib.load().gm_solver_set_flags(
-            self._h, self.flags | (_lib.GM_F_KERNEL_TIMING if on else 0)))
+            self._h, self._cflags | (_lib.GM_F_KERNEL_TIMING if on else 0)))
 
     def solve(self, max_retries=4):
         """Full solve from the root; grows the buffers on GM_EFULL."""

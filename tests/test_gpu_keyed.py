@@ -168,3 +168,19 @@ def test_gpu_keyed_two_processes_torch_exchange(name, golden_summary):
     np.testing.assert_array_equal(canon[order], t["canon"])
     np.testing.assert_array_equal(val[order], t["value"])
     np.testing.assert_array_equal(rem[order], t["remoteness"])
+
+
+@pytest.mark.parametrize("layout", ["bucketed", "hashed", "auto"])
+def test_gpu_kernel_timing_toggles_on_explicit_layouts(layout):
+    """set_kernel_timing re-sends the flags the solver was CREATED with
+    (layout bits included): per-kernel timing on a bucketed or hashed
+    solver, same root and counts as without."""
+    from gamesmanmpi_amd.games import GameSpec
+    from gamesmanmpi_amd.solver import Solver
+    s = Solver(GameSpec("toot_and_otto_bitstring", "length=4,height=3"), layout=layout)
+    r0 = s.solve()
+    s.set_kernel_timing(True)
+    r1 = s.solve()
+    s.set_kernel_timing(False)
+    assert (r0.positions, r0.edges, r0.root_line) == (r1.positions, r1.edges, r1.root_line)
+    assert r1.n_resolve_launches > 0
