@@ -154,6 +154,20 @@ def pmc_traffic(kernel, workload):
     return row["bytes_per_launch"], "profiles/pmc_traffic.json (%s)" % row.get("source", "?")
 
 
+def pmc_traffic_total(kernel, workload):
+    """(HBM bytes per launch, launches per solve) of `kernel` from the
+    committed PMC summary, or (None, 0)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as fh:
+            row = json.load(fh).get(kernel)
+    except (OSError, ValueError):
+        return None, 0
+    if not row or row.get("workload") != workload:
+        return None, 0
+    return row["bytes_per_launch"], row.get("launches", 0)
+
+
 def golden(name):
     try:
         with open(os.path.join(ROOT, "tests", "golden", "checksums.json")) as fh:
@@ -356,10 +370,16 @@ def main():
     t_launch = kms / kn / 1e3  # seconds per launch
     achieved = (kb / kn) / t_launch / 1e9  # GB/s
     traffic, traffic_src = pmc_traffic(kname, workload)
+    if layout == "planes" and traffic is not None:
+        # the backward's launches are this kernel plus the one-workgroup runs
+        # of narrow levels (k_plane_run): their PMC bytes over all of them
+        per_solve = sum(b * n for b, n in (pmc_traffic_total(k, workload) for k in (kname, "k_plane_run")) if b)
+        traffic = per_solve / world / kn if per_solve else traffic
     roof = {"bound": "hbm", "kernel": kname,
             "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "traffic_unit": "HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE)",
+            "traffic_unit": "HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE; PLANES: over the backward's "
+                            "grid launches and one-workgroup runs together)",
             "traffic_source": traffic_src,
             "frac_pmc": (traffic / t_launch / 1e9 / HBM_PEAK_GBS) if traffic else None,
             "frac_per_edge_model": (ke / kn) / t_launch / 1e9 / HBM_PEAK_GBS,
