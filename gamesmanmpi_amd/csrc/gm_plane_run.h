@@ -176,15 +176,7 @@ struct PlaneShape {
 static uint32_t plane_stage_k(int world) { return world <= 2 ? 2u : world <= 4 ? 4u : 5u; }
 
 static u64 rup256(u64 x) { return (x + 255) & ~255ull; }
-// A/B switches read once from the environment ("0" turns the feature off)
-static bool getenv_flag_off(const char* name) {
-  const char* v = getenv(name);
-  return v && v[0] == '0';
-}
-static bool plane_prefetch_on() {
-  static const bool on = !getenv_flag_off("GM_PLANE_PREFETCH");
-  return on;
-}
+
 
 static int plane_shape(const Desc* d, int rank, int world, uint32_t flags, PlaneShape* ps) {
   memset(ps, 0, sizeof *ps);
@@ -546,7 +538,6 @@ static void plane_launch_w(gm_solver* s, u64 a, u64 n, u64 pa, u64 pn) {
 // entries the next launch starts with, prefetched (pn = 0: none)
 static void plane_launch_range(gm_solver* s, u64 a, u64 n, u64 pa = 0, u64 pn = 0) {
   const bool sh = s->world > 1;
-  if (!plane_prefetch_on()) pn = 0;
   if (s->pwb == 1) {
     if (sh) plane_launch_w<1, true>(s, a, n, pa, pn);
     else plane_launch_w<1, false>(s, a, n, pa, pn);
