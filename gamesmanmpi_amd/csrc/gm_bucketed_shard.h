@@ -108,7 +108,7 @@ __global__ __launch_bounds__(kBkStreamThreads) void k_bks_answer(const uint32_t*
         else hi = m;
       }
       const uint32_t w = bk_pack_word(WX[lcs[lo] + c], &err);
-      bk_stage_put(S, ((u64)(ref & 0x1FFFFFFFu) << 32) | w, 0u, ref >> 29);
+      bk_stage_put_few(S, ((u64)(ref & 0x1FFFFFFFu) << 32) | w, 0u, ref >> 29);
     }
     bk_stage_reserve(S, at, cur, [](uint32_t b) { return b; });
     bk_stage_flush(S, at, out, (uint32_t*)nullptr);

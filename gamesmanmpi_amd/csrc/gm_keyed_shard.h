@@ -69,13 +69,26 @@ __device__ __forceinline__ uint32_t md5_mod_words(const uint32_t M[16], uint32_t
     b = b + __builtin_amdgcn_alignbit(f, f, 32 - R[(i >> 4) * 4 + (i & 3)]);
   }
   const uint32_t h[4] = {a + 0x67452301u, b + 0xefcdab89u, c + 0x98badcfeu, e + 0x10325476u};
-  // int(hexdigest, 16) % P: the 16 digest bytes as a big-endian integer
-  uint32_t acc = 0;  // < P <= 2^23: (acc << 8 | byte) fits 32 bits
+  // int(hexdigest, 16) % P: the 16 digest bytes as a big-endian integer.  A
+  // power-of-two P (every bench world) keeps the low bits of the last byte;
+  // otherwise Horner over the bytes (< P <= 2^23: acc << 8 | byte fits 32
+  // bits), sixteen dependent 32-bit remainders
+  if ((P & (P - 1)) == 0 && P <= 256u) return (h[3] >> 24) & (P - 1u);
+  uint32_t acc = 0;
 #pragma unroll
   for (int i = 0; i < 16; i++) acc = ((acc << 8) | ((h[i >> 2] >> (8 * (i & 3))) & 0xFFu)) % P;
   return acc;
 }
+// (the descriptor fields the rule reads, as values: a call passes them in
+// registers instead of materialising the whole Desc in scratch)
+struct OwnerGeom {
+  int kind, variant, A, nbits;
+};
+__device__ __forceinline__ uint32_t owner_fast_g(const OwnerGeom d, u64 k, uint32_t P);
 __device__ __forceinline__ uint32_t owner_fast(const Desc& d, u64 k, uint32_t P) {
+  return owner_fast_g(OwnerGeom{d.kind, d.variant, d.A, d.nbits}, k, P);
+}
+__device__ __forceinline__ uint32_t owner_fast_g(const OwnerGeom d, u64 k, uint32_t P) {
   if (P <= 1) return 0;
   uint32_t M[16];
 #pragma unroll
@@ -152,10 +165,34 @@ __device__ __forceinline__ uint32_t owner_dev(const Desc& d, u64 key, uint32_t P
   return owner_of(d, key, P);
 }
 
+// the owner rule for a kernel specialised to game kind KIND: the kinds the
+// bucketed shards serve get the register-resident MD5 with no runtime branch
+// to owner_of, whose byte arrays live in scratch (inlined beside the fast
+// form they cost the sharded expand 672 B of scratch per lane and half its
+// occupancy)
+template <int KIND>
+__device__ __forceinline__ uint32_t owner_k(const Desc& d, u64 key, uint32_t P) {
+  if constexpr (KIND == K_TTT || KIND == K_TOOT || KIND == K_OTHELLO || KIND == K_TOOT_6x4 || KIND == K_TOOT_5x4 ||
+                KIND == K_TOOT_4x4)
+    return owner_fast(d, key, P);
+  else
+    return owner_dev(d, key, P);
+}
+
 // the same as a call: the bucketed kernels ask for owners inside the
 // unrolled move generators, where an inlined MD5 per move site multiplies the
 // code (and the compile time) by the number of sites
 __device__ __noinline__ uint32_t owner_of_call(const Desc& d, u64 key, uint32_t P) { return owner_dev(d, key, P); }
+__device__ __noinline__ uint32_t owner_fast_call(const OwnerGeom d, u64 key, uint32_t P) { return owner_fast_g(d, key, P); }
+// as a call, for a kernel specialised to KIND (no scratch-array path for the fast kinds)
+template <int KIND>
+__device__ __forceinline__ uint32_t owner_call_k(const Desc& d, u64 key, uint32_t P) {
+  if constexpr (KIND == K_TTT || KIND == K_TOOT || KIND == K_OTHELLO || KIND == K_TOOT_6x4 || KIND == K_TOOT_5x4 ||
+                KIND == K_TOOT_4x4)
+    return owner_fast_call(OwnerGeom{d.kind, d.variant, d.A, d.nbits}, key, P);
+  else
+    return owner_of_call(d, key, P);
+}
 
 // rank owning the root seeds its table and level 0; every rank zeroes state
 __global__ void k_ks_seed(gm_slot* tab, u64 mask, u64* lv, DevState* st, u64 root, int owned) {
