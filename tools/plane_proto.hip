@@ -33,7 +33,10 @@ static void launch(void* tab, const uint32_t* list, uint32_t n, const PlaneGeom&
   const uint32_t waves = g_x2 ? (n + 3) / 4 : (n + 1) / 2;
   uint32_t blocks = (waves + 3) / 4;
   blocks = (blocks + 7) / 8 * 8;
-  if (g_x2 == 9 && WB == 1)
+  if (g_x2 == 10 && WB == 1)
+    hipLaunchKernelGGL((k_plane_resolve_x2d<1, NO, false>), dim3(blocks), dim3(256), 0, st, (uint8_t*)tab, list, n, g,
+                       zero, (const uint8_t*)nullptr, (uint8_t*)nullptr);
+  else if (g_x2 == 9 && WB == 1)
     hipLaunchKernelGGL((k_plane_resolve_x2c<1, NO, false>), dim3(blocks), dim3(256), 0, st, (uint8_t*)tab, list, n, g,
                        zero, (const uint8_t*)nullptr, (uint8_t*)nullptr);
   else if (g_x2 == 8 && WB == 1)

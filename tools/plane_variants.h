@@ -548,6 +548,152 @@ __global__ __launch_bounds__(256, 4) void k_plane_resolve_x2b(typename PlaneWord
   }
 }
 
+// k_plane_resolve_x2 with a plain grid-stride share (no XCD chunking of the level list)
+template <int WB, int NO, bool SH>
+__global__ __launch_bounds__(256) void k_plane_resolve_x2d(typename PlaneWord<WB>::T* __restrict__ tab,
+                                                          const void* __restrict__ list, uint32_t n, PlaneGeom g,
+                                                          const uint4* __restrict__ zero,
+                                                          const typename PlaneWord<WB>::T* __restrict__ recv,
+                                                          typename PlaneWord<WB>::T* __restrict__ send) {
+  typedef PlaneWord<WB> W;
+  typedef typename W::T T;
+  constexpr int DW = W::DW, NQ = DW / 4;
+  const uint32_t lane = threadIdx.x & 63, L = lane & 31;
+  const bool l32 = lane == 32;
+  const uint32_t gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const PlaneShare sh{gw * 4u, n, gridDim.x * (blockDim.x >> 6) * 4u};
+  for (uint32_t i0 = sh.first; i0 < sh.end; i0 += sh.stride) {
+    const uint32_t ix = i0 + 2 * (lane >> 5), iy = ix + 1;
+    const bool livex = ix < sh.end, livey = iy < sh.end;
+    PlaneEntry ex, ey;
+    if (SH) {
+      ex = ((const PlaneEntry*)list)[livex ? ix : i0];
+      ey = ((const PlaneEntry*)list)[livey ? iy : i0];
+    } else {
+      ex.p = ((const uint32_t*)list)[livex ? ix : i0];
+      ey.p = ((const uint32_t*)list)[livey ? iy : i0];
+    }
+    uint32_t dx[NO > 0 ? NO : 1], dy[NO > 0 ? NO : 1];
+    plane_digits<NO>(g, ex.p, dx);
+    plane_digits<NO>(g, ey.p, dy);
+    const size_t ox = (size_t)ex.p * 1024u + L * 32u, oy = (size_t)ey.p * 1024u + L * 32u;
+    // E rows of both planes (8-bit: odd bytes exact in Ehi, even bytes in
+    // the high bytes of Elo; 16-bit: Ehi exact)
+    uint32_t Xh[DW], Xl[WB == 1 ? DW : 1], Yh[DW], Yl[WB == 1 ? DW : 1];
+#pragma unroll
+    for (int d = 0; d < DW; d++) {
+      Xh[d] = Yh[d] = 0;
+      if (WB == 1) Xl[d] = Yl[d] = 0;
+    }
+    auto nb = [&](const PlaneEntry& e, const uint32_t* dig, size_t off, int j, int k) -> const uint4* {
+      if (SH && j == NO - 1) {
+        const uint32_t w = k == 1 ? e.top1 : e.top2;
+        return w == kPlaneAbsent ? zero
+               : w == kPlaneLocal ? (const uint4*)(tab + off - (size_t)k * g.Z * 1024u)
+                                  : (const uint4*)(recv + (size_t)w * 1024u + L * 32u);
+      }
+      return dig[j] >= (uint32_t)k ? (const uint4*)(tab + off - (size_t)k * g.stride[j] * 1024u) : zero;
+    };
+#pragma unroll
+    for (int j = 0; j < NO; j++) {
+#pragma unroll
+      for (int k = 1; k <= 2; k++) {
+        const uint4* sx = nb(ex, dx, ox, j, k);
+        const uint4* sy = nb(ey, dy, oy, j, k);
+        uint4 vx[NQ], vy[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; q++) {
+          vx[q] = sx[q];
+          vy[q] = sy[q];
+        }
+#pragma unroll
+        for (int q = 0; q < NQ; q++) {
+          const uint32_t a[4] = {vx[q].x, vx[q].y, vx[q].z, vx[q].w};
+          const uint32_t b[4] = {vy[q].x, vy[q].y, vy[q].z, vy[q].w};
+#pragma unroll
+          for (int c = 0; c < 4; c++) {
+            Xh[4 * q + c] = pk_max16(Xh[4 * q + c], a[c]);
+            Yh[4 * q + c] = pk_max16(Yh[4 * q + c], b[c]);
+            if (WB == 1) {
+              Xl[4 * q + c] = pk_max16(Xl[4 * q + c], pk_shl8(a[c]));
+              Yl[4 * q + c] = pk_max16(Yl[4 * q + c], pk_shl8(b[c]));
+            }
+          }
+        }
+      }
+    }
+    const uint32_t primv =
+        (g.rank == 0 && L == 0) ? ((ex.p == 0 ? W::kPrim : 0u) | (ey.p == 0 ? W::kPrim << 16 : 0u)) : 0u;
+    // step q's results of both planes stay packed [X | Y] in op[q] (OR of
+    // the two phases: an idle lane contributes 0) and are unpacked into the
+    // two rows once, after the wavefront
+    uint32_t cur = 0, prev = 0, u1p = 0;
+    uint32_t op[32];
+#pragma unroll
+    for (int q = 0; q < 32; q++) op[q] = 0;
+#pragma unroll 1
+    for (uint32_t ph = 0; ph < 2; ph++) {
+      const uint32_t flip = ph ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+      for (int q = 0; q < 32; q++) {
+        uint32_t a;
+        if (WB == 1) {
+          // byte q of X's and Y's E rows -> [X, 0, Y, 0]
+          const int d = q >> 2, b = q & 3;
+          const uint32_t bx = (b & 1) ? (uint32_t)b : (uint32_t)b + 1;  // byte inside the split dword
+          const uint32_t sel = 0x0C000C00u | ((4u + bx) << 16) | bx;     // hi = Y (bytes 4-7), lo = X
+          a = (b & 1) ? perm(Yh[d], Xh[d], sel) : perm(Yl[d], Xl[d], sel);
+        } else {
+          const int d = q >> 1, h = q & 1;
+          const uint32_t b0 = 2 * h;
+          const uint32_t sel = ((5u + b0) << 24) | ((4u + b0) << 16) | ((1u + b0) << 8) | b0;
+          a = perm(Yh[d], Xh[d], sel);
+        }
+        const uint32_t u1r = from_lane_below(cur), u2r = from_lane_below(u1p);
+        uint32_t m = pk_max16(pk_max16(a, cur), prev);
+        const uint32_t m2 = pk_max16(pk_max16(m, u1r), u2r);
+        m = l32 ? m : m2;  // row 0 of the upper pair has no row below
+        const uint32_t am = (uint32_t)(q == 31 ? 0xFFFFFFFFull : ((2ull << q) - 1)) ^ flip;
+        uint32_t f = keep_rows(am, L, parent_x2<WB>(m));
+        if (q == 0) f = pk_max16(f, ph ? 0u : primv);
+        op[q] |= f;
+        prev = cur;
+        cur = f;
+        u1p = l32 ? 0u : u1r;
+      }
+    }
+    uint32_t ox_[DW], oy_[DW];
+    if (WB == 1) {
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const uint32_t t1 = perm(op[4 * k + 1], op[4 * k], 0x06020400u);      // [X0 X1 Y0 Y1]
+        const uint32_t t2 = perm(op[4 * k + 3], op[4 * k + 2], 0x06020400u);  // [X2 X3 Y2 Y3]
+        ox_[k] = perm(t2, t1, 0x05040100u);
+        oy_[k] = perm(t2, t1, 0x07060302u);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        ox_[k] = perm(op[2 * k + 1], op[2 * k], 0x05040100u);
+        oy_[k] = perm(op[2 * k + 1], op[2 * k], 0x07060302u);
+      }
+    }
+    auto store = [&](T* dst, const uint32_t* o) {
+      uint4* p = (uint4*)dst;
+#pragma unroll
+      for (int q = 0; q < NQ; q++) p[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+    };
+    if (livex) {
+      store(tab + ox, ox_);
+      if (SH && ex.send != kPlaneAbsent) store(send + (size_t)ex.send * 1024u + L * 32u, ox_);
+    }
+    if (livey) {
+      store(tab + oy, oy_);
+      if (SH && ey.send != kPlaneAbsent) store(send + (size_t)ey.send * 1024u + L * 32u, oy_);
+    }
+  }
+}
+
 // k_plane_resolve_x2 held to 5 waves / SIMD (<= 96 VGPRs): the widest levels hold ~4.2 K waves
 template <int WB, int NO, bool SH>
 __global__ __launch_bounds__(256, 5) void k_plane_resolve_x2c(typename PlaneWord<WB>::T* __restrict__ tab,
