@@ -31,9 +31,11 @@ GM_F_PLANE_X1 = 1024  # PLANES A/B: one plane per half-wave (k_plane_resolve)
 GM_F_PLANE_ROUND_ROBIN = 2048  # PLANES shards A/B: round-robin blocks (one halo link)
 GM_F_PLANE_LEVEL_SYNC = 4096  # PLANES shards A/B: level-synchronous deal instead of the staged pipeline
 GM_F_PLANE_NO_RUNS = 8192  # PLANES A/B: no one-workgroup runs of narrow levels / keys
+GM_F_BKS_LOCAL = 16384  # md5-sharded bucketed: local dedup before hashing / sending
 KERNEL_FLAGS = (GM_F_WORDS32 | GM_F_RESOLVE_SCALAR | GM_F_SHARD_INORDER | GM_F_WORDS16 | GM_F_BK_EXACT
                 | GM_F_GRAPH | GM_F_LEVEL_MAJOR | GM_F_PLANE_X1 | GM_F_PLANE_ROUND_ROBIN
-                | GM_F_PLANE_LEVEL_SYNC | GM_F_PLANE_NO_RUNS)
+                | GM_F_PLANE_LEVEL_SYNC | GM_F_PLANE_NO_RUNS
+                | GM_F_BKS_LOCAL)
 # gm_result.kernels codes (gm_solver.hip DenseResolveKind / DensePullKind)
 RESOLVE_KERNELS = {1: "k_dense_resolve8p", 2: "k_dense_resolve8c", 3: "k_dense_resolve4p",
                    4: "k_dense_resolve4c", 5: "k_dense_resolve4", 6: "k_dense_resolve",

@@ -141,6 +141,69 @@ __global__ __launch_bounds__(kBkStreamThreads) void k_bks_answer_in(const u64* _
   }
 }
 
+// Local-dedup form (GM_F_BKS_LOCAL): a rank first builds the UNIQUE children
+// of its own parents with the one-GPU passes (expand, fine, LDS dedup), then
+// hashes and sends each of them once.  k_bks_ownbin: block j over the local
+// unique children of fine buckets [j bpb, (j + 1) bpb) -- compact index u in
+// [cst[b0], cst[b1]), key at U[fo[b] + u - cst[b]] -- staged by owner rank
+// (md5) and written to the owner's region [o cap, (o + 1) cap) of the send
+// buffer at runs reserved on cur[o]: (key, ref = rank << 29 | u).  A region
+// past cap sets *oflag (the level fails with GM_EFULL).
+template <int KIND>
+__global__ __launch_bounds__(kBkStreamThreads) void k_bks_ownbin(Desc d, const u64* __restrict__ U,
+                                                                const uint32_t* __restrict__ fo,
+                                                                const uint32_t* __restrict__ cst, uint32_t NB,
+                                                                uint32_t bpb, uint32_t W, uint32_t pref, uint32_t cap,
+                                                                uint32_t* cur, u64* outk, uint32_t* outr,
+                                                                uint32_t* oflag) {
+  __shared__ BkStage<u64, true, kBksAnswerCap> S;
+  __shared__ uint32_t at[kBkC], lfo[kBkC + 1], lcs[kBkC + 1];
+  const uint32_t b0 = blockIdx.x * bpb, b1 = min(NB, b0 + bpb), nb = b1 > b0 ? b1 - b0 : 0u;
+  if (threadIdx.x <= nb) {
+    lfo[threadIdx.x] = fo[b0 + threadIdx.x];
+    lcs[threadIdx.x] = cst[b0 + threadIdx.x];
+  }
+  bk_stage_init(S);
+  if (nb == 0) return;  // block-uniform
+  const uint32_t a = lcs[0], e = lcs[nb];
+  constexpr int UA = kBksAnswerCap / kBkStreamThreads;
+  for (uint32_t i0 = a; i0 < e; i0 += UA * blockDim.x) {  // block-uniform rounds
+#pragma unroll
+    for (int u = 0; u < UA; u++) {
+      const uint32_t i = i0 + u * blockDim.x + threadIdx.x;
+      if (i >= e) continue;
+      uint32_t lo = 0, hi = nb;  // bucket: lcs[lo] <= i < lcs[lo + 1]
+      while (hi - lo > 1) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (lcs[m] <= i) lo = m;
+        else hi = m;
+      }
+      const u64 key = U[lfo[lo] + (i - lcs[lo])];
+      bk_stage_put_few(S, key, pref | i, owner_k<KIND>(d, key, W));
+    }
+    __syncthreads();
+    if (threadIdx.x < W) {
+      const uint32_t v = S.binc[threadIdx.x];
+      if (v) {
+        const uint32_t p = atomicAdd(&cur[threadIdx.x], v);
+        if (p + v > cap) S.stop = 1;
+        at[threadIdx.x] = threadIdx.x * cap + p;
+      }
+    }
+    bk_stage_flush(S, at, outk, outr);
+  }
+  if (threadIdx.x == 0 && S.stop) atomicOr(oflag, 1u);
+}
+
+// sender side of the local-dedup backward: the owners' answers (u << 32 |
+// word) -> the words of the local unique children, Wu[u]
+__global__ void k_bks_wu(const u64* __restrict__ in, u64 n, uint32_t* Wu) {
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+    const u64 r = in[i];
+    Wu[r >> 32] = (uint32_t)r & 0x3FFu;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // host
 // ---------------------------------------------------------------------------
@@ -253,6 +316,22 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
         return fail(GM_EINVAL, "group shards must be ranks 0..n-1 on one stream");
   }
   if (s0->step_first || s0->step_stop) return fail(GM_EINVAL, "sharded bucketed solves run whole (no steps)");
+  // Which form a level's children take: the local-dedup form pays an extra
+  // host sync and a second dedup per level, won back where a shard expands
+  // many parents (toot 6x4 on 2 shards 500 -> 356 ms; toot 5x4 on 8 shards,
+  // ~0.5 M parents per level and shard, 64 -> 74 ms).  Default: local for a
+  // level whose largest shard expands >= kBksLocalMin parents (2 M: toot 5x4 on 4 and 8 shards ran 1-4 ms
+  // slower with 1 M); GM_F_BKS_LOCAL:
+  // every level.  Ranks may decide differently (the owners' side is the same
+  // in both forms; each rank reads its answers by its own choice).
+  constexpr u64 kBksLocalMin = 1ull << 21;
+  const bool local_all = (s0->flags & GM_F_BKS_LOCAL) != 0;
+  auto local_level = [&](int L) {
+    if (local_all) return true;
+    u64 mx = 0;
+    for (gm_solver* s : ss) mx = std::max<u64>(mx, s->lvh[(size_t)L].n);
+    return mx >= kBksLocalMin;
+  };
   hipStream_t st = s0->stream;
   auto t0 = std::chrono::steady_clock::now();
   hipEvent_t e0, e1, e2;
@@ -279,6 +358,7 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
     s->lvh[0].n = s->rank == (int)root_owner ? 1 : 0;
     HIPCHK(hipMemcpyAsync(s->bkK, &s->d.root, sizeof(u64), hipMemcpyHostToDevice, st));
     s->bks_sc.assign((size_t)T, std::vector<u64>((size_t)W, 0));
+    s->bksl.assign((size_t)T, gm_solver::BksLocal{});
     s->bks_rc.assign((size_t)T, std::vector<u64>((size_t)W, 0));
   }
   std::vector<std::vector<uint32_t>> keep;  // host arrays of async H2D copies
@@ -303,11 +383,238 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
       }
     return 0;
   };
+  // Local-dedup forward of level L (GM_F_BKS_LOCAL): per shard the one-GPU
+  // count-free expand of its own parents into coarse partitions, the fine
+  // pass (the local in-edges' parents, REpl), the LDS dedup (REcl) and the
+  // unique local children binned by owner (k_bks_ownbin, one MD5 each) into
+  // the send regions; then the size matrix and the all-to-all as the
+  // occurrence form.  Two host syncs for all shards, plus the size matrix.
+  auto forward_local = [&](int L, std::vector<u64>& meta_at) -> int {
+    struct Q {
+      std::vector<uint32_t> g;
+      uint32_t herr = 0, cap = 0;
+      u64 NR = 0, nblk = 0, chunk = 0;
+      bool active = false;
+    };
+    std::vector<Q> q(ss.size());
+    for (size_t gi = 0; gi < ss.size(); gi++) {
+      gm_solver* s = ss[gi];
+      std::vector<BkLevel>& lv = s->lvh;
+      BkLevel& P = lv[(size_t)L];
+      BkLevel& X = lv[(size_t)L + 1];
+      u64 meta_used = 0;
+      for (int i = 0; i <= L; i++) {
+        const BkLevel& Qv = lv[(size_t)i];
+        if (Qv.nbits) meta_used = std::max<u64>(meta_used, Qv.cst_off + 2 * ((1ull << Qv.nbits) + 1));
+        if (i < L && Qv.eout) meta_used = std::max<u64>(meta_used, Qv.rfo_off + ((Qv.n + (1ull << Qv.fb) - 1) >> Qv.fb) + 1);
+        const gm_solver::BksLocal& B = s->bksl[(size_t)i];
+        if (i < L && B.nbits) meta_used = std::max<u64>(meta_used, B.cst_off + 2 * ((1ull << B.nbits) + 1));
+      }
+      X = BkLevel{};
+      X.lb = P.lb + P.n;
+      X.rb = P.rb + P.ein;
+      P.eout = 0;
+      gm_solver::BksLocal& B = s->bksl[(size_t)L];
+      B = gm_solver::BksLocal{};
+      B.used = true;
+      for (int i = 0; i < L; i++) B.rb = std::max<u64>(B.rb, s->bksl[(size_t)i].rb + s->bksl[(size_t)i].ein);
+      Q& z = q[gi];
+      z.g.assign(2 * kBkC + 1, 0);
+      if (!bk_ranges(P.n, &P.pshift, &P.fb))
+        defer(fail(GM_ELIMIT, "level %d holds %llu positions: more than a bucketed level supports", L,
+                   (unsigned long long)P.n));
+      meta_at[gi] = meta_used;
+      if (!P.n || prc) continue;
+      z.nblk = std::min<u64>(kBkExpandBlocks, (P.n + kBkExpandThreads - 1) / kBkExpandThreads);
+      z.chunk = (P.n + z.nblk - 1) / z.nblk;
+      z.NR = (P.n + (1ull << P.fb) - 1) >> P.fb;
+      if (meta_used + z.NR + 1 > s->meta_cap) {
+        defer(fail(GM_ECORRUPT, "bucket tables exceed the scratch"));
+        continue;
+      }
+      P.rfo_off = (uint32_t)meta_used;
+      meta_used += z.NR + 1;
+      meta_at[gi] = meta_used;
+      z.active = true;
+      uint32_t* rfo = s->meta + P.rfo_off;
+      uint32_t ck_sh = 14;
+      while (ck_sh > 6 && (s->Emax / kBkC) < (1ull << ck_sh)) ck_sh--;
+      z.cap = (uint32_t)((s->Emax / kBkC) >> ck_sh << ck_sh);
+      const BkChunked ck{(char*)s->S1k, ck_sh};
+      HIPCHK(hipMemsetAsync(rfo, 0, (z.NR + 1) * 4, st));
+      HIPCHK(hipMemsetAsync(s->bkgc, 0, (2 * kBkC + 4) * 4, st));
+      const double avg =
+          (L > 0 && s->lvh[(size_t)L - 1].n) ? std::max(1.0, (double)s->lvh[(size_t)L - 1].eout / (double)s->lvh[(size_t)L - 1].n)
+                                              : 4.0;
+      bk_dispatch(s->d, [&](auto kind_) {
+        constexpr int K_ = decltype(kind_)::value;
+        hipLaunchKernelGGL((k_bk_expand<K_, true>), dim3(z.nblk), dim3(kBkExpandThreads), 0, st, s->d, s->bkK + P.lb,
+                           P.n, z.chunk, (const uint32_t*)nullptr, (const uint32_t*)nullptr, bk_ppr(avg), s->S1k, s->S1p,
+                           s->S1f, z.cap, s->bkgc, P.pshift, P.fb, s->bkgc + kBkC, rfo, s->bkgc + 2 * kBkC, s->st, ck);
+      });
+      hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, st, rfo, (uint32_t)z.NR + 1, rfo, s->bktotal + 1);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipMemcpyAsync(z.g.data(), s->bkgc, z.g.size() * 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(&z.herr, &s->st->err, 4, hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    std::vector<std::vector<uint32_t>> oc(ss.size(), std::vector<uint32_t>((size_t)W + 1, 0));
+    std::vector<u64> nu(ss.size(), 0);
+    std::vector<uint32_t> derr(ss.size(), 0);
+    for (size_t gi = 0; gi < ss.size(); gi++) {
+      gm_solver* s = ss[gi];
+      Q& z = q[gi];
+      if (!z.active) continue;
+      BkLevel& P = s->lvh[(size_t)L];
+      gm_solver::BksLocal& B = s->bksl[(size_t)L];
+      if (z.herr) {
+        defer(fail(GM_ECORRUPT, "shard %d level %d:%s", s->rank, L, err_text(z.herr).c_str()));
+        z.active = false;
+        continue;
+      }
+      if (z.g[2 * kBkC]) {  // a coarse partition past its provisioned share
+        defer(fail(GM_EFULL, "shard %d level %d: a partition of the local children exceeds its share", s->rank, L));
+        z.active = false;
+        continue;
+      }
+      keep.emplace_back(2 * (kBkC + 1));
+      std::vector<uint32_t>& hb = keep.back();
+      u64 E = 0, Ep = 0;
+      for (int j = 0; j < kBkC; j++) {
+        hb[(size_t)j] = (uint32_t)E;
+        hb[(size_t)kBkC + 1 + j] = (uint32_t)Ep;
+        E += z.g[(size_t)j];
+        Ep += z.g[(size_t)kBkC + j];
+      }
+      hb[(size_t)kBkC] = (uint32_t)E;
+      hb[(size_t)2 * kBkC + 1] = (uint32_t)Ep;
+      if (E != Ep) defer(fail(GM_ECORRUPT, "shard %d level %d: %llu children by partition, %llu by parent", s->rank, L,
+                              (unsigned long long)E, (unsigned long long)Ep));
+      if (E > s->Emax || B.rb + E > s->Ecap)
+        defer(fail(GM_EFULL, "shard %d level %d: %llu local children exceed the plan", s->rank, L, (unsigned long long)E));
+      if (prc || !E) {
+        z.active = false;
+        continue;
+      }
+      P.eout = E;
+      B.ein = E;
+      HIPCHK(hipMemcpyAsync(s->cbase, hb.data(), (kBkC + 1) * 4, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(s->pbase + (size_t)L * (kBkC + 1), hb.data() + kBkC + 1, (kBkC + 1) * 4,
+                            hipMemcpyHostToDevice, st));
+      uint32_t f = 0;
+      while (f < (uint32_t)kBkMaxFineBits && (E >> f) > (u64)kBkC * 4096) f++;
+      const uint32_t F = 1u << f, NB = (uint32_t)kBkC << f;
+      if (meta_at[gi] + 2 * (NB + 1) > s->meta_cap) {
+        defer(fail(GM_ECORRUPT, "bucket tables exceed the scratch"));
+        z.active = false;
+        continue;
+      }
+      B.nbits = 8 + f;
+      B.cst_off = (uint32_t)meta_at[gi];
+      meta_at[gi] += 2 * (NB + 1);
+      uint32_t* cst = s->meta + B.cst_off;
+      uint32_t* fo = cst + NB + 1;
+      uint32_t ck_sh = 14;
+      while (ck_sh > 6 && (s->Emax / kBkC) < (1ull << ck_sh)) ck_sh--;
+      const BkChunked ck{(char*)s->S1k, ck_sh};
+      hipLaunchKernelGGL(k_bk_fine, dim3(kBkC), dim3(kBkFineThreads), 0, st, (const u64*)s->S1k, (const uint32_t*)s->S1p,
+                         (const uint8_t*)s->S1f, (const uint32_t*)s->cbase, 8u - f, F, s->S2k, s->REpl + B.rb, fo,
+                         P.pshift, s->bkah + (size_t)L * kBkC * kBkC, z.cap, ck);
+      const int gd = (int)std::min<uint32_t>(NB, 512);
+      hipLaunchKernelGGL(k_bk_dedup, dim3(gd), dim3(kBkDedupThreads), 0, st, s->S2k, (const uint32_t*)fo, NB, s->S1k,
+                         s->ucnt, s->REcl + B.rb, s->st);
+      hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, st, s->ucnt, NB, cst, s->bktotal);
+      HIPCHK(hipMemsetAsync(s->bkgc, 0, (2 * kBkC + 4) * 4, st));
+      const uint32_t capd = (uint32_t)(s->Emax / (u64)W);
+      bk_dispatch(s->d, [&](auto kind_) {
+        constexpr int K_ = decltype(kind_)::value;
+        hipLaunchKernelGGL((k_bks_ownbin<K_>), dim3(kBkC), dim3(kBkStreamThreads), 0, st, s->d, (const u64*)s->S1k,
+                           (const uint32_t*)fo, (const uint32_t*)cst, NB, F, (uint32_t)W, (uint32_t)s->rank << 29, capd,
+                           s->bkgc, s->XSk, s->XSr, s->bkgc + 2 * kBkC);
+      });
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipMemcpyAsync(oc[gi].data(), s->bkgc, (size_t)W * 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(&oc[gi][(size_t)W], s->bkgc + 2 * kBkC, 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(&nu[gi], s->bktotal, 8, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(&derr[gi], &s->st->err, 4, hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    std::vector<std::vector<u64>> sendc(ss.size(), std::vector<u64>((size_t)W + 3, 0));
+    for (size_t gi = 0; gi < ss.size(); gi++) {
+      gm_solver* s = ss[gi];
+      Q& z = q[gi];
+      if (z.active) {
+        if (derr[gi]) {
+          const bool lim = derr[gi] & ERR_BUCKET_FULL;
+          defer(fail(lim ? GM_ELIMIT : GM_ECORRUPT, "shard %d level %d:%s", s->rank, L + 1, err_text(derr[gi]).c_str()));
+        } else if (oc[gi][(size_t)W]) {
+          defer(fail(GM_EFULL, "shard %d level %d: an owner's region of unique children overflowed", s->rank, L));
+        } else {
+          u64 t = 0;
+          for (int p = 0; p < W; p++) t += oc[gi][(size_t)p];
+          if (t != nu[gi]) defer(fail(GM_ECORRUPT, "shard %d level %d: %llu unique children, %llu binned", s->rank, L,
+                                      (unsigned long long)nu[gi], (unsigned long long)t));
+          s->bksl[(size_t)L].nu = nu[gi];
+          for (int p = 0; p < W; p++) sendc[gi][(size_t)p] = oc[gi][(size_t)p];
+        }
+      }
+      sendc[gi][(size_t)W] = (u64)(int64_t)prc;
+      sendc[gi][(size_t)W + 1] = s->Emax;
+      sendc[gi][(size_t)W + 2] = s->Ecap - std::min(s->Ecap, s->lvh[(size_t)L + 1].rb);
+    }
+    // the size matrix (with every rank's status and room), then the records
+    std::vector<u64> MA;
+    int rc = bks_allgather(ss, mode, st, sendc, MA);
+    if (rc) return rc;
+    if ((rc = status_of(MA, (size_t)W + 3))) return rc;
+    const size_t m3 = (size_t)W + 3;
+    for (int p = 0; p < W; p++) {
+      u64 in = 0, outn = 0;
+      for (int r = 0; r < W; r++) {
+        in += MA[(size_t)r * m3 + p];
+        outn += MA[(size_t)p * m3 + r];
+      }
+      const u64 emax = MA[(size_t)p * m3 + W + 1], room = MA[(size_t)p * m3 + W + 2];
+      if (in > emax || outn > emax || in > room)
+        return fail(GM_EFULL, "level %d: shard %d sends %llu / receives %llu records; its plan holds %llu per level and "
+                              "%llu more edges", L, p, (unsigned long long)outn, (unsigned long long)in,
+                    (unsigned long long)emax, (unsigned long long)room);
+    }
+    std::vector<BksA2A> ak(ss.size()), ar(ss.size());
+    for (size_t gi = 0; gi < ss.size(); gi++) {
+      gm_solver* s = ss[gi];
+      const int r = s->rank;
+      std::vector<u64>& sc = s->bks_sc[(size_t)L];
+      std::vector<u64>& rcv = s->bks_rc[(size_t)L];
+      for (int p = 0; p < W; p++) {
+        sc[(size_t)p] = MA[(size_t)r * m3 + p];
+        rcv[(size_t)p] = MA[(size_t)p * m3 + r];
+      }
+      std::vector<u64> so((size_t)W + 1, 0);
+      for (int p = 0; p < W; p++) so[(size_t)p] = (u64)p * (s->Emax / (u64)W);  // owner p's records at [p cap, ...)
+      const std::vector<u64> ro = bks_prefix(rcv);
+      s->lvh[(size_t)L + 1].ein = ro[(size_t)W];
+      ak[gi] = BksA2A{(char*)s->XSk, (char*)s->XRk, sc, std::vector<u64>(so.begin(), so.end() - 1), rcv,
+                      std::vector<u64>(ro.begin(), ro.end() - 1)};
+      ar[gi] = ak[gi];
+      ar[gi].sbuf = (char*)s->XSr;
+      ar[gi].rbuf = (char*)s->XRr;
+    }
+    if ((rc = bks_alltoall(ss, mode, st, ak, 8)) || (rc = bks_alltoall(ss, mode, st, ar, 4))) return rc;
+    return 0;
+  };
   // ---- forward ----
   for (int L = 0; L + 1 < T; L++) {
     // (a) per shard: children per owner and per parent range
+    std::vector<u64> meta_at(ss.size(), 0);
+    const bool local = local_level(L);
+    for (gm_solver* s : ss) s->bksl[(size_t)L].used = local;
+    if (local) {
+      int rc = forward_local(L, meta_at);
+      if (rc) return bail(rc);
+    } else {
     std::vector<std::vector<u64>> sendc(ss.size());
-    std::vector<u64> meta_at(ss.size(), 0), ptot_all(ss.size() * kBkC, 0);
+    std::vector<u64> ptot_all(ss.size() * kBkC, 0);
     std::vector<char> over(ss.size(), 0);  // the count-free expand already filled the send regions
     // every shard's launches first, then ONE host sync for all of them (and
     // a second only when some owner region overflowed)
@@ -329,6 +636,8 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
         const BkLevel& Q = lv[(size_t)i];
         if (Q.nbits) meta_used = std::max<u64>(meta_used, Q.cst_off + 2 * ((1ull << Q.nbits) + 1));
         if (i < L && Q.eout) meta_used = std::max<u64>(meta_used, Q.rfo_off + ((Q.n + (1ull << Q.fb) - 1) >> Q.fb) + 1);
+        const gm_solver::BksLocal& B = s->bksl[(size_t)i];  // an earlier level's local-dedup tables
+        if (i < L && B.nbits) meta_used = std::max<u64>(meta_used, B.cst_off + 2 * ((1ull << B.nbits) + 1));
       }
       X = BkLevel{};
       X.lb = P.lb + P.n;
@@ -358,8 +667,9 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
       uint32_t* rfo = s->meta + P.rfo_off;
       HIPCHK(hipMemsetAsync(rfo, 0, (q.NR + 1) * 4, st));
       HIPCHK(hipMemsetAsync(s->bkgc, 0, (2 * kBkC + 4) * 4, st));
-      const double avg =
-          (L > 0 && s->lvh[(size_t)L - 1].n) ? std::max(1.0, (double)P.ein / (double)s->lvh[(size_t)L - 1].n) : 4.0;
+      const double avg =  // children per parent of the level before (this shard's own)
+          (L > 0 && s->lvh[(size_t)L - 1].n) ? std::max(1.0, (double)s->lvh[(size_t)L - 1].eout / (double)s->lvh[(size_t)L - 1].n)
+                                              : 4.0;
       const uint32_t capd = (uint32_t)(s->Emax / (u64)W);
       bk_dispatch(s->d, [&](auto kind_) {
         constexpr int K_ = decltype(kind_)::value;
@@ -494,6 +804,7 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
       ar[g].rbuf = (char*)s->XRr;
     }
     if ((rc = bks_alltoall(ss, mode, st, ak, 8)) || (rc = bks_alltoall(ss, mode, st, ar, 4))) return bail(rc);
+    }  // !local
     // (d) per shard: the received occurrences -> level X
     std::vector<u64> ncnt(ss.size(), 0);
     for (size_t g = 0; g < ss.size(); g++) {
@@ -526,10 +837,12 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
       hipLaunchKernelGGL(k_bks_part, dim3(nblk), dim3(kBkStreamThreads), 0, st, (const u64*)s->XRk,
                          (const uint32_t*)s->XRr, E, chunk, (const uint32_t*)s->boff, (const uint32_t*)s->cbase, s->S1k,
                          s->S1p, s->S1f);
-      // refs ride in the parent slot: pshift 31 puts every record in parent range 0 of ah (unused here)
+      // refs ride in the parent slot: pshift 31 puts every record in parent range 0 of ah, whose counts
+      // nothing reads -- the last level's ah (no level expands from it), so the local-dedup form's
+      // parent-range counts of level L stay intact
       hipLaunchKernelGGL(k_bk_fine, dim3(kBkC), dim3(kBkFineThreads), 0, st, (const u64*)s->S1k, (const uint32_t*)s->S1p,
                          (const uint8_t*)s->S1f, (const uint32_t*)s->cbase, 8u - f, F, s->S2k, s->REp + X.rb, fo, 31u,
-                         s->bkah + (size_t)L * kBkC * kBkC, 0u, BkChunked{nullptr, 0});
+                         s->bkah + (size_t)(T - 1) * kBkC * kBkC, 0u, BkChunked{nullptr, 0});
       const int gd = (int)std::min<uint32_t>(NB, 512);
       hipLaunchKernelGGL(k_bk_dedup, dim3(gd), dim3(kBkDedupThreads), 0, st, s->S2k, (const uint32_t*)fo, NB, s->S1k,
                          s->ucnt, s->REc + X.rb, s->st);
@@ -616,7 +929,42 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
       bk_ranges(P.n, &P.pshift, &P.fb);  // checked in the forward
       const uint32_t NR = (uint32_t)((P.n + (1ull << P.fb) - 1) >> P.fb);
       const int gr = (int)std::min<uint32_t>(NR, 512);
-      if (edges && P.eout) {
+      if (edges && P.eout && s->bksl[(size_t)L].used) {
+        // the owners' words of this rank's unique children, then the one-GPU
+        // backward over its local in-edges
+        const gm_solver::BksLocal& B = s->bksl[(size_t)L];
+        const uint32_t* rfo = s->meta + P.rfo_off;
+        const uint32_t* pb = s->pbase + (size_t)L * (kBkC + 1);
+        uint32_t* Ap = (uint32_t*)s->S1k;
+        uint32_t* Wu = (uint32_t*)s->XSk;  // the answers it held have left in the exchange
+        u64 na = 0;
+        for (int p = 0; p < W; p++) na += s->bks_sc[(size_t)L][(size_t)p];
+        if (na != B.nu) {
+          (void)hipStreamSynchronize(st);
+          return bail(fail(GM_ECORRUPT, "shard %d level %d: %llu answers for %llu unique children", s->rank, L,
+                           (unsigned long long)na, (unsigned long long)B.nu));
+        }
+        if (na)
+          hipLaunchKernelGGL(k_bks_wu, dim3((uint32_t)std::min<u64>((na + 255) / 256, 4096)), dim3(256), 0, st,
+                             (const u64*)s->XRk, na, Wu);
+        const uint32_t NB = 1u << B.nbits, F = NB / kBkC;
+        const uint32_t* cst = s->meta + B.cst_off;
+        hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, st, s->bkah + (size_t)L * kBkC * kBkC, (uint32_t)kBkC,
+                           s->boff, s->tot);
+        hipLaunchKernelGGL(k_bk_answer, dim3(kBkC), dim3(kBkStreamThreads), 0, st, s->REpl + B.rb, s->REcl + B.rb,
+                           cst + NB + 1, cst, NB, F, P.pshift, s->boff, pb, (const uint32_t*)Wu, Ap, s->st);
+        const uint32_t Fp = 1u << (P.pshift - P.fb);
+        const uint32_t* ap = Ap;
+        if (Fp > 1) {
+          constexpr uint32_t K = kBkSplitK;
+          HIPCHK(hipMemcpyAsync(s->bkcur + kBkC, rfo, (size_t)NR * 4, hipMemcpyDeviceToDevice, st));
+          hipLaunchKernelGGL(k_bk_split, dim3(kBkC * K), dim3(kBkStreamThreads), 0, st, (const uint32_t*)Ap, pb,
+                             10u + P.fb, Fp, K, s->bkcur + kBkC, (uint32_t*)s->S2k);
+          ap = (uint32_t*)s->S2k;
+        }
+        BK_KIND_LAUNCH(k_bk_reduce, gr, kBkReduceThreads, s, s->d, s->bkK + P.lb, P.n, ap, rfo, P.fb, Fp - 1, NR,
+                       s->bkW + P.lb, s->st);
+      } else if (edges && P.eout) {
         const uint32_t* rfo = s->meta + P.rfo_off;
         const uint32_t* pb = s->pbase + (size_t)L * (kBkC + 1);
         uint32_t* Ap = (uint32_t*)s->S1k;

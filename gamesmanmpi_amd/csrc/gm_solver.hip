@@ -971,6 +971,14 @@ struct gm_solver {
   u64 *XSk = nullptr, *XRk = nullptr;  // md5-sharded bucketed levels: exchange buffers
   uint32_t *XSr = nullptr, *XRr = nullptr;
   std::vector<std::vector<u64>> bks_sc, bks_rc;  // per forward level: records sent to / received from each rank
+  uint32_t* REpl = nullptr;  // md5 shards, local-dedup form: in-edges of the rank's own parents' children
+  uint16_t* REcl = nullptr;
+  struct BksLocal {
+    u64 rb = 0, ein = 0, nu = 0;  // local in-edges [rb, rb + ein), unique local children
+    uint32_t nbits = 0, cst_off = 0;
+    bool used = false;  // this level's children went out in the local-dedup form
+  };
+  std::vector<BksLocal> bksl;  // per parent level
   u64* xdev = nullptr;  // RCCL all-gather staging of the sharded bucketed loop
   size_t xdev_n = 0;
   u64 Pcap = 0, Ecap = 0, Emax = 0;
@@ -1607,7 +1615,8 @@ static BkScratch bk_scratch(int T) {
   x.total = o; o += r(2 * 8);
   x.gc = o; o += r((2 * kBkC + 4) * 4);  // k_bk_expand<OVER>: partition cursors, parent-range totals, overflow flag
   const size_t NRmax = (size_t)1 << (29 - kBkRangeBits);
-  x.meta = o; o += r((size_t)T * (2 * (NBmax + 1) + NRmax + 1) * 4);  // per level: cst, fo, rfo
+  // per level: cst, fo, rfo (twice: md5 shards' local-dedup form keeps a second cst / fo per level)
+  x.meta = o; o += r((size_t)T * 2 * (2 * (NBmax + 1) + NRmax + 1) * 4);
   x.end = o;
   return x;
 }
@@ -1682,7 +1691,7 @@ int gm_plan_keyed_shard(int game, int rank, int world, uint64_t positions, uint3
   }
   const u64 P = positions + 64, E = bk_edges_bound(d, positions), Em = bk_emax_bound(E);
   if (Em >= 0xFFFFFFF0ull) return fail(GM_EINVAL, "a level of more than 2^32 edges: not supported");
-  const u64 bytes = 4 * P + 6 * E + 48 * Em;  // the one-GPU layout + the exchange buffers
+  const u64 bytes = 4 * P + 12 * E + 48 * Em + 64;  // the one-GPU layout + local in-edges + the exchange buffers
   if (max_table_bytes && bytes > max_table_bytes)
     return fail(GM_EFULL, "bucketed shard needs %llu bytes", (unsigned long long)bytes);
   out->mode = GM_MODE_BUCKETED;
@@ -1963,7 +1972,9 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
     s->Pcap = buf->level_capacity;
     s->Ecap = buf->table_slots;
     // a shard of a world > 1 job also holds the md5 exchange buffers (24 B per staged record)
-    s->Emax = std::min<u64>((buf->table_bytes - 4 * s->Pcap - 6 * s->Ecap) / (world > 1 ? 48 : 24), 0xFFFFFFF0ull);
+    // (world > 1 also: the local-dedup form's in-edges, another 6 B per edge)
+    s->Emax = std::min<u64>((buf->table_bytes - 4 * s->Pcap - (world > 1 ? 12 : 6) * s->Ecap) / (world > 1 ? 48 : 24),
+                            0xFFFFFFF0ull);
     s->bkK = (u64*)buf->levels;
     s->bkW = (uint32_t*)t;
     t += (4 * s->Pcap + 7) & ~7ull;
@@ -1971,6 +1982,12 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
     t += 4 * s->Ecap;
     s->REc = (uint16_t*)t;
     t += (2 * s->Ecap + 7) & ~7ull;
+    if (world > 1) {
+      s->REpl = (uint32_t*)t;
+      t += 4 * s->Ecap;
+      s->REcl = (uint16_t*)t;
+      t += (2 * s->Ecap + 7) & ~7ull;
+    }
     // staging: [S1k | S1p | S1f] (the count-free expand writes the first 13
     // Emax bytes of it in its chunked layout, BkChunked) then S2k
     s->S1k = (u64*)t;

@@ -372,7 +372,7 @@ def _pick(spec, world, layout):
     return "hashed"
 
 
-def group_keyed_solve(spec, world, device=None, layout="auto"):
+def group_keyed_solve(spec, world, device=None, layout="auto", flags=0):
     """Every md5 shard of a `world`-rank job in this process, on one GPU
     and one stream.  layout "auto": md5-sharded BUCKETED levels where they
     apply (the library's all-to-all level loop, gm_bucketed_shard.h), else
@@ -385,7 +385,7 @@ def group_keyed_solve(spec, world, device=None, layout="auto"):
     if _pick(spec, world, layout) == "bucketed":
         per = _shard_bound(spec, world, 0)
         shards = [Solver(spec, positions=per, device=dev, layout="bucketed",
-                         rank=g, world=world, stream=stream)
+                         rank=g, world=world, stream=stream, flags=flags)
                   for g in range(world)]
         arr = (ctypes.c_void_p * world)(*[s.handle.value for s in shards])
         r = _lib.gm_result()

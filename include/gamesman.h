@@ -141,6 +141,10 @@ typedef struct gm_buffers {
 #define GM_F_PLANE_NO_RUNS 8192u /* PLANES: one launch per narrow plane level /
                                   staged key instead of one-workgroup runs of
                                   them (A/B runs) */
+#define GM_F_BKS_LOCAL 16384u /* md5-sharded BUCKETED levels: dedup each rank's
+                                  children locally first and hash / send each
+                                  unique child once (A/B against hashing and
+                                  sending every child occurrence) */
 #define GM_F_GRAPH 256u      /* dense one-table full solves: capture the
                                   forward and backward launches as HIP graphs
                                   on the first solve, replay them after

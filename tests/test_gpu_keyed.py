@@ -80,8 +80,26 @@ def test_gpu_group_keyed_hashed_shards_still_golden(name, world, golden_summary)
     _check_golden_shards(name, r, shards, world, golden_summary)
 
 
+LOCAL = 16384  # _lib.GM_F_BKS_LOCAL
+
+
+@pytest.mark.parametrize("name,world", [("othello_4x4", 8), ("toot_4x3", 3), ("tic_tac_toe_np", 2), ("mttt", 5),
+                                        ("toot_3x3", 4)])
+def test_gpu_group_keyed_local_dedup_matches_golden(name, world, golden_summary):
+    """md5-sharded BUCKETED levels in the local-dedup form (GM_F_BKS_LOCAL:
+    each rank dedups its own children first and hashes / sends each unique
+    child once): every position on its md5 owner, words equal to the
+    reference-generated tables."""
+    from gamesmanmpi_amd.games import GameSpec
+    from gamesmanmpi_amd.keyed import group_keyed_solve
+    r, shards = group_keyed_solve(GameSpec(*CASES[name]), world, flags=LOCAL)
+    assert r.extra["layout"] == "bucketed"
+    _check_golden_shards(name, r, shards, world, golden_summary)
+
+
+@pytest.mark.parametrize("flags", [0, LOCAL])
 @pytest.mark.parametrize("world", [2, 4, 7])
-def test_gpu_bucketed_shards_toot_5x4_checksum(world):
+def test_gpu_bucketed_shards_toot_5x4_checksum(world, flags):
     """toot 5x4 (70,184,763 positions) on 2 / 4 / 7 md5 BUCKETED shards: the
     shards' fingerprints (each over the positions it owns) add up to the CPU
     restatement's golden (oracle/oracle_mt.c; beyond 4x4 no reference
@@ -93,7 +111,7 @@ def test_gpu_bucketed_shards_toot_5x4_checksum(world):
     from gamesmanmpi_amd.games import GameSpec
     from gamesmanmpi_amd.keyed import group_keyed_solve
     e = json.load(open(os.path.join(GOLDEN, "checksums.json")))["toot_5x4"]
-    r, shards = group_keyed_solve(GameSpec(e["game"], e["params"]), world)
+    r, shards = group_keyed_solve(GameSpec(e["game"], e["params"]), world, flags=flags)
     assert r.extra["layout"] == "bucketed"
     assert (r.positions, r.edges, r.primitives, r.root_line) == (e["positions"], e["edges"], e["primitives"],
                                                                   e["root_line"])

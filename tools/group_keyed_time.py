@@ -2,7 +2,8 @@
 """Wall / device time of an md5-sharded keyed group solve (every shard of a
 W-rank job in this process on one GPU; BUCKETED shards where they apply),
 the same shards re-solved REPS times, next to the one-GPU solve:
-    python tools/group_keyed_time.py GAME PARAMS WORLD [REPS]"""
+    python tools/group_keyed_time.py GAME PARAMS WORLD [REPS] [FLAGS]
+(FLAGS 16384 = GM_F_BKS_LOCAL: local dedup before the owners)"""
 import ctypes
 import json
 import sys
@@ -19,6 +20,7 @@ def main():
     from gamesmanmpi_amd.solver import Solver
     game, params, world = sys.argv[1], sys.argv[2], int(sys.argv[3])
     reps = int(sys.argv[4]) if len(sys.argv) > 4 else 3
+    flags = int(sys.argv[5]) if len(sys.argv) > 5 else 0
     spec = GameSpec(game, params)
     if world == 1:
         s = Solver(spec)
@@ -32,7 +34,7 @@ def main():
                                   "root": r.root_line, "wall_ms": wall, "ms_forward": r.ms_forward,
                                   "ms_backward": r.ms_backward}), flush=True)
         return
-    r, shards = group_keyed_solve(spec, world)
+    r, shards = group_keyed_solve(spec, world, flags=flags)
     arr = (ctypes.c_void_p * world)(*[s.handle.value for s in shards])
     L = _lib.load()
     for i in range(reps):
@@ -44,7 +46,7 @@ def main():
         torch.cuda.synchronize()
         wall = (time.perf_counter() - t0) * 1e3
         rr = shards[0]._result(res)
-        print(json.dumps({"world": world, "layout": rr.extra["layout"], "positions": rr.positions,
+        print(json.dumps({"world": world, "flags": flags, "layout": rr.extra["layout"], "positions": rr.positions,
                           "root": rr.root_line, "wall_ms": wall, "ms_forward": rr.ms_forward,
                           "ms_backward": rr.ms_backward}), flush=True)
 
