@@ -439,9 +439,11 @@ def main():
                    "positions_per_gpu": P // world, "edges_per_gpu": E // world,
                    "levels": r.levels, "root": r.root_line, "root_checked_against": root_src,
                    "layout": layout,
-                   "parallelism": (("round-robin top-heap blocks x%d, %s halo exchange" %
-                                    (world, "host-staged (gloo, all ranks on one GPU: rehearsal, "
-                                            "not a performance figure)" if host else "RCCL"))
+                   "parallelism": ((("staged pipeline: one block of the top heap per rank x%d, halo rows "
+                                     "streamed to the next rank" if layout == "planes" else
+                                     "round-robin top-heap blocks x%d, one halo exchange per level") % world
+                                    + ", %s" % ("host-staged (gloo, all ranks on one GPU: rehearsal, not a "
+                                                "performance figure)" if host else "RCCL"))
                                    if world > 1 else "1 GPU")},
         "roofline": roof,
         "phase_ms": {"forward": r.ms_forward, "backward": r.ms_backward,
