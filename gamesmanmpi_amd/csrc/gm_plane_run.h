@@ -573,14 +573,19 @@ static void plane_run_w(gm_solver* s, const PlaneRun& run) {
 // (k_plane_run, one workgroup), a wider one flushes the run and gets its own
 // grid-wide launch.  flush() before anything that must see the groups so
 // far done on the stream (an event, an exchange).
+#ifndef GM_PLANE_RUN_PASSES
+#define GM_PLANE_RUN_PASSES 1  // (A/B builds, tools/ab_runs.sh: 1 pass 1.607 ms, 2: 1.631, 3: 1.657, 4: 1.697)
+#endif
 struct PlaneBatcher {
   gm_solver* s;
   PlaneRun run{};
   u64 narrow;
   u64 launches = 0;  // grid launches + runs issued
   explicit PlaneBatcher(gm_solver* sv) : s(sv) {
-    // two passes of the run's waves: one CU beats a launch up to about there
-    narrow = (s->flags & GM_F_PLANE_NO_RUNS) ? 0 : (u64)(kPlaneRunThreads / 64) * (plane_x1(s) ? 2 : 4) * 2;
+    // one pass of the run's waves: one CU beats a grid launch up to about there
+    narrow = (s->flags & GM_F_PLANE_NO_RUNS)
+                 ? 0
+                 : (u64)((double)(kPlaneRunThreads / 64) * (plane_x1(s) ? 2 : 4) * GM_PLANE_RUN_PASSES);
     run.n = 0;
   }
   void flush() {
