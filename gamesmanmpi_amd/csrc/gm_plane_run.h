@@ -639,8 +639,8 @@ static void plane_no_dispatch(uint32_t no, F&& f) {
   }
 }
 static void plane_reach_launch(gm_solver* s) {
-  const u64 nw = (u64)s->pg.nplanes * 32u;
-  const int grid = (int)std::min<u64>((nw + 255) / 256, (u64)std::min(s->grid, kCountSlots));
+  const u64 nq = (u64)s->pg.nplanes * 8u;  // one thread per four row words
+  const int grid = (int)std::max<u64>(1, std::min<u64>((nq + 255) / 256, (u64)std::min(s->grid, kCountSlots)));
   plane_no_dispatch(s->pg.no, [&](auto NO) {
     hipLaunchKernelGGL((k_plane_reach<decltype(NO)::value>), dim3(grid), dim3(256), 0, s->stream, s->pbits, s->pg,
                        s->bcount, s->st);
