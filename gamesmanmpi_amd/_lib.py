@@ -115,7 +115,7 @@ EXPORTS = (
     "gm_encode_batch", "gm_decode_batch", "gm_str_utf8", "gm_host_expand", "gm_host_level", "gm_symmetry", "gm_abi_sizes", "gm_plan", "gm_solver_create",
     "gm_solver_solve", "gm_solver_query", "gm_solver_positions",
     "gm_solver_checksum",
-    "gm_solver_destroy", "gm_solve", "gm_query", "gm_release", "gm_owner", "gm_owner_host",
+    "gm_solver_destroy", "gm_solve", "gm_plan_multi", "gm_query", "gm_release", "gm_owner", "gm_owner_host",
     "gm_plan_shard", "gm_plan_keyed_shard", "gm_solver_create_shard", "gm_comm_unique_id",
     "gm_solver_comm_init", "gm_solve_group", "gm_solver_set_flags", "gm_solver_set_steps",
     "gm_shard_info", "gm_solver_set_transport", "gm_shard_halo_sigs", "gm_plane_halo_plan",
@@ -169,6 +169,7 @@ def load():
         "gm_solver_checksum": [c.c_void_p, c.c_void_p],
         "gm_solve": [c.c_int, c.c_uint64, c.c_int, P(gm_buffers),
                      P(gm_result)],
+        "gm_plan_multi": [c.c_int, c.c_int, c.c_uint64, c.c_uint32, c.c_uint64, P(gm_plan_t)],
         "gm_query": [c.c_int, c.c_void_p, c.c_size_t, c.c_void_p],
         "gm_release": [c.c_int],
         "gm_owner": [c.c_int, c.c_void_p, c.c_uint64, c.c_int, c.c_void_p,

@@ -153,12 +153,16 @@ def save(solver, directory, step):
     os.makedirs(tmp)
     for name, t in zip(_NAMES, solver.buffers):
         _stream_out(t, os.path.join(tmp, name + ".bin"), torch)
+    plan = _plan_dict(solver)
     meta = {"format": FORMAT, "game": solver.spec.name,
             "params": solver.spec.params, "layout": solver.layout,
+            # what "auto" resolved to in this build: a later build may
+            # resolve "auto" differently, and restore() falls back to this
+            "layout_resolved": _lib.MODE_NAMES[plan["mode"]],
             "positions_hint": solver.positions_hint,
             "max_table_bytes": solver.max_table_bytes,
             "flags": solver.flags,
-            "plan": _plan_dict(solver), "step": int(step),
+            "plan": plan, "step": int(step),
             "steps": solver.steps}
     with open(os.path.join(tmp, "meta.json"), "w") as fh:
         json.dump(meta, fh, indent=1)
@@ -200,10 +204,18 @@ def restore(directory, device=None):
         raise FileNotFoundError("no checkpoint in %s (or %s.old)" % (directory, directory.rstrip("/")))
     meta = read_meta(src)
     spec = GameSpec(meta["game"], meta["params"])
-    solver = Solver(spec, positions=meta["positions_hint"], device=device,
-                    layout=meta["layout"],
-                    max_table_bytes=meta["max_table_bytes"],
-                    flags=meta.get("flags", 0))
+
+    def make(layout):
+        return Solver(spec, positions=meta["positions_hint"], device=device,
+                      layout=layout, max_table_bytes=meta["max_table_bytes"],
+                      flags=meta.get("flags", 0))
+    solver = make(meta["layout"])
+    if _plan_dict(solver) != meta["plan"] and meta["layout"] == "auto":
+        # "auto" resolves differently in this build: rebuild the layout the
+        # checkpoint was planned with (older checkpoints: from its plan mode)
+        resolved = meta.get("layout_resolved") or _lib.MODE_NAMES.get(int(meta["plan"]["mode"]))
+        if resolved:
+            solver = make(resolved)
     if _plan_dict(solver) != meta["plan"]:
         raise ValueError("checkpoint plan %r does not match this build's %r"
                          % (meta["plan"], _plan_dict(solver)))

@@ -79,6 +79,8 @@ __global__ __launch_bounds__(kBkStreamThreads) void k_bks_part(const u64* __rest
 // k_bk_answer); one answer per in-edge, (parent index << 32 | child's word),
 // to the parent's rank (ref >> 29), runs reserved on cur[rank]
 constexpr int kBksAnswerCap = 4096;
+// local-dedup refs: rank << 29 | unique local child index
+constexpr uint32_t kBksRefLimit = 1u << 29;
 __global__ __launch_bounds__(kBkStreamThreads) void k_bks_answer(const uint32_t* __restrict__ REp,
                                                                 const uint16_t* __restrict__ REc,
                                                                 const uint32_t* __restrict__ fo,
@@ -179,20 +181,21 @@ __global__ __launch_bounds__(kBkStreamThreads) void k_bks_ownbin(Desc d, const u
         else hi = m;
       }
       const u64 key = U[lfo[lo] + (i - lcs[lo])];
-      bk_stage_put_few(S, key, pref | i, owner_k<KIND>(d, key, W));
+      if (i >= kBksRefLimit) atomicOr(&S.stop, 2u);  // the index would spill into the rank bits (the host refuses first)
+      bk_stage_put_few(S, key, pref | (i & (kBksRefLimit - 1u)), owner_k<KIND>(d, key, W));
     }
     __syncthreads();
     if (threadIdx.x < W) {
       const uint32_t v = S.binc[threadIdx.x];
       if (v) {
         const uint32_t p = atomicAdd(&cur[threadIdx.x], v);
-        if (p + v > cap) S.stop = 1;
+        if (p + v > cap) atomicOr(&S.stop, 1u);
         at[threadIdx.x] = threadIdx.x * cap + p;
       }
     }
     bk_stage_flush(S, at, outk, outr);
   }
-  if (threadIdx.x == 0 && S.stop) atomicOr(oflag, 1u);
+  if (threadIdx.x == 0 && S.stop) atomicOr(oflag, S.stop);
 }
 
 // sender side of the local-dedup backward: the owners' answers (u << 32 |
@@ -209,7 +212,8 @@ __global__ void k_bks_wu(const u64* __restrict__ in, u64 n, uint32_t* Wu) {
 // ---------------------------------------------------------------------------
 // One all-to-all of eb-byte elements: shard r sends sbuf[so[p] ..) (sc[p]
 // elements) to p and receives rbuf[ro[p] ..) (rc[p]) from p.  mode 1 RCCL,
-// 2 in-process copies (every shard in ss), 3 host-staged transport.
+// 2 in-process copies (every shard in ss), 3 host-staged transport, 4 the
+// rehearsal of mode 1 (every shard in ss, each on its own stream).
 struct BksA2A {
   char* sbuf;
   char* rbuf;
@@ -217,6 +221,40 @@ struct BksA2A {
 };
 static int bks_alltoall(std::vector<gm_solver*>& ss, int mode, hipStream_t st, std::vector<BksA2A>& a, u64 eb) {
   const int W = ss[0]->world;
+  if (mode == 4) {
+    // RCCL's grouped send / receive on each rank's own stream (mode 1),
+    // rehearsed with the shards on streams of their own: every sender's
+    // records are final on its stream (ready[r]); each receiver's stream
+    // waits for every sender and copies its incoming segments; every
+    // stream then waits for every receiver (done[p]) -- a send completes
+    // only with the transfer, so no rank reuses its buffers early
+    for (gm_solver* s : ss)
+      while (s->pev.size() < 2) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        s->pev.push_back(e);
+      }
+    for (gm_solver* s : ss) HIPCHK(hipEventRecord(s->pev[0], s->stream));
+    for (int p = 0; p < W; p++) {
+      gm_solver* t = ss[(size_t)p];
+      for (int r = 0; r < W; r++) {
+        const u64 n = a[(size_t)r].sc[(size_t)p];
+        if (n != a[(size_t)p].rc[(size_t)r])
+          return fail(GM_ECORRUPT, "exchange: shard %d sends %llu to %d, which expects %llu", r, (unsigned long long)n,
+                      p, (unsigned long long)a[(size_t)p].rc[(size_t)r]);
+        if (!n) continue;
+        if (r != p) HIPCHK(hipStreamWaitEvent(t->stream, ss[(size_t)r]->pev[0], 0));
+        HIPCHK(hipMemcpyAsync(a[(size_t)p].rbuf + a[(size_t)p].ro[(size_t)r] * eb,
+                              a[(size_t)r].sbuf + a[(size_t)r].so[(size_t)p] * eb, n * eb, hipMemcpyDeviceToDevice,
+                              t->stream));
+      }
+      HIPCHK(hipEventRecord(t->pev[1], t->stream));
+    }
+    for (gm_solver* s : ss)
+      for (gm_solver* t : ss)
+        if (t != s) HIPCHK(hipStreamWaitEvent(s->stream, t->pev[1], 0));
+    return 0;
+  }
   if (mode == 2) {
     for (int r = 0; r < W; r++)
       for (int p = 0; p < W; p++) {
@@ -271,7 +309,7 @@ static int bks_allgather(std::vector<gm_solver*>& ss, int mode, hipStream_t st, 
   const int W = ss[0]->world;
   const size_t m = mine[0].size();
   out.assign((size_t)W * m, 0);
-  if (mode == 2) {
+  if (mode == 2 || mode == 4) {
     for (int r = 0; r < W; r++) std::copy(mine[(size_t)r].begin(), mine[(size_t)r].end(), out.begin() + (size_t)r * m);
     return 0;
   }
@@ -307,13 +345,21 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
   gm_solver* s0 = ss[0];
   const Desc& d = s0->d;
   const int T = d.max_levels, W = s0->world;
-  const int mode = ss.size() != 1 ? 2 : s0->xfer ? 3 : 1;
+  // mode 2: a group on one stream; mode 4: a group whose shards run on
+  // streams of their own -- mode 1's per-rank stream order, the all-to-alls
+  // as device copies between the shards' streams (bks_alltoall)
+  const bool own_streams = ss.size() > 1 && ss[1]->stream != s0->stream;
+  const int mode = ss.size() != 1 ? (own_streams ? 4 : 2) : s0->xfer ? 3 : 1;
   if (mode == 1 && !s0->comm) return fail(GM_EINVAL, "shard %d/%d has no communicator (gm_solver_comm_init)", s0->rank, W);
-  if (mode == 2) {
+  if (mode == 2 || mode == 4) {
     if ((int)ss.size() != W) return fail(GM_EINVAL, "group solve needs all %d shards", W);
-    for (size_t g = 0; g < ss.size(); g++)
-      if (ss[g]->rank != (int)g || ss[g]->stream != s0->stream || ss[g]->mode != GM_MODE_BUCKETED)
-        return fail(GM_EINVAL, "group shards must be ranks 0..n-1 on one stream");
+    for (size_t g = 0; g < ss.size(); g++) {
+      if (ss[g]->rank != (int)g || ss[g]->mode != GM_MODE_BUCKETED)
+        return fail(GM_EINVAL, "group shards must be ranks 0..n-1");
+      for (size_t h = 0; h < g; h++)
+        if ((mode == 2) != (ss[g]->stream == ss[h]->stream))
+          return fail(GM_EINVAL, "group shards share one stream, or (the RCCL rehearsal) each has its own");
+    }
   }
   if (s0->step_first || s0->step_stop) return fail(GM_EINVAL, "sharded bucketed solves run whole (no steps)");
   // Which form a level's children take: the local-dedup form pays an extra
@@ -326,13 +372,20 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
   // in both forms; each rank reads its answers by its own choice).
   constexpr u64 kBksLocalMin = 1ull << 21;
   const bool local_all = (s0->flags & GM_F_BKS_LOCAL) != 0;
-  auto local_level = [&](int L) {
-    if (local_all) return true;
-    u64 mx = 0;
-    for (gm_solver* s : ss) mx = std::max<u64>(mx, s->lvh[(size_t)L].n);
-    return mx >= kBksLocalMin;
-  };
+  // lmax[L]: the largest shard's level L, known to EVERY rank (all-gathered
+  // with the level sizes in modes 1 / 3), so all ranks pick the same form --
+  // the one the in-process group, which the tests run, picks
+  std::vector<u64> lmax((size_t)T, 0);
+  lmax[0] = 1;
+  auto local_level = [&](int L) { return local_all || lmax[(size_t)L] >= kBksLocalMin; };
   hipStream_t st = s0->stream;
+  auto sync_all = [&]() -> hipError_t {  // every shard's stream (one stream in modes 1-3)
+    for (gm_solver* s : ss) {
+      const hipError_t e = hipStreamSynchronize(s->stream);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  };
   auto t0 = std::chrono::steady_clock::now();
   hipEvent_t e0, e1, e2;
   HIPCHK(hipEventCreate(&e0));
@@ -344,19 +397,20 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
     (void)hipEventDestroy(e2);
   };
   auto bail = [&](int code) {
-    (void)hipStreamSynchronize(st);
+    (void)sync_all();
     done_events();
     return code;
   };
   HIPCHK(hipEventRecord(e0, st));
+  if (mode == 4) HIPCHK(sync_all());  // the shards' streams start after e0 (host order)
   // the root's owner seeds level 0
   const uint32_t root_owner = owner_host(d, d.root, (uint32_t)W);
   for (gm_solver* s : ss) {
-    HIPCHK(hipMemsetAsync(s->st, 0, devstate_bytes(T), st));
-    HIPCHK(hipMemsetAsync(s->bkL, 0, sizeof(BkLevel) * (size_t)T, st));
+    HIPCHK(hipMemsetAsync(s->st, 0, devstate_bytes(T), s->stream));
+    HIPCHK(hipMemsetAsync(s->bkL, 0, sizeof(BkLevel) * (size_t)T, s->stream));
     s->lvh.assign((size_t)T, BkLevel{});
     s->lvh[0].n = s->rank == (int)root_owner ? 1 : 0;
-    HIPCHK(hipMemcpyAsync(s->bkK, &s->d.root, sizeof(u64), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(s->bkK, &s->d.root, sizeof(u64), hipMemcpyHostToDevice, s->stream));
     s->bks_sc.assign((size_t)T, std::vector<u64>((size_t)W, 0));
     s->bksl.assign((size_t)T, gm_solver::BksLocal{});
     s->bks_rc.assign((size_t)T, std::vector<u64>((size_t)W, 0));
@@ -367,6 +421,7 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
   // every rank returns together.
   int prc = 0;
   std::string perr;
+  u64 host_err = 0;  // error bits found on the host (sent with the final totals)
   auto defer = [&](int code) {
     if (!prc) {
       prc = code;
@@ -441,23 +496,23 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
       while (ck_sh > 6 && (s->Emax / kBkC) < (1ull << ck_sh)) ck_sh--;
       z.cap = (uint32_t)((s->Emax / kBkC) >> ck_sh << ck_sh);
       const BkChunked ck{(char*)s->S1k, ck_sh};
-      HIPCHK(hipMemsetAsync(rfo, 0, (z.NR + 1) * 4, st));
-      HIPCHK(hipMemsetAsync(s->bkgc, 0, (2 * kBkC + 4) * 4, st));
+      HIPCHK(hipMemsetAsync(rfo, 0, (z.NR + 1) * 4, s->stream));
+      HIPCHK(hipMemsetAsync(s->bkgc, 0, (2 * kBkC + 4) * 4, s->stream));
       const double avg =
           (L > 0 && s->lvh[(size_t)L - 1].n) ? std::max(1.0, (double)s->lvh[(size_t)L - 1].eout / (double)s->lvh[(size_t)L - 1].n)
                                               : 4.0;
       bk_dispatch(s->d, [&](auto kind_) {
         constexpr int K_ = decltype(kind_)::value;
-        hipLaunchKernelGGL((k_bk_expand<K_, true>), dim3(z.nblk), dim3(kBkExpandThreads), 0, st, s->d, s->bkK + P.lb,
+        hipLaunchKernelGGL((k_bk_expand<K_, true>), dim3(z.nblk), dim3(kBkExpandThreads), 0, s->stream, s->d, s->bkK + P.lb,
                            P.n, z.chunk, (const uint32_t*)nullptr, (const uint32_t*)nullptr, bk_ppr(avg), s->S1k, s->S1p,
                            s->S1f, z.cap, s->bkgc, P.pshift, P.fb, s->bkgc + kBkC, rfo, s->bkgc + 2 * kBkC, s->st, ck);
       });
-      hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, st, rfo, (uint32_t)z.NR + 1, rfo, s->bktotal + 1);
+      hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, s->stream, rfo, (uint32_t)z.NR + 1, rfo, s->bktotal + 1);
       HIPCHK(hipGetLastError());
-      HIPCHK(hipMemcpyAsync(z.g.data(), s->bkgc, z.g.size() * 4, hipMemcpyDeviceToHost, st));
-      HIPCHK(hipMemcpyAsync(&z.herr, &s->st->err, 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(z.g.data(), s->bkgc, z.g.size() * 4, hipMemcpyDeviceToHost, s->stream));
+      HIPCHK(hipMemcpyAsync(&z.herr, &s->st->err, 4, hipMemcpyDeviceToHost, s->stream));
     }
-    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(sync_all());
     std::vector<std::vector<uint32_t>> oc(ss.size(), std::vector<uint32_t>((size_t)W + 1, 0));
     std::vector<u64> nu(ss.size(), 0);
     std::vector<uint32_t> derr(ss.size(), 0);
@@ -492,15 +547,20 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
                               (unsigned long long)E, (unsigned long long)Ep));
       if (E > s->Emax || B.rb + E > s->Ecap)
         defer(fail(GM_EFULL, "shard %d level %d: %llu local children exceed the plan", s->rank, L, (unsigned long long)E));
+      // the refs sent to the owners pack rank << 29 | unique index, and the
+      // unique children are at most the E occurrences
+      if (E >= kBksRefLimit)
+        defer(fail(GM_ELIMIT, "shard %d level %d: %llu local children; the local-dedup form indexes fewer than 2^29",
+                   s->rank, L, (unsigned long long)E));
       if (prc || !E) {
         z.active = false;
         continue;
       }
       P.eout = E;
       B.ein = E;
-      HIPCHK(hipMemcpyAsync(s->cbase, hb.data(), (kBkC + 1) * 4, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(s->cbase, hb.data(), (kBkC + 1) * 4, hipMemcpyHostToDevice, s->stream));
       HIPCHK(hipMemcpyAsync(s->pbase + (size_t)L * (kBkC + 1), hb.data() + kBkC + 1, (kBkC + 1) * 4,
-                            hipMemcpyHostToDevice, st));
+                            hipMemcpyHostToDevice, s->stream));
       uint32_t f = 0;
       while (f < (uint32_t)kBkMaxFineBits && (E >> f) > (u64)kBkC * 4096) f++;
       const uint32_t F = 1u << f, NB = (uint32_t)kBkC << f;
@@ -517,28 +577,28 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
       uint32_t ck_sh = 14;
       while (ck_sh > 6 && (s->Emax / kBkC) < (1ull << ck_sh)) ck_sh--;
       const BkChunked ck{(char*)s->S1k, ck_sh};
-      hipLaunchKernelGGL(k_bk_fine, dim3(kBkC), dim3(kBkFineThreads), 0, st, (const u64*)s->S1k, (const uint32_t*)s->S1p,
+      hipLaunchKernelGGL(k_bk_fine, dim3(kBkC), dim3(kBkFineThreads), 0, s->stream, (const u64*)s->S1k, (const uint32_t*)s->S1p,
                          (const uint8_t*)s->S1f, (const uint32_t*)s->cbase, 8u - f, F, s->S2k, s->REpl + B.rb, fo,
                          P.pshift, s->bkah + (size_t)L * kBkC * kBkC, z.cap, ck);
       const int gd = (int)std::min<uint32_t>(NB, 512);
-      hipLaunchKernelGGL(k_bk_dedup, dim3(gd), dim3(kBkDedupThreads), 0, st, s->S2k, (const uint32_t*)fo, NB, s->S1k,
+      hipLaunchKernelGGL(k_bk_dedup, dim3(gd), dim3(kBkDedupThreads), 0, s->stream, s->S2k, (const uint32_t*)fo, NB, s->S1k,
                          s->ucnt, s->REcl + B.rb, s->st);
-      hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, st, s->ucnt, NB, cst, s->bktotal);
-      HIPCHK(hipMemsetAsync(s->bkgc, 0, (2 * kBkC + 4) * 4, st));
+      hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, s->stream, s->ucnt, NB, cst, s->bktotal);
+      HIPCHK(hipMemsetAsync(s->bkgc, 0, (2 * kBkC + 4) * 4, s->stream));
       const uint32_t capd = (uint32_t)(s->Emax / (u64)W);
       bk_dispatch(s->d, [&](auto kind_) {
         constexpr int K_ = decltype(kind_)::value;
-        hipLaunchKernelGGL((k_bks_ownbin<K_>), dim3(kBkC), dim3(kBkStreamThreads), 0, st, s->d, (const u64*)s->S1k,
+        hipLaunchKernelGGL((k_bks_ownbin<K_>), dim3(kBkC), dim3(kBkStreamThreads), 0, s->stream, s->d, (const u64*)s->S1k,
                            (const uint32_t*)fo, (const uint32_t*)cst, NB, F, (uint32_t)W, (uint32_t)s->rank << 29, capd,
                            s->bkgc, s->XSk, s->XSr, s->bkgc + 2 * kBkC);
       });
       HIPCHK(hipGetLastError());
-      HIPCHK(hipMemcpyAsync(oc[gi].data(), s->bkgc, (size_t)W * 4, hipMemcpyDeviceToHost, st));
-      HIPCHK(hipMemcpyAsync(&oc[gi][(size_t)W], s->bkgc + 2 * kBkC, 4, hipMemcpyDeviceToHost, st));
-      HIPCHK(hipMemcpyAsync(&nu[gi], s->bktotal, 8, hipMemcpyDeviceToHost, st));
-      HIPCHK(hipMemcpyAsync(&derr[gi], &s->st->err, 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(oc[gi].data(), s->bkgc, (size_t)W * 4, hipMemcpyDeviceToHost, s->stream));
+      HIPCHK(hipMemcpyAsync(&oc[gi][(size_t)W], s->bkgc + 2 * kBkC, 4, hipMemcpyDeviceToHost, s->stream));
+      HIPCHK(hipMemcpyAsync(&nu[gi], s->bktotal, 8, hipMemcpyDeviceToHost, s->stream));
+      HIPCHK(hipMemcpyAsync(&derr[gi], &s->st->err, 4, hipMemcpyDeviceToHost, s->stream));
     }
-    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(sync_all());
     std::vector<std::vector<u64>> sendc(ss.size(), std::vector<u64>((size_t)W + 3, 0));
     for (size_t gi = 0; gi < ss.size(); gi++) {
       gm_solver* s = ss[gi];
@@ -547,6 +607,8 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
         if (derr[gi]) {
           const bool lim = derr[gi] & ERR_BUCKET_FULL;
           defer(fail(lim ? GM_ELIMIT : GM_ECORRUPT, "shard %d level %d:%s", s->rank, L + 1, err_text(derr[gi]).c_str()));
+        } else if (oc[gi][(size_t)W] & 2u) {
+          defer(fail(GM_ELIMIT, "shard %d level %d: a unique child index reached 2^29", s->rank, L));
         } else if (oc[gi][(size_t)W]) {
           defer(fail(GM_EFULL, "shard %d level %d: an owner's region of unique children overflowed", s->rank, L));
         } else {
@@ -665,25 +727,25 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
       // regions of the send buffer (one MD5 per child); an owner past its
       // region (Emax / W records) -> count, then the exact form in (c).
       uint32_t* rfo = s->meta + P.rfo_off;
-      HIPCHK(hipMemsetAsync(rfo, 0, (q.NR + 1) * 4, st));
-      HIPCHK(hipMemsetAsync(s->bkgc, 0, (2 * kBkC + 4) * 4, st));
+      HIPCHK(hipMemsetAsync(rfo, 0, (q.NR + 1) * 4, s->stream));
+      HIPCHK(hipMemsetAsync(s->bkgc, 0, (2 * kBkC + 4) * 4, s->stream));
       const double avg =  // children per parent of the level before (this shard's own)
           (L > 0 && s->lvh[(size_t)L - 1].n) ? std::max(1.0, (double)s->lvh[(size_t)L - 1].eout / (double)s->lvh[(size_t)L - 1].n)
                                               : 4.0;
       const uint32_t capd = (uint32_t)(s->Emax / (u64)W);
       bk_dispatch(s->d, [&](auto kind_) {
         constexpr int K_ = decltype(kind_)::value;
-        hipLaunchKernelGGL((k_bk_expand<K_, true, true>), dim3(q.nblk), dim3(kBkExpandThreads), 0, st, s->d,
+        hipLaunchKernelGGL((k_bk_expand<K_, true, true>), dim3(q.nblk), dim3(kBkExpandThreads), 0, s->stream, s->d,
                            s->bkK + P.lb, P.n, q.chunk, (const uint32_t*)nullptr, (const uint32_t*)nullptr, bk_ppr(avg),
                            s->XSk, s->XSr, (uint8_t*)nullptr, capd, s->bkgc, P.pshift, P.fb, s->bkgc + kBkC, rfo,
                            s->bkgc + 2 * kBkC, s->st, BkChunked{nullptr, 0}, (uint32_t)W, (uint32_t)s->rank << 29);
       });
-      hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, st, rfo, q.NR + 1, rfo, s->bktotal + 1);
+      hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, s->stream, rfo, q.NR + 1, rfo, s->bktotal + 1);
       HIPCHK(hipGetLastError());
-      HIPCHK(hipMemcpyAsync(q.htot.data(), s->bkgc, q.htot.size() * 4, hipMemcpyDeviceToHost, st));
-      HIPCHK(hipMemcpyAsync(&q.herr, &s->st->err, 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(q.htot.data(), s->bkgc, q.htot.size() * 4, hipMemcpyDeviceToHost, s->stream));
+      HIPCHK(hipMemcpyAsync(&q.herr, &s->st->err, 4, hipMemcpyDeviceToHost, s->stream));
     }
-    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(sync_all());
     bool any_exact = false;
     for (size_t g = 0; g < ss.size(); g++) {
       gm_solver* s = ss[g];
@@ -697,20 +759,20 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
       any_exact = true;
       BkLevel& P = s->lvh[(size_t)L];
       uint32_t* rfo = s->meta + P.rfo_off;
-      HIPCHK(hipMemsetAsync(rfo, 0, (q.NR + 1) * 4, st));
+      HIPCHK(hipMemsetAsync(rfo, 0, (q.NR + 1) * 4, s->stream));
       bk_dispatch(s->d, [&](auto kind_) {
         constexpr int K_ = decltype(kind_)::value;
-        hipLaunchKernelGGL((k_bk_count<K_, true>), dim3(q.nblk), dim3(kBkStreamThreads), 0, st, s->d, s->bkK + P.lb,
+        hipLaunchKernelGGL((k_bk_count<K_, true>), dim3(q.nblk), dim3(kBkStreamThreads), 0, s->stream, s->d, s->bkK + P.lb,
                            P.n, q.chunk, P.pshift, P.fb, s->bh, s->ph, rfo, s->st, (uint32_t)W);
       });
-      hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, st, s->bh, (uint32_t)q.nblk, s->boff, s->tot);
-      hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, st, s->ph, (uint32_t)q.nblk, s->ph, s->tot + kBkC);
-      hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, st, rfo, q.NR + 1, rfo, s->bktotal + 1);
+      hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, s->stream, s->bh, (uint32_t)q.nblk, s->boff, s->tot);
+      hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, s->stream, s->ph, (uint32_t)q.nblk, s->ph, s->tot + kBkC);
+      hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, s->stream, rfo, q.NR + 1, rfo, s->bktotal + 1);
       HIPCHK(hipGetLastError());
-      HIPCHK(hipMemcpyAsync(q.htot.data(), s->tot, 2 * kBkC * 4, hipMemcpyDeviceToHost, st));
-      HIPCHK(hipMemcpyAsync(&q.herr, &s->st->err, 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(q.htot.data(), s->tot, 2 * kBkC * 4, hipMemcpyDeviceToHost, s->stream));
+      HIPCHK(hipMemcpyAsync(&q.herr, &s->st->err, 4, hipMemcpyDeviceToHost, s->stream));
     }
-    if (any_exact) HIPCHK(hipStreamSynchronize(st));
+    if (any_exact) HIPCHK(sync_all());
     for (size_t g = 0; g < ss.size(); g++) {
       gm_solver* s = ss[g];
       Pending& q = pd[g];
@@ -780,16 +842,16 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
       }
       hb[(size_t)kBkC] = (uint32_t)Eout;
       hb[(size_t)2 * kBkC + 1] = (uint32_t)acc;
-      HIPCHK(hipMemcpyAsync(s->cbase, hb.data(), (kBkC + 1) * 4, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(s->cbase, hb.data(), (kBkC + 1) * 4, hipMemcpyHostToDevice, s->stream));
       HIPCHK(hipMemcpyAsync(s->pbase + (size_t)L * (kBkC + 1), hb.data() + kBkC + 1, (kBkC + 1) * 4,
-                            hipMemcpyHostToDevice, st));
+                            hipMemcpyHostToDevice, s->stream));
       if (P.n && Eout && !over[g]) {
         const u64 nblk = std::min<u64>(kBkExpandBlocks, (P.n + kBkExpandThreads - 1) / kBkExpandThreads),
                   chunk = (P.n + nblk - 1) / nblk;
         const uint32_t ppr = bk_ppr((double)Eout / (double)P.n);
         bk_dispatch(s->d, [&](auto kind_) {
           constexpr int K_ = decltype(kind_)::value;
-          hipLaunchKernelGGL((k_bk_expand<K_, false, true>), dim3(nblk), dim3(kBkExpandThreads), 0, st, s->d,
+          hipLaunchKernelGGL((k_bk_expand<K_, false, true>), dim3(nblk), dim3(kBkExpandThreads), 0, s->stream, s->d,
                              s->bkK + P.lb, P.n, chunk, (const uint32_t*)s->boff, (const uint32_t*)s->cbase, ppr, s->XSk,
                              s->XSr, (uint8_t*)nullptr, 0u, (uint32_t*)nullptr, 0u, 0u, (uint32_t*)nullptr,
                              (uint32_t*)nullptr, (uint32_t*)nullptr, s->st, BkChunked{nullptr, 0}, (uint32_t)W,
@@ -831,22 +893,22 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
       uint32_t* cst = s->meta + X.cst_off;
       uint32_t* fo = cst + NB + 1;
       const u64 nblk = std::min<u64>(kBkExpandBlocks, (E + kBksPartCap - 1) / kBksPartCap), chunk = (E + nblk - 1) / nblk;
-      hipLaunchKernelGGL(k_bks_hist, dim3(nblk), dim3(kBkStreamThreads), 0, st, (const u64*)s->XRk, E, chunk, s->bh);
-      hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, st, s->bh, (uint32_t)nblk, s->boff, s->tot);
-      hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, st, s->tot, (uint32_t)kBkC, s->cbase, s->bktotal + 1);
-      hipLaunchKernelGGL(k_bks_part, dim3(nblk), dim3(kBkStreamThreads), 0, st, (const u64*)s->XRk,
+      hipLaunchKernelGGL(k_bks_hist, dim3(nblk), dim3(kBkStreamThreads), 0, s->stream, (const u64*)s->XRk, E, chunk, s->bh);
+      hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, s->stream, s->bh, (uint32_t)nblk, s->boff, s->tot);
+      hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, s->stream, s->tot, (uint32_t)kBkC, s->cbase, s->bktotal + 1);
+      hipLaunchKernelGGL(k_bks_part, dim3(nblk), dim3(kBkStreamThreads), 0, s->stream, (const u64*)s->XRk,
                          (const uint32_t*)s->XRr, E, chunk, (const uint32_t*)s->boff, (const uint32_t*)s->cbase, s->S1k,
                          s->S1p, s->S1f);
       // refs ride in the parent slot: pshift 31 puts every record in parent range 0 of ah, whose counts
       // nothing reads -- the last level's ah (no level expands from it), so the local-dedup form's
       // parent-range counts of level L stay intact
-      hipLaunchKernelGGL(k_bk_fine, dim3(kBkC), dim3(kBkFineThreads), 0, st, (const u64*)s->S1k, (const uint32_t*)s->S1p,
+      hipLaunchKernelGGL(k_bk_fine, dim3(kBkC), dim3(kBkFineThreads), 0, s->stream, (const u64*)s->S1k, (const uint32_t*)s->S1p,
                          (const uint8_t*)s->S1f, (const uint32_t*)s->cbase, 8u - f, F, s->S2k, s->REp + X.rb, fo, 31u,
                          s->bkah + (size_t)(T - 1) * kBkC * kBkC, 0u, BkChunked{nullptr, 0});
       const int gd = (int)std::min<uint32_t>(NB, 512);
-      hipLaunchKernelGGL(k_bk_dedup, dim3(gd), dim3(kBkDedupThreads), 0, st, s->S2k, (const uint32_t*)fo, NB, s->S1k,
+      hipLaunchKernelGGL(k_bk_dedup, dim3(gd), dim3(kBkDedupThreads), 0, s->stream, s->S2k, (const uint32_t*)fo, NB, s->S1k,
                          s->ucnt, s->REc + X.rb, s->st);
-      hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, st, s->ucnt, NB, cst, s->bktotal);
+      hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, s->stream, s->ucnt, NB, cst, s->bktotal);
       HIPCHK(hipGetLastError());
       (void)P;
     }
@@ -854,10 +916,10 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
     for (size_t g = 0; g < ss.size(); g++) {
       gm_solver* s = ss[g];
       if (!s->lvh[(size_t)L + 1].ein) continue;
-      HIPCHK(hipMemcpyAsync(&ncnt[g], s->bktotal, 8, hipMemcpyDeviceToHost, st));
-      HIPCHK(hipMemcpyAsync(&derr[g], &s->st->err, 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(&ncnt[g], s->bktotal, 8, hipMemcpyDeviceToHost, s->stream));
+      HIPCHK(hipMemcpyAsync(&derr[g], &s->st->err, 4, hipMemcpyDeviceToHost, s->stream));
     }
-    HIPCHK(hipStreamSynchronize(st));  // one host sync for every shard's level size
+    HIPCHK(sync_all());  // one host sync for every shard's level size
     for (size_t g = 0; g < ss.size(); g++) {
       gm_solver* s = ss[g];
       BkLevel& X = s->lvh[(size_t)L + 1];
@@ -876,9 +938,17 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
       if (!X.n) continue;
       const uint32_t NB = 1u << X.nbits;
       const uint32_t* cst = s->meta + X.cst_off;
-      hipLaunchKernelGGL(k_bk_compact, dim3(std::min<uint32_t>(NB, 4096)), dim3(256), 0, st, (const u64*)s->S1k,
+      hipLaunchKernelGGL(k_bk_compact, dim3(std::min<uint32_t>(NB, 4096)), dim3(256), 0, s->stream, (const u64*)s->S1k,
                          (const uint32_t*)(cst + NB + 1), cst, NB, s->bkK + X.lb);
       HIPCHK(hipGetLastError());
+    }
+    if (L + 2 < T) {  // the largest shard of level L + 1 (the next level's form)
+      std::vector<std::vector<u64>> row(ss.size(), std::vector<u64>(1, 0));
+      for (size_t g = 0; g < ss.size(); g++) row[g][0] = ss[g]->lvh[(size_t)L + 1].n;
+      std::vector<u64> all;
+      int rc = bks_allgather(ss, mode, st, row, all);
+      if (rc) return bail(rc);
+      for (u64 v : all) lmax[(size_t)L + 1] = std::max(lmax[(size_t)L + 1], v);
     }
   }
   {  // the last level's status, before any rank starts the backward exchanges
@@ -889,6 +959,7 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
     if (!rc) rc = status_of(MA, (size_t)W + 3);
     if (rc) return bail(rc);
   }
+  if (mode == 4) HIPCHK(sync_all());  // e1 after every shard's forward
   HIPCHK(hipEventRecord(e1, st));
   // ---- backward ----
   for (int L = T - 1; L >= 0; L--) {
@@ -906,10 +977,10 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
         keep.emplace_back((size_t)W);
         std::vector<uint32_t>& cb = keep.back();
         for (int p = 0; p < W; p++) cb[(size_t)p] = (uint32_t)ro[(size_t)p];
-        HIPCHK(hipMemcpyAsync(s->bkcur, cb.data(), (size_t)W * 4, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(s->bkcur, cb.data(), (size_t)W * 4, hipMemcpyHostToDevice, s->stream));
         const uint32_t NB = 1u << X.nbits, F = NB / kBkC;
         const uint32_t* cst = s->meta + X.cst_off;
-        hipLaunchKernelGGL(k_bks_answer, dim3(kBkC), dim3(kBkStreamThreads), 0, st, s->REp + X.rb, s->REc + X.rb,
+        hipLaunchKernelGGL(k_bks_answer, dim3(kBkC), dim3(kBkStreamThreads), 0, s->stream, s->REp + X.rb, s->REc + X.rb,
                            cst + NB + 1, cst, NB, F, s->bkW + X.lb, s->bkcur, s->XSk, s->st);
         HIPCHK(hipGetLastError());
       }
@@ -940,25 +1011,30 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
         u64 na = 0;
         for (int p = 0; p < W; p++) na += s->bks_sc[(size_t)L][(size_t)p];
         if (na != B.nu) {
-          (void)hipStreamSynchronize(st);
-          return bail(fail(GM_ECORRUPT, "shard %d level %d: %llu answers for %llu unique children", s->rank, L,
-                           (unsigned long long)na, (unsigned long long)B.nu));
+          // recorded, not returned: the other ranks are about to enter the
+          // next level's exchange with this one; the error travels in the
+          // final totals (error mask OR-ed over ranks) and every rank
+          // returns together
+          defer(fail(GM_ECORRUPT, "shard %d level %d: %llu answers for %llu unique children", s->rank, L,
+                     (unsigned long long)na, (unsigned long long)B.nu));
+          host_err |= ERR_EDGE_COUNT;
+          continue;
         }
         if (na)
-          hipLaunchKernelGGL(k_bks_wu, dim3((uint32_t)std::min<u64>((na + 255) / 256, 4096)), dim3(256), 0, st,
+          hipLaunchKernelGGL(k_bks_wu, dim3((uint32_t)std::min<u64>((na + 255) / 256, 4096)), dim3(256), 0, s->stream,
                              (const u64*)s->XRk, na, Wu);
         const uint32_t NB = 1u << B.nbits, F = NB / kBkC;
         const uint32_t* cst = s->meta + B.cst_off;
-        hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, st, s->bkah + (size_t)L * kBkC * kBkC, (uint32_t)kBkC,
+        hipLaunchKernelGGL(k_bk_colscan, dim3(kBkC), dim3(256), 0, s->stream, s->bkah + (size_t)L * kBkC * kBkC, (uint32_t)kBkC,
                            s->boff, s->tot);
-        hipLaunchKernelGGL(k_bk_answer, dim3(kBkC), dim3(kBkStreamThreads), 0, st, s->REpl + B.rb, s->REcl + B.rb,
+        hipLaunchKernelGGL(k_bk_answer, dim3(kBkC), dim3(kBkStreamThreads), 0, s->stream, s->REpl + B.rb, s->REcl + B.rb,
                            cst + NB + 1, cst, NB, F, P.pshift, s->boff, pb, (const uint32_t*)Wu, Ap, s->st);
         const uint32_t Fp = 1u << (P.pshift - P.fb);
         const uint32_t* ap = Ap;
         if (Fp > 1) {
           constexpr uint32_t K = kBkSplitK;
-          HIPCHK(hipMemcpyAsync(s->bkcur + kBkC, rfo, (size_t)NR * 4, hipMemcpyDeviceToDevice, st));
-          hipLaunchKernelGGL(k_bk_split, dim3(kBkC * K), dim3(kBkStreamThreads), 0, st, (const uint32_t*)Ap, pb,
+          HIPCHK(hipMemcpyAsync(s->bkcur + kBkC, rfo, (size_t)NR * 4, hipMemcpyDeviceToDevice, s->stream));
+          hipLaunchKernelGGL(k_bk_split, dim3(kBkC * K), dim3(kBkStreamThreads), 0, s->stream, (const uint32_t*)Ap, pb,
                              10u + P.fb, Fp, K, s->bkcur + kBkC, (uint32_t*)s->S2k);
           ap = (uint32_t*)s->S2k;
         }
@@ -968,17 +1044,17 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
         const uint32_t* rfo = s->meta + P.rfo_off;
         const uint32_t* pb = s->pbase + (size_t)L * (kBkC + 1);
         uint32_t* Ap = (uint32_t*)s->S1k;
-        HIPCHK(hipMemcpyAsync(s->bkcur, pb, kBkC * 4, hipMemcpyDeviceToDevice, st));
+        HIPCHK(hipMemcpyAsync(s->bkcur, pb, kBkC * 4, hipMemcpyDeviceToDevice, s->stream));
         const u64 nblk = std::min<u64>(kBkExpandBlocks, (P.eout + kBksAnswerCap - 1) / kBksAnswerCap),
                   chunk = (P.eout + nblk - 1) / nblk;
-        hipLaunchKernelGGL(k_bks_answer_in, dim3(nblk), dim3(kBkStreamThreads), 0, st, (const u64*)s->XRk, P.eout, chunk,
+        hipLaunchKernelGGL(k_bks_answer_in, dim3(nblk), dim3(kBkStreamThreads), 0, s->stream, (const u64*)s->XRk, P.eout, chunk,
                            P.pshift, s->bkcur, Ap);
         const uint32_t Fp = 1u << (P.pshift - P.fb);
         const uint32_t* ap = Ap;
         if (Fp > 1) {
           constexpr uint32_t K = kBkSplitK;
-          HIPCHK(hipMemcpyAsync(s->bkcur + kBkC, rfo, (size_t)NR * 4, hipMemcpyDeviceToDevice, st));
-          hipLaunchKernelGGL(k_bk_split, dim3(kBkC * K), dim3(kBkStreamThreads), 0, st, (const uint32_t*)Ap, pb,
+          HIPCHK(hipMemcpyAsync(s->bkcur + kBkC, rfo, (size_t)NR * 4, hipMemcpyDeviceToDevice, s->stream));
+          hipLaunchKernelGGL(k_bk_split, dim3(kBkC * K), dim3(kBkStreamThreads), 0, s->stream, (const uint32_t*)Ap, pb,
                              10u + P.fb, Fp, K, s->bkcur + kBkC, (uint32_t*)s->S2k);
           ap = (uint32_t*)s->S2k;
         }
@@ -991,17 +1067,18 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
       HIPCHK(hipGetLastError());
     }
   }
+  if (mode == 4) HIPCHK(sync_all());  // e2 after every shard's backward
   HIPCHK(hipEventRecord(e2, st));
   // ---- totals: positions, edges, primitives, root word + 1, error bits, per-level sizes ----
   std::vector<std::vector<u64>> mine(ss.size(), std::vector<u64>(5 + (size_t)T, 0));
   for (size_t g = 0; g < ss.size(); g++) {
     gm_solver* s = ss[g];
-    HIPCHK(hipMemcpyAsync(s->bkL, s->lvh.data(), sizeof(BkLevel) * (size_t)T, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(s->bkL, s->lvh.data(), sizeof(BkLevel) * (size_t)T, hipMemcpyHostToDevice, s->stream));
     uint32_t root_word = NO_WORD;
-    if (s->lvh[0].n) HIPCHK(hipMemcpyAsync(&root_word, s->bkW, 4, hipMemcpyDeviceToHost, st));
+    if (s->lvh[0].n) HIPCHK(hipMemcpyAsync(&root_word, s->bkW, 4, hipMemcpyDeviceToHost, s->stream));
     std::vector<unsigned char> host(devstate_bytes(T));
-    HIPCHK(hipMemcpyAsync(host.data(), s->st, host.size(), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipMemcpyAsync(host.data(), s->st, host.size(), hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(sync_all());
     const DevState* hs = (const DevState*)host.data();
     std::vector<u64>& m = mine[g];
     for (int L = 0; L < T; L++) {
@@ -1011,7 +1088,7 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
     m[1] = hs->edges;
     m[2] = hs->prims;
     m[3] = root_word != NO_WORD ? (u64)root_word + 1 : 0;
-    m[4] = hs->err;
+    m[4] = hs->err | host_err;
   }
   std::vector<u64> all;
   int rc = bks_allgather(ss, mode, st, mine, all);
@@ -1043,6 +1120,10 @@ static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out) {
   out->max_level_width = (uint32_t)std::min<u64>(wmax, 0xFFFFFFFFull);
   const uint32_t word = tot[3] ? (uint32_t)(tot[3] - 1) : NO_WORD;
   out->root_word = word;
+  if (prc) {  // this rank's own deferred failure (its bits are in tot[4] too)
+    g_err = perr;
+    return prc;
+  }
   if (tot[4]) {
     const bool full = tot[4] & (ERR_TABLE_FULL | ERR_LEVELS_FULL);
     const bool lim = tot[4] & ERR_BUCKET_FULL;

@@ -197,7 +197,6 @@ __device__ __forceinline__ void plane_x1_range(typename PlaneWord<WB>::T* __rest
   typedef PlaneWord<WB> W;
   constexpr int DW = W::DW, NQ = DW / 4;  // dwords / 16-B loads per row
   const uint32_t lane = threadIdx.x & 63, L = lane & 31;
-  const uint32_t lm = lane == 32 ? 0u : ~0u;  // row 0 of the upper plane has no row below
   for (uint32_t i0 = sh.first; i0 < sh.end; i0 += sh.stride) {
     const uint32_t idx = i0 + (lane >> 5);
     const bool live = idx < sh.end;
@@ -250,13 +249,16 @@ __device__ __forceinline__ void plane_x1_range(typename PlaneWord<WB>::T* __rest
     // active-row mask is formed in SALU per step (a table of 63 constants
     // would be hoisted into SGPRs and spill).
     const bool prim = g.rank == 0 && P == 0 && L == 0;  // every heap 0: the primitive LOSS
+    // (the lean step chain of plane_x2_range: no lane-32 masks, ready
+    // children folded off the chain, active rows from a per-lane word)
     uint32_t cur = 0, prev = 0, u1p = 0;
     uint32_t out[DW];
 #pragma unroll
     for (int d = 0; d < DW; d++) out[d] = 0;
+    const uint32_t A0 = ~0u << L;  // bit q set: row L is active at step q of phase 0
 #pragma unroll 1
     for (uint32_t ph = 0; ph < 2; ph++) {
-      const uint32_t flip = ph ? 0xFFFFFFFFu : 0u;  // phase 1: the lanes past their row's start
+      const uint32_t A = ph ? ~A0 : A0;  // phase 1: the lanes past their row's start
 #pragma unroll
       for (int q = 0; q < 32; q++) {
         uint32_t a;
@@ -266,13 +268,11 @@ __device__ __forceinline__ void plane_x1_range(typename PlaneWord<WB>::T* __rest
         } else {
           a = __builtin_amdgcn_ubfe(Ehi[q >> 1], 16 * (q & 1), 16);
         }
-        const uint32_t u1 = from_lane_below(cur) & lm;
-        const uint32_t u2 = from_lane_below(u1p) & lm;
-        uint32_t m = max(max(a, cur), prev);
-        m = max(max(m, u1), u2);
-        // active lanes: phase 0 rows 0..q, phase 1 rows q+1..31 (both halves)
-        const uint32_t am = (uint32_t)(q == 31 ? 0xFFFFFFFFull : ((2ull << q) - 1)) ^ flip;
-        uint32_t f = keep_rows(am, L, W::parent(m));
+        const uint32_t u2 = from_lane_below(u1p);
+        const uint32_t pre = max(max(a, prev), u2);
+        const uint32_t u1 = from_lane_below(cur);
+        const uint32_t m = max(max(pre, cur), u1);
+        uint32_t f = W::parent(m) & (uint32_t)__builtin_amdgcn_sbfe((int)A, q, 1);
         if (q == 0) f = (prim && ph == 0) ? W::kPrim : f;
         if (WB == 1)
           out[q >> 2] |= f << (8 * (q & 3));
@@ -358,7 +358,6 @@ __device__ __forceinline__ void plane_x2_range(typename PlaneWord<WB>::T* __rest
   typedef typename W::T T;
   constexpr int DW = W::DW, NQ = DW / 4;
   const uint32_t lane = threadIdx.x & 63, L = lane & 31;
-  const bool l32 = lane == 32;
   for (uint32_t i0 = sh.first; i0 < sh.end; i0 += sh.stride) {
     const uint32_t ix = i0 + 2 * (lane >> 5), iy = ix + 1;
     const bool livex = ix < sh.end, livey = iy < sh.end;
@@ -424,13 +423,23 @@ __device__ __forceinline__ void plane_x2_range(typename PlaneWord<WB>::T* __rest
     // step q's results of both planes stay packed [X | Y] in op[q] (OR of
     // the two phases: an idle lane contributes 0) and are unpacked into the
     // two rows once, after the wavefront
+    // The step chain (lean form, round 4: backward 1.624 -> 1.540 ms per
+    // 2^30 in tools/plane_lab, bit-exact): the children that are ready a
+    // step early -- the E byte, this row's h0 - 2 result, the h1 - 2 row's
+    // -- are folded off the chain, so cur -> (lane below) -> max -> parent
+    // -> active mask is the whole dependency per step.  No lane-32 masks:
+    // the upper pair's row 0 (lane 32) reads lane 31 (the lower pair's row
+    // 31) only at steps <= 31, where row 31 is still idle and holds 0, and
+    // row 1 reads lane 31's u1 of step <= 30, also 0.  Active rows: bit q of
+    // A, one bit extract per step (phase 0: rows 0..q; phase 1: q+1..31).
     uint32_t cur = 0, prev = 0, u1p = 0;
     uint32_t op[32];
 #pragma unroll
     for (int q = 0; q < 32; q++) op[q] = 0;
+    const uint32_t A0 = ~0u << L;  // bit q set: row L is active at step q of phase 0
 #pragma unroll 1
     for (uint32_t ph = 0; ph < 2; ph++) {
-      const uint32_t flip = ph ? 0xFFFFFFFFu : 0u;
+      const uint32_t A = ph ? ~A0 : A0;
 #pragma unroll
       for (int q = 0; q < 32; q++) {
         uint32_t a;
@@ -446,17 +455,17 @@ __device__ __forceinline__ void plane_x2_range(typename PlaneWord<WB>::T* __rest
           const uint32_t sel = ((5u + b0) << 24) | ((4u + b0) << 16) | ((1u + b0) << 8) | b0;
           a = perm(Yh[d], Xh[d], sel);
         }
-        const uint32_t u1r = from_lane_below(cur), u2r = from_lane_below(u1p);
-        uint32_t m = pk_max16(pk_max16(a, cur), prev);
-        const uint32_t m2 = pk_max16(pk_max16(m, u1r), u2r);
-        m = l32 ? m : m2;  // row 0 of the upper pair has no row below
-        const uint32_t am = (uint32_t)(q == 31 ? 0xFFFFFFFFull : ((2ull << q) - 1)) ^ flip;
-        uint32_t f = keep_rows(am, L, parent_x2<WB>(m));
+        const uint32_t u2r = from_lane_below(u1p);
+        const uint32_t pre = pk_max16(pk_max16(a, prev), u2r);
+        const uint32_t u1r = from_lane_below(cur);
+        const uint32_t m = pk_max16(pk_max16(pre, cur), u1r);
+        const uint32_t keep = (uint32_t)__builtin_amdgcn_sbfe((int)A, q, 1);
+        uint32_t f = parent_x2<WB>(m) & keep;
         if (q == 0) f = pk_max16(f, ph ? 0u : primv);
         op[q] |= f;
         prev = cur;
         cur = f;
-        u1p = l32 ? 0u : u1r;
+        u1p = u1r;
       }
     }
     uint32_t ox_[DW], oy_[DW];

@@ -19,10 +19,14 @@ extern "C++" {
 // kernels (need DevState / BlockCount / Desc from gm_solver.hip)
 // ---------------------------------------------------------------------------
 template <int NO>
-__global__ __launch_bounds__(256) void k_plane_reach(uint32_t* bits, PlaneGeom g, BlockCount* bc, DevState* st) {
+__global__ __launch_bounds__(256) void k_plane_reach(uint32_t* bits, PlaneGeom g, BlockCount* bc, DevState* st,
+                                                     uint32_t word_bits) {
   plane_reach_body<NO>(bits, g, [&](u64 npos, u64 edges) { block_count(bc, npos, edges); });
-  // the only primitive, every heap 0: global plane 0 of rank 0, row 0, bit 0
-  if (blockIdx.x == 0 && threadIdx.x == 0 && g.rank == 0) atomicAdd(&st->prims, 1ull);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st->word_bits = word_bits;  // the solve in progress (a resume checks it)
+    // the only primitive, every heap 0: global plane 0 of rank 0, row 0, bit 0
+    if (g.rank == 0) atomicAdd(&st->prims, 1ull);
+  }
 }
 
 // word of local position (h0, h1, P) in value | remoteness << 2 form
@@ -71,15 +75,20 @@ __global__ void k_plane_query(Desc d, PlaneGeom g, const void* tab, const uint32
   }
 }
 
-// the root's word (only the shard that owns it): DevState::root_word
+// the end of a solve, one launch: the root's word (only the shard that owns
+// it; DevState::root_word), then the counts and reduction words (k_fill_red's
+// body) -- one block of 1024 threads
 template <int WB>
-__global__ void k_plane_root(Desc d, PlaneGeom g, const void* tab, const uint32_t* bits, DevState* st) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+__global__ __launch_bounds__(1024) void k_plane_finish(Desc d, PlaneGeom g, const void* tab, const uint32_t* bits,
+                                                       DevState* st, const BlockCount* bc) {
+  if (threadIdx.x == 0) {
     u64 P;
     uint32_t h0, h1, w = NO_WORD;
     if (plane_locate(d, g, d.root, &P, &h0, &h1) && ((bits[P * 32u + h1] >> h0) & 1u)) w = plane_vr<WB>(tab, P, h0, h1);
     st->root_word = w;
   }
+  __syncthreads();
+  fill_red_body(st, bc);
 }
 
 // global rank of local position (h0, h1, P)
@@ -643,7 +652,7 @@ static void plane_reach_launch(gm_solver* s) {
   const int grid = (int)std::max<u64>(1, std::min<u64>((nq + 255) / 256, (u64)std::min(s->grid, kCountSlots)));
   plane_no_dispatch(s->pg.no, [&](auto NO) {
     hipLaunchKernelGGL((k_plane_reach<decltype(NO)::value>), dim3(grid), dim3(256), 0, s->stream, s->pbits, s->pg,
-                       s->bcount, s->st);
+                       s->bcount, s->st, 8u * s->pwb);
   });
 }
 
@@ -781,7 +790,7 @@ static u64 plane_stage_sig(const gm_solver* s) {
 static int plane_check_stage(std::vector<gm_solver*>& ss, int mode, hipStream_t st) {
   const int W = ss[0]->world;
   std::vector<u64> all((size_t)W);
-  if (mode == 2) {
+  if (mode == 2 || mode == 4) {
     for (gm_solver* s : ss) all[(size_t)s->rank] = plane_stage_sig(s);
   } else {
     u64 mine = plane_stage_sig(ss[0]);
@@ -818,6 +827,12 @@ static int plane_check_stage(std::vector<gm_solver*>& ss, int mode, hipStream_t 
 //    can never hold up the sends, which follow the rank's own keys on the
 //    send stream.
 //  mode 3 (host-staged transport): blocking row transfers in key order.
+//  mode 4 (one-GPU rehearsal of mode 1, every shard in one process on its
+//    own streams): mode 1's code path -- key loop, receive window, send /
+//    receive streams, SE / RE events, end-of-solve joins -- with a device
+//    copy on the receiver's receive stream in place of each ncclSend /
+//    ncclRecv pair.  What only RCCL itself exercises: ncclCommSplit, the
+//    send / receive matching on the two communicators, RCCL's own progress.
 static int plane_backward_staged(std::vector<gm_solver*>& ss, int mode, hipStream_t st, u64* nlaunch) {
   gm_solver* s0 = ss[0];
   const uint32_t k = s0->pstage_k, K = s0->pkeys, R = s0->prows, B = s0->pg.B;
@@ -865,13 +880,13 @@ static int plane_backward_staged(std::vector<gm_solver*>& ss, int mode, hipStrea
     }
     return 0;
   }
-  gm_solver* s = s0;
-  PlaneBatcher bat(s);
-  const int rank = s->rank;
-  const bool rx = rank > 0, tx = rank + 1 < W;
-  auto rbuf = [&](uint32_t r, u64* n) { return (void*)((char*)s->precv + seg(s->prcv_off, r, n) * pb); };
-  auto sbuf = [&](uint32_t r, u64* n) { return (void*)((char*)s->psend + seg(s->psnd_off, r, n) * pb); };
   if (mode == 3) {
+    gm_solver* s = s0;
+    PlaneBatcher bat(s);
+    const int rank = s->rank;
+    const bool rx = rank > 0, tx = rank + 1 < W;
+    auto rbuf = [&](uint32_t r, u64* n) { return (void*)((char*)s->precv + seg(s->prcv_off, r, n) * pb); };
+    auto sbuf = [&](uint32_t r, u64* n) { return (void*)((char*)s->psend + seg(s->psnd_off, r, n) * pb); };
     for (uint32_t key = 0; key < K; key++) {
       uint32_t r;
       if (rx && row_need(key, &r)) {
@@ -898,70 +913,120 @@ static int plane_backward_staged(std::vector<gm_solver*>& ss, int mode, hipStrea
     *nlaunch = bat.launches;
     return 0;
   }
-  // mode 1
-  if (!s->comm2) {
-    ncclResult_t e = ncclCommSplit(s->comm, 0, rank, &s->comm2, nullptr);
-    if (e != ncclSuccess) return fail(GM_EHIP, "ncclCommSplit: %s", ncclGetErrorString(e));
-  }
-  if (!s->cstream) HIPCHK(hipStreamCreateWithFlags(&s->cstream, hipStreamNonBlocking));
-  if (!s->cstream2) HIPCHK(hipStreamCreateWithFlags(&s->cstream2, hipStreamNonBlocking));
-  while (s->pev.size() < 2 * (size_t)R + 3) {
-    hipEvent_t e;
-    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    s->pev.push_back(e);
-  }
-  hipEvent_t* RE = s->pev.data();      // row r received
-  hipEvent_t* SE = RE + R;             // row r final on this rank
-  hipEvent_t* XE = SE + R;             // [0] start, [1] sends done, [2] receives done
-  ncclComm_t csend = (rank % 2 == 0) ? s->comm : s->comm2, crecv = (rank % 2 == 1) ? s->comm : s->comm2;
-  hipStream_t ts = s->cstream, rs = s->cstream2;
-  HIPCHK(hipEventRecord(XE[0], st));
-  HIPCHK(hipStreamWaitEvent(ts, XE[0], 0));
-  HIPCHK(hipStreamWaitEvent(rs, XE[0], 0));
-  constexpr uint32_t kAhead = 8;  // rows whose receives are posted ahead of the key that reads them
-  uint32_t posted = 0;            // rows [0, posted) have their receive posted
-  auto post_to = [&](uint32_t lim) -> int {
-    for (; rx && posted < std::min(lim, R); posted++) {
-      u64 n;
-      void* b = rbuf(posted, &n);
-      if (n) {
-        const ncclResult_t e = ncclRecv(b, n * pb, ncclUint8, rank - 1, crecv, rs);
-        if (e != ncclSuccess) return fail(GM_EHIP, "RCCL halo receive: %s", ncclGetErrorString(e));
-      }
-      HIPCHK(hipEventRecord(RE[posted], rs));
+  // mode 1 (RCCL) and mode 4 (its one-GPU rehearsal): the same key loop,
+  // receive window, streams, events and joins per shard; only the two
+  // transfer calls differ.  Per shard: compute stream s->stream, send
+  // stream ts, receive stream rs; RE[r] row r received, SE[r] row r final
+  // here, XS[r] row r handed to the send stream's transfer.
+  auto staged_rank = [&](gm_solver* s, auto&& recv_op, auto&& send_op) -> int {
+    PlaneBatcher bat(s);
+    const int rank = s->rank;
+    const bool rx = rank > 0, tx = rank + 1 < W;
+    hipStream_t cst = s->stream;
+    if (!s->cstream) HIPCHK(hipStreamCreateWithFlags(&s->cstream, hipStreamNonBlocking));
+    if (!s->cstream2) HIPCHK(hipStreamCreateWithFlags(&s->cstream2, hipStreamNonBlocking));
+    while (s->pev.size() < 3 * (size_t)R + 3) {
+      hipEvent_t e;
+      HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      s->pev.push_back(e);
     }
+    hipEvent_t* RE = s->pev.data();      // row r received
+    hipEvent_t* SE = RE + R;             // row r final on this rank
+    hipEvent_t* XS = SE + R;             // row r's send issued on the send stream
+    hipEvent_t* XE = XS + R;             // [0] start, [1] sends done, [2] receives done
+    hipStream_t ts = s->cstream, rs = s->cstream2;
+    HIPCHK(hipEventRecord(XE[0], cst));
+    HIPCHK(hipStreamWaitEvent(ts, XE[0], 0));
+    HIPCHK(hipStreamWaitEvent(rs, XE[0], 0));
+    constexpr uint32_t kAhead = 8;  // rows whose receives are posted ahead of the key that reads them
+    uint32_t posted = 0;            // rows [0, posted) have their receive posted
+    auto post_to = [&](uint32_t lim) -> int {
+      for (; rx && posted < std::min(lim, R); posted++) {
+        u64 n;
+        void* b = (void*)((char*)s->precv + seg(s->prcv_off, posted, &n) * pb);
+        int rc = recv_op(s, posted, b, n, rs);
+        if (rc) return rc;
+        HIPCHK(hipEventRecord(RE[posted], rs));
+      }
+      return 0;
+    };
+    for (uint32_t key = 0; key < K; key++) {
+      uint32_t r;
+      if (rx && row_need(key, &r)) {
+        bat.flush();
+        int rc = post_to(r + 1 + kAhead);
+        if (rc) return rc;
+        HIPCHK(hipStreamWaitEvent(cst, RE[r], 0));
+      }
+      launch_key(bat, key);
+      if (tx && row_done(key, &r)) {
+        bat.flush();
+        HIPCHK(hipEventRecord(SE[r], cst));
+        HIPCHK(hipStreamWaitEvent(ts, SE[r], 0));
+        u64 n;
+        void* b = (void*)((char*)s->psend + seg(s->psnd_off, r, &n) * pb);
+        int rc = send_op(s, r, b, n, ts);
+        if (rc) return rc;
+        HIPCHK(hipEventRecord(XS[r], ts));
+      }
+    }
+    bat.flush();
+    if (rank == 0 || mode == 1) *nlaunch = bat.launches;
+    int rc = post_to(R);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(XE[1], ts));
+    HIPCHK(hipEventRecord(XE[2], rs));
+    HIPCHK(hipStreamWaitEvent(cst, XE[1], 0));
+    HIPCHK(hipStreamWaitEvent(cst, XE[2], 0));
     return 0;
   };
-  for (uint32_t key = 0; key < K; key++) {
-    uint32_t r;
-    if (rx && row_need(key, &r)) {
-      bat.flush();
-      int rc = post_to(r + 1 + kAhead);
+  if (mode == 4) {
+    // the ranks' host loops in pipeline order (a row's XS event exists before
+    // the next rank's receive waits on it); every rank on its own streams of
+    // the one GPU, so its keys overlap the ranks before it as on separate
+    // GPUs; a device copy on the receiver's receive stream stands in for the
+    // ncclSend / ncclRecv pair: it waits for the sender's XS[r], i.e. row r
+    // final there and handed to its send stream
+    for (int c = 0; c < W; c++) {
+      int rc = staged_rank(
+          ss[(size_t)c],
+          [&](gm_solver* t, uint32_t row, void* b, u64 n, hipStream_t rs) -> int {
+            gm_solver* f = ss[(size_t)t->rank - 1];
+            u64 ns;
+            const u64 so = seg(f->psnd_off, row, &ns);
+            if (ns != n) return fail(GM_ECORRUPT, "row %u: shard %d sends %llu planes, shard %d expects %llu", row,
+                                     f->rank, (unsigned long long)ns, t->rank, (unsigned long long)n);
+            if (!n) return 0;
+            HIPCHK(hipStreamWaitEvent(rs, f->pev[2 * (size_t)R + row], 0));
+            HIPCHK(hipMemcpyAsync(b, (const char*)f->psend + so * pb, n * pb, hipMemcpyDeviceToDevice, rs));
+            return 0;
+          },
+          [&](gm_solver*, uint32_t, void*, u64, hipStream_t) -> int { return 0; });
       if (rc) return rc;
-      HIPCHK(hipStreamWaitEvent(st, RE[r], 0));
     }
-    launch_key(bat, key);
-    if (tx && row_done(key, &r)) {
-      bat.flush();
-      HIPCHK(hipEventRecord(SE[r], st));
-      HIPCHK(hipStreamWaitEvent(ts, SE[r], 0));
-      u64 n;
-      void* b = sbuf(r, &n);
-      if (n) {
-        const ncclResult_t e = ncclSend(b, n * pb, ncclUint8, rank + 1, csend, ts);
-        if (e != ncclSuccess) return fail(GM_EHIP, "RCCL halo send: %s", ncclGetErrorString(e));
-      }
-    }
+    return 0;
   }
-  bat.flush();
-  *nlaunch = bat.launches;
-  int rc = post_to(R);
-  if (rc) return rc;
-  HIPCHK(hipEventRecord(XE[1], ts));
-  HIPCHK(hipEventRecord(XE[2], rs));
-  HIPCHK(hipStreamWaitEvent(st, XE[1], 0));
-  HIPCHK(hipStreamWaitEvent(st, XE[2], 0));
-  return 0;
+  // mode 1: transfers r -> r + 1 on comm when r is even and on comm2 when odd
+  gm_solver* s = s0;
+  if (!s->comm2) {
+    ncclResult_t e = ncclCommSplit(s->comm, 0, s->rank, &s->comm2, nullptr);
+    if (e != ncclSuccess) return fail(GM_EHIP, "ncclCommSplit: %s", ncclGetErrorString(e));
+  }
+  ncclComm_t csend = (s->rank % 2 == 0) ? s->comm : s->comm2, crecv = (s->rank % 2 == 1) ? s->comm : s->comm2;
+  return staged_rank(
+      s,
+      [&](gm_solver* t, uint32_t, void* b, u64 n, hipStream_t rs) -> int {
+        if (!n) return 0;
+        const ncclResult_t e = ncclRecv(b, n * pb, ncclUint8, t->rank - 1, crecv, rs);
+        if (e != ncclSuccess) return fail(GM_EHIP, "RCCL halo receive: %s", ncclGetErrorString(e));
+        return 0;
+      },
+      [&](gm_solver* t, uint32_t, void* b, u64 n, hipStream_t ts) -> int {
+        if (!n) return 0;
+        const ncclResult_t e = ncclSend(b, n * pb, ncclUint8, t->rank + 1, csend, ts);
+        if (e != ncclSuccess) return fail(GM_EHIP, "RCCL halo send: %s", ncclGetErrorString(e));
+        return 0;
+      });
 }
 
 // The PLANES solve.  Steps (gm_solver_set_steps, one table only): 2T like
@@ -972,13 +1037,22 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
   const Desc& d = s0->d;
   const int T = d.max_levels;
   const uint32_t S = s0->pS;
-  const int mode = s0->world <= 1 ? 0 : ss.size() != 1 ? 2 : s0->xfer ? 3 : 1;
+  // mode 2: a group on ONE stream; mode 4: a group whose shards have their
+  // own streams -- the rehearsal of mode 1's staged schedule
+  const bool own_streams = ss.size() > 1 && ss[1]->stream != s0->stream;
+  const int mode = s0->world <= 1 ? 0 : ss.size() != 1 ? (own_streams ? 4 : 2) : s0->xfer ? 3 : 1;
   if (mode == 1 && !s0->comm) return fail(GM_EINVAL, "shard %d/%d has no communicator (gm_solver_comm_init)", s0->rank, s0->world);
-  if (mode == 2) {
+  if (mode == 2 || mode == 4) {
     if ((int)ss.size() != s0->world) return fail(GM_EINVAL, "group solve needs all %d shards", s0->world);
-    for (size_t g = 0; g < ss.size(); g++)
-      if (ss[g]->rank != (int)g || ss[g]->stream != s0->stream || ss[g]->mode != GM_MODE_PLANES)
-        return fail(GM_EINVAL, "group shards must be ranks 0..n-1 on one stream");
+    for (size_t g = 0; g < ss.size(); g++) {
+      if (ss[g]->rank != (int)g || ss[g]->mode != GM_MODE_PLANES)
+        return fail(GM_EINVAL, "group shards must be ranks 0..n-1");
+      for (size_t h = 0; h < g; h++)
+        if ((mode == 2) != (ss[g]->stream == ss[h]->stream))
+          return fail(GM_EINVAL, "group shards share one stream, or (the staged rehearsal) each has its own");
+    }
+    if (mode == 4 && !s0->pstage_k)
+      return fail(GM_EINVAL, "shards on their own streams rehearse the staged deal only (this shape is level-synchronous)");
   }
   const int first = mode == 0 ? (int)s0->step_first : 0;
   const int stop = mode == 0 && s0->step_stop ? (int)s0->step_stop : 2 * T;
@@ -1014,23 +1088,54 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
       if (new_event(&e)) return GM_EHIP;
     if (new_event(&kx[0]) || new_event(&kx[1])) return GM_EHIP;
   }
+  // mode 4: the shards' own streams fork from st after e0 and join it
+  // before e1, fork again for the backward and join before e2 (other modes:
+  // every shard runs on st)
+  hipEvent_t ef = nullptr;
+  std::vector<hipEvent_t> ej;
+  if (mode == 4) {
+    if (new_event(&ef)) return GM_EHIP;
+    ej.resize(ss.size());
+    for (auto& e : ej)
+      if (new_event(&e)) return GM_EHIP;
+  }
+  auto fork = [&]() -> int {
+    if (mode != 4) return 0;
+    HIPCHK(hipEventRecord(ef, st));
+    for (gm_solver* s : ss)
+      if (s->stream != st) HIPCHK(hipStreamWaitEvent(s->stream, ef, 0));
+    return 0;
+  };
+  auto join = [&]() -> int {
+    if (mode != 4) return 0;
+    for (size_t g = 0; g < ss.size(); g++)
+      if (ss[g]->stream != st) {
+        HIPCHK(hipEventRecord(ej[g], ss[g]->stream));
+        HIPCHK(hipStreamWaitEvent(st, ej[g], 0));
+      }
+    return 0;
+  };
   auto t0 = std::chrono::steady_clock::now();
   HIPCHK(hipEventRecord(e0, st));
+  if (fork()) return GM_EHIP;
   if (first == 0) {
     for (gm_solver* s : ss) {
-      HIPCHK(hipMemsetAsync(s->st, 0, devstate_bytes(T), st));
-      HIPCHK(hipMemsetAsync(s->bcount, 0, kCountSlots * sizeof(BlockCount), st));
-      const uint32_t wb = 8 * s->pwb;
-      HIPCHK(hipMemcpyAsync(&s->st->word_bits, &wb, sizeof wb, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemsetAsync(s->st, 0, devstate_bytes(T), s->stream));
+      HIPCHK(hipMemsetAsync(s->bcount, 0, kCountSlots * sizeof(BlockCount), s->stream));
+      // the word width: written by k_plane_reach below (no reach: here)
+      if (stop == 0) HIPCHK(hipMemsetD32Async((hipDeviceptr_t)&s->st->word_bits, (int)(8 * s->pwb), 1, s->stream));
     }
     if (stop > 0) {
       if (timing) HIPCHK(hipEventRecord(kx[0], st));
       for (gm_solver* s : ss) plane_reach_launch(s);
+      if (timing && join()) return GM_EHIP;
       if (timing) HIPCHK(hipEventRecord(kx[1], st));
     }
   }
   HIPCHK(hipGetLastError());
+  if (join()) return GM_EHIP;
   HIPCHK(hipEventRecord(e1, st));
+  if (fork()) return GM_EHIP;
   // kernel timing: one table -- the backward is nothing but the resolve
   // launches, so one event pair around all of them (no events between
   // launches: they would add their own gaps to what they time); shards --
@@ -1068,6 +1173,7 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
       cleanup();
       return rc;
     }
+    if (timing && join()) return GM_EHIP;
     if (timing) HIPCHK(hipEventRecord(kr[2 * (size_t)S + 1], st));
   }
   for (uint32_t l = 0; l <= S && !staged; l++) {
@@ -1105,6 +1211,7 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
   if (!staged) nlaunch = mode == 0 && !per_level ? bat0.launches : (u64)(S + 1) * (pipe ? 2 : 1);
   if (last_x >= 0) HIPCHK(hipStreamWaitEvent(st, PE[S + 1 + last_x], 0));  // join the comm stream
   HIPCHK(hipGetLastError());
+  if (join()) return GM_EHIP;
   HIPCHK(hipEventRecord(e2, st));
   if (stop < 2 * T) {
     HIPCHK(hipStreamSynchronize(st));
@@ -1115,10 +1222,11 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
   }
   for (gm_solver* s : ss) {
     if (s->pwb == 1)
-      hipLaunchKernelGGL(k_plane_root<1>, dim3(1), dim3(64), 0, st, s->d, s->pg, (const void*)s->ptab, s->pbits, s->st);
+      hipLaunchKernelGGL(k_plane_finish<1>, dim3(1), dim3(1024), 0, st, s->d, s->pg, (const void*)s->ptab, s->pbits,
+                         s->st, (const BlockCount*)s->bcount);
     else
-      hipLaunchKernelGGL(k_plane_root<2>, dim3(1), dim3(64), 0, st, s->d, s->pg, (const void*)s->ptab, s->pbits, s->st);
-    hipLaunchKernelGGL(k_fill_red, dim3(1), dim3(1024), 0, st, s->st, s->bcount);
+      hipLaunchKernelGGL(k_plane_finish<2>, dim3(1), dim3(1024), 0, st, s->d, s->pg, (const void*)s->ptab, s->pbits,
+                         s->st, (const BlockCount*)s->bcount);
   }
   HIPCHK(hipGetLastError());
   if (mode == 1) {

@@ -46,6 +46,7 @@
 #include <type_traits>
 #include <map>
 #include <mutex>
+#include <thread>
 
 #include "../../include/gamesman.h"
 #include "gm_codec.h"
@@ -1576,18 +1577,35 @@ static bool bk_ok(const Desc* d) {
 // edges bound for a positions bound: the known counts where the board and
 // bound match (SURVEY Appendix B / tests/golden), else a branching factor
 // above every known board's
-static u64 bk_edges_bound(const Desc* d, u64 P) {
-  struct Known { int kind, L, H; u64 P, E; };
-  static const Known kn[] = {
+struct BkKnown {
+  int kind, L, H;
+  u64 P, E;
+};
+static const BkKnown* bk_known(const Desc* d) {
+  static const BkKnown kn[] = {
       {K_TOOT, 3, 3, 11097ull, 27774ull},          {K_TOOT, 4, 3, 200127ull, 640648ull},
       {K_TOOT, 4, 4, 3468773ull, 9932808ull},      {K_TOOT, 5, 4, 70184763ull, 226547754ull},
       {K_TOOT, 6, 4, 1187212827ull, 4243234712ull}, {K_OTHELLO, 4, 4, 54089ull, 69916ull},
       {K_TTT, 0, 0, 5478ull, 16167ull}};
-  for (const Known& k : kn)
-    if (k.kind == d->kind && (d->kind == K_TTT || (k.L == d->L && k.H == d->H)) && P <= k.P)
-      return k.E + 1024;
+  for (const BkKnown& k : kn)
+    if (k.kind == d->kind && (d->kind == K_TTT || (k.L == d->L && k.H == d->H))) return &k;
+  return nullptr;
+}
+static u64 bk_edges_bound(const Desc* d, u64 P) {
+  const BkKnown* k = bk_known(d);
+  if (k && P <= k->P) return k->E + 1024;
   const double ratio = d->kind == K_TOOT ? 3.6 : d->kind == K_TTT ? 3.0 : 2.0;
   return (u64)(ratio * (double)P) + 1024;
+}
+// out-edges of the P positions an md5 shard owns: the md5 partition spreads
+// positions evenly and regardless of their move counts, so a shard's share of
+// the edges is its share of the positions -- the board's known edge / position
+// ratio (+2 %), else the per-kind ratio; not the whole board's edges, which
+// sized every shard of toot 6x4 for the full 4.2e9 (4 shards: out of memory)
+static u64 bk_shard_edges_bound(const Desc* d, u64 P) {
+  const BkKnown* k = bk_known(d);
+  if (k && P < k->P) return std::min<u64>(k->E, (u64)((double)k->E / (double)k->P * (double)P * 1.02)) + 1024;
+  return bk_edges_bound(d, P);
 }
 // in-edges of the widest level: a quarter of all edges (every known board
 // is below a fifth; a level over it returns GM_EFULL and the host re-plans)
@@ -1689,7 +1707,7 @@ int gm_plan_keyed_shard(int game, int rank, int world, uint64_t positions, uint3
     gm_game_info(game, &positions, nullptr, nullptr);
     if (positions == 0) return fail(GM_EINVAL, "no known position bound for this board; pass an estimate");
   }
-  const u64 P = positions + 64, E = bk_edges_bound(d, positions), Em = bk_emax_bound(E);
+  const u64 P = positions + 64, E = bk_shard_edges_bound(d, positions), Em = bk_emax_bound(E);
   if (Em >= 0xFFFFFFF0ull) return fail(GM_EINVAL, "a level of more than 2^32 edges: not supported");
   const u64 bytes = 4 * P + 12 * E + 48 * Em + 64;  // the one-GPU layout + local in-edges + the exchange buffers
   if (max_table_bytes && bytes > max_table_bytes)
@@ -2275,7 +2293,10 @@ int gm_solver_solve(gm_solver* s, gm_result* out) {
   return 0;
 }
 
-__global__ __launch_bounds__(1024) void k_fill_red(DevState* st, const BlockCount* bc) {  // one block of 1024
+// the per-block counts summed into the table's totals and the solve's
+// reduction words (one block of 1024 threads; also the tail of the PLANES
+// finish kernel, k_plane_finish)
+__device__ __forceinline__ void fill_red_body(DevState* st, const BlockCount* bc) {
   __shared__ u64 rn[16], re[16];
   u64 sn = 0, se = 0;
   for (int i = (int)threadIdx.x; i < kCountSlots; i += (int)blockDim.x) {
@@ -2306,6 +2327,7 @@ __global__ __launch_bounds__(1024) void k_fill_red(DevState* st, const BlockCoun
     st->red[4] = st->err;
   }
 }
+__global__ __launch_bounds__(1024) void k_fill_red(DevState* st, const BlockCount* bc) { fill_red_body(st, bc); }
 
 // Band of level L: every non-hole slot has digit sum s(p) in [S - H0, S]
 // (S = root_sum - L), so its prefix lies between the smallest prefix with
@@ -3661,12 +3683,122 @@ int gm_solver_checksum(gm_solver* s, uint64_t out[6]) {
 static std::mutex g_solved_mu;
 static std::map<int, gm_solver*> g_solved;
 
+// gm_solve over several GPUs of this process (SURVEY §8b's `ngpus`; the
+// reference's `mpiexec -n P`, solver_launcher.py:30,76-84): shard i of the
+// plan gm_plan_multi gives lives on device i in buf[i]; one RCCL
+// communicator per device (ncclCommInitAll) and one host thread per device
+// driving its shard's gm_solver_solve -- the halo rows (PLANES / DENSE) and
+// the md5 all-to-alls (BUCKETED) are RCCL calls every rank's thread must
+// enter.  Every rank ends with the job's totals and root word.
+struct MultiSolve {
+  std::vector<gm_solver*> ss;
+};
+static std::map<int, MultiSolve> g_multi;  // under g_solved_mu
+
+static void multi_destroy(MultiSolve& m) {
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  for (size_t i = 0; i < m.ss.size(); i++)
+    if (m.ss[i]) {
+      (void)hipSetDevice((int)i);
+      gm_solver_destroy(m.ss[i]);
+      m.ss[i] = nullptr;
+    }
+  (void)hipSetDevice(cur);
+}
+
+static int solve_multi(int game, int ngpus, const gm_buffers* buf, gm_result* out) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+  if (ngpus > ndev) return fail(GM_EINVAL, "ngpus %d: %d GPU(s) visible", ngpus, ndev);
+  for (int i = 0; i < ngpus; i++)
+    if (buf[i].mode != buf[0].mode) return fail(GM_EINVAL, "buf[%d]: every shard needs the mode of gm_plan_multi", i);
+  int cur = 0;
+  HIPCHK(hipGetDevice(&cur));
+  MultiSolve m;
+  m.ss.assign((size_t)ngpus, nullptr);
+  std::vector<ncclComm_t> comms((size_t)ngpus, nullptr);
+  std::vector<int> devs((size_t)ngpus);
+  for (int i = 0; i < ngpus; i++) devs[(size_t)i] = i;
+  auto bail = [&](int rc) {
+    for (size_t i = 0; i < comms.size(); i++)
+      if (comms[i] && !(m.ss[i] && m.ss[i]->comm == comms[i])) (void)ncclCommDestroy(comms[i]);
+    multi_destroy(m);
+    (void)hipSetDevice(cur);
+    return rc;
+  };
+  for (int i = 0; i < ngpus; i++) {
+    HIPCHK(hipSetDevice(i));
+    const int rc = gm_solver_create_shard(game, i, ngpus, &buf[i], &m.ss[(size_t)i]);
+    if (rc) return bail(fail(rc, "shard %d: %s", i, gm_last_error()));
+  }
+  const ncclResult_t r = ncclCommInitAll(comms.data(), ngpus, devs.data());
+  if (r != ncclSuccess) return bail(fail(GM_EHIP, "ncclCommInitAll: %s", ncclGetErrorString(r)));
+  for (int i = 0; i < ngpus; i++) {
+    gm_solver* sh = m.ss[(size_t)i];
+    sh->comm = comms[(size_t)i];
+    HIPCHK(hipSetDevice(i));
+    if (!sh->errg && hipMalloc((void**)&sh->errg, (size_t)ngpus * sizeof(u64)) != hipSuccess)
+      return bail(fail(GM_EHIP, "error-mask gather buffer"));
+  }
+  std::vector<gm_result> res((size_t)ngpus);
+  std::vector<int> rcs((size_t)ngpus, 0);
+  std::vector<std::string> msg((size_t)ngpus);
+  std::vector<std::thread> th;
+  for (int i = 0; i < ngpus; i++)
+    th.emplace_back([&, i]() {
+      if (hipSetDevice(i) != hipSuccess) {
+        rcs[(size_t)i] = GM_EHIP;
+        msg[(size_t)i] = "hipSetDevice";
+        return;
+      }
+      rcs[(size_t)i] = gm_solver_solve(m.ss[(size_t)i], &res[(size_t)i]);
+      if (rcs[(size_t)i]) msg[(size_t)i] = gm_last_error();
+    });
+  for (auto& t : th) t.join();
+  (void)hipSetDevice(cur);
+  for (int i = 0; i < ngpus; i++)
+    if (rcs[(size_t)i]) return bail(fail(rcs[(size_t)i], "shard %d: %s", i, msg[(size_t)i].c_str()));
+  *out = res[0];
+  std::lock_guard<std::mutex> lk(g_solved_mu);
+  g_multi[game] = std::move(m);
+  return 0;
+}
+
+int gm_plan_multi(int game, int ngpus, uint64_t positions, uint32_t flags, uint64_t max_table_bytes,
+                  gm_plan_t* plans) {
+  const Desc* d = get_game(game);
+  if (!d || !plans || ngpus < 1) return fail(GM_EINVAL, "bad argument");
+  if (ngpus == 1) return gm_plan(game, positions, flags, max_table_bytes, plans);
+  if (d->dense_ok) {  // sum games: PLANES (or level-major DENSE) blocks of the last heap
+    for (int r = 0; r < ngpus; r++) {
+      const int rc = gm_plan_shard(game, r, ngpus, flags, max_table_bytes, &plans[r]);
+      if (rc) return rc;
+    }
+    return 0;
+  }
+  if (!bk_ok(d)) return fail(GM_EINVAL, "%d GPUs in one process: the game needs a dense or bucketed shard layout "
+                                        "(keyed games of other shapes: one process per GPU, keyed.py)", ngpus);
+  if (positions == 0) {
+    gm_game_info(game, &positions, nullptr, nullptr);
+    if (positions == 0) return fail(GM_EINVAL, "no known position bound for this board; pass an estimate");
+  }
+  // the md5 shard bound of keyed._shard_bound: the share + 3 % + 64 K
+  const u64 per = (u64)((double)positions * 1.03) / (u64)ngpus + 65536;
+  for (int r = 0; r < ngpus; r++) {
+    const int rc = gm_plan_keyed_shard(game, r, ngpus, per, flags, max_table_bytes, &plans[r]);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
 int gm_solve(int game, uint64_t root, int ngpus, const gm_buffers* buf, gm_result* out) {
   const Desc* d = get_game(game);
   if (!d) return fail(GM_EINVAL, "bad game id %d", game);
-  if (ngpus != 1) return fail(GM_EINVAL, "gm_solve drives one GPU; run one process per GPU for sharded solves");
+  if (ngpus < 1 || !buf || !out) return fail(GM_EINVAL, "bad argument");
   if (root != d->root) return fail(GM_EINVAL, "root must be the game's initial position");
   (void)gm_release(game);
+  if (ngpus > 1) return solve_multi(game, ngpus, buf, out);
   gm_solver* s = nullptr;
   int rc = gm_solver_create(game, buf, &s);
   if (rc) return rc;
@@ -3687,7 +3819,12 @@ int gm_query(int game, const uint64_t* keys_dev, size_t n, uint32_t* words_dev) 
     auto it = g_solved.find(game);
     if (it != g_solved.end()) s = it->second;
   }
-  if (!s) return fail(GM_EINVAL, "game %d has no finished gm_solve to query", game);
+  if (!s) {
+    std::lock_guard<std::mutex> lk(g_solved_mu);
+    if (g_multi.count(game))
+      return fail(GM_EINVAL, "game %d was solved on several GPUs: query its shards (gm_solver_query per device)", game);
+    return fail(GM_EINVAL, "game %d has no finished gm_solve to query", game);
+  }
   int rc = gm_solver_query(s, keys_dev, (uint64_t)n, words_dev);
   if (rc) return rc;
   HIPCHK(hipStreamSynchronize(s->stream));
@@ -3696,14 +3833,22 @@ int gm_query(int game, const uint64_t* keys_dev, size_t n, uint32_t* words_dev) 
 
 int gm_release(int game) {
   gm_solver* s = nullptr;
+  MultiSolve m;
   {
     std::lock_guard<std::mutex> lk(g_solved_mu);
     auto it = g_solved.find(game);
-    if (it == g_solved.end()) return 0;
-    s = it->second;
-    g_solved.erase(it);
+    if (it != g_solved.end()) {
+      s = it->second;
+      g_solved.erase(it);
+    }
+    auto jt = g_multi.find(game);
+    if (jt != g_multi.end()) {
+      m = std::move(jt->second);
+      g_multi.erase(jt);
+    }
   }
-  gm_solver_destroy(s);
+  if (s) gm_solver_destroy(s);
+  multi_destroy(m);
   return 0;
 }
 

@@ -16,6 +16,7 @@ one enqueued solve (no host round trip per level).
                   geometry, for parity tests on a single device
 """
 import ctypes
+import types
 
 from . import _lib
 from .games import GameSpec
@@ -120,17 +121,21 @@ def plane_halo_plan(spec, rank, world, flags=0):
     return out
 
 
-def group_solve(spec, world, device=None, kernel_timing=False, flags=0, layout="auto"):
-    """Solve all `world` shards in this process (one GPU, one stream).
-    Returns (SolveResult of the whole job, [shard Solvers])."""
+def group_solve(spec, world, device=None, kernel_timing=False, flags=0, layout="auto", streams="one"):
+    """Solve all `world` shards in this process (one GPU).  streams="one":
+    every shard on one stream, halos copied in order (the parity path);
+    "own": every shard on a stream of its own -- the one-GPU rehearsal of
+    the RCCL staged schedule (send / receive streams, receive window,
+    events and joins of gm_plane_run.h's mode 1, device copies for the
+    transfers).  Returns (SolveResult of the whole job, [shard Solvers])."""
     import torch
     spec = spec if isinstance(spec, GameSpec) else GameSpec(*spec)
     dev = torch.device(device if device is not None else "cuda")
-    # one explicit stream for every shard (torch's default stream has handle
-    # 0, which the ABI reads as "library-owned stream per solver")
-    stream = torch.cuda.Stream(device=dev)
+    # explicit streams (torch's default stream has handle 0, which the ABI
+    # reads as "library-owned stream per solver")
+    ss = _group_streams(dev, world, streams)
     shards = [Solver(spec, device=dev, rank=g, world=world, layout=layout,
-                     kernel_timing=kernel_timing, stream=stream, flags=flags)
+                     kernel_timing=kernel_timing, stream=ss[g], flags=flags)
               for g in range(world)]
     arr = (ctypes.c_void_p * world)(*[s.handle.value for s in shards])
     r = _lib.gm_result()
@@ -138,3 +143,60 @@ def group_solve(spec, world, device=None, kernel_timing=False, flags=0, layout="
     with torch.cuda.device(dev):
         _lib.check(_lib.load().gm_solve_group(arr, world, ctypes.byref(r)))
     return shards[0]._result(r), shards
+
+
+def _group_streams(dev, world, streams):
+    import torch
+    if streams == "one":
+        return [torch.cuda.Stream(device=dev)] * int(world)
+    if streams == "own":
+        return [torch.cuda.Stream(device=dev) for _ in range(int(world))]
+    raise ValueError("streams: 'one' or 'own'")
+
+
+def plan_multi(spec, ngpus, positions=0, flags=0, max_table_bytes=0):
+    """The ngpus shard plans gm_solve(.., ngpus, ..) runs (host only): a
+    list of gm_plan_t, shard i for device i."""
+    spec = spec if isinstance(spec, GameSpec) else GameSpec(*spec)
+    plans = (_lib.gm_plan_t * int(ngpus))()
+    _lib.check(_lib.load().gm_plan_multi(spec.id, int(ngpus), int(positions), int(flags),
+                                         int(max_table_bytes), plans))
+    return list(plans)
+
+
+def solve_one_process(spec, ngpus, positions=0, flags=0):
+    """SURVEY §8b's gm_solve(game, root, ngpus, ..) from ONE process: shard
+    i on cuda:i (buffers from torch), one RCCL communicator per device and
+    one host thread per device inside the library.  The reference runs the
+    same job as `mpiexec -n P` (solver_launcher.py:30,76-84).  Returns the
+    whole job's SolveResult; the shards' buffers are kept alive until the
+    next solve of the game (gm_release)."""
+    import torch
+    spec = spec if isinstance(spec, GameSpec) else GameSpec(*spec)
+    plans = plan_multi(spec, ngpus, positions, flags)
+    L = _lib.load()
+    bufs = (_lib.gm_buffers * int(ngpus))()
+    keep = []
+    for i, plan in enumerate(plans):
+        dev = torch.device("cuda", i)
+        with torch.cuda.device(dev):
+            table = torch.empty(plan.table_bytes, dtype=torch.uint8, device=dev)
+            levels = torch.empty(max(1, plan.level_capacity), dtype=torch.int64, device=dev)
+            scratch = torch.empty(plan.scratch_bytes, dtype=torch.uint8, device=dev)
+        keep.append((table, levels, scratch))
+        b = bufs[i]
+        b.table, b.table_slots, b.table_bytes = table.data_ptr(), plan.table_slots, plan.table_bytes
+        b.levels, b.level_capacity = levels.data_ptr(), plan.level_capacity
+        b.scratch, b.scratch_bytes = scratch.data_ptr(), plan.scratch_bytes
+        b.stream, b.flags, b.mode = 0, int(flags), plan.mode
+    for i in range(int(ngpus)):
+        torch.cuda.synchronize(i)
+    r = _lib.gm_result()
+    _lib.check(L.gm_solve(spec.id, spec.root_key, int(ngpus), bufs, ctypes.byref(r)))
+    _KEEP[spec.id] = keep
+    res = Solver._result(types.SimpleNamespace(spec=spec, plan=plans[0]), r)
+    res.extra.update({"gpus": int(ngpus), "process": "one"})
+    return res
+
+
+_KEEP = {}  # game id -> the torch buffers of its last one-process multi-GPU solve

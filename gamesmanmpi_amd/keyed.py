@@ -355,8 +355,14 @@ def bucketed_shards_apply(spec, world):
 
 
 def _shard_bound(spec, world, positions):
-    """positions bound of one md5 shard (2x its share of the job's bound)"""
-    return 2 * int(positions or spec.positions_bound) // int(world) + 4096
+    """positions bound of one md5 shard: its share of the job's bound plus
+    3 % and 64 K.  md5 (src/game_state.py:22-30) is a uniform hash, so the
+    largest of W shards of P positions exceeds P / W by a few sqrt(P / W)
+    (tests/test_dist_cpu.py checks the bound against the owners of the
+    golden tables' positions); the 64 K floor covers small games.  Round 3
+    planned 2x the share, which put toot 6x4 on 4 shards of one GPU out of
+    memory."""
+    return int(int(positions or spec.positions_bound) * 1.03) // int(world) + 65536
 
 
 def _pick(spec, world, layout):
@@ -372,20 +378,25 @@ def _pick(spec, world, layout):
     return "hashed"
 
 
-def group_keyed_solve(spec, world, device=None, layout="auto", flags=0):
-    """Every md5 shard of a `world`-rank job in this process, on one GPU
-    and one stream.  layout "auto": md5-sharded BUCKETED levels where they
-    apply (the library's all-to-all level loop, gm_bucketed_shard.h), else
-    HASHED shards driven by keyed_solve.  Returns (SolveResult, shards):
-    Solvers (bucketed) or GpuShards (hashed), both with dump()."""
+def group_keyed_solve(spec, world, device=None, layout="auto", flags=0, streams="one"):
+    """Every md5 shard of a `world`-rank job in this process, on one GPU.
+    layout "auto": md5-sharded BUCKETED levels where they apply (the
+    library's all-to-all level loop, gm_bucketed_shard.h), else HASHED
+    shards driven by keyed_solve.  streams "one": every shard on one stream;
+    "own" (bucketed): each shard on a stream of its own, the all-to-alls as
+    device copies between them -- the one-GPU rehearsal of the RCCL
+    stream order.  Returns (SolveResult, shards): Solvers (bucketed) or
+    GpuShards (hashed), both with dump()."""
     import torch
+    from .dist import _group_streams
     spec = spec if isinstance(spec, GameSpec) else GameSpec(*spec)
     dev = torch.device(device if device is not None else "cuda")
-    stream = torch.cuda.Stream(device=dev)
+    ss = _group_streams(dev, world, streams)
+    stream = ss[0]
     if _pick(spec, world, layout) == "bucketed":
         per = _shard_bound(spec, world, 0)
         shards = [Solver(spec, positions=per, device=dev, layout="bucketed",
-                         rank=g, world=world, stream=stream, flags=flags)
+                         rank=g, world=world, stream=ss[g], flags=flags)
                   for g in range(world)]
         arr = (ctypes.c_void_p * world)(*[s.handle.value for s in shards])
         r = _lib.gm_result()

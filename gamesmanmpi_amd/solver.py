@@ -81,6 +81,9 @@ class Solver:
             raise ValueError("flags: kernel-family flags only (%#x)" % _lib.KERNEL_FLAGS)
         self.flags = int(flags)
         self.positions_hint = int(positions or self.spec.positions_bound)
+        # the layout planned: `layout`, except that "auto" falls back to the
+        # hashed table when a bucketed plan hits a layout limit (solve())
+        self._planned_layout = layout
         self._h = None
         self._bufs = None
         self._alloc(self.positions_hint)
@@ -92,7 +95,7 @@ class Solver:
         plan = _lib.gm_plan_t()
         flags = self.flags | {"hashed": _lib.GM_F_FORCE_HASHED | _lib.GM_F_HASH_TABLE,
                               "bucketed": _lib.GM_F_FORCE_HASHED,
-                              "dense": _lib.GM_F_LEVEL_MAJOR}.get(self.layout, 0)
+                              "dense": _lib.GM_F_LEVEL_MAJOR}.get(self._planned_layout, 0)
         if self.world > 1 and self.layout == "bucketed":
             # an md5 shard of bucketed levels: `positions` bounds this shard
             _lib.check(L.gm_plan_keyed_shard(self.spec.id, self.rank,
@@ -172,7 +175,8 @@ class Solver:
         r = _lib.gm_result()
         if self.world > 1:
             max_retries = 0  # shard tables are sized exactly
-        for attempt in range(max_retries + 1):
+        attempt = 0
+        while True:
             try:
                 with self.torch.cuda.device(self.device):
                     _lib.check(L.gm_solver_solve(self._h, ctypes.byref(r)))
@@ -180,7 +184,17 @@ class Solver:
             except _lib.TableFull:
                 if attempt == max_retries:
                     raise
+                attempt += 1
                 self.positions_hint *= 2
+                self._alloc(self.positions_hint)
+            except _lib.LayoutLimit:
+                # a bucketed level past 2^29 positions or a fine bucket past
+                # its LDS capacity: "auto" may use the hashed table instead
+                # (once); an explicit layout keeps the error
+                if (self.layout != "auto" or self._planned_layout != "auto" or self.world > 1
+                        or int(self.plan.mode) != _lib.GM_MODE_BUCKETED):
+                    raise
+                self._planned_layout = "hashed"
                 self._alloc(self.positions_hint)
         return self._result(r)
 

@@ -389,11 +389,24 @@ int gm_graph_solve(const uint8_t *prim_dev, const uint64_t *offsets_dev,
 /* One-shot pair: gm_solve creates a solver on the caller's
  * buffers and solves from the game's root; the solver is kept per game id
  * (the buffers must stay valid) until the next gm_solve of that game or
- * gm_release(game).  ngpus must be 1; multi-GPU runs are driven one process
- * per GPU by the Python host.  Replaces solver_launcher.py:68-72 (Process
- * construction + run). */
+ * gm_release(game).  Replaces solver_launcher.py:68-72 (Process
+ * construction + run) and the rank count of `mpiexec -n P`
+ * (solver_launcher.py:30,76-84).
+ * ngpus > 1: buf points to ngpus gm_buffers, buf[i] allocated on device i
+ * with the sizes gm_plan_multi gives for shard i; the library makes one RCCL
+ * communicator per device (ncclCommInitAll) and drives every shard from its
+ * own host thread; *out holds the whole job's counts and root.  GM_EINVAL
+ * when fewer than ngpus devices are visible.  gm_query serves one-GPU
+ * solves (shards: gm_solver_query per device). */
 int gm_solve(int game, uint64_t root, int ngpus, const gm_buffers *buf,
              gm_result *out);
+/* Plans of the ngpus shards gm_solve(.., ngpus, ..) runs, plans[0..ngpus):
+ * ngpus 1 is gm_plan; sum games: gm_plan_shard per rank (PLANES blocks of
+ * the last heap, or level-major DENSE); keyed games whose moves advance one
+ * level: gm_plan_keyed_shard per rank, each bounded by its md5 share of
+ * `positions` (0: the board's own count) + 3 % + 64 K.  Host only. */
+int gm_plan_multi(int game, int ngpus, uint64_t positions, uint32_t flags,
+                  uint64_t max_table_bytes, gm_plan_t *plans);
 /* words_dev[i] = word of keys_dev[i] in the table of the game's last
  * gm_solve (GM_NO_WORD if unreachable); device pointers, synchronous.
  * Replaces the resolved/remote CacheDict lookups (src/cache_dict.py:62-79). */

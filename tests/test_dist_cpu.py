@@ -77,3 +77,92 @@ def test_gloo_bootstrap_and_geometry(world, params):
         # bench shape: 2^30 positions per GPU, blocks of 8, four per rank
         assert (B, nblocks, Z) == (8, 4 * world, 32 ** 4)
         assert all(i["nb"] == 4 for i in infos)
+
+
+@pytest.mark.parametrize("case,params", [("toot_4x3", "length=4,height=3"),
+                                         ("othello_4x4", "length=4,height=4")])
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_md5_shard_bound_holds_every_shard(case, params, world):
+    """keyed._shard_bound (the positions one md5 shard is planned for) covers
+    the largest shard of the golden table's positions, per level too, and
+    gm_plan_keyed_shard scales the shard's edge bound with its share (round
+    3 planned every shard for the whole board's edges)."""
+    import ctypes
+    import numpy as np
+    from conftest import load_table
+    from gamesmanmpi_amd import _lib, keyed
+    from gamesmanmpi_amd.games import GameSpec
+    name = "toot_and_otto_bitstring" if case.startswith("toot") else "othello_bit_new"
+    spec = GameSpec(name, params)
+    t = load_table(case)
+    keys = spec.encode_batch(t["canon"], t["clen"])
+    own = spec.owners_host(keys, world)
+    sizes = np.bincount(own, minlength=world)
+    bound = keyed._shard_bound(spec, world, len(keys))
+    assert sizes.max() <= bound and sizes.sum() == len(keys)
+    # the uniform-hash spread the 3 % slack is for: a few sqrt of the share
+    share = len(keys) / world
+    assert sizes.max() - share < 6 * share ** 0.5 + 16
+    for lv in np.unique(t["level"]):
+        m = t["level"] == lv
+        per = np.bincount(own[m], minlength=world)
+        assert per.max() - m.sum() / world < 6 * (m.sum() / world) ** 0.5 + 16
+    # edges: a shard of half the positions is planned for about half the edges
+    full, half = _lib.gm_plan_t(), _lib.gm_plan_t()
+    P = len(keys)
+    _lib.check(_lib.load().gm_plan_keyed_shard(spec.id, 0, world, P, 0, 0, ctypes.byref(full)))
+    _lib.check(_lib.load().gm_plan_keyed_shard(spec.id, 0, world, P // 2, 0, 0, ctypes.byref(half)))
+    assert half.table_slots < 0.6 * full.table_slots + 2048
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_plan_multi_sum_bench_shapes(n):
+    """gm_plan_multi for the bench's N-GPU workloads (31^5 x (32N - 1)):
+    N PLANES shards of the staged deal, about equal in size, each about the 2^30
+    one-table plan (the sizes gm_solve(.., ngpus = N, ..) allocates)."""
+    from gamesmanmpi_amd import _lib, dist as gdist
+    from gamesmanmpi_amd.games import GameSpec
+    spec = GameSpec("sum_four_to_one", "heaps=" + ":".join(["31"] * 5 + [str(32 * n - 1)]))
+    plans = gdist.plan_multi(spec, n)
+    assert len(plans) == n
+    assert {int(p.mode) for p in plans} == {_lib.GM_MODE_PLANES}
+    sizes = [int(p.table_bytes) for p in plans]  # the end ranks carry one halo fewer
+    assert max(sizes) <= 1.1 * min(sizes)
+    one = gdist.plan_multi(GameSpec("sum_four_to_one", "heaps=" + ":".join(["31"] * 6)), 1)[0]
+    assert int(one.mode) == _lib.GM_MODE_PLANES
+    # a shard holds 2^30 positions (1 GiB of 8- or 16-bit words + bits + halo rows)
+    assert one.table_bytes <= plans[0].table_bytes <= 2.5 * one.table_bytes
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_plan_multi_keyed_shards_fit_together(n):
+    """toot 6x4 (BASELINE config 3's board) on n md5 shards: every shard's
+    plan is about 1/n of the job, so the n shards together stay near the
+    one-table plan (round 3: each shard planned for the whole board's
+    edges, 4 shards > 288 GB)."""
+    from gamesmanmpi_amd import _lib, dist as gdist
+    from gamesmanmpi_amd.games import GameSpec
+    spec = GameSpec("toot_and_otto_bitstring", "length=6,height=4")
+    plans = gdist.plan_multi(spec, n)
+    one = gdist.plan_multi(spec, 1)[0]
+    assert {int(p.mode) for p in plans} == {_lib.GM_MODE_BUCKETED}
+    total = sum(int(p.table_bytes) + 8 * int(p.level_capacity) for p in plans)
+    single = int(one.table_bytes) + 8 * int(one.level_capacity)
+    assert total < 2.3 * single, (total / 2 ** 30, single / 2 ** 30)
+    assert total < 250 * 2 ** 30  # n shards fit one MI355X as an in-process group
+
+
+def test_gm_solve_more_gpus_than_visible_is_an_error():
+    """gm_solve(.., ngpus, ..) with more GPUs than the process sees fails
+    with GM_EINVAL before touching any buffer (this box sees none)."""
+    import ctypes
+    from gamesmanmpi_amd import _lib
+    from gamesmanmpi_amd.games import GameSpec
+    spec = GameSpec("sum_four_to_one", "heaps=31:31:31:63")
+    bufs = (_lib.gm_buffers * 2)()
+    r = _lib.gm_result()
+    L = _lib.load()
+    rc = L.gm_solve(spec.id, spec.root_key, 2, bufs, ctypes.byref(r))
+    assert rc == _lib.GM_EINVAL
+    assert b"visible" in L.gm_last_error()
+    assert L.gm_solve(spec.id, spec.root_key, 0, bufs, ctypes.byref(r)) == _lib.GM_EINVAL

@@ -89,7 +89,7 @@ def test_gpu_sum_31x6_checksum():
     _check("sum_31x6", layout="dense")
 
 
-def _check_group(name, world):
+def _check_group(name, world, streams="one"):
     """The N-GPU bench shape (PLANES shards: round-robin blocks of 8 values of
     the last heap), all `world` shards solved in this process
     (dist.group_solve: the halo exchange runs device-to-device on one
@@ -98,7 +98,7 @@ def _check_group(name, world):
     from gamesmanmpi_amd.dist import group_solve
     from gamesmanmpi_amd.games import GameSpec
     e = _gold(name)
-    r, shards = group_solve(GameSpec(e["game"], e["params"]), world)
+    r, shards = group_solve(GameSpec(e["game"], e["params"]), world, streams=streams)
     assert r.extra["layout"] == "planes"
     assert (r.positions, r.edges, r.primitives) == (e["positions"], e["edges"], e["primitives"])
     assert r.root_line == e["root_line"]
@@ -162,5 +162,35 @@ def test_gpu_toot_6x4_two_md5_shards_checksum():
     assert sum(c["positions"] for c in cks) == e["positions"]
     assert (sum(c["win"] for c in cks), sum(c["loss"] for c in cks), sum(c["tie"] for c in cks)) == (
         e["win"], e["loss"], e["tie"])
+    del shards
+    torch.cuda.empty_cache()
+
+
+# The one-GPU rehearsal of the RCCL staged schedule (gm_plane_run.h mode 4):
+# every shard on a stream of its own with mode 1's send / receive streams,
+# receives posted ahead, SE / RE events and end-of-solve joins; a device copy
+# on the receiver's stream stands in for each ncclSend / ncclRecv pair.
+@pytest.mark.parametrize("name,world", [("sum_31x5_63", 2), ("sum_31x5_127", 4), ("sum_31x5_255", 8)])
+def test_gpu_planes_staged_rccl_rehearsal(name, world):
+    import torch
+    _check_group(name, world, streams="own")
+    torch.cuda.empty_cache()
+
+
+def test_gpu_toot_6x4_four_md5_shards_checksum():
+    """toot 6x4 on FOUR md5 shards as an in-process group (round 3: out of
+    memory -- every shard was planned for the whole board's edges); the
+    shards' fingerprints add up to the golden."""
+    import torch
+    from gamesmanmpi_amd.games import GameSpec
+    from gamesmanmpi_amd.keyed import group_keyed_solve
+    e = _gold("toot_6x4")
+    r, shards = group_keyed_solve(GameSpec(e["game"], e["params"]), 4)
+    assert r.extra["layout"] == "bucketed"
+    assert (r.positions, r.edges, r.primitives, r.root_line) == (e["positions"], e["edges"], e["primitives"],
+                                                                  e["root_line"])
+    cks = [s.checksum() for s in shards]
+    assert "%016x" % (sum(int(c["checksum"], 16) for c in cks) % (1 << 64)) == e["checksum"]
+    assert sum(c["positions"] for c in cks) == e["positions"]
     del shards
     torch.cuda.empty_cache()

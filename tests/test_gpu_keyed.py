@@ -202,3 +202,19 @@ def test_gpu_kernel_timing_toggles_on_explicit_layouts(layout):
     s.set_kernel_timing(False)
     assert (r0.positions, r0.edges, r0.root_line) == (r1.positions, r1.edges, r1.root_line)
     assert r1.n_resolve_launches > 0
+
+
+@pytest.mark.parametrize("name,world,flags", [("othello_4x4", 8, 0), ("othello_4x4", 8, LOCAL), ("toot_4x3", 3, 0),
+                                              ("toot_4x3", 5, LOCAL)])
+def test_gpu_group_keyed_rccl_stream_rehearsal(name, world, flags, golden_summary):
+    """The md5 all-to-alls' RCCL stream order rehearsed on one GPU
+    (gm_bucketed_shard.h mode 4): every shard on a stream of its own, its
+    kernels and copies there as one rank's would be, each all-to-all as
+    device copies on the receivers' streams behind every sender's ready
+    event, then every stream behind every receiver's -- BASELINE config 5
+    (othello 4x4 on 8 md5 shards) against the reference-generated table."""
+    from gamesmanmpi_amd.games import GameSpec
+    from gamesmanmpi_amd.keyed import group_keyed_solve
+    r, shards = group_keyed_solve(GameSpec(*CASES[name]), world, flags=flags, streams="own")
+    assert r.extra["layout"] == "bucketed"
+    _check_golden_shards(name, r, shards, world, golden_summary)

@@ -194,3 +194,37 @@ def test_gpu_one_shot_solve_and_query(name, golden_summary):
     np.testing.assert_array_equal(w >> 2, t["remoteness"])
     _lib.check(L.gm_release(spec.id))
     assert L.gm_query(spec.id, kd.data_ptr(), len(keys), wd.data_ptr()) == _lib.GM_EINVAL
+
+
+@pytest.mark.gpu
+def test_gpu_one_process_multi_gpu_solve():
+    """gm_solve(game, root, ngpus, buf[ngpus]) from one process: with every
+    visible GPU (the driver's 8-GPU node) the sum bench shape of that many
+    GPUs solves to the closed-form counts and root value; with more GPUs than
+    visible it fails with GM_EINVAL before any allocation (a one-GPU box
+    runs only this half)."""
+    import ctypes
+    import torch
+    from gamesmanmpi_amd import _lib, dist as gdist
+    from gamesmanmpi_amd.games import GameSpec
+    n = torch.cuda.device_count()
+    L = _lib.load()
+    spec = GameSpec("sum_four_to_one", "heaps=31:31:31:%d" % (32 * (n + 1) - 1))
+    bufs = (_lib.gm_buffers * (n + 1))()
+    r = _lib.gm_result()
+    assert L.gm_solve(spec.id, spec.root_key, n + 1, bufs, ctypes.byref(r)) == _lib.GM_EINVAL
+    assert b"visible" in L.gm_last_error()
+    if n < 2:
+        return
+    heaps = [31, 31, 31, 32 * n - 1]
+    spec = GameSpec("sum_four_to_one", "heaps=" + ":".join(map(str, heaps)))
+    res = gdist.solve_one_process(spec, n)
+    P = 1
+    for h in heaps:
+        P *= h + 1
+    assert res.positions == P
+    g = 0
+    for h in heaps:
+        g ^= h % 3
+    assert res.root_value == (1 if g == 0 else 0)  # Sprague-Grundy: LOSS iff the XOR of h mod 3 is 0
+    _lib.check(L.gm_release(spec.id))

@@ -1,0 +1,21 @@
+#!/bin/bash
+# Runs tools/plane_lab over a list of "[ENV=..] K variant reps level_times"
+# argument sets, each under its own time limit; output to
+# gpurun_out/lab_<tag>.log.  Usage (GPU box):
+#   bash tools/lab_run.sh TAG "6 0 10 1" "LAB_ORDER=4 6 1 10 0" ...
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+mkdir -p gpurun_out
+tag=$1
+shift
+log=gpurun_out/lab_$tag.log
+: > "$log"
+for a in "$@"; do
+  echo "== plane_lab $a" >> "$log"
+  envs=()
+  set -- $a
+  while [[ "$1" == *=* ]]; do envs+=("$1"); shift; done
+  timeout -k 10 120 env "${envs[@]}" ./tools/plane_lab "$@" >> "$log" 2>&1
+  rc=$?
+  if [ $rc -ne 0 ] && [ $rc -ne 2 ]; then echo "plane_lab $a: exit $rc" >> "$log"; cat "$log"; exit $rc; fi
+done
+cat "$log"
