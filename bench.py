@@ -138,11 +138,23 @@ def keyed_bytes(positions, edges):
     return 24 * positions + 8 * edges, 12 * positions + 12 * edges
 
 
-def pmc_traffic(kernel, workload):
-    """HBM bytes per launch of `kernel` from the committed PMC summary
-    (profiles/pmc_traffic.json, tools/pmc_summary.py --traffic over separate
-    rocprofv3 --pmc passes of this bench), or None when no pass of this
-    workload and kernel is recorded."""
+def _kernel_sources_sha16():
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    try:
+        from pmc_summary import kernel_sources_sha16
+        return kernel_sources_sha16(ROOT)
+    except (ImportError, OSError):
+        return None
+    finally:
+        sys.path.pop(0)
+
+
+def _pmc_row(kernel, workload):
+    """The committed PMC summary's row for `kernel` (profiles/pmc_traffic.json,
+    tools/pmc_summary.py --traffic over separate rocprofv3 --pmc passes of
+    this bench) and a note: None when no pass of this workload and kernel is
+    recorded, or when the kernel sources changed since the passes ran (the
+    counters describe other code: rerun tools/gpu_session.sh TAG pmc)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as fh:
@@ -151,19 +163,25 @@ def pmc_traffic(kernel, workload):
         return None, None
     if not row or row.get("workload") != workload:
         return None, None
-    return row["bytes_per_launch"], "profiles/pmc_traffic.json (%s)" % row.get("source", "?")
+    now = _kernel_sources_sha16()
+    if row.get("kernel_sources_sha16") != now:
+        return None, "stale: profiles/pmc_traffic.json (%s) measured kernel sources %s, these are %s" % (
+            row.get("source", "?"), row.get("kernel_sources_sha16"), now)
+    return row, "profiles/pmc_traffic.json (%s, kernel sources %s)" % (row.get("source", "?"), now)
+
+
+def pmc_traffic(kernel, workload):
+    """HBM bytes per launch of `kernel` from the committed PMC summary, or
+    None (see _pmc_row), and where the figure comes from."""
+    row, note = _pmc_row(kernel, workload)
+    return (row["bytes_per_launch"] if row else None), note
 
 
 def pmc_traffic_total(kernel, workload):
     """(HBM bytes per launch, launches per solve) of `kernel` from the
     committed PMC summary, or (None, 0)."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    try:
-        with open(path) as fh:
-            row = json.load(fh).get(kernel)
-    except (OSError, ValueError):
-        return None, 0
-    if not row or row.get("workload") != workload:
+    row, _ = _pmc_row(kernel, workload)
+    if not row:
         return None, 0
     return row["bytes_per_launch"], row.get("launches", 0)
 

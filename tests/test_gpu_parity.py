@@ -155,11 +155,13 @@ def test_gpu_full_size_synthetic_properties():
     _sprague_grundy_check(keys, (w & 3).astype(np.uint8), heaps)
 
 
-@pytest.mark.parametrize("name", ["tic_tac_toe_np", "othello_4x4", "sum_fto_6_6_6_6"])
+@pytest.mark.parametrize("name", ["tic_tac_toe_np", "othello_4x4", "sum_fto_6_6_6_6", "toot_4x3"])
 def test_gpu_one_shot_solve_and_query(name, golden_summary):
     """SURVEY §8b's one-shot pair: gm_solve(game, root, 1, buffers) then
     gm_query(game, keys, n, words) on the table it keeps, every golden
-    position's word bit-exact; gm_release drops it and a query then fails."""
+    position's word bit-exact (toot 4x3 and tic-tac-toe on BUCKETED levels:
+    the home-slot search of k_bk_query); gm_release drops it and a query then
+    fails."""
     import ctypes
     import torch
     from gamesmanmpi_amd import _lib

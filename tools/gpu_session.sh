@@ -7,7 +7,7 @@
 #   smoke          __graft_entry__.smoke()                        -> TAG_smoke.log
 #   bench          python bench.py --steps 20 --warmup 5          -> TAG_bench.json
 #   prof           rocprofv3 --kernel-trace --stats of a short bench -> TAG_prof/
-#   pmc            the PMC passes of one bench step (tools/pmc_passes.sh) -> TAG_pmc/
+#   pmc            the PMC passes of one bench step (tools/pmc_passes.sh) -> TAG_pmc/, TAG_pmc_traffic.json
 #   groups         per-shard PLANES group timings, N = 2 4 8 (tools/group_planes.py)
 #   keyed[:B]      toot B (default 6x4) md5 group timings, N = 1 2 4 (tools/group_keyed_time.py)
 # Replaces the round-by-round session scripts (tools/gpu_r0*.sh).
@@ -39,8 +39,10 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d ${o}_prof -o run \
         -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > ${o}_prof.log 2>&1 || fail prof ${o}_prof.log
       python3 tools/kstats.py $(find ${o}_prof -name '*kernel_stats.csv' | head -1) | head -20 ;;
-    pmc)
+    pmc)  # + the per-launch traffic bench.py reads (copy it to profiles/pmc_traffic.json)
       bash tools/pmc_passes.sh ${o}_pmc > ${o}_pmc.log 2>&1 || fail pmc ${o}_pmc.log
+      python3 tools/pmc_summary.py --traffic "sum_four_to_one heaps=31:31:31:31:31:31" ${o}_pmc_traffic.json \
+        ${o}_pmc > /dev/null || fail pmc-summary ${o}_pmc.log
       tail -3 ${o}_pmc.log ;;
     groups)
       for w in 2 4 8; do

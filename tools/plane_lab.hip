@@ -42,7 +42,7 @@ template <int NO, int DIAG, bool LEAN, bool OPQ = false, int MINW = 1>
 __global__ __launch_bounds__(256, MINW) void lab_x2(uint8_t* __restrict__ tab, const uint32_t* __restrict__ list,
                                                     uint32_t n, PlaneGeom g, const uint4* __restrict__ zero,
                                                     uint64_t* __restrict__ stamps = nullptr) {
-  uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+  uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, items = 0;
   if (DIAG == 5) t0 = __builtin_amdgcn_s_memtime();
   const PlaneShare sh = plane_share(n, 4);
   const uint32_t lane = threadIdx.x & 63, L = lane & 31;
@@ -53,7 +53,8 @@ __global__ __launch_bounds__(256, MINW) void lab_x2(uint8_t* __restrict__ tab, c
     const uint32_t px = list[livex ? ix : i0], py = list[livey ? iy : i0];
     if (DIAG == 5) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      t1 = __builtin_amdgcn_s_memtime() + (px & 0 ? 1 : 0);
+      if (!items) t1 = __builtin_amdgcn_s_memtime() + (px & 0 ? 1 : 0);
+      items++;
     }
     uint32_t dx[NO > 0 ? NO : 1], dy[NO > 0 ? NO : 1];
     plane_digits<NO>(g, px, dx);
@@ -92,7 +93,7 @@ __global__ __launch_bounds__(256, MINW) void lab_x2(uint8_t* __restrict__ tab, c
         }
       }
     }
-    if (DIAG == 5) {
+    if (DIAG == 5 && items == 1) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       t2 = __builtin_amdgcn_s_memtime();
     }
@@ -165,7 +166,7 @@ __global__ __launch_bounds__(256, MINW) void lab_x2(uint8_t* __restrict__ tab, c
       p[0] = make_uint4(o[0], o[1], o[2], o[3]);
       p[1] = make_uint4(o[4], o[5], o[6], o[7]);
     };
-    if (DIAG == 5) t3 = __builtin_amdgcn_s_memtime() + (ox_[0] & 0 ? 1 : 0);
+    if (DIAG == 5 && items == 1) t3 = __builtin_amdgcn_s_memtime() + (ox_[0] & 0 ? 1 : 0);
     if (livex) store(tab + ox, ox_);
     if (livey) store(tab + oy, oy_);
   }
@@ -173,14 +174,14 @@ __global__ __launch_bounds__(256, MINW) void lab_x2(uint8_t* __restrict__ tab, c
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint64_t t4 = __builtin_amdgcn_s_memtime();
     const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    if ((threadIdx.x & 63) == 0 && w < 65536) {
+    if ((threadIdx.x & 63) == 0 && w < 65536 && items) {
       uint64_t* o = stamps + (size_t)w * 6;
       o[0] = t0;
       o[1] = t1;
       o[2] = t2;
       o[3] = t3;
       o[4] = t4;
-      o[5] = __builtin_amdgcn_s_memrealtime();
+      o[5] = items;
     }
   }
 }
@@ -287,32 +288,33 @@ int main(int argc, char** argv) {
   for (auto& evt : ev) CK(hipEventCreate(&evt));
   if (var == 15) CK(hipMalloc(&g_stamps, 65536 * 6 * 8));
   std::vector<uint64_t> hst(65536 * 6);
-  auto trace = [&](int s) {  // per-wave stamps of level s's launch (variant 15)
+  auto trace = [&](int s) {  // per-wave stamps of level s's launch (variant 15): first item's phases
     CK(hipStreamSynchronize(st));
     CK(hipMemcpy(hst.data(), g_stamps, hst.size() * 8, hipMemcpyDeviceToHost));
-    const uint32_t waves = std::min<uint32_t>((cnt[s] + 3) / 4, 65536);
-    uint64_t t0min = ~0ull, t4max = 0, r0 = ~0ull, r1 = 0;
-    double a[4] = {0, 0, 0, 0};
-    uint32_t nw = 0;
+    std::vector<double> ph[5];  // start offset, list, fold, wavefront, (store + later items)
+    uint64_t t0min = ~0ull, t4max = 0, multi = 0;
     for (uint32_t w = 0; w < 65536; w++) {
       const uint64_t* o = &hst[(size_t)w * 6];
-      if (!o[0]) continue;
-      nw++;
+      if (!o[5]) continue;
       t0min = std::min(t0min, o[0]);
       t4max = std::max(t4max, o[4]);
-      r0 = std::min(r0, o[5]);
-      r1 = std::max(r1, o[5]);
-      for (int i = 0; i < 4; i++) a[i] += (double)(o[i + 1] - o[i]);
+      multi += o[5] > 1;
     }
-    // ramp: when the waves start relative to the first one
-    std::vector<uint64_t> starts;
-    for (uint32_t w = 0; w < 65536; w++)
-      if (hst[(size_t)w * 6]) starts.push_back(hst[(size_t)w * 6] - t0min);
-    std::sort(starts.begin(), starts.end());
-    printf("trace level %d planes %u waves %u (stamped %u): cycles list %.0f fold %.0f wavefront %.0f store %.0f; span %llu cycles, start p50 %llu p90 %llu max %llu\n",
-           s, cnt[s], waves, nw, a[0] / nw, a[1] / nw, a[2] / nw, a[3] / nw, (unsigned long long)(t4max - t0min),
-           (unsigned long long)starts[starts.size() / 2], (unsigned long long)starts[starts.size() * 9 / 10],
-           (unsigned long long)starts.back());
+    for (uint32_t w = 0; w < 65536; w++) {
+      const uint64_t* o = &hst[(size_t)w * 6];
+      if (!o[5]) continue;
+      ph[0].push_back((double)(o[0] - t0min));
+      for (int k = 1; k < 5; k++) ph[k].push_back((double)(o[k] - o[k - 1]));
+    }
+    auto q = [](std::vector<double>& v, double f) {
+      std::sort(v.begin(), v.end());
+      return v[(size_t)std::min<double>(v.size() - 1, f * v.size())];
+    };
+    const char* nm[5] = {"start", "list", "fold", "wavefront", "store+rest"};
+    printf("trace level %d: %u planes, %zu waves (%llu with >1 item), span %llu cycles;", s, cnt[s], ph[0].size(),
+           (unsigned long long)multi, (unsigned long long)(t4max - t0min));
+    for (int k = 0; k < 5; k++) printf(" %s p50 %.0f p90 %.0f max %.0f;", nm[k], q(ph[k], 0.5), q(ph[k], 0.9), q(ph[k], 1.0));
+    printf("\n");
   };
   const char* tl = getenv("LAB_TRACE");  // levels to trace, "10,40,62"
   std::vector<int> traced;

@@ -32,9 +32,25 @@ def load(root):
     return per, launches
 
 
+KERNEL_SOURCES = ("gamesmanmpi_amd/csrc/gm_plane.h", "gamesmanmpi_amd/csrc/gm_plane_run.h",
+                  "gamesmanmpi_amd/csrc/gm_dense.h")
+
+
+def kernel_sources_sha16(root_dir):
+    """Fingerprint of the kernel sources the PMC passes measured: bench.py
+    reports the counter traffic only while its own sources still match."""
+    import hashlib
+    h = hashlib.sha256()
+    for rel in KERNEL_SOURCES:
+        with open(os.path.join(root_dir, rel), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def traffic(workload, out_path, root):
     per, launches = load(root)
     res = {}
+    src_sha = kernel_sources_sha16(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     for name, ctr in per.items():
         if "FETCH_SIZE" not in ctr or "WRITE_SIZE" not in ctr:
             continue
@@ -44,7 +60,7 @@ def traffic(workload, out_path, root):
         w = ctr["WRITE_SIZE"] * 1024 / n
         row = {"workload": workload, "bytes_per_launch": f + w,
                "fetch_bytes_per_launch": f, "write_bytes_per_launch": w,
-               "launches": n, "source": root}
+               "launches": n, "source": root, "kernel_sources_sha16": src_sha}
         if "TCC_HIT_sum" in ctr:
             row["l2_hit_rate"] = ctr["TCC_HIT_sum"] / max(1.0, ctr["TCC_HIT_sum"] + ctr["TCC_MISS_sum"])
         res[short] = row
