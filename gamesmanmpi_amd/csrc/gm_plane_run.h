@@ -647,12 +647,12 @@ static void plane_no_dispatch(uint32_t no, F&& f) {
     default: f(std::integral_constant<int, 6>()); break;
   }
 }
-static void plane_reach_launch(gm_solver* s) {
+static void plane_reach_launch(gm_solver* s, hipStream_t stream = nullptr) {
   const u64 nq = (u64)s->pg.nplanes * 8u;  // one thread per four row words
   const int grid = (int)std::max<u64>(1, std::min<u64>((nq + 255) / 256, (u64)std::min(s->grid, kCountSlots)));
   plane_no_dispatch(s->pg.no, [&](auto NO) {
-    hipLaunchKernelGGL((k_plane_reach<decltype(NO)::value>), dim3(grid), dim3(256), 0, s->stream, s->pbits, s->pg,
-                       s->bcount, s->st, 8u * s->pwb);
+    hipLaunchKernelGGL((k_plane_reach<decltype(NO)::value>), dim3(grid), dim3(256), 0, stream ? stream : s->stream,
+                       s->pbits, s->pg, s->bcount, s->st, 8u * s->pwb);
   });
 }
 
@@ -1115,26 +1115,39 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
       }
     return 0;
   };
+  // One table, whole solve: the forward -- state and count-slot resets,
+  // reach map + counts -- runs on a side stream BESIDE the backward, which
+  // never reads any of it (a plane's words follow from its neighbours'
+  // words alone); the finish kernel waits for both.  The reach launch then
+  // overlaps the first, narrow plane levels instead of preceding them.
+  const bool overlap = mode == 0 && first == 0 && stop == 2 * T && !timing;
+  hipStream_t fs = st;  // the forward's stream
+  if (overlap) {
+    if (!s0->cstream) HIPCHK(hipStreamCreateWithFlags(&s0->cstream, hipStreamNonBlocking));
+    fs = s0->cstream;
+  }
   auto t0 = std::chrono::steady_clock::now();
   HIPCHK(hipEventRecord(e0, st));
+  if (overlap) HIPCHK(hipStreamWaitEvent(fs, e0, 0));
   if (fork()) return GM_EHIP;
   if (first == 0) {
     for (gm_solver* s : ss) {
-      HIPCHK(hipMemsetAsync(s->st, 0, devstate_bytes(T), s->stream));
-      HIPCHK(hipMemsetAsync(s->bcount, 0, kCountSlots * sizeof(BlockCount), s->stream));
+      hipStream_t ws = overlap ? fs : s->stream;
+      HIPCHK(hipMemsetAsync(s->st, 0, devstate_bytes(T), ws));
+      HIPCHK(hipMemsetAsync(s->bcount, 0, kCountSlots * sizeof(BlockCount), ws));
       // the word width: written by k_plane_reach below (no reach: here)
-      if (stop == 0) HIPCHK(hipMemsetD32Async((hipDeviceptr_t)&s->st->word_bits, (int)(8 * s->pwb), 1, s->stream));
+      if (stop == 0) HIPCHK(hipMemsetD32Async((hipDeviceptr_t)&s->st->word_bits, (int)(8 * s->pwb), 1, ws));
     }
     if (stop > 0) {
       if (timing) HIPCHK(hipEventRecord(kx[0], st));
-      for (gm_solver* s : ss) plane_reach_launch(s);
+      for (gm_solver* s : ss) plane_reach_launch(s, overlap ? fs : nullptr);
       if (timing && join()) return GM_EHIP;
       if (timing) HIPCHK(hipEventRecord(kx[1], st));
     }
   }
   HIPCHK(hipGetLastError());
   if (join()) return GM_EHIP;
-  HIPCHK(hipEventRecord(e1, st));
+  HIPCHK(hipEventRecord(e1, fs));  // overlap: the forward's end on its own stream
   if (fork()) return GM_EHIP;
   // kernel timing: one table -- the backward is nothing but the resolve
   // launches, so one event pair around all of them (no events between
@@ -1213,6 +1226,7 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
   HIPCHK(hipGetLastError());
   if (join()) return GM_EHIP;
   HIPCHK(hipEventRecord(e2, st));
+  if (overlap) HIPCHK(hipStreamWaitEvent(st, e1, 0));  // the counts and state resets before the finish
   if (stop < 2 * T) {
     HIPCHK(hipStreamSynchronize(st));
     cleanup();
@@ -1261,7 +1275,7 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
   auto t1 = std::chrono::steady_clock::now();
   float f = 0, b = 0;
   HIPCHK(hipEventElapsedTime(&f, e0, e1));
-  HIPCHK(hipEventElapsedTime(&b, e1, e2));
+  HIPCHK(hipEventElapsedTime(&b, overlap ? e0 : e1, e2));  // overlap: both phases start at e0
   out->ms_forward = f;
   out->ms_backward = b;
   out->ms_total = std::chrono::duration<double, std::milli>(t1 - t0).count();

@@ -38,7 +38,7 @@ using namespace gm;
 // without the lane-32 masks (lane 31's idle steps already read 0 there), the
 // in-lane and lane-below-by-two children folded off the chain first, and the
 // active-row mask one bit extract of a per-lane word.
-template <int NO, int DIAG, bool LEAN, bool OPQ = false, int MINW = 1>
+template <int NO, int DIAG, bool LEAN, bool OPQ = false, int MINW = 1, bool ELDS = false, bool IMAX = false>
 __global__ __launch_bounds__(256, MINW) void lab_x2(uint8_t* __restrict__ tab, const uint32_t* __restrict__ list,
                                                     uint32_t n, PlaneGeom g, const uint4* __restrict__ zero,
                                                     uint64_t* __restrict__ stamps = nullptr) {
@@ -105,6 +105,20 @@ __global__ __launch_bounds__(256, MINW) void lab_x2(uint8_t* __restrict__ tab, c
         oy_[k] = Yh[k] | (Yl[k] >> 8);
       }
     } else {
+      // ELDS: the folded E rows go to LDS as interleaved bytes [X0 Y0 X1 Y1
+      // ...] (64 B per lane, 4 KiB per wave) and come back 4 steps at a time
+      // during the wavefront, so the 32 E registers die before it starts
+      __shared__ uint2 elds[ELDS ? 4 * 8 * 64 : 1];  // [wave][quad of steps][lane]
+      uint2* ew = elds + (threadIdx.x >> 6) * (8 * 64) + (threadIdx.x & 63);
+      if (ELDS) {
+#pragma unroll
+        for (int d = 0; d < 8; d++) {
+          // bytes 0-3 of X's and Y's rows at dword d: even bytes from the
+          // high bytes of the low-shifted fold, odd bytes from the other
+          const uint32_t xb = perm(Xh[d], Xl[d], 0x07030501u), yb = perm(Yh[d], Yl[d], 0x07030501u);
+          ew[d * 64] = make_uint2(perm(yb, xb, 0x05010400u), perm(yb, xb, 0x07030602u));
+        }
+      }
       const uint32_t primv = L == 0 ? ((px == 0 ? 0xFFu : 0u) | (py == 0 ? 0xFFu << 16 : 0u)) : 0u;
       uint32_t cur = 0, prev = 0, u1p = 0;
       uint32_t op[32];
@@ -119,14 +133,32 @@ __global__ __launch_bounds__(256, MINW) void lab_x2(uint8_t* __restrict__ tab, c
 #pragma unroll
           for (int d = 0; d < 8; d++) asm volatile("" : "+v"(Xh[d]), "+v"(Xl[d]), "+v"(Yh[d]), "+v"(Yl[d]));
         }
+        uint2 eq = make_uint2(0, 0);
 #pragma unroll
         for (int q = 0; q < 32; q++) {
           const int d = q >> 2, b = q & 3;
-          const uint32_t bx = (b & 1) ? (uint32_t)b : (uint32_t)b + 1;
-          const uint32_t sel = 0x0C000C00u | ((4u + bx) << 16) | bx;
-          const uint32_t a = (b & 1) ? perm(Yh[d], Xh[d], sel) : perm(Yl[d], Xl[d], sel);
+          uint32_t a;
+          if (ELDS) {
+            if (b == 0) eq = ew[d * 64];
+            const uint32_t w2 = b < 2 ? eq.x : eq.y;  // [Xq Yq Xq+1 Yq+1]
+            a = (b & 1) ? perm(0u, w2, 0x0C030C02u) : perm(0u, w2, 0x0C010C00u);
+          } else {
+            const uint32_t bx = (b & 1) ? (uint32_t)b : (uint32_t)b + 1;
+            const uint32_t sel = 0x0C000C00u | ((4u + bx) << 16) | bx;
+            a = (b & 1) ? perm(Yh[d], Xh[d], sel) : perm(Yl[d], Xl[d], sel);
+          }
           uint32_t f;
-          if (LEAN) {
+          if (LEAN && IMAX) {
+            // idle rows: max with 0xFF per half, whose parent is 0 -- the mask
+            // leaves the chain (folded into the off-chain max)
+            const uint32_t idle = (uint32_t)__builtin_amdgcn_sbfe((int)~A, q, 1) & 0x00FF00FFu;
+            const uint32_t u2r = from_lane_below(u1p);
+            const uint32_t pre = pk_max16(pk_max16(a, prev), pk_max16(u2r, idle));
+            const uint32_t u1r = from_lane_below(cur);
+            const uint32_t m = pk_max16(pk_max16(pre, cur), u1r);
+            f = parent_x2<1>(m);
+            u1p = u1r;
+          } else if (LEAN) {
             const uint32_t u2r = from_lane_below(u1p);
             const uint32_t pre = pk_max16(pk_max16(a, prev), u2r);
             const uint32_t u1r = from_lane_below(cur);
@@ -212,6 +244,11 @@ static void launch(int var, uint8_t* tab, const uint32_t* list, uint32_t n, cons
     case 2: hipLaunchKernelGGL((lab_x2<NO, 0, true, true>), G, B, 0, st, tab, list, n, g, zero); break;
     case 3: hipLaunchKernelGGL((lab_x2<NO, 0, true, true, 5>), G, B, 0, st, tab, list, n, g, zero); break;
     case 15: hipLaunchKernelGGL((lab_x2<NO, 5, true, true>), G, B, 0, st, tab, list, n, g, zero, g_stamps); break;
+    case 4: hipLaunchKernelGGL((lab_x2<NO, 0, true, false, 1, true>), G, B, 0, st, tab, list, n, g, zero); break;
+    case 5: hipLaunchKernelGGL((lab_x2<NO, 0, true, false, 5, true>), G, B, 0, st, tab, list, n, g, zero); break;
+    case 6: hipLaunchKernelGGL((lab_x2<NO, 0, true, false, 6, true>), G, B, 0, st, tab, list, n, g, zero); break;
+    case 7: hipLaunchKernelGGL((lab_x2<NO, 0, true, false, 1, false, true>), G, B, 0, st, tab, list, n, g, zero); break;
+    case 8: hipLaunchKernelGGL((lab_x2<NO, 0, true, false, 1, true, true>), G, B, 0, st, tab, list, n, g, zero); break;
     default: fprintf(stderr, "unknown variant %d\n", var); exit(1);
   }
 }
