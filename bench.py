@@ -233,6 +233,38 @@ def cpu_baseline(params):
     return out, sol.root_line
 
 
+def keyed_atomics():
+    """Atomic operations of the keyed solve (north_star: "rocprof must show
+    ... atomic throughput"), from the committed counter passes
+    (tools/pmc_atomics.sh -> profiles/keyed_atomics.json): L2 atomic requests
+    and LDS atomic wave-instructions per solve and per second of kernel
+    time, with a reference rate; None when absent or measured on other
+    kernel sources."""
+    path = os.path.join(ROOT, "profiles", "keyed_atomics.json")
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        try:
+            from pmc_atomics_summary import sources_sha16
+            now = sources_sha16(ROOT)
+        finally:
+            sys.path.pop(0)
+    except (OSError, ValueError, ImportError):
+        return None
+    if d.get("sources_sha16") != now:
+        return {"stale": "profiles/keyed_atomics.json measured sources %s, these are %s" % (d.get("sources_sha16"), now)}
+    t = d["total"]
+    top = sorted(d["kernels"].items(), key=lambda kv: -(kv[1].get("l2_atomic_requests", 0) + kv[1].get("lds_atomic_insts", 0)))
+    return {"source": "profiles/keyed_atomics.json (%s)" % d.get("source"),
+            "l2_atomic_requests": t["l2_atomic_requests"], "l2_atomic_per_s": t.get("l2_atomic_per_s"),
+            "lds_atomic_insts": t["lds_atomic_insts"], "lds_atomic_insts_per_s": t.get("lds_atomic_insts_per_s"),
+            "reference": "memory-side atomics ~5e9 wave-instructions/s chip-wide (1.3 TB/s, MI355X_MICROARCH.md); "
+                         "one L2 atomic request = one 64-B piece",
+            "by_kernel": {k: {"l2": v.get("l2_atomic_requests"), "lds": v.get("lds_atomic_insts"),
+                              "ms": v.get("kernel_ms")} for k, v in top[:6]}}
+
+
 def keyed_record(device):
     """BASELINE config 3 as shipped: toot_and_otto_bitstring 6x4 on the
     keyed path the planner picks (BUCKETED levels; one warm-up solve, one
@@ -270,6 +302,7 @@ def keyed_record(device):
                                     "achieved_GBps": b / (ms / 1e3) / 1e9,
                                     "frac": b / (ms / 1e3) / 1e9 / HBM_PEAK_GBS}
     out["model_8d_frac_whole_solve"] = (fwd_b + bwd_b) / wall / 1e9 / HBM_PEAK_GBS
+    out["atomics"] = keyed_atomics()
     e = golden("toot_6x4")
     if e is not None:
         ck = s.checksum()

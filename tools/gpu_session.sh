@@ -8,6 +8,7 @@
 #   bench          python bench.py --steps 20 --warmup 5          -> TAG_bench.json
 #   prof           rocprofv3 --kernel-trace --stats of a short bench -> TAG_prof/
 #   pmc            the PMC passes of one bench step (tools/pmc_passes.sh) -> TAG_pmc/, TAG_pmc_traffic.json
+#   atomics        toot 6x4 atomic counters (tools/pmc_atomics.sh)    -> TAG_atomics.json
 #   groups         per-shard PLANES group timings, N = 2 4 8 (tools/group_planes.py)
 #   keyed[:B]      toot B (default 6x4) md5 group timings, N = 1 2 4 (tools/group_keyed_time.py)
 # Replaces the round-by-round session scripts (tools/gpu_r0*.sh).
@@ -44,6 +45,10 @@ for step in "$@"; do
       python3 tools/pmc_summary.py --traffic "sum_four_to_one heaps=31:31:31:31:31:31" ${o}_pmc_traffic.json \
         ${o}_pmc > /dev/null || fail pmc-summary ${o}_pmc.log
       tail -3 ${o}_pmc.log ;;
+    atomics)  # keyed toot 6x4 atomic counters -> TAG_atomics.json (copy to profiles/keyed_atomics.json)
+      bash tools/pmc_atomics.sh ${o}_atomics > ${o}_atomics.log 2>&1 || fail atomics ${o}_atomics.log
+      python3 tools/pmc_atomics_summary.py ${o}_atomics > ${o}_atomics.json || fail atomics-summary ${o}_atomics.log
+      python3 -c "import json,sys; print(json.load(open(sys.argv[1]))['total'])" ${o}_atomics.json ;;
     groups)
       for w in 2 4 8; do
         timeout -k 10 300 python -u tools/group_planes.py $w 3 > ${o}_group$w.jsonl 2>&1 \

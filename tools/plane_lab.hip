@@ -38,7 +38,8 @@ using namespace gm;
 // without the lane-32 masks (lane 31's idle steps already read 0 there), the
 // in-lane and lane-below-by-two children folded off the chain first, and the
 // active-row mask one bit extract of a per-lane word.
-template <int NO, int DIAG, bool LEAN, bool OPQ = false, int MINW = 1, bool ELDS = false, bool IMAX = false>
+template <int NO, int DIAG, bool LEAN, bool OPQ = false, int MINW = 1, bool ELDS = false, bool IMAX = false,
+          bool PPAR = false>
 __global__ __launch_bounds__(256, MINW) void lab_x2(uint8_t* __restrict__ tab, const uint32_t* __restrict__ list,
                                                     uint32_t n, PlaneGeom g, const uint4* __restrict__ zero,
                                                     uint64_t* __restrict__ stamps = nullptr) {
@@ -164,7 +165,16 @@ __global__ __launch_bounds__(256, MINW) void lab_x2(uint8_t* __restrict__ tab, c
             const uint32_t u1r = from_lane_below(cur);
             const uint32_t m = pk_max16(pk_max16(pre, cur), u1r);
             const uint32_t keep = (uint32_t)__builtin_amdgcn_sbfe((int)A, q, 1);
-            f = parent_x2<1>(m) & keep;
+            if (PPAR) {
+              // parent as (0xFE - m) and (m >> 7) side by side, then one add:
+              // the asm keeps the compiler from re-associating it into
+              // ((m >> 7) - m) + 0xFE, one dependent op longer
+              uint32_t t1;
+              asm("v_pk_sub_u16 %0, %1, %2" : "=v"(t1) : "s"(0x00FE00FEu), "v"(m));
+              f = pk_add16(t1, pk_shr16(m, 7)) & keep;
+            } else {
+              f = parent_x2<1>(m) & keep;
+            }
             u1p = u1r;
           } else {
             const uint32_t u1r = from_lane_below(cur), u2r = from_lane_below(u1p);
@@ -249,6 +259,7 @@ static void launch(int var, uint8_t* tab, const uint32_t* list, uint32_t n, cons
     case 6: hipLaunchKernelGGL((lab_x2<NO, 0, true, false, 6, true>), G, B, 0, st, tab, list, n, g, zero); break;
     case 7: hipLaunchKernelGGL((lab_x2<NO, 0, true, false, 1, false, true>), G, B, 0, st, tab, list, n, g, zero); break;
     case 8: hipLaunchKernelGGL((lab_x2<NO, 0, true, false, 1, true, true>), G, B, 0, st, tab, list, n, g, zero); break;
+    case 9: hipLaunchKernelGGL((lab_x2<NO, 0, true, false, 1, false, false, true>), G, B, 0, st, tab, list, n, g, zero); break;
     default: fprintf(stderr, "unknown variant %d\n", var); exit(1);
   }
 }
