@@ -374,6 +374,36 @@ static int plane_lists(gm_solver* s, const PlaneShape& ps, std::vector<uint8_t>&
     uint32_t* L = (uint32_t*)bytes.data();
     std::vector<u64> pos(s->ploff.begin(), s->ploff.end());
     for (u64 P = 0; P < ps.nlocal; P++) L[pos[lev[P]]++] = (uint32_t)P;
+    // Within a level: the planes in 3-D tiles of kPlaneTile^3 over the outer
+    // digits above the lowest (the lowest follows from the level), tiles and
+    // the planes inside a tile lexicographic.  A child plane's four parents
+    // at the next level (one outer digit + 1) then mostly share its tile, so
+    // they run on one XCD close together and its lines are fetched into that
+    // L2 about once per level (plane index order: -2 % backward time,
+    // tools/plane_lab LAB_ORDER=8, profiles/r04b_plane_lab.txt).
+    if (g.no >= 2) {
+      constexpr uint32_t kPlaneTile = 8;
+      auto key = [&](uint32_t P) {
+        uint32_t dig[kPlaneMaxOuter];
+        u64 x = P;
+        for (uint32_t j = 0; j < g.no; j++) {
+          dig[j] = (uint32_t)(x % g.base[j]);
+          x /= g.base[j];
+        }
+        u64 k = 0;  // mixed radix: < 8^5 * 2^32 (the plane index is 32-bit)
+        for (int j = (int)g.no - 1; j >= 1; j--) k = k * ((g.base[j] + kPlaneTile - 1) / kPlaneTile) + dig[j] / kPlaneTile;
+        for (int j = (int)g.no - 1; j >= 1; j--) k = k * kPlaneTile + dig[j] % kPlaneTile;
+        return k * g.base[0] + dig[0];
+      };
+      std::vector<std::pair<u64, uint32_t>> tmp;
+      for (uint32_t l = 0; l <= S; l++) {
+        const u64 a = s->ploff[l], b = s->ploff[(size_t)l + 1];
+        tmp.resize(b - a);
+        for (u64 i = a; i < b; i++) tmp[i - a] = {key(L[i]), L[i]};
+        std::sort(tmp.begin(), tmp.end());
+        for (u64 i = a; i < b; i++) L[i] = tmp[i - a].second;
+      }
+    }
     return 0;
   }
   const u64 Z = g.Z, B = g.B;

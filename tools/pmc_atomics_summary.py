@@ -37,14 +37,13 @@ def short(name):
 def main():
     root = sys.argv[1]
     per = {}
-    for sub in ("l2", "lds"):
-        p, _ = load(os.path.join(root, sub))
-        for name, ctr in p.items():
-            d = per.setdefault(short(name), {})
-            for c, v in ctr.items():
-                d[c] = d.get(c, 0.0) + v
+    p, _ = load(root)  # root/l2/, root/lds/: one counter pass each
+    for name, ctr in p.items():
+        d = per.setdefault(short(name), {})
+        for c, v in ctr.items():
+            d[c] = d.get(c, 0.0) + v
     ns = {}
-    for path in glob.glob(os.path.join(root, "trace", "*", "run_kernel_trace.csv")):
+    for path in glob.glob(os.path.join(root, "trace", "**", "run_kernel_trace.csv"), recursive=True):
         for r in csv.DictReader(open(path)):
             k = short(r["Kernel_Name"])
             ns[k] = ns.get(k, 0) + int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
