@@ -39,6 +39,23 @@
 //   16-bit: WIN r -> r, LOSS r -> 0x8000 | (0x7FFF - r);
 //          parent of max m: h(m) = 0xFFFE - m + 2 (m >> 15)
 // The only primitive (every heap 0, a LOSS) is LOSS 0 = 0xFF / 0xFFFF.
+//
+// Relative 8-bit forms (word form 3; root digit sums 254 .. 505, e.g. the
+// sharded bench shapes 31^5 x 127 and 31^5 x 255): a position of digit sum e
+// (all heaps) has remoteness in [ceil(e / 2), e], a window of e / 2 + 1
+// values, so its word is taken relative to an offset o(e) = (e + 1) / 4 - 1:
+//   WIN r -> (r - 1) / 2 - o(e),  LOSS r -> 0xFF - r / 2 + o(e)
+// (o is one below the smallest (r - 1) / 2 of the window: every real WIN
+// word is >= 1, so 0 still reads as "no child" after the shift below; the
+// primitive is LOSS 0 = 0xFE).  A parent at e = d reduces its children in
+// the frame of d - 1: children at d - 1 are already in it, children at
+// d - 2 (a heap lowered by 2) are shifted by o(d - 1) - o(d - 2), which is 1
+// exactly when d % 4 == 0 (WIN w -> w - 1, LOSS l -> l + 1, 0 stays 0: a
+// saturating subtract); the parent word from the frame-(d - 1) max m is
+// h(m) above when o(d) == o(d - 1), and 0xFF - m - (m >> 7) when
+// o(d) = o(d - 1) + 1 (d % 4 == 3).  d % 4 = (s + t) % 4 for outer digit sum
+// s and wavefront step t, so with s % 4 (RS) a template parameter of the
+// launch every shift and parent form is static per step.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -109,6 +126,12 @@ struct PlaneWord<1> {
   __device__ static __forceinline__ uint32_t parent(uint32_t m) { return 0xFEu - m + (m >> 7); }
 };
 template <>
+struct PlaneWord<3> {  // relative 8-bit forms (above)
+  typedef uint8_t T;
+  static constexpr int DW = 8;
+  static constexpr uint32_t kPrim = 0xFEu;
+};
+template <>
 struct PlaneWord<2> {
   typedef uint16_t T;
   static constexpr int DW = 16;
@@ -126,6 +149,16 @@ __host__ __device__ inline uint32_t plane_word_to_vr(uint32_t w, int wb) {
   if (w & 0x8000u) return 1u | ((0x7FFFu - (w & 0x7FFFu)) << 2);
   return 0u | (w << 2);
 }
+
+// relative forms: the offset at digit sum e, the word -> value | remoteness
+// << 2, and the largest root digit sum whose every window fits a byte
+__host__ __device__ inline int plane_rel_off(uint32_t e) { return (int)((e + 1) / 4) - 1; }
+__host__ __device__ inline uint32_t plane_rel_to_vr(uint32_t w, uint32_t e) {
+  const int o = plane_rel_off(e);
+  if (w & 0x80u) return 1u | ((uint32_t)(2 * (0xFF - (int)w + o)) << 2);
+  return 0u | ((uint32_t)(2 * ((int)w + o) + 1) << 2);
+}
+constexpr uint32_t kPlaneRelMaxSum = 505;  // e = 506: the WIN window's top word reaches 0x80
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
@@ -195,6 +228,7 @@ __device__ __forceinline__ void plane_x1_range(typename PlaneWord<WB>::T* __rest
                                                const typename PlaneWord<WB>::T* __restrict__ recv,
                                                typename PlaneWord<WB>::T* __restrict__ send) {
   typedef PlaneWord<WB> W;
+  static_assert(WB != 3, "relative words: the packed form only");
   constexpr int DW = W::DW, NQ = DW / 4;  // dwords / 16-B loads per row
   const uint32_t lane = threadIdx.x & 63, L = lane & 31;
   for (uint32_t i0 = sh.first; i0 < sh.end; i0 += sh.stride) {
@@ -343,12 +377,36 @@ __device__ __forceinline__ uint32_t parent_x2(uint32_t m) {
   if (WB == 1) return pk_add16(pk_sub16(0x00FE00FEu, m), pk_shr16(m, 7));
   return pk_add16(pk_sub16(0xFFFEFFFEu, m), pk_shr16(m, 15) << 1);  // (m>>15)<<1 stays in its half
 }
+__device__ __forceinline__ uint32_t pk_sub_sat16(uint32_t a, uint32_t b) {
+  u16x2 x = __builtin_bit_cast(u16x2, a), y = __builtin_bit_cast(u16x2, b);
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(x, y));
+}
+// relative forms, the d - 2 -> d - 1 frame shift of byte B0 (a HIGH byte of
+// its 16-bit half, B0 odd) of a folded E dword (WIN w -> w - 1, LOSS l ->
+// l + 1).  The byte is 0 only when every folded row was a zero row (absent
+// neighbour: real WIN words are >= 1), and then so is the half's low byte:
+// the saturating 16-bit subtract leaves 0 there and never borrows otherwise.
+template <int B0>
+__device__ __forceinline__ uint32_t rel_shift_byte(uint32_t x) {
+  const uint32_t t = pk_sub_sat16(x, 1u << (8 * B0));
+  return t + (__builtin_amdgcn_ubfe(x, 8 * B0 + 7, 1) << (8 * B0 + 1));
+}
+// the same shift of packed step values (one word in the low byte of each
+// 16-bit half; 0 -- no child, an idle lane -- stays 0)
+__device__ __forceinline__ uint32_t rel_shift_pk(uint32_t v) {
+  return pk_sub_sat16(v, 0x00010001u) + (pk_shr16(v, 7) << 1);
+}
+// relative forms, parent word when o(d) = o(d - 1) + 1
+__device__ __forceinline__ uint32_t parent_rel_up(uint32_t m) {
+  return pk_sub16(pk_sub16(0x00FF00FFu, m), pk_shr16(m, 7));
+}
 // v_perm_b32 selector bytes
 __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
   return __builtin_amdgcn_perm(hi, lo, sel);
 }
 
-template <int WB, int NO, bool SH>
+// (RS: with WB = 3, the launch's outer digit sum s mod 4)
+template <int WB, int NO, bool SH, int RS = 0>
 __device__ __forceinline__ void plane_x2_range(typename PlaneWord<WB>::T* __restrict__ tab,
                                                const void* __restrict__ list, const PlaneShare sh,
                                                const PlaneGeom& g, const uint4* __restrict__ zero,
@@ -357,6 +415,8 @@ __device__ __forceinline__ void plane_x2_range(typename PlaneWord<WB>::T* __rest
   typedef PlaneWord<WB> W;
   typedef typename W::T T;
   constexpr int DW = W::DW, NQ = DW / 4;
+  constexpr bool B8 = DW == 8, REL = WB == 3;
+  constexpr int B0 = (4 - RS) & 3;  // relative: row bytes j = B0 mod 4 are parents with d % 4 == 0
   const uint32_t lane = threadIdx.x & 63, L = lane & 31;
   for (uint32_t i0 = sh.first; i0 < sh.end; i0 += sh.stride) {
     const uint32_t ix = i0 + 2 * (lane >> 5), iy = ix + 1;
@@ -375,11 +435,11 @@ __device__ __forceinline__ void plane_x2_range(typename PlaneWord<WB>::T* __rest
     const size_t ox = (size_t)ex.p * 1024u + L * 32u, oy = (size_t)ey.p * 1024u + L * 32u;
     // E rows of both planes (8-bit: odd bytes exact in Ehi, even bytes in
     // the high bytes of Elo; 16-bit: Ehi exact)
-    uint32_t Xh[DW], Xl[WB == 1 ? DW : 1], Yh[DW], Yl[WB == 1 ? DW : 1];
+    uint32_t Xh[DW], Xl[B8 ? DW : 1], Yh[DW], Yl[B8 ? DW : 1];
 #pragma unroll
     for (int d = 0; d < DW; d++) {
       Xh[d] = Yh[d] = 0;
-      if (WB == 1) Xl[d] = Yl[d] = 0;
+      if (B8) Xl[d] = Yl[d] = 0;
     }
     auto nb = [&](const PlaneEntry& e, const uint32_t* dig, size_t off, int j, int k) -> const uint4* {
       if (SH && j == NO - 1) {
@@ -390,32 +450,55 @@ __device__ __forceinline__ void plane_x2_range(typename PlaneWord<WB>::T* __rest
       }
       return dig[j] >= (uint32_t)k ? (const uint4*)(tab + off - (size_t)k * g.stride[j] * 1024u) : zero;
     };
+    auto fold = [&](int j, int k) {
+      const uint4* sx = nb(ex, dx, ox, j, k);
+      const uint4* sy = nb(ey, dy, oy, j, k);
+      uint4 vx[NQ], vy[NQ];
 #pragma unroll
-    for (int j = 0; j < NO; j++) {
+      for (int q = 0; q < NQ; q++) {
+        vx[q] = sx[q];
+        vy[q] = sy[q];
+      }
 #pragma unroll
-      for (int k = 1; k <= 2; k++) {
-        const uint4* sx = nb(ex, dx, ox, j, k);
-        const uint4* sy = nb(ey, dy, oy, j, k);
-        uint4 vx[NQ], vy[NQ];
+      for (int q = 0; q < NQ; q++) {
+        const uint32_t a[4] = {vx[q].x, vx[q].y, vx[q].z, vx[q].w};
+        const uint32_t b[4] = {vy[q].x, vy[q].y, vy[q].z, vy[q].w};
 #pragma unroll
-        for (int q = 0; q < NQ; q++) {
-          vx[q] = sx[q];
-          vy[q] = sy[q];
-        }
-#pragma unroll
-        for (int q = 0; q < NQ; q++) {
-          const uint32_t a[4] = {vx[q].x, vx[q].y, vx[q].z, vx[q].w};
-          const uint32_t b[4] = {vy[q].x, vy[q].y, vy[q].z, vy[q].w};
-#pragma unroll
-          for (int c = 0; c < 4; c++) {
-            Xh[4 * q + c] = pk_max16(Xh[4 * q + c], a[c]);
-            Yh[4 * q + c] = pk_max16(Yh[4 * q + c], b[c]);
-            if (WB == 1) {
-              Xl[4 * q + c] = pk_max16(Xl[4 * q + c], pk_shl8(a[c]));
-              Yl[4 * q + c] = pk_max16(Yl[4 * q + c], pk_shl8(b[c]));
-            }
+        for (int c = 0; c < 4; c++) {
+          Xh[4 * q + c] = pk_max16(Xh[4 * q + c], a[c]);
+          Yh[4 * q + c] = pk_max16(Yh[4 * q + c], b[c]);
+          if (B8) {
+            Xl[4 * q + c] = pk_max16(Xl[4 * q + c], pk_shl8(a[c]));
+            Yl[4 * q + c] = pk_max16(Yl[4 * q + c], pk_shl8(b[c]));
           }
         }
+      }
+    };
+    if constexpr (REL) {
+      // children at d - 2 first, then their frame shift -- ONCE on the
+      // folded maxima (the shift is monotone: it commutes with max), on the
+      // one split array whose high bytes hold row bytes B0 mod 4 (Xh: odd
+      // bytes, Xl: even ones), half B0 / 2 of every dword -- then the
+      // children at d - 1
+#pragma unroll
+      for (int j = 0; j < NO; j++) fold(j, 2);
+#pragma unroll
+      for (int d = 0; d < DW; d++) {
+        if (B0 & 1) {
+          Xh[d] = rel_shift_byte<2 * (B0 >> 1) + 1>(Xh[d]);
+          Yh[d] = rel_shift_byte<2 * (B0 >> 1) + 1>(Yh[d]);
+        } else {
+          Xl[d] = rel_shift_byte<2 * (B0 >> 1) + 1>(Xl[d]);
+          Yl[d] = rel_shift_byte<2 * (B0 >> 1) + 1>(Yl[d]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NO; j++) fold(j, 1);
+    } else {
+#pragma unroll
+      for (int j = 0; j < NO; j++) {
+#pragma unroll
+        for (int k = 1; k <= 2; k++) fold(j, k);
       }
     }
     const uint32_t primv =
@@ -443,7 +526,7 @@ __device__ __forceinline__ void plane_x2_range(typename PlaneWord<WB>::T* __rest
 #pragma unroll
       for (int q = 0; q < 32; q++) {
         uint32_t a;
-        if (WB == 1) {
+        if (B8) {
           // byte q of X's and Y's E rows -> [X, 0, Y, 0]
           const int d = q >> 2, b = q & 3;
           const uint32_t bx = (b & 1) ? (uint32_t)b : (uint32_t)b + 1;  // byte inside the split dword
@@ -456,11 +539,13 @@ __device__ __forceinline__ void plane_x2_range(typename PlaneWord<WB>::T* __rest
           a = perm(Yh[d], Xh[d], sel);
         }
         const uint32_t u2r = from_lane_below(u1p);
-        const uint32_t pre = pk_max16(pk_max16(a, prev), u2r);
+        const int dcls = (RS + q) & 3;  // relative forms: d % 4 of this step's positions
+        const uint32_t pre = REL && dcls == 0 ? pk_max16(a, rel_shift_pk(pk_max16(prev, u2r)))
+                                              : pk_max16(pk_max16(a, prev), u2r);
         const uint32_t u1r = from_lane_below(cur);
         const uint32_t m = pk_max16(pk_max16(pre, cur), u1r);
         const uint32_t keep = (uint32_t)__builtin_amdgcn_sbfe((int)A, q, 1);
-        uint32_t f = parent_x2<WB>(m) & keep;
+        uint32_t f = (REL && dcls == 3 ? parent_rel_up(m) : parent_x2<WB == 2 ? 2 : 1>(m)) & keep;
         if (q == 0) f = pk_max16(f, ph ? 0u : primv);
         op[q] |= f;
         prev = cur;
@@ -469,7 +554,7 @@ __device__ __forceinline__ void plane_x2_range(typename PlaneWord<WB>::T* __rest
       }
     }
     uint32_t ox_[DW], oy_[DW];
-    if (WB == 1) {
+    if (B8) {
 #pragma unroll
       for (int k = 0; k < 8; k++) {
         const uint32_t t1 = perm(op[4 * k + 1], op[4 * k], 0x06020400u);      // [X0 X1 Y0 Y1]
@@ -500,7 +585,7 @@ __device__ __forceinline__ void plane_x2_range(typename PlaneWord<WB>::T* __rest
   }
 }
 
-template <int WB, int NO, bool SH>
+template <int WB, int NO, bool SH, int RS>
 __global__ __launch_bounds__(256) void k_plane_resolve_x2(typename PlaneWord<WB>::T* __restrict__ tab,
                                                           const void* __restrict__ list, uint32_t n, PlaneGeom g,
                                                           const uint4* __restrict__ zero,
@@ -508,7 +593,7 @@ __global__ __launch_bounds__(256) void k_plane_resolve_x2(typename PlaneWord<WB>
                                                           typename PlaneWord<WB>::T* __restrict__ send,
                                                           const uint32_t* __restrict__ pf, uint32_t pflines) {
   const uint32_t v = plane_prefetch(pf, pflines);
-  plane_x2_range<WB, NO, SH>(tab, list, plane_share(n, 4), g, zero, recv, send);
+  plane_x2_range<WB, NO, SH, RS>(tab, list, plane_share(n, 4), g, zero, recv, send);
   plane_keep(v);
 }
 
@@ -526,6 +611,7 @@ constexpr int kPlaneRunThreads = 512;  // 8 waves: <= 256 VGPRs, every kernel va
 struct PlaneRun {
   uint32_t n;
   uint32_t off[kPlaneRunMax + 1];  // list entries, absolute
+  uint64_t rs;                     // relative forms: group i's outer digit sum mod 4 in bits 2i, 2i + 1
 };
 template <int WB, int NO, bool SH, bool X1>
 __global__ __launch_bounds__(kPlaneRunThreads) void k_plane_run(typename PlaneWord<WB>::T* __restrict__ tab,
@@ -537,10 +623,18 @@ __global__ __launch_bounds__(kPlaneRunThreads) void k_plane_run(typename PlaneWo
   const uint32_t w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   for (uint32_t i = 0; i < run.n; i++) {
     const PlaneShare sh{run.off[i] + w * per, run.off[i + 1], nw * per};
-    if (X1)
+    if constexpr (WB == 3) {
+      switch ((run.rs >> (2 * i)) & 3u) {
+        case 0: plane_x2_range<WB, NO, SH, 0>(tab, list, sh, g, zero, recv, send); break;
+        case 1: plane_x2_range<WB, NO, SH, 1>(tab, list, sh, g, zero, recv, send); break;
+        case 2: plane_x2_range<WB, NO, SH, 2>(tab, list, sh, g, zero, recv, send); break;
+        default: plane_x2_range<WB, NO, SH, 3>(tab, list, sh, g, zero, recv, send); break;
+      }
+    } else if constexpr (X1) {
       plane_x1_range<WB, NO, SH>(tab, list, sh, g, zero, recv, send);
-    else
+    } else {
       plane_x2_range<WB, NO, SH>(tab, list, sh, g, zero, recv, send);
+    }
     __syncthreads();
   }
 }

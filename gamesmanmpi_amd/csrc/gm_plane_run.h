@@ -29,25 +29,28 @@ __global__ __launch_bounds__(256) void k_plane_reach(uint32_t* bits, PlaneGeom g
   }
 }
 
-// word of local position (h0, h1, P) in value | remoteness << 2 form
+// word of local position (h0, h1, P) in value | remoteness << 2 form; e:
+// the position's digit sum (all heaps; read by the relative forms only)
 template <int WB>
-__device__ __forceinline__ uint32_t plane_vr(const void* tab, u64 P, uint32_t h0, uint32_t h1) {
+__device__ __forceinline__ uint32_t plane_vr(const void* tab, u64 P, uint32_t h0, uint32_t h1, uint32_t e) {
   const u64 i = P * 1024u + h1 * 32u + ((h0 + h1) & 31u);
-  const uint32_t w = WB == 1 ? ((const uint8_t*)tab)[i] : ((const uint16_t*)tab)[i];
-  return plane_word_to_vr(w, WB);
+  const uint32_t w = WB == 2 ? ((const uint16_t*)tab)[i] : ((const uint8_t*)tab)[i];
+  return WB == 3 ? plane_rel_to_vr(w, e) : plane_word_to_vr(w, WB);
 }
 
-// rank (key) -> local plane, h0, h1; false if another shard owns it or the
-// key lies outside the heaps
+// rank (key) -> local plane, h0, h1 and the key's digit sum; false if
+// another shard owns it or the key lies outside the heaps
 __device__ __forceinline__ bool plane_locate(const Desc& d, const PlaneGeom& g, u64 key, u64* P, uint32_t* h0,
-                                             uint32_t* h1) {
+                                             uint32_t* h1, uint32_t* esum) {
   u64 x = key;
-  uint32_t dig[16];
+  uint32_t dig[16], e = 0;
   for (int i = 0; i < d.nheaps; i++) {
     dig[i] = (uint32_t)(x % d.base[i]);
+    e += dig[i];
     x /= d.base[i];
   }
   if (x) return false;
+  *esum = e;
   *h0 = dig[0];
   *h1 = dig[1];
   u64 p = 0;
@@ -69,8 +72,9 @@ __global__ void k_plane_query(Desc d, PlaneGeom g, const void* tab, const uint32
                               uint32_t* out) {
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
     u64 P;
-    uint32_t h0, h1, w = NO_WORD;
-    if (plane_locate(d, g, keys[i], &P, &h0, &h1) && ((bits[P * 32u + h1] >> h0) & 1u)) w = plane_vr<WB>(tab, P, h0, h1);
+    uint32_t h0, h1, e, w = NO_WORD;
+    if (plane_locate(d, g, keys[i], &P, &h0, &h1, &e) && ((bits[P * 32u + h1] >> h0) & 1u))
+      w = plane_vr<WB>(tab, P, h0, h1, e);
     out[i] = w;
   }
 }
@@ -83,22 +87,29 @@ __global__ __launch_bounds__(1024) void k_plane_finish(Desc d, PlaneGeom g, cons
                                                        DevState* st, const BlockCount* bc) {
   if (threadIdx.x == 0) {
     u64 P;
-    uint32_t h0, h1, w = NO_WORD;
-    if (plane_locate(d, g, d.root, &P, &h0, &h1) && ((bits[P * 32u + h1] >> h0) & 1u)) w = plane_vr<WB>(tab, P, h0, h1);
+    uint32_t h0, h1, e, w = NO_WORD;
+    if (plane_locate(d, g, d.root, &P, &h0, &h1, &e) && ((bits[P * 32u + h1] >> h0) & 1u))
+      w = plane_vr<WB>(tab, P, h0, h1, e);
     st->root_word = w;
   }
   __syncthreads();
   fill_red_body(st, bc);
 }
 
-// global rank of local position (h0, h1, P)
+// global rank of local position (h0, h1, P); *osum: its outer digit sum
 template <int NO>
-__device__ __forceinline__ u64 plane_key(const Desc& d, const PlaneGeom& g, uint32_t P, uint32_t h0, uint32_t h1) {
+__device__ __forceinline__ u64 plane_key(const Desc& d, const PlaneGeom& g, uint32_t P, uint32_t h0, uint32_t h1,
+                                         uint32_t* osum = nullptr) {
   uint32_t dig[NO > 0 ? NO : 1];
   plane_global_digits<NO>(g, P, dig);
   u64 k = (u64)h0 + (u64)h1 * d.stride[1];
+  uint32_t t = 0;
 #pragma unroll
-  for (int j = 0; j < NO; j++) k += (u64)dig[j] * d.stride[2 + j];
+  for (int j = 0; j < NO; j++) {
+    k += (u64)dig[j] * d.stride[2 + j];
+    t += dig[j];
+  }
+  if (osum) *osum = t;
   return k;
 }
 
@@ -124,10 +135,11 @@ __global__ __launch_bounds__(256) void k_plane_checksum(Desc d, PlaneGeom g, con
     const uint32_t P = (uint32_t)(i >> 5), h1 = (uint32_t)i & 31u;
     uint32_t w = bits[i];
     if (!w) continue;
-    const u64 base = plane_key<NO>(d, g, P, 0, h1);
+    uint32_t os;
+    const u64 base = plane_key<NO>(d, g, P, 0, h1, &os);
     for (; w; w &= w - 1) {
       const uint32_t h0 = (uint32_t)__builtin_ctz(w);
-      ck_add(d, base + h0, plane_vr<WB>(tab, P, h0, h1), a);
+      ck_add(d, base + h0, plane_vr<WB>(tab, P, h0, h1, os + h0 + h1), a);
     }
   }
   ck_block_add(acc, a);
@@ -146,10 +158,13 @@ static bool plane_ok(const Desc* d) {
   for (int i = 2; i < d->nheaps; i++) np *= d->base[i];
   return np <= 0xFFFFFFF0ull;
 }
-// 8-bit order forms when every remoteness < 255 (they carry the value in the
-// remoteness parity: every K_SUM position is WIN or LOSS), else 16-bit
-static uint32_t plane_wb(const Desc* d, uint32_t flags) {
-  return (d->root_sum <= 253 && !(flags & GM_F_WORDS16)) ? 1u : 2u;
+// Word form: 8-bit order forms when every remoteness < 255 (they carry the
+// value in the remoteness parity: every K_SUM position is WIN or LOSS); the
+// relative 8-bit forms (gm_plane.h) up to root digit sum kPlaneRelMaxSum;
+// else (or GM_F_WORDS16) 16-bit
+static uint32_t plane_form(const Desc* d, uint32_t flags) {
+  if (flags & GM_F_WORDS16) return 2u;
+  return d->root_sum <= 253 ? 1u : d->root_sum <= kPlaneRelMaxSum ? 3u : 2u;
 }
 static bool plane_wanted(const Desc* d, uint32_t flags) {
   return plane_ok(d) && !(flags & (GM_F_LEVEL_MAJOR | GM_F_FORCE_HASHED | GM_F_WORDS32 | GM_F_RESOLVE_SCALAR));
@@ -157,7 +172,8 @@ static bool plane_wanted(const Desc* d, uint32_t flags) {
 
 struct PlaneShape {
   PlaneGeom g;
-  uint32_t wb;
+  uint32_t wb;           // word bytes
+  uint32_t form;         // plane_form
   uint32_t S;            // largest plane level (sum of the outer heaps)
   uint32_t nblocks, nb;  // shards: blocks of the top digit over all ranks / of this rank
   u64 nlocal;            // planes of this table
@@ -181,8 +197,11 @@ struct PlaneShape {
 // trails rank r - 1 by about B keys, and the transfers hide under B - 1 keys
 // of compute.  Larger k shortens the trail (fewer planes per key) but adds
 // launches (each >= ~9 us: profiles/r03l_group*.jsonl); k by world from the
-// pipeline model with that floor (tools/stage_model.py --floor 9e-6).
-static uint32_t plane_stage_k(int world) { return world <= 2 ? 2u : world <= 4 ? 4u : 5u; }
+// pipeline model with that floor (tools/stage_model.py --floor 9e-6).  The
+// relative word forms need k = 1 mod 4: a key's planes then share their
+// outer digit sum mod 4 (s = rB + o + c = rB + key - (k - 1) c), which the
+// launch's kernel is specialised for.
+static uint32_t plane_stage_k(int world, bool rel) { return rel ? 5u : world <= 2 ? 2u : world <= 4 ? 4u : 5u; }
 
 static u64 rup256(u64 x) { return (x + 255) & ~255ull; }
 
@@ -224,7 +243,8 @@ static int plane_shape(const Desc* d, int rank, int world, uint32_t flags, Plane
       if (seen[v] != (v <= r)) return fail(GM_EINVAL, "heap %d: reachable values are not a prefix", i);
     g.rlim[i] = r;
   }
-  ps->wb = plane_wb(d, flags);
+  ps->form = plane_form(d, flags);
+  ps->wb = ps->form == 2 ? 2u : 1u;
   ps->S = 0;
   for (int i = 2; i < d->nheaps; i++) ps->S += d->heap[i];
   if (world <= 1) {
@@ -248,7 +268,7 @@ static int plane_shape(const Desc* d, int rank, int world, uint32_t flags, Plane
     if (staged) {
       uint32_t smax = 0;  // largest digit sum below the top
       for (uint32_t j = 0; j + 1 < g.no; j++) smax += g.base[j] - 1;
-      ps->stage_k = plane_stage_k(world);
+      ps->stage_k = plane_stage_k(world, ps->form == 3);
       ps->nrows = smax + 1;
       ps->nkeys = (uint32_t)(B - 1) + ps->stage_k * smax + 1;
     }
@@ -507,6 +527,7 @@ static int plane_setup(gm_solver* s, const gm_buffers* buf) {
                 (unsigned long long)ps.table_bytes, (unsigned long long)ps.scratch_bytes);
   s->pg = ps.g;
   s->pwb = ps.wb;
+  s->pform = ps.form;
   s->pS = ps.S;
   char* t = (char*)buf->table;
   s->ptab = t + ps.words_off;
@@ -526,7 +547,7 @@ static int plane_setup(gm_solver* s, const gm_buffers* buf) {
   if (rc) return rc;
   HIPCHK(hipMemset((void*)s->pzero, 0, 4096));
   HIPCHK(hipMemcpy((void*)s->plist, lb.data(), lb.size(), hipMemcpyHostToDevice));
-  s->w8 = ps.wb == 1;
+  s->w8 = ps.wb == 1;  // (the dense flags; the planes paths read pform)
   s->w16 = ps.wb == 2;
   return 0;
 }
@@ -538,11 +559,14 @@ static int plane_setup(gm_solver* s, const gm_buffers* buf) {
 // words (1.65 vs 1.87 ms per 2^30 backward); one plane per half-wave for
 // 16-bit words, where the packed form's register and byte footprint made it
 // slower (3.80 vs 2.77 ms; profiles/r03b_plane_proto.txt); GM_F_PLANE_X1
-// forces the one-plane form (A/B)
-static bool plane_x1(const gm_solver* s) { return s->pwb == 2 || (s->flags & GM_F_PLANE_X1); }
+// forces the one-plane form (A/B) of the absolute 8-bit forms; the relative
+// forms have the packed form only
+static bool plane_x1(const gm_solver* s) { return s->pform == 2 || (s->pform == 1 && (s->flags & GM_F_PLANE_X1)); }
 
+// rs: the launch's outer digit sum mod 4 (the relative forms' kernels are
+// specialised for it)
 template <int WB, int NO, bool SH>
-static void plane_launch_t(gm_solver* s, u64 a, u64 n, u64 pa, u64 pn) {
+static void plane_launch_t(gm_solver* s, u64 a, u64 n, u64 pa, u64 pn, uint32_t rs) {
   if (!n) return;
   // next launch's entries [pa, pa + pn): lines to prefetch (none: pn = 0)
   const size_t esz = SH ? sizeof(PlaneEntry) : 4;
@@ -554,41 +578,62 @@ static void plane_launch_t(gm_solver* s, u64 a, u64 n, u64 pa, u64 pn) {
   blocks = std::min<u64>((blocks + 7) & ~7ull, (u64)s->grid * 4);  // plane_share loops past the grid
   typedef typename PlaneWord<WB>::T T;
   const void* list = (const char*)s->plist + a * (SH ? sizeof(PlaneEntry) : 4);
-  if (x1)
-    hipLaunchKernelGGL((k_plane_resolve<WB, NO, SH>), dim3((uint32_t)blocks), dim3(256), 0, s->stream, (T*)s->ptab,
-                       list, (uint32_t)n, s->pg, s->pzero, (const T*)s->precv, (T*)s->psend, pf, pfl);
-  else
-    hipLaunchKernelGGL((k_plane_resolve_x2<WB, NO, SH>), dim3((uint32_t)blocks), dim3(256), 0, s->stream,
-                       (T*)s->ptab, list, (uint32_t)n, s->pg, s->pzero, (const T*)s->precv, (T*)s->psend, pf, pfl);
+  const dim3 grid((uint32_t)blocks), blk(256);
+  if constexpr (WB == 3) {
+    auto go = [&](auto RS) {
+      hipLaunchKernelGGL((k_plane_resolve_x2<3, NO, SH, decltype(RS)::value>), grid, blk, 0, s->stream, (T*)s->ptab,
+                         list, (uint32_t)n, s->pg, s->pzero, (const T*)s->precv, (T*)s->psend, pf, pfl);
+    };
+    switch (rs & 3u) {
+      case 0: go(std::integral_constant<int, 0>()); break;
+      case 1: go(std::integral_constant<int, 1>()); break;
+      case 2: go(std::integral_constant<int, 2>()); break;
+      default: go(std::integral_constant<int, 3>()); break;
+    }
+  } else if (x1) {
+    hipLaunchKernelGGL((k_plane_resolve<WB, NO, SH>), grid, blk, 0, s->stream, (T*)s->ptab, list, (uint32_t)n, s->pg,
+                       s->pzero, (const T*)s->precv, (T*)s->psend, pf, pfl);
+  } else {
+    hipLaunchKernelGGL((k_plane_resolve_x2<WB, NO, SH, 0>), grid, blk, 0, s->stream, (T*)s->ptab, list, (uint32_t)n,
+                       s->pg, s->pzero, (const T*)s->precv, (T*)s->psend, pf, pfl);
+  }
 }
 template <int WB, bool SH>
-static void plane_launch_w(gm_solver* s, u64 a, u64 n, u64 pa, u64 pn) {
+static void plane_launch_w(gm_solver* s, u64 a, u64 n, u64 pa, u64 pn, uint32_t rs) {
   switch (s->pg.no) {
-    case 0: if (!SH) plane_launch_t<WB, 0, false>(s, a, n, pa, pn); break;
-    case 1: plane_launch_t<WB, 1, SH>(s, a, n, pa, pn); break;
-    case 2: plane_launch_t<WB, 2, SH>(s, a, n, pa, pn); break;
-    case 3: plane_launch_t<WB, 3, SH>(s, a, n, pa, pn); break;
-    case 4: plane_launch_t<WB, 4, SH>(s, a, n, pa, pn); break;
-    case 5: plane_launch_t<WB, 5, SH>(s, a, n, pa, pn); break;
-    default: plane_launch_t<WB, 6, SH>(s, a, n, pa, pn); break;
+    case 0: if (!SH) plane_launch_t<WB, 0, false>(s, a, n, pa, pn, rs); break;
+    case 1: plane_launch_t<WB, 1, SH>(s, a, n, pa, pn, rs); break;
+    case 2: plane_launch_t<WB, 2, SH>(s, a, n, pa, pn, rs); break;
+    case 3: plane_launch_t<WB, 3, SH>(s, a, n, pa, pn, rs); break;
+    case 4: plane_launch_t<WB, 4, SH>(s, a, n, pa, pn, rs); break;
+    case 5: plane_launch_t<WB, 5, SH>(s, a, n, pa, pn, rs); break;
+    default: plane_launch_t<WB, 6, SH>(s, a, n, pa, pn, rs); break;
   }
 }
-// list entries [a, a + n) of the solver's level lists; [pa, pa + pn): the
-// entries the next launch starts with, prefetched (pn = 0: none)
-static void plane_launch_range(gm_solver* s, u64 a, u64 n, u64 pa = 0, u64 pn = 0) {
+// the solver's word form and shard flag as template arguments
+template <class F>
+static void plane_form_dispatch(const gm_solver* s, F&& f) {
   const bool sh = s->world > 1;
-  if (s->pwb == 1) {
-    if (sh) plane_launch_w<1, true>(s, a, n, pa, pn);
-    else plane_launch_w<1, false>(s, a, n, pa, pn);
-  } else {
-    if (sh) plane_launch_w<2, true>(s, a, n, pa, pn);
-    else plane_launch_w<2, false>(s, a, n, pa, pn);
-  }
+  auto w = [&](auto WB) {
+    if (sh) f(WB, std::true_type());
+    else f(WB, std::false_type());
+  };
+  if (s->pform == 3) w(std::integral_constant<int, 3>());
+  else if (s->pform == 2) w(std::integral_constant<int, 2>());
+  else w(std::integral_constant<int, 1>());
+}
+// list entries [a, a + n) of the solver's level lists, all of outer digit
+// sum = rs mod 4; [pa, pa + pn): the entries the next launch starts with,
+// prefetched (pn = 0: none)
+static void plane_launch_range(gm_solver* s, u64 a, u64 n, uint32_t rs, u64 pa = 0, u64 pn = 0) {
+  plane_form_dispatch(s, [&](auto WB, auto SH) {
+    plane_launch_w<decltype(WB)::value, decltype(SH)::value>(s, a, n, pa, pn, rs);
+  });
 }
 template <int WB, int NO, bool SH>
 static void plane_run_t(gm_solver* s, const PlaneRun& run) {
   typedef typename PlaneWord<WB>::T T;
-  if (plane_x1(s))
+  if (WB != 3 && plane_x1(s))
     hipLaunchKernelGGL((k_plane_run<WB, NO, SH, true>), dim3(1), dim3(kPlaneRunThreads), 0, s->stream, (T*)s->ptab,
                        s->plist, run, s->pg, s->pzero, (const T*)s->precv, (T*)s->psend);
   else
@@ -629,29 +674,26 @@ struct PlaneBatcher {
   }
   void flush() {
     launches += run.n ? 1 : 0;
-    if (run.n == 1) plane_launch_range(s, run.off[0], run.off[1] - run.off[0]);
+    if (run.n == 1) plane_launch_range(s, run.off[0], run.off[1] - run.off[0], (uint32_t)run.rs & 3u);
     else if (run.n > 1) {
-      const bool sh = s->world > 1;
-      if (s->pwb == 1) {
-        if (sh) plane_run_w<1, true>(s, run);
-        else plane_run_w<1, false>(s, run);
-      } else {
-        if (sh) plane_run_w<2, true>(s, run);
-        else plane_run_w<2, false>(s, run);
-      }
+      plane_form_dispatch(s, [&](auto WB, auto SH) { plane_run_w<decltype(WB)::value, decltype(SH)::value>(s, run); });
     }
     run.n = 0;
+    run.rs = 0;
   }
-  void add(u64 a, u64 b, u64 next = 0) {  // list entries [a, b); the next group's size (prefetch)
+  // list entries [a, b), outer digit sum = rs mod 4; the next group's size
+  // (prefetch)
+  void add(u64 a, u64 b, uint32_t rs, u64 next = 0) {
     if (b == a) return;
     if (b - a > narrow) {
       flush();
-      plane_launch_range(s, a, b - a, b, next);
+      plane_launch_range(s, a, b - a, rs, b, next);
       launches++;
       return;
     }
     if (run.n == (uint32_t)kPlaneRunMax || (run.n && run.off[run.n] != a)) flush();
     if (run.n == 0) run.off[0] = (uint32_t)a;
+    run.rs |= (u64)(rs & 3u) << (2 * run.n);
     run.off[++run.n] = (uint32_t)b;
   }
 };
@@ -661,9 +703,9 @@ struct PlaneBatcher {
 static void plane_launch(gm_solver* s, uint32_t l, int part = 0) {
   const u64 a = s->ploff[l], b = s->ploff[(size_t)l + 1];
   const u64 m = s->world > 1 ? s->pbnd[l] : b;
-  if (part == 0) plane_launch_range(s, a, b - a);
-  else if (part == 1) plane_launch_range(s, a, m - a);
-  else plane_launch_range(s, m, b - m);
+  if (part == 0) plane_launch_range(s, a, b - a, l);
+  else if (part == 1) plane_launch_range(s, a, m - a, l);
+  else plane_launch_range(s, m, b - m, l);
 }
 template <class F>
 static void plane_no_dispatch(uint32_t no, F&& f) {
@@ -682,7 +724,7 @@ static void plane_reach_launch(gm_solver* s, hipStream_t stream = nullptr) {
   const int grid = (int)std::max<u64>(1, std::min<u64>((nq + 255) / 256, (u64)std::min(s->grid, kCountSlots)));
   plane_no_dispatch(s->pg.no, [&](auto NO) {
     hipLaunchKernelGGL((k_plane_reach<decltype(NO)::value>), dim3(grid), dim3(256), 0, stream ? stream : s->stream,
-                       s->pbits, s->pg, s->bcount, s->st, 8u * s->pwb);
+                       s->pbits, s->pg, s->bcount, s->st, s->pmark());
   });
 }
 
@@ -882,9 +924,11 @@ static int plane_backward_staged(std::vector<gm_solver*>& ss, int mode, hipStrea
     *n = off[r + 1] - off[r];
     return off[r];
   };
-  auto launch_key = [K](PlaneBatcher& pb_, uint32_t key) {
+  auto launch_key = [K, B](PlaneBatcher& pb_, uint32_t key) {
     const std::vector<u64>& o = pb_.s->ploff;
-    pb_.add(o[key], o[(size_t)key + 1], key + 1 < K ? o[(size_t)key + 2] - o[(size_t)key + 1] : 0);
+    // outer digit sums of the key: rank * B + key (mod 4; plane_stage_k)
+    const uint32_t rs = (uint32_t)pb_.s->rank * B + key;
+    pb_.add(o[key], o[(size_t)key + 1], rs, key + 1 < K ? o[(size_t)key + 2] - o[(size_t)key + 1] : 0);
   };
   if (mode == 2) {
     for (int c = 0; c < W; c++) {
@@ -1092,7 +1136,9 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
   if (first > 0) {
     uint32_t wb = 0;
     HIPCHK(hipMemcpy(&wb, &s0->st->word_bits, sizeof wb, hipMemcpyDeviceToHost));
-    if (wb != 8 * s0->pwb) return fail(GM_EINVAL, "resume: the scratch holds no %u-bit planes solve", 8 * s0->pwb);
+    if (wb != s0->pmark())
+      return fail(GM_EINVAL, "resume: the scratch holds no %u-bit%s planes solve", 8 * s0->pwb,
+                  s0->pform == 3 ? " relative" : "");
   }
   const bool staged = mode != 0 && s0->pstage_k;
   if (mode != 0 && !s0->halo_ok) {
@@ -1166,7 +1212,7 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
       HIPCHK(hipMemsetAsync(s->st, 0, devstate_bytes(T), ws));
       HIPCHK(hipMemsetAsync(s->bcount, 0, kCountSlots * sizeof(BlockCount), ws));
       // the word width: written by k_plane_reach below (no reach: here)
-      if (stop == 0) HIPCHK(hipMemsetD32Async((hipDeviceptr_t)&s->st->word_bits, (int)(8 * s->pwb), 1, ws));
+      if (stop == 0) HIPCHK(hipMemsetD32Async((hipDeviceptr_t)&s->st->word_bits, (int)s->pmark(), 1, ws));
     }
     if (stop > 0) {
       if (timing) HIPCHK(hipEventRecord(kx[0], st));
@@ -1225,7 +1271,7 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
     if (k >= stop) break;
     if (per_level || (timing && l == 0)) HIPCHK(hipEventRecord(kr[2 * l], st));
     if (mode == 0 && !per_level) {
-      bat0.add(s0->ploff[l], s0->ploff[(size_t)l + 1], l < S ? s0->ploff[(size_t)l + 2] - s0->ploff[(size_t)l + 1] : 0);
+      bat0.add(s0->ploff[l], s0->ploff[(size_t)l + 1], l, l < S ? s0->ploff[(size_t)l + 2] - s0->ploff[(size_t)l + 1] : 0);
       if (l == S) bat0.flush();
     } else if (!pipe) {
       for (gm_solver* s : ss) plane_launch(s, l);
@@ -1264,14 +1310,11 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
     out->word_bits = 8 * s0->pwb;
     return GM_PARTIAL;
   }
-  for (gm_solver* s : ss) {
-    if (s->pwb == 1)
-      hipLaunchKernelGGL(k_plane_finish<1>, dim3(1), dim3(1024), 0, st, s->d, s->pg, (const void*)s->ptab, s->pbits,
-                         s->st, (const BlockCount*)s->bcount);
-    else
-      hipLaunchKernelGGL(k_plane_finish<2>, dim3(1), dim3(1024), 0, st, s->d, s->pg, (const void*)s->ptab, s->pbits,
-                         s->st, (const BlockCount*)s->bcount);
-  }
+  for (gm_solver* s : ss)
+    plane_form_dispatch(s, [&](auto WB, auto) {
+      hipLaunchKernelGGL(k_plane_finish<decltype(WB)::value>, dim3(1), dim3(1024), 0, st, s->d, s->pg,
+                         (const void*)s->ptab, s->pbits, s->st, (const BlockCount*)s->bcount);
+    });
   HIPCHK(hipGetLastError());
   if (mode == 1) {
     ncclGroupStart();
@@ -1346,12 +1389,10 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
 
 static int plane_query(gm_solver* s, const uint64_t* keys_dev, uint64_t n, uint32_t* words_dev) {
   const int grid = (int)std::min<u64>((n + kBlock - 1) / kBlock, (u64)s->grid);
-  if (s->pwb == 1)
-    hipLaunchKernelGGL(k_plane_query<1>, dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->pg, (const void*)s->ptab,
-                       s->pbits, (const u64*)keys_dev, n, words_dev);
-  else
-    hipLaunchKernelGGL(k_plane_query<2>, dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->pg, (const void*)s->ptab,
-                       s->pbits, (const u64*)keys_dev, n, words_dev);
+  plane_form_dispatch(s, [&](auto WB, auto) {
+    hipLaunchKernelGGL(k_plane_query<decltype(WB)::value>, dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->pg,
+                       (const void*)s->ptab, s->pbits, (const u64*)keys_dev, n, words_dev);
+  });
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(s->stream));
   return 0;
@@ -1375,13 +1416,10 @@ static int plane_positions(gm_solver* s, uint64_t* keys_dev, uint64_t cap, uint6
 
 static void plane_checksum_launch(gm_solver* s, u64* acc) {
   plane_no_dispatch(s->pg.no, [&](auto NO) {
-    constexpr int N = decltype(NO)::value;
-    if (s->pwb == 1)
-      hipLaunchKernelGGL((k_plane_checksum<N, 1>), dim3(s->grid), dim3(kBlock), 0, s->stream, s->d, s->pg,
-                         (const void*)s->ptab, (const uint32_t*)s->pbits, acc);
-    else
-      hipLaunchKernelGGL((k_plane_checksum<N, 2>), dim3(s->grid), dim3(kBlock), 0, s->stream, s->d, s->pg,
-                         (const void*)s->ptab, (const uint32_t*)s->pbits, acc);
+    plane_form_dispatch(s, [&](auto WB, auto) {
+      hipLaunchKernelGGL((k_plane_checksum<decltype(NO)::value, decltype(WB)::value>), dim3(s->grid), dim3(kBlock), 0,
+                         s->stream, s->d, s->pg, (const void*)s->ptab, (const uint32_t*)s->pbits, acc);
+    });
   });
 }
 

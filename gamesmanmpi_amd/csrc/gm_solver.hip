@@ -994,6 +994,10 @@ struct gm_solver {
   // PLANES (gm_plane.h, gm_plane_run.h)
   PlaneGeom pg{};
   uint32_t pwb = 1;     // word bytes
+  uint32_t pform = 1;   // word form: 1 8-bit, 2 16-bit, 3 relative 8-bit (gm_plane.h)
+  // DevState::word_bits of a planes solve in progress (a resume checks it):
+  // the word width, 0x100 set for the relative forms
+  uint32_t pmark() const { return 8u * pwb | (pform == 3 ? 0x100u : 0u); }
   uint32_t pS = 0;      // last plane level
   void* ptab = nullptr;  // words
   uint32_t* pbits = nullptr;  // reach map, 32 bits per plane row

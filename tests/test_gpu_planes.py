@@ -239,3 +239,93 @@ def test_planes_runs_equal_single_launches(flags):
     keys = np.arange(32 * 32 * 8 * 8 * 16, dtype=np.uint64)
     np.testing.assert_array_equal(sa.query(keys), sb.query(keys))
     assert sa.checksum() == sb.checksum()
+
+
+# Relative 8-bit order forms (gm_plane.h, word form 3): root digit sums
+# 254 .. 505 -- remoteness beyond the absolute 8-bit forms' 254 -- in one byte
+# per position, each word taken relative to its digit sum's window.
+REL_CASES = ["heaps=31:31:200",      # root sum 262: the smallest kind, one outer heap
+             "heaps=31:31:3:230",    # 295, every d % 4 class on both phases
+             "heaps=31:31:443"]      # 505 = kPlaneRelMaxSum: the window's edge
+
+
+@pytest.mark.parametrize("params", REL_CASES)
+def test_planes_relative_match_oracle(params):
+    """Every position's value and remoteness equals the oracle's at root
+    digit sums above 253 (relative forms: 8-bit words, the packed kernel)."""
+    s, r = _planes(params)
+    sol = _oracle(params)
+    assert r.extra["word_bits"] == 8 and r.extra["resolve_kernel"] == "k_plane_resolve_x2"
+    assert (r.positions, r.edges, r.primitives, r.root_line) == (sol.count, sol.edges, sol.stats["primitives"],
+                                                                  sol.root_line)
+    keys = np.arange(sol.count, dtype=np.uint64)
+    np.testing.assert_array_equal(s.query(keys), _oracle_words(sol, sol.count))
+    ck = s.checksum()
+    assert (ck["checksum"], ck["win"], ck["loss"]) == ("%016x" % sol.stats["checksum"], sol.stats["win"],
+                                                       sol.stats["loss"])
+
+
+def test_planes_relative_root_beyond_absolute_bytes():
+    """A root whose remoteness itself exceeds 254 (the absolute 8-bit forms'
+    limit), and one digit sum past the relative window: 16-bit words."""
+    from gamesmanmpi_amd import _lib
+    s, r = _planes("heaps=31:31:3:400")  # root sum 465
+    assert r.extra["word_bits"] == 8 and r.root_remoteness > 254
+    s16, r16 = _planes("heaps=31:31:3:400", flags=_lib.GM_F_WORDS16)
+    assert r16.extra["word_bits"] == 16 and r16.root_line == r.root_line
+    keys = np.arange(32 * 32 * 4 * 401, dtype=np.uint64)
+    np.testing.assert_array_equal(s.query(keys), s16.query(keys))
+    assert s.checksum() == s16.checksum()
+    _, rw = _planes("heaps=31:31:444")  # root sum 506
+    assert rw.extra["word_bits"] == 16
+
+
+def test_planes_relative_runs_and_resume():
+    """Relative forms: one-workgroup runs (per-group specialisation by the
+    outer digit sum mod 4) equal one launch per level, and a solve stopped
+    mid-backward resumes to the same words."""
+    from gamesmanmpi_amd import _lib
+    from gamesmanmpi_amd.games import GameSpec
+    from gamesmanmpi_amd.solver import Solver
+    params = "heaps=31:31:7:7:200"  # root sum 276
+    sa, ra = _planes(params)
+    sb, rb = _planes(params, flags=_lib.GM_F_PLANE_NO_RUNS)
+    assert ra.extra["word_bits"] == 8 and ra.root_line == rb.root_line
+    keys = np.arange(32 * 32 * 8 * 8 * 201, dtype=np.uint64)
+    w = sa.query(keys)
+    np.testing.assert_array_equal(w, sb.query(keys))
+    sc = Solver(GameSpec("sum_four_to_one", params), layout="planes")
+    T = sc.steps // 2
+    assert sc.solve_steps(0, T + 101) is None
+    rc = sc.solve_steps(T + 101, 0)
+    assert rc.root_line == ra.root_line
+    np.testing.assert_array_equal(sc.query(keys), w)
+
+
+REL_GROUP_CASES = [
+    (4, "heaps=31:31:3:255", 0, "one"),    # staged, k = 5, blocks of 64
+    (8, "heaps=31:31:3:255", 0, "own"),    # staged, blocks of 32, the RCCL schedule's rehearsal
+    (2, "heaps=31:31:3:255", 0, "one"),    # staged, k = 5 (1 mod 4) also for two ranks
+    (8, "heaps=31:31:1:255", LS, "one"),   # level-synchronous, link-spreading deal
+]
+
+
+@pytest.mark.parametrize("world,params,flags,streams", REL_GROUP_CASES)
+def test_planes_relative_group_matches_oracle(world, params, flags, streams):
+    """Relative forms on shards (the 4- and 8-GPU bench shapes' word form):
+    every position's word from its one owner equals the oracle's."""
+    from gamesmanmpi_amd.dist import group_solve
+    from gamesmanmpi_amd.games import GameSpec
+    rg, shards = group_solve(GameSpec("sum_four_to_one", params), world, flags=flags, streams=streams)
+    sol = _oracle(params)
+    assert rg.extra["word_bits"] == 8
+    assert (rg.positions, rg.edges, rg.root_line) == (sol.count, sol.edges, sol.root_line)
+    keys = np.arange(sol.count, dtype=np.uint64)
+    want = _oracle_words(sol, sol.count)
+    got = np.full(sol.count, 0xFFFFFFFF, np.uint32)
+    for sh in shards:
+        w = sh.query(keys)
+        own = w != 0xFFFFFFFF
+        assert (got[own] == 0xFFFFFFFF).all()
+        got[own] = w[own]
+    np.testing.assert_array_equal(got, want)
