@@ -54,17 +54,22 @@ typedef __attribute__((address_space(1))) uint32_t gu32;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr uint32_t kSpinLimit = 1u << 21;  // passes of ~0.1 us: a stuck wave gives up after ~0.2 s
 
-template <int NO, int LD>
+// ST: 1 write-through (sc1) stores; 0 plain stores (timing only: not a
+// valid hand-off).  TR: s_memtime stamps of each wave's first 16 items.
+template <int NO, int LD, int ST = 1, bool TR = false>
 __global__ __launch_bounds__(256) void k_flow(uint8_t* __restrict__ tab, const uint32_t* __restrict__ items,
                                               uint32_t nitems, uint32_t W, uint32_t* __restrict__ flags,
                                               uint32_t* __restrict__ tmo, PlaneGeom g, const uint4* __restrict__ zero,
-                                              uint32_t tabbytes) {
+                                              uint32_t tabbytes, uint64_t* __restrict__ stamps = nullptr) {
+  uint32_t nit = 0;
+  uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
   const uint32_t lane = threadIdx.x & 63, L = lane & 31;
   const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(tab, 0, tabbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc((void*)zero, 0, 4096, 0x00020000);
   constexpr int AUX = LD == 1 ? 16 : LD == 2 ? 17 : 0;
-  for (uint32_t it = w; it < nitems; it += W) {
+  for (uint32_t it = w; it < nitems; it += W, nit++) {
+    if (TR) t0 = __builtin_amdgcn_s_memtime();
     const uint32_t* ip = items + (size_t)it * 4;
     // the wave's four planes: [X0, Y0] on lanes 0-31, [X1, Y1] on 32-63
     const uint32_t px = ip[2 * (lane >> 5)], py = ip[2 * (lane >> 5) + 1];
@@ -96,6 +101,7 @@ __global__ __launch_bounds__(256) void k_flow(uint8_t* __restrict__ tab, const u
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
     }
+    if (TR) t1 = __builtin_amdgcn_s_memtime();
     uint32_t dx[NO], dy[NO];
     plane_digits<NO>(g, livex ? px : 0u, dx);
     plane_digits<NO>(g, livey ? py : 0u, dy);
@@ -137,6 +143,7 @@ __global__ __launch_bounds__(256) void k_flow(uint8_t* __restrict__ tab, const u
         }
       }
     }
+    if (TR) t2 = __builtin_amdgcn_s_memtime() + (Xh[0] & Yl[7] & 0 ? 1 : 0);
     const uint32_t primv = L == 0 ? ((px == 0 ? 0xFFu : 0u) | (py == 0 ? 0xFFu << 16 : 0u)) : 0u;
     uint32_t cur = 0, prev = 0, u1p = 0;
     uint32_t op[32];
@@ -174,15 +181,26 @@ __global__ __launch_bounds__(256) void k_flow(uint8_t* __restrict__ tab, const u
       oy_[k] = perm(t2, t1, 0x07060302u);
     }
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    if (TR) t3 = __builtin_amdgcn_s_memtime() + (ox_[0] & oy_[7] & 0 ? 1 : 0);
+    constexpr int SAUX = ST == 1 ? 16 : 0;
     if (livex) {
-      __builtin_amdgcn_raw_buffer_store_b128((v4u){ox_[0], ox_[1], ox_[2], ox_[3]}, rt, ox, 0, 16);
-      __builtin_amdgcn_raw_buffer_store_b128((v4u){ox_[4], ox_[5], ox_[6], ox_[7]}, rt, ox + 16, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b128((v4u){ox_[0], ox_[1], ox_[2], ox_[3]}, rt, ox, 0, SAUX);
+      __builtin_amdgcn_raw_buffer_store_b128((v4u){ox_[4], ox_[5], ox_[6], ox_[7]}, rt, ox + 16, 0, SAUX);
     }
     if (livey) {
-      __builtin_amdgcn_raw_buffer_store_b128((v4u){oy_[0], oy_[1], oy_[2], oy_[3]}, rt, oy, 0, 16);
-      __builtin_amdgcn_raw_buffer_store_b128((v4u){oy_[4], oy_[5], oy_[6], oy_[7]}, rt, oy + 16, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b128((v4u){oy_[0], oy_[1], oy_[2], oy_[3]}, rt, oy, 0, SAUX);
+      __builtin_amdgcn_raw_buffer_store_b128((v4u){oy_[4], oy_[5], oy_[6], oy_[7]}, rt, oy + 16, 0, SAUX);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every lane's rows written through before any flag
+    if (TR && nit < 16 && lane == 0) {
+      const uint64_t t4 = __builtin_amdgcn_s_memtime();
+      uint64_t* o = stamps + ((size_t)w * 16 + nit) * 5;
+      o[0] = t0;
+      o[1] = t1;
+      o[2] = t2;
+      o[3] = t3;
+      o[4] = t4;
+    }
     if ((lane & 31) < 2) {
       const uint32_t p = (lane & 1) ? py : px;
       if (p != kNone) __hip_atomic_store((gu32*)(flags + p), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -277,6 +295,9 @@ int main(int argc, char** argv) {
   tmo = flags + np;
   hipStream_t st;
   CK(hipStreamCreate(&st));
+  uint64_t* dstamps = nullptr;
+  CK(hipMalloc(&dstamps, (size_t)W * 16 * 5 * 8));
+  CK(hipMemset(dstamps, 0, (size_t)W * 16 * 5 * 8));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -301,9 +322,11 @@ int main(int argc, char** argv) {
     CK(hipMemsetAsync(flags, 0, np * 4 + 256, st));
     auto go = [&](auto NOc) {
       constexpr int NO = decltype(NOc)::value;
-      if (v == 1) hipLaunchKernelGGL((k_flow<NO, 1>), dim3(blocks), dim3(256), 0, st, tab, ditems, nitems, W, flags, tmo, g, (const uint4*)zero, (uint32_t)tbytes);
-      else if (v == 2) hipLaunchKernelGGL((k_flow<NO, 2>), dim3(blocks), dim3(256), 0, st, tab, ditems, nitems, W, flags, tmo, g, (const uint4*)zero, (uint32_t)tbytes);
-      else hipLaunchKernelGGL((k_flow<NO, 3>), dim3(blocks), dim3(256), 0, st, tab, ditems, nitems, W, flags, tmo, g, (const uint4*)zero, (uint32_t)tbytes);
+      if (v == 1) hipLaunchKernelGGL((k_flow<NO, 1>), dim3(blocks), dim3(256), 0, st, tab, ditems, nitems, W, flags, tmo, g, (const uint4*)zero, (uint32_t)tbytes, (uint64_t*)nullptr);
+      else if (v == 4) hipLaunchKernelGGL((k_flow<NO, 1, 0>), dim3(blocks), dim3(256), 0, st, tab, ditems, nitems, W, flags, tmo, g, (const uint4*)zero, (uint32_t)tbytes, (uint64_t*)nullptr);
+      else if (v == 5) hipLaunchKernelGGL((k_flow<NO, 1, 1, true>), dim3(blocks), dim3(256), 0, st, tab, ditems, nitems, W, flags, tmo, g, (const uint4*)zero, (uint32_t)tbytes, dstamps);
+      else if (v == 2) hipLaunchKernelGGL((k_flow<NO, 2>), dim3(blocks), dim3(256), 0, st, tab, ditems, nitems, W, flags, tmo, g, (const uint4*)zero, (uint32_t)tbytes, (uint64_t*)nullptr);
+      else hipLaunchKernelGGL((k_flow<NO, 3>), dim3(blocks), dim3(256), 0, st, tab, ditems, nitems, W, flags, tmo, g, (const uint4*)zero, (uint32_t)tbytes, (uint64_t*)nullptr);
     };
     switch (K) {
       case 3: go(std::integral_constant<int, 1>()); break;
@@ -352,10 +375,32 @@ int main(int argc, char** argv) {
         bad++;
       }
     if (bad) {
-      printf("rep %d: %zu differing bytes, first at %zu (plane %zu): got %02x want %02x MISMATCH\n", r, bad, first,
-             first / 1024, got[first], ref[first]);
-      return 2;
+      printf("rep %d: %zu differing bytes, first at %zu (plane %zu): got %02x want %02x MISMATCH%s\n", r, bad, first,
+             first / 1024, got[first], ref[first], var == 4 ? " (expected: plain stores are no hand-off)" : "");
+      if (var != 4) return 2;
     }
+  }
+  if (var == 5) {  // per-item phases (cycles of the wave's XCD clock): wait, load+fold, wavefront, store+drain, gap to the next item
+    std::vector<uint64_t> h((size_t)W * 16 * 5);
+    CK(hipMemcpy(h.data(), dstamps, h.size() * 8, hipMemcpyDeviceToHost));
+    std::vector<double> ph[5];
+    for (uint32_t w = 0; w < W; w++)
+      for (int n = 0; n < 16; n++) {
+        const uint64_t* o = &h[((size_t)w * 16 + n) * 5];
+        if (!o[4]) continue;
+        for (int k = 0; k < 4; k++) ph[k].push_back((double)(o[k + 1] - o[k]));
+        const uint64_t* nx = o + 5;
+        if (n + 1 < 16 && nx[4]) ph[4].push_back((double)(nx[0] - o[4]));
+      }
+    const char* nm[5] = {"wait", "load+fold", "wavefront", "store+drain", "gap"};
+    printf("item phases (memtime ticks, 100 MHz):");
+    for (int k = 0; k < 5; k++) {
+      std::sort(ph[k].begin(), ph[k].end());
+      if (ph[k].empty()) continue;
+      printf(" %s p10 %.0f p50 %.0f p90 %.0f;", nm[k], ph[k][ph[k].size() / 10], ph[k][ph[k].size() / 2],
+             ph[k][ph[k].size() * 9 / 10]);
+    }
+    printf("\n");
   }
   float best = 1e9, sum = 0;
   for (float t : ts) {
