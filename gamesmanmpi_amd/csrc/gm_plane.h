@@ -60,6 +60,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace gm {
 
 constexpr int kPlaneMaxOuter = 6;  // K <= 8 heaps
@@ -194,6 +196,17 @@ __device__ __forceinline__ void plane_digits(const PlaneGeom& g, uint32_t P, uin
       dig[j] = x % g.base[j];
       x /= g.base[j];
     }
+  }
+}
+
+// global digits of a local plane: outer digits j < NO - 1 from the lower
+// index, the top one from the shard's block layout (world 1: plain digits)
+template <int NO>
+__device__ __forceinline__ void plane_global_digits(const PlaneGeom& g, uint32_t P, uint32_t* dig) {
+  plane_digits<NO>(g, P, dig);
+  if (g.world > 1 && NO > 0) {
+    const uint32_t u = P / g.Z, j = u / g.B, o = u - j * g.B;
+    dig[NO - 1] = plane_gblock(g, j) * g.B + o;
   }
 }
 
@@ -405,7 +418,9 @@ __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
   return __builtin_amdgcn_perm(hi, lo, sel);
 }
 
-// (RS: with WB = 3, the launch's outer digit sum s mod 4)
+// (RS: with WB = 3, the launch's outer digit sum s mod 4; -1: per wave
+// visit, from its first plane -- the list deals every four consecutive
+// entries one s mod 4, padding with kPlaneAbsent entries)
 template <int WB, int NO, bool SH, int RS = 0>
 __device__ __forceinline__ void plane_x2_range(typename PlaneWord<WB>::T* __restrict__ tab,
                                                const void* __restrict__ list, const PlaneShare sh,
@@ -416,19 +431,26 @@ __device__ __forceinline__ void plane_x2_range(typename PlaneWord<WB>::T* __rest
   typedef typename W::T T;
   constexpr int DW = W::DW, NQ = DW / 4;
   constexpr bool B8 = DW == 8, REL = WB == 3;
-  constexpr int B0 = (4 - RS) & 3;  // relative: row bytes j = B0 mod 4 are parents with d % 4 == 0
   const uint32_t lane = threadIdx.x & 63, L = lane & 31;
   for (uint32_t i0 = sh.first; i0 < sh.end; i0 += sh.stride) {
     const uint32_t ix = i0 + 2 * (lane >> 5), iy = ix + 1;
-    const bool livex = ix < sh.end, livey = iy < sh.end;
+    bool livex = ix < sh.end, livey = iy < sh.end;
     PlaneEntry ex, ey;
     if (SH) {
       ex = ((const PlaneEntry*)list)[livex ? ix : i0];
       ey = ((const PlaneEntry*)list)[livey ? iy : i0];
+      if (RS < 0) {  // padding entries: compute on the visit's first plane, store nothing
+        const PlaneEntry e0 = ((const PlaneEntry*)list)[i0];
+        if (ex.p == kPlaneAbsent) ex = e0, livex = false;
+        if (ey.p == kPlaneAbsent) ey = e0, livey = false;
+      }
     } else {
       ex.p = ((const uint32_t*)list)[livex ? ix : i0];
       ey.p = ((const uint32_t*)list)[livey ? iy : i0];
     }
+    auto visit = [&](auto RSc) {
+    constexpr int RS_ = decltype(RSc)::value;
+    constexpr int B0 = (4 - RS_) & 3;  // relative: row bytes j = B0 mod 4 are parents with d % 4 == 0
     uint32_t dx[NO > 0 ? NO : 1], dy[NO > 0 ? NO : 1];
     plane_digits<NO>(g, ex.p, dx);
     plane_digits<NO>(g, ey.p, dy);
@@ -539,7 +561,7 @@ __device__ __forceinline__ void plane_x2_range(typename PlaneWord<WB>::T* __rest
           a = perm(Yh[d], Xh[d], sel);
         }
         const uint32_t u2r = from_lane_below(u1p);
-        const int dcls = (RS + q) & 3;  // relative forms: d % 4 of this step's positions
+        const int dcls = (RS_ + q) & 3;  // relative forms: d % 4 of this step's positions
         const uint32_t pre = REL && dcls == 0 ? pk_max16(a, rel_shift_pk(pk_max16(prev, u2r)))
                                               : pk_max16(pk_max16(a, prev), u2r);
         const uint32_t u1r = from_lane_below(cur);
@@ -582,6 +604,21 @@ __device__ __forceinline__ void plane_x2_range(typename PlaneWord<WB>::T* __rest
       store(tab + oy, oy_);
       if (SH && ey.send != kPlaneAbsent) store(send + (size_t)ey.send * 1024u + L * 32u, oy_);
     }
+    };
+    if constexpr (RS >= 0) {
+      visit(std::integral_constant<int, RS>());
+    } else {  // the visit's outer digit sum (global digits) mod 4, wave-uniform
+      uint32_t dg[NO > 0 ? NO : 1], sum = 0;
+      plane_global_digits<NO>(g, ex.p, dg);
+#pragma unroll
+      for (int j = 0; j < NO; j++) sum += dg[j];
+      switch (__builtin_amdgcn_readfirstlane(sum) & 3u) {
+        case 0: visit(std::integral_constant<int, 0>()); break;
+        case 1: visit(std::integral_constant<int, 1>()); break;
+        case 2: visit(std::integral_constant<int, 2>()); break;
+        default: visit(std::integral_constant<int, 3>()); break;
+      }
+    }
   }
 }
 
@@ -612,6 +649,7 @@ struct PlaneRun {
   uint32_t n;
   uint32_t off[kPlaneRunMax + 1];  // list entries, absolute
   uint64_t rs;                     // relative forms: group i's outer digit sum mod 4 in bits 2i, 2i + 1
+  uint32_t visit;                  // relative forms: per wave visit instead (staged lists)
 };
 template <int WB, int NO, bool SH, bool X1>
 __global__ __launch_bounds__(kPlaneRunThreads) void k_plane_run(typename PlaneWord<WB>::T* __restrict__ tab,
@@ -624,7 +662,14 @@ __global__ __launch_bounds__(kPlaneRunThreads) void k_plane_run(typename PlaneWo
   for (uint32_t i = 0; i < run.n; i++) {
     const PlaneShare sh{run.off[i] + w * per, run.off[i + 1], nw * per};
     if constexpr (WB == 3) {
-      switch ((run.rs >> (2 * i)) & 3u) {
+      bool done = false;
+      if constexpr (SH) {
+        if (run.visit) {
+          plane_x2_range<WB, NO, SH, -1>(tab, list, sh, g, zero, recv, send);
+          done = true;
+        }
+      }
+      if (!done) switch ((run.rs >> (2 * i)) & 3u) {
         case 0: plane_x2_range<WB, NO, SH, 0>(tab, list, sh, g, zero, recv, send); break;
         case 1: plane_x2_range<WB, NO, SH, 1>(tab, list, sh, g, zero, recv, send); break;
         case 2: plane_x2_range<WB, NO, SH, 2>(tab, list, sh, g, zero, recv, send); break;
@@ -639,16 +684,6 @@ __global__ __launch_bounds__(kPlaneRunThreads) void k_plane_run(typename PlaneWo
   }
 }
 
-// global digits of a local plane: outer digits j < NO - 1 from the lower
-// index, the top one from the shard's block layout (world 1: plain digits)
-template <int NO>
-__device__ __forceinline__ void plane_global_digits(const PlaneGeom& g, uint32_t P, uint32_t* dig) {
-  plane_digits<NO>(g, P, dig);
-  if (g.world > 1 && NO > 0) {
-    const uint32_t u = P / g.Z, j = u / g.B, o = u - j * g.B;
-    dig[NO - 1] = plane_gblock(g, j) * g.B + o;
-  }
-}
 
 // Forward pass: the reach bitmap (one bit per position, plane P's row h1 is
 // the 32-bit word bits[P * 32 + h1], bit h0) and the counts.  Moves act on

@@ -196,12 +196,26 @@ struct PlaneShape {
 // first needs row s at key k s: the ranks form a pipeline in which rank r
 // trails rank r - 1 by about B keys, and the transfers hide under B - 1 keys
 // of compute.  Larger k shortens the trail (fewer planes per key) but adds
-// launches (each >= ~9 us: profiles/r03l_group*.jsonl); k by world from the
-// pipeline model with that floor (tools/stage_model.py --floor 9e-6).  The
-// relative word forms need k = 1 mod 4: a key's planes then share their
-// outer digit sum mod 4 (s = rB + o + c = rB + key - (k - 1) c), which the
-// launch's kernel is specialised for.
-static uint32_t plane_stage_k(int world, bool rel) { return rel ? 5u : world <= 2 ? 2u : world <= 4 ? 4u : 5u; }
+// launches.  Measured per-shard sweeps of the 4- and 8-GPU bench shapes
+// (8-bit relative words, profiles/r04j/): 2.32 / 2.89 / 3.51 / 4.01 ms (N = 4)
+// and 2.35 / 2.92 / 3.54 / 4.03 ms (N = 8) at k = 2 / 3 / 4 / 5 -- every key
+// costs ~4.5 us beyond its planes, while the trail is B - 1 keys whatever k
+// is (narrower keys only shorten each of them) -- so k = 2.  A
+// key's planes have outer digit sums s = rB + o + c = rB + key - (k - 1) c of
+// several residues mod 4: with the relative word forms the staged lists deal
+// each key's planes by s mod 4 in whole wave visits (padded) and the kernel
+// picks its specialisation per visit (plane_x2_range, RS = -1).
+// GM_PLANE_STAGE_K overrides k (A/B).
+static uint32_t plane_stage_k(int world) {
+  if (const char* e = getenv("GM_PLANE_STAGE_K")) {
+    const int k = atoi(e);
+    if (k >= 1 && k <= 64) return (uint32_t)k;
+  }
+  return 2u;
+}
+// list padding of the relative forms' staged deal: at most 3 entries per
+// (key, s mod 4) class
+static u64 plane_stage_pad(const PlaneShape* ps) { return ps->form == 3 ? 12ull * ps->nkeys : 0ull; }
 
 static u64 rup256(u64 x) { return (x + 255) & ~255ull; }
 
@@ -268,7 +282,7 @@ static int plane_shape(const Desc* d, int rank, int world, uint32_t flags, Plane
     if (staged) {
       uint32_t smax = 0;  // largest digit sum below the top
       for (uint32_t j = 0; j + 1 < g.no; j++) smax += g.base[j] - 1;
-      ps->stage_k = plane_stage_k(world, ps->form == 3);
+      ps->stage_k = plane_stage_k(world);
       ps->nrows = smax + 1;
       ps->nkeys = (uint32_t)(B - 1) + ps->stage_k * smax + 1;
     }
@@ -288,7 +302,7 @@ static int plane_shape(const Desc* d, int rank, int world, uint32_t flags, Plane
   ps->table_bytes = ps->send_off + rup256(ps->nsend * pb);
   ps->zero_off = rup256(scratch_bytes_for(d->max_levels));
   ps->list_off = ps->zero_off + 4096;
-  ps->scratch_bytes = ps->list_off + rup256(ps->nlocal * (world > 1 ? sizeof(PlaneEntry) : 4));
+  ps->scratch_bytes = ps->list_off + rup256((ps->nlocal + plane_stage_pad(ps)) * (world > 1 ? sizeof(PlaneEntry) : 4));
   return 0;
 }
 
@@ -342,16 +356,32 @@ static int plane_lists_staged(gm_solver* s, const PlaneShape& ps, const std::vec
     return fail(GM_ECORRUPT, "staged halo plan: %llu / %llu planes, sized %llu / %llu",
                 (unsigned long long)s->prcv_off[R], (unsigned long long)s->psnd_off[R],
                 (unsigned long long)ps.nrecv, (unsigned long long)ps.nsend);
-  s->ploff.assign(K + 1, 0);
-  for (u64 o = 0; o < B; o++)
-    for (u64 l = 0; l < Z; l++) s->ploff[o + k * sig[l] + 1]++;
-  for (u64 q = 0; q < K; q++) s->ploff[q + 1] += s->ploff[q];
-  if (s->ploff[K] != ps.nlocal) return fail(GM_ECORRUPT, "staged lists: %llu entries for %llu planes",
-                                            (unsigned long long)s->ploff[K], (unsigned long long)ps.nlocal);
-  bytes.resize(ps.nlocal * sizeof(PlaneEntry));
-  PlaneEntry* E = (PlaneEntry*)bytes.data();
-  std::vector<u64> pos(s->ploff.begin(), s->ploff.end());
+  // entries per key; relative forms: per (key, s mod 4) class, each class
+  // padded to whole wave visits of 4 entries (plane_x2_range, RS = -1)
+  const bool rel = ps.form == 3;
   const u64 t0 = (u64)g.rank * B;
+  const u64 ncls = rel ? 4 : 1;
+  auto cls_of = [&](u64 o, uint32_t c) -> u64 { return rel ? (t0 + o + c) & 3u : 0u; };
+  std::vector<u64> cnt(K * ncls, 0);
+  for (u64 o = 0; o < B; o++)
+    for (u64 l = 0; l < Z; l++) cnt[(o + k * sig[l]) * ncls + cls_of(o, sig[l])]++;
+  s->ploff.assign(K + 1, 0);
+  std::vector<u64> cpos(K * ncls, 0);  // first entry of each (key, class)
+  u64 at = 0;
+  for (u64 q = 0; q < K; q++) {
+    s->ploff[q] = at;
+    for (u64 c = 0; c < ncls; c++) {
+      cpos[q * ncls + c] = at;
+      at += rel ? (cnt[q * ncls + c] + 3) / 4 * 4 : cnt[q * ncls + c];
+    }
+  }
+  s->ploff[K] = at;
+  if (at < ps.nlocal || at > ps.nlocal + plane_stage_pad(&ps))
+    return fail(GM_ECORRUPT, "staged lists: %llu entries for %llu planes", (unsigned long long)at,
+                (unsigned long long)ps.nlocal);
+  bytes.assign(at * sizeof(PlaneEntry), 0xFF);  // padding: every field kPlaneAbsent
+  PlaneEntry* E = (PlaneEntry*)bytes.data();
+  std::vector<u64>& pos = cpos;
   for (u64 o = 0; o < B; o++)
     for (u64 l = 0; l < Z; l++) {
       const uint32_t c = sig[l];
@@ -365,7 +395,7 @@ static int plane_lists_staged(gm_solver* s, const PlaneShape& ps, const std::vec
       e.top1 = halo(1);
       e.top2 = halo(2);
       e.send = (tx && o + 2 >= B) ? (uint32_t)(row[c] + (o + 2 - B) * ncl[c] + rk[l]) : kPlaneAbsent;
-      E[pos[o + k * c]++] = e;
+      E[pos[(o + k * c) * ncls + cls_of(o, c)]++] = e;
     }
   s->pbnd.clear();
   return 0;
@@ -564,7 +594,8 @@ static int plane_setup(gm_solver* s, const gm_buffers* buf) {
 static bool plane_x1(const gm_solver* s) { return s->pform == 2 || (s->pform == 1 && (s->flags & GM_F_PLANE_X1)); }
 
 // rs: the launch's outer digit sum mod 4 (the relative forms' kernels are
-// specialised for it)
+// specialised for it), or kPlaneRsVisit: per wave visit (staged lists)
+constexpr uint32_t kPlaneRsVisit = 4;
 template <int WB, int NO, bool SH>
 static void plane_launch_t(gm_solver* s, u64 a, u64 n, u64 pa, u64 pn, uint32_t rs) {
   if (!n) return;
@@ -584,6 +615,10 @@ static void plane_launch_t(gm_solver* s, u64 a, u64 n, u64 pa, u64 pn, uint32_t 
       hipLaunchKernelGGL((k_plane_resolve_x2<3, NO, SH, decltype(RS)::value>), grid, blk, 0, s->stream, (T*)s->ptab,
                          list, (uint32_t)n, s->pg, s->pzero, (const T*)s->precv, (T*)s->psend, pf, pfl);
     };
+    if (SH && rs == kPlaneRsVisit) {
+      go(std::integral_constant<int, -1>());
+      return;
+    }
     switch (rs & 3u) {
       case 0: go(std::integral_constant<int, 0>()); break;
       case 1: go(std::integral_constant<int, 1>()); break;
@@ -674,12 +709,13 @@ struct PlaneBatcher {
   }
   void flush() {
     launches += run.n ? 1 : 0;
-    if (run.n == 1) plane_launch_range(s, run.off[0], run.off[1] - run.off[0], (uint32_t)run.rs & 3u);
+    if (run.n == 1) plane_launch_range(s, run.off[0], run.off[1] - run.off[0], run.visit ? kPlaneRsVisit : (uint32_t)run.rs & 3u);
     else if (run.n > 1) {
       plane_form_dispatch(s, [&](auto WB, auto SH) { plane_run_w<decltype(WB)::value, decltype(SH)::value>(s, run); });
     }
     run.n = 0;
     run.rs = 0;
+    run.visit = 0;
   }
   // list entries [a, b), outer digit sum = rs mod 4; the next group's size
   // (prefetch)
@@ -694,6 +730,7 @@ struct PlaneBatcher {
     if (run.n == (uint32_t)kPlaneRunMax || (run.n && run.off[run.n] != a)) flush();
     if (run.n == 0) run.off[0] = (uint32_t)a;
     run.rs |= (u64)(rs & 3u) << (2 * run.n);
+    run.visit = rs == kPlaneRsVisit;
     run.off[++run.n] = (uint32_t)b;
   }
 };
@@ -926,8 +963,8 @@ static int plane_backward_staged(std::vector<gm_solver*>& ss, int mode, hipStrea
   };
   auto launch_key = [K, B](PlaneBatcher& pb_, uint32_t key) {
     const std::vector<u64>& o = pb_.s->ploff;
-    // outer digit sums of the key: rank * B + key (mod 4; plane_stage_k)
-    const uint32_t rs = (uint32_t)pb_.s->rank * B + key;
+    (void)B;  // relative forms: s mod 4 per wave visit (plane_lists_staged)
+    const uint32_t rs = kPlaneRsVisit;
     pb_.add(o[key], o[(size_t)key + 1], rs, key + 1 < K ? o[(size_t)key + 2] - o[(size_t)key + 1] : 0);
   };
   if (mode == 2) {

@@ -13,6 +13,7 @@ level-synchronous deal instead.
     python tools/group_planes.py WORLD [REPS] [FLAGS]"""
 import ctypes
 import json
+import os
 import sys
 import time
 
@@ -47,7 +48,8 @@ def main():
         print(json.dumps({"world": world, "heaps": heaps, "flags": flags, "positions": res.positions, "root": res.root_line,
                           "layout": res.extra.get("layout"), "wall_ms": wall, "ms_forward": res.ms_forward,
                           "ms_backward": res.ms_backward, "ms_backward_per_shard": res.ms_backward / world,
-                          "word_bits": res.extra.get("word_bits")}), flush=True)
+                          "word_bits": res.extra.get("word_bits"),
+                          "stage_k": os.environ.get("GM_PLANE_STAGE_K", "default")}), flush=True)
 
 
 if __name__ == "__main__":
