@@ -39,14 +39,15 @@ KERNEL_FLAGS = (GM_F_WORDS32 | GM_F_RESOLVE_SCALAR | GM_F_SHARD_INORDER | GM_F_W
 # gm_result.kernels codes (gm_solver.hip DenseResolveKind / DensePullKind)
 RESOLVE_KERNELS = {1: "k_dense_resolve8p", 2: "k_dense_resolve8c", 3: "k_dense_resolve4p",
                    4: "k_dense_resolve4c", 5: "k_dense_resolve4", 6: "k_dense_resolve",
-                   7: "k_dense_resolve16p", 8: "k_plane_resolve", 9: "k_plane_resolve_x2"}
+                   7: "k_dense_resolve16p", 8: "k_plane_resolve", 9: "k_plane_resolve_x2",
+                   10: "k_rk_backward"}
 PULL_KERNELS = {1: "k_dense_pull_words", 2: "k_dense_pull", 3: "k_plane_reach"}
-GM_MODE_HASHED, GM_MODE_DENSE, GM_MODE_BUCKETED, GM_MODE_PLANES = 0, 1, 2, 3
+GM_MODE_HASHED, GM_MODE_DENSE, GM_MODE_BUCKETED, GM_MODE_PLANES, GM_MODE_RANKED = 0, 1, 2, 3, 4
 # host-staged transport (include/gamesman.h gm_xfer_fn)
 GM_XFER_SENDRECV, GM_XFER_ALLGATHER = 0, 1
 XFER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,
                            ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int)
-MODE_NAMES = {0: "hashed", 1: "dense", 2: "bucketed", 3: "planes"}
+MODE_NAMES = {0: "hashed", 1: "dense", 2: "bucketed", 3: "planes", 4: "ranked"}
 GM_MAXCHILD = 32
 GM_COMM_ID_BYTES = 128
 GM_NO_WORD = 0xFFFFFFFF

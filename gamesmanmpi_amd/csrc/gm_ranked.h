@@ -1,0 +1,561 @@
+// gm_ranked.h -- RANKED layout (GM_MODE_RANKED): toot_and_otto_bitstring
+// positions at COMPUTED indices -- no keys stored, no dedup, no hash.
+// Included by gm_solver.hip after the solver object, the count helpers and
+// the keyed layouts (inside its extern "C" block: templates need C++ linkage,
+// see the extern "C++" below).
+//
+// Replaces, for toot-and-otto, the keyed pipeline of the reference's
+// per-position job loop (src/process.py:109-267: expand, look up, dedup in
+// the resolved/remote CacheDicts, resolve) the way PLANES replaces it for the
+// sum game: the state space is rank-indexable.  A position is
+//   * per column x: its height h_x in [0, H] and the letters of its stack,
+//     bit y = 1 for T (gravity: do_move fills the lowest blank cell,
+//     toot_and_otto_bitstring.py:106-116, so a column is a contiguous stack);
+//   * a = how many T's the first player has placed, in [0, 6].
+// Everything else in the key follows: pieces on the board L = sum h_x (the
+// level; the first player moves at even L), the T's on the board nT (the
+// popcount of the stacks), hence every hand (6 each at the start, :38-40:
+// first player T = 6 - a, O = 6 - (ceil(L/2) - a); second player T =
+// 6 - (nT - a), O = 6 - (floor(L/2) - (nT - a))) and the turn bit.
+//
+// Index space: the height vectors (h_0 .. h_{C-1}) of one level in ascending
+// code order (hvcode = sum h_x (H+1)^x), each a BLOCK of 8 x 2^L slots
+// [a][stack bits] -- a-major, the stacks' L bits concatenated column after
+// column (column x at bits [off_x, off_x + h_x), off_x = sum_{c<x} h_c) --
+// and the levels one after another, each padded to 64 slots.  toot 6x4:
+// 8 x 31^6 = 7.1e9 slots, one byte of word each (value | remoteness << 2,
+// remoteness <= 24) + a reach and an "expandable" bit = 8.9 GB against the
+// BUCKETED layout's ~70 GB of keys, in-edges and partitions.
+//
+// A move in column x with letter l: child block = hvcode + (H+1)^x, child
+// stack bits = the parent's with bit l inserted at off_x + h_x, a + 1 if the
+// first player placed a T.  Consecutive lanes take consecutive stack bits of
+// one block, so for a fixed move their children are consecutive bytes too
+// (one or two lines per wave): every access is coalesced, and the only
+// random access left is none.
+//
+// Forward, level L (pull): a slot is reached iff its hands are valid and one
+// of its parents -- remove the top piece of some column -- is reached and not
+// primitive ("expandable" bit); primitive = the reference rule on the key
+// (toot_prim).  Backward, level L: every reached slot gathers its children's
+// words (the legal moves: a column not full, a letter left in the mover's
+// hand) and applies the reference reduction (_res_red/_remote_red, SURVEY
+// §8a A8/A9) -- the same words, counts and fingerprint as the keyed layouts
+// (tests/test_gpu_ranked.py).
+extern "C++" {
+
+constexpr uint32_t kRankHand = 6;  // every hand starts at 6 (toot_and_otto_bitstring.py:38-40)
+
+// (RankGeom: gm_solver.hip, before the solver object that holds one)
+
+struct RankPos {
+  uint32_t h[kRankMaxCols], off[kRankMaxCols];
+};
+__device__ __forceinline__ void rk_unpack(const RankGeom& g, uint32_t ph, RankPos& p) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int x = 0; x < kRankMaxCols; x++) {
+    p.h[x] = x < (int)g.C ? (ph >> (4 * x)) & 15u : 0u;
+    p.off[x] = o;
+    o += p.h[x];
+  }
+}
+// every hand count in [0, 6]: the first player's T's used = a; O's = ceil(L/2) - a;
+// the second player's T's = nT - a, O's = floor(L/2) - (nT - a)
+struct RankHands {
+  int t1, o1, t2, o2;
+};
+__device__ __forceinline__ RankHands rk_hands(uint32_t L, uint32_t nT, uint32_t a) {
+  RankHands u;
+  u.t1 = (int)a;
+  u.o1 = (int)((L + 1) / 2) - (int)a;
+  u.t2 = (int)nT - (int)a;
+  u.o2 = (int)(L / 2) - u.t2;
+  return u;
+}
+__device__ __forceinline__ bool rk_valid(const RankHands& u) {
+  return u.t1 >= 0 && u.t1 <= (int)kRankHand && u.o1 >= 0 && u.o1 <= (int)kRankHand && u.t2 >= 0 &&
+         u.t2 <= (int)kRankHand && u.o2 >= 0 && u.o2 <= (int)kRankHand;
+}
+// the toot key (gm_games.h layout) of a slot with valid hands
+__device__ __forceinline__ u64 rk_key(const RankGeom& g, const RankPos& p, uint32_t pat, uint32_t L, const RankHands& u) {
+  u64 t = 0, o = 0;
+#pragma unroll
+  for (int x = 0; x < kRankMaxCols; x++) {
+    if (x >= (int)g.C) break;
+    const uint32_t hb = p.h[x], col = (pat >> p.off[x]) & ((1u << hb) - 1u);
+    for (uint32_t y = 0; y < hb; y++) {
+      const u64 cell = 1ull << (g.C * y + (uint32_t)x);
+      if ((col >> y) & 1u) t |= cell;
+      else o |= cell;
+    }
+  }
+  const uint32_t A = g.A;
+  return t | (o << A) | ((u64)(kRankHand - u.t1) << (2 * A)) | ((u64)(kRankHand - u.o1) << (2 * A + 3)) |
+         ((u64)(kRankHand - u.t2) << (2 * A + 6)) | ((u64)(kRankHand - u.o2) << (2 * A + 9)) |
+         ((u64)((L & 1u) == 0) << (2 * A + 12));
+}
+// key -> slot (false: not a gravity board with consistent hands)
+__device__ __forceinline__ bool rk_slot_of(const RankGeom& g, u64 key, u64* slot, uint32_t* level) {
+  const uint32_t A = g.A;
+  const u64 full = (A >= 64) ? ~0ull : ((1ull << A) - 1);
+  const u64 t = key & full, o = (key >> A) & full;
+  if (t & o) return false;
+  if (key >> (2 * A + 13)) return false;
+  uint32_t hv = 0, pat = 0, L = 0;
+  for (uint32_t x = 0; x < g.C; x++) {
+    uint32_t h = 0;
+    while (h < g.H && (((t | o) >> (g.C * h + x)) & 1)) h++;
+    for (uint32_t y = h; y < g.H; y++)
+      if (((t | o) >> (g.C * y + x)) & 1) return false;  // a gap under a piece
+    for (uint32_t y = 0; y < h; y++) pat |= (uint32_t)((t >> (g.C * y + x)) & 1) << (L + y);
+    hv += h * g.stride[x];
+    L += h;
+  }
+  const uint32_t nT = __builtin_popcount(pat);
+  const uint32_t h1t = (uint32_t)((key >> (2 * A)) & 7), h1o = (uint32_t)((key >> (2 * A + 3)) & 7);
+  const uint32_t h2t = (uint32_t)((key >> (2 * A + 6)) & 7), h2o = (uint32_t)((key >> (2 * A + 9)) & 7);
+  const uint32_t turn = (uint32_t)((key >> (2 * A + 12)) & 1);
+  if (h1t > kRankHand) return false;
+  const uint32_t a = kRankHand - h1t;
+  const RankHands u = rk_hands(L, nT, a);
+  if (!rk_valid(u) || kRankHand - u.o1 != h1o || kRankHand - u.t2 != h2t || kRankHand - u.o2 != h2o ||
+      turn != ((L & 1u) == 0))
+    return false;
+  *slot = g.base[hv] + ((u64)a << L) + pat;
+  *level = L;
+  return true;
+}
+
+// The level's slots as one index space: item i of level L = slot lvstart + i,
+// block i >> (L + 3) of the level's list (lvoff + that), a = (i >> L) & 7,
+// stack bits = i & (2^L - 1).  A wave's 64 items are one aligned 64-bit word
+// of each bitmap (levels start 64-aligned).
+// (nitems: the level's slots rounded up to 64, so every bitmap word of the
+// level is written -- no clearing -- nreal: its slots)
+template <int KIND>
+__global__ __launch_bounds__(256) void k_rk_forward(Desc d, RankGeom g, uint32_t L, u64 lvstart, uint32_t lvoff,
+                                                    u64 nitems, u64 nreal, BlockCount* bc, DevState* st) {
+  u64 npos = 0, prims = 0;
+  const uint32_t lane = threadIdx.x & 63;
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i0 = (u64)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); i0 < nitems; i0 += stride) {
+    const u64 i = i0 + lane;
+    bool reach = false, ex = false;
+    if (i < nreal) {
+      const u64 blk = i >> (L + 3);
+      const uint32_t a = (uint32_t)((i >> L) & 7u), pat = (uint32_t)(i & ((1ull << L) - 1));
+      const uint32_t hvc = g.lvhv[lvoff + blk];
+      RankPos p;
+      rk_unpack(g, g.lvph[lvoff + blk], p);
+      const RankHands u = rk_hands(L, (uint32_t)__builtin_popcount(pat), a);
+      if (rk_valid(u)) {
+        if (L == 0) {
+          reach = true;  // the root (hands 6 / 6 / 6 / 6, first player to move)
+        } else {
+          const bool p1moved = ((L - 1) & 1u) == 0;  // the move into level L was the first player's
+#pragma unroll
+          for (int x = 0; x < kRankMaxCols; x++) {
+            if (x >= (int)g.C || p.h[x] == 0) continue;
+            const uint32_t q = p.off[x] + p.h[x] - 1, l = (pat >> q) & 1u;
+            if (p1moved && l && a == 0) continue;
+            const uint32_t pp = (pat & ((1u << q) - 1u)) | ((pat >> (q + 1)) << q);
+            const uint32_t pa = a - (p1moved && l ? 1u : 0u);
+            const u64 ps = g.base[hvc - g.stride[x]] + ((u64)pa << (L - 1)) + pp;
+            if ((g.expd[ps >> 5] >> (ps & 31)) & 1u) {
+              reach = true;
+              break;
+            }
+          }
+        }
+        if (reach) {
+          const int pr = Game<KIND>::prim(d, rk_key(g, p, pat, L, u));
+          ex = pr == UNDECIDED;
+          prims += !ex;
+          npos++;
+        }
+      }
+    }
+    const u64 br = __ballot(reach), be = __ballot(ex);
+    if (lane == 0) {
+      const u64 w = (lvstart + i0) >> 6;  // aligned: lvstart and i0 are multiples of 64
+      reinterpret_cast<u64*>(g.reach)[w] = br;
+      reinterpret_cast<u64*>(g.expd)[w] = be;
+    }
+  }
+  block_count(bc, npos, 0);
+  block_add(&st->prims, prims);
+}
+
+template <int KIND>
+__global__ __launch_bounds__(256) void k_rk_backward(Desc d, RankGeom g, uint32_t L, u64 lvstart, uint32_t lvoff,
+                                                     u64 nitems, BlockCount* bc, DevState* st) {
+  u64 edges = 0;
+  uint32_t err = 0;
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < nitems; i += stride) {
+    const u64 slot = lvstart + i;
+    if (!((g.reach[slot >> 5] >> (slot & 31)) & 1u)) continue;
+    const u64 blk = i >> (L + 3);
+    const uint32_t a = (uint32_t)((i >> L) & 7u), pat = (uint32_t)(i & ((1ull << L) - 1));
+    const uint32_t hvc = g.lvhv[lvoff + blk];
+    RankPos p;
+    rk_unpack(g, g.lvph[lvoff + blk], p);
+    const RankHands u = rk_hands(L, (uint32_t)__builtin_popcount(pat), a);
+    const int pr = Game<KIND>::prim(d, rk_key(g, p, pat, L, u));
+    uint32_t word;
+    if (pr != UNDECIDED) {
+      word = make_word(pr, 0);  // process.py:120-123
+    } else {
+      const bool p1 = (L & 1u) == 0;  // the first player moves at even levels
+      const bool hasT = p1 ? u.t1 < (int)kRankHand : u.t2 < (int)kRankHand;
+      const bool hasO = p1 ? u.o1 < (int)kRankHand : u.o2 < (int)kRankHand;
+      const uint32_t at = a + (p1 ? 1u : 0u);
+      bool any_loss = false, any_tie = false, any_draw = false;
+      uint32_t min_loss = 0xFFFFFFFFu, max_all = 0, nch = 0;
+      auto take = [&](uint32_t w) {
+        const uint32_t v = w & 3u, r = w >> 2;
+        if (v == LOSS) {
+          any_loss = true;
+          min_loss = min(min_loss, r);
+        }
+        any_tie |= v == TIE;
+        any_draw |= v == DRAW;
+        max_all = max(max_all, r);
+        nch++;
+      };
+#pragma unroll
+      for (int x = 0; x < kRankMaxCols; x++) {
+        if (x >= (int)g.C || p.h[x] >= g.H) continue;
+        const uint32_t q = p.off[x] + p.h[x];
+        const uint32_t lo = pat & ((1u << q) - 1u), hi = (pat >> q) << (q + 1);
+        const u64 cb = g.base[hvc + g.stride[x]];
+        if (hasT) take(g.words[cb + ((u64)at << (L + 1)) + (lo | (1u << q) | hi)]);
+        if (hasO) take(g.words[cb + ((u64)a << (L + 1)) + (lo | hi)]);
+      }
+      if (nch == 0) err |= ERR_NO_MOVES;
+      edges += nch;
+      // reference-canonical _res_red / _remote_red
+      word = any_loss ? make_word(WIN, min_loss + 1) : make_word(any_tie ? TIE : any_draw ? DRAW : LOSS, max_all + 1);
+    }
+    g.words[slot] = (uint8_t)word;
+  }
+  if (err) atomicOr(&st->err, err);
+  block_count(bc, 0, edges);
+}
+
+// the end of a solve: the root's word, then the counts (fill_red_body)
+__global__ __launch_bounds__(1024) void k_rk_finish(RankGeom g, u64 root_slot, DevState* st, const BlockCount* bc) {
+  if (threadIdx.x == 0)
+    st->root_word = ((g.reach[root_slot >> 5] >> (root_slot & 31)) & 1u) ? (uint32_t)g.words[root_slot] : NO_WORD;
+  __syncthreads();
+  fill_red_body(st, bc);
+}
+
+__global__ void k_rk_query(Desc d, RankGeom g, const u64* keys, u64 n, uint32_t* out) {
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+    u64 s;
+    uint32_t L, w = NO_WORD;
+    if (rk_slot_of(g, keys[i], &s, &L) && ((g.reach[s >> 5] >> (s & 31)) & 1u)) w = g.words[s];
+    out[i] = w;
+  }
+}
+
+// every reached slot of every level: its key (positions) or its fingerprint
+// term (checksum); one thread per 64-slot word of the reach bitmap
+// (lvt: the levels' first slots [0, T], then their first block entries [T + 1, 2T + 1])
+template <bool CK>
+__global__ __launch_bounds__(256) void k_rk_scan(Desc d, RankGeom g, const u64* lvt, uint32_t T, u64 nwords, u64* keys,
+                                                 u64 cap, u64* count, u64* acc) {
+  const u64* lvstart = lvt;
+  const u64* lvoff = lvt + T + 1;
+  u64 v[6] = {0, 0, 0, 0, 0, 0};
+  for (u64 wi = (u64)blockIdx.x * blockDim.x + threadIdx.x; wi < nwords; wi += (u64)gridDim.x * blockDim.x) {
+    u64 m = reinterpret_cast<const u64*>(g.reach)[wi];
+    if (!m) continue;
+    const u64 s0 = wi << 6;
+    uint32_t L = 0;
+    while (L + 1 < T && lvstart[L + 1] <= s0) L++;
+    u64 k = 0;
+    if (!CK) k = atomicAdd(count, (u64)__builtin_popcountll(m));
+    for (; m; m &= m - 1, k++) {
+      const u64 i = s0 + (u64)__builtin_ctzll(m) - lvstart[L];
+      const u64 blk = i >> (L + 3);
+      const uint32_t a = (uint32_t)((i >> L) & 7u), pat = (uint32_t)(i & ((1ull << L) - 1));
+      RankPos p;
+      rk_unpack(g, g.lvph[lvoff[L] + blk], p);
+      const u64 key = rk_key(g, p, pat, L, rk_hands(L, (uint32_t)__builtin_popcount(pat), a));
+      if (CK) ck_add(d, key, g.words[lvstart[L] + i], v);
+      else if (k < cap) keys[k] = key;
+    }
+  }
+  if (CK) ck_block_add(acc, v);
+}
+
+// ---------------------------------------------------------------------------
+// host
+// ---------------------------------------------------------------------------
+static bool rank_ok(const Desc* d) {
+  if (d->kind != K_TOOT || d->L < 1 || d->L > kRankMaxCols || d->H < 1 || d->H > 7) return false;
+  if (d->max_levels > 64 || (int)d->max_levels != d->L * d->H + 1) return false;  // remoteness in 6 bits
+  double n = 8;
+  for (int x = 0; x < d->L; x++) n *= (double)((2u << d->H) - 1);
+  return n <= (double)(1ull << 36);
+}
+static bool rank_wanted(const Desc* d, uint32_t flags) {
+  return rank_ok(d) && !(flags & (GM_F_FORCE_HASHED | GM_F_HASH_TABLE));
+}
+
+struct RankShape {
+  RankGeom g;
+  std::vector<u64> base;                // per hvcode
+  std::vector<uint32_t> lvhv, lvph;     // hvcodes level by level, packed heights
+  std::vector<uint32_t> lvoff;          // per level: first entry in lvhv (T + 1)
+  std::vector<u64> lvstart, lvitems;    // per level: first slot, slots
+  u64 words_off, reach_off, expd_off, base_off, lvhv_off, lvph_off, table_bytes;
+};
+
+static int rank_shape(const Desc* d, RankShape* rs) {
+  RankGeom& g = rs->g;
+  memset(&g, 0, sizeof g);
+  g.C = (uint32_t)d->L;
+  g.H = (uint32_t)d->H;
+  g.R = g.H + 1;
+  g.A = g.C * g.H;
+  g.T = g.A + 1;
+  uint32_t nhv = 1;
+  for (uint32_t x = 0; x < g.C; x++) {
+    g.stride[x] = nhv;
+    nhv *= g.R;
+  }
+  std::vector<std::vector<uint32_t>> byl(g.T);
+  for (uint32_t c = 0; c < nhv; c++) {
+    uint32_t s = 0, v = c;
+    for (uint32_t x = 0; x < g.C; x++) {
+      s += v % g.R;
+      v /= g.R;
+    }
+    byl[s].push_back(c);
+  }
+  rs->base.assign(nhv, 0);
+  rs->lvhv.clear();
+  rs->lvph.clear();
+  rs->lvoff.assign(g.T + 1, 0);
+  rs->lvstart.assign(g.T + 1, 0);
+  rs->lvitems.assign(g.T, 0);
+  u64 at = 0;
+  for (uint32_t L = 0; L < g.T; L++) {
+    rs->lvoff[L] = (uint32_t)rs->lvhv.size();
+    rs->lvstart[L] = at;
+    const u64 nb = 8ull << L;
+    for (size_t j = 0; j < byl[L].size(); j++) {
+      const uint32_t c = byl[L][j];
+      rs->base[c] = at + j * nb;
+      uint32_t ph = 0, v = c;
+      for (uint32_t x = 0; x < g.C; x++) {
+        ph |= (v % g.R) << (4 * x);
+        v /= g.R;
+      }
+      rs->lvhv.push_back(c);
+      rs->lvph.push_back(ph);
+    }
+    rs->lvitems[L] = (u64)byl[L].size() * nb;
+    at += (rs->lvitems[L] + 63) & ~63ull;
+  }
+  rs->lvoff[g.T] = (uint32_t)rs->lvhv.size();
+  rs->lvstart[g.T] = at;
+  g.nslots = at;
+  rs->words_off = 0;
+  rs->reach_off = rup256(at);
+  rs->expd_off = rs->reach_off + rup256(at / 8);
+  rs->base_off = rs->expd_off + rup256(at / 8);
+  rs->lvhv_off = rs->base_off + rup256((u64)nhv * 8);
+  rs->lvph_off = rs->lvhv_off + rup256((u64)nhv * 4);
+  rs->table_bytes = rs->lvph_off + rup256((u64)nhv * 4);
+  return 0;
+}
+
+static int plan_ranked(const Desc* d, uint64_t max_table_bytes, gm_plan_t* out, bool* fits) {
+  RankShape rs;
+  int rc = rank_shape(d, &rs);
+  if (rc) return rc;
+  *fits = max_table_bytes == 0 || rs.table_bytes <= max_table_bytes;
+  out->mode = GM_MODE_RANKED;
+  out->table_slots = rs.g.nslots;
+  out->table_bytes = rs.table_bytes;
+  out->level_capacity = 1;
+  out->scratch_bytes = scratch_bytes_for(d->max_levels);
+  out->max_levels = (uint32_t)d->max_levels;
+  return 0;
+}
+
+static int rank_setup(gm_solver* s, const gm_buffers* buf) {
+  RankShape rs;
+  int rc = rank_shape(&s->d, &rs);
+  if (rc) return rc;
+  if (buf->table_bytes < rs.table_bytes)
+    return fail(GM_EINVAL, "ranked table of %llu bytes, the plan needs %llu", (unsigned long long)buf->table_bytes,
+                (unsigned long long)rs.table_bytes);
+  char* t = (char*)buf->table;
+  rs.g.words = (uint8_t*)(t + rs.words_off);
+  rs.g.reach = (uint32_t*)(t + rs.reach_off);
+  rs.g.expd = (uint32_t*)(t + rs.expd_off);
+  rs.g.base = (const u64*)(t + rs.base_off);
+  rs.g.lvhv = (const uint32_t*)(t + rs.lvhv_off);
+  rs.g.lvph = (const uint32_t*)(t + rs.lvph_off);
+  HIPCHK(hipMemcpy((void*)rs.g.base, rs.base.data(), rs.base.size() * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy((void*)rs.g.lvhv, rs.lvhv.data(), rs.lvhv.size() * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy((void*)rs.g.lvph, rs.lvph.data(), rs.lvph.size() * 4, hipMemcpyHostToDevice));
+  s->rg = rs.g;
+  s->rlvoff = rs.lvoff;
+  s->rlvstart = rs.lvstart;
+  s->rlvitems = rs.lvitems;
+  // the per-level tables the scans read on the device (k_rk_scan's lvt)
+  if (!s->rlv_dev) HIPCHK(hipMalloc((void**)&s->rlv_dev, (size_t)(2 * (rs.g.T + 1)) * 8));
+  std::vector<u64> tabs(2 * (rs.g.T + 1), 0);
+  for (uint32_t L = 0; L <= rs.g.T; L++) {
+    tabs[L] = rs.lvstart[L];
+    tabs[rs.g.T + 1 + L] = rs.lvoff[L];
+  }
+  HIPCHK(hipMemcpy(s->rlv_dev, tabs.data(), tabs.size() * 8, hipMemcpyHostToDevice));
+  return 0;
+}
+
+template <class F>
+static void rank_kind_dispatch(const Desc& d, F&& f) {
+  switch (fixed_kind(d)) {
+    case K_TOOT_6x4: f(std::integral_constant<int, K_TOOT_6x4>()); break;
+    case K_TOOT_5x4: f(std::integral_constant<int, K_TOOT_5x4>()); break;
+    case K_TOOT_4x4: f(std::integral_constant<int, K_TOOT_4x4>()); break;
+    default: f(std::integral_constant<int, K_TOOT>()); break;
+  }
+}
+
+static int rank_grid(const gm_solver* s, u64 nitems) {
+  return (int)std::max<u64>(1, std::min<u64>((nitems + 255) / 256, (u64)std::min(s->grid * 2, kCountSlots)));
+}
+
+// Steps (gm_solver_set_steps): forward level L is step L, backward level L
+// step 2T - 1 - L, as for the other layouts.
+static int run_ranked(gm_solver* s, gm_result* out) {
+  const Desc& d = s->d;
+  const RankGeom& g = s->rg;
+  const int T = (int)g.T;
+  const int first = (int)s->step_first, stop = s->step_stop ? (int)s->step_stop : 2 * T;
+  s->step_first = s->step_stop = 0;
+  const bool timing = (s->flags & GM_F_KERNEL_TIMING) && first == 0 && stop == 2 * T;
+  hipStream_t st = s->stream;
+  if (first > 0) {
+    uint32_t wb = 0;
+    HIPCHK(hipMemcpy(&wb, &s->st->word_bits, sizeof wb, hipMemcpyDeviceToHost));
+    if (wb != 0x208u) return fail(GM_EINVAL, "resume: the scratch holds no ranked solve");
+  }
+  hipEvent_t ev[4];
+  for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+  auto t0 = std::chrono::steady_clock::now();
+  HIPCHK(hipEventRecord(ev[0], st));
+  if (first == 0) {
+    HIPCHK(hipMemsetAsync(s->st, 0, devstate_bytes(T), st));
+    HIPCHK(hipMemsetAsync(s->bcount, 0, kCountSlots * sizeof(BlockCount), st));
+    HIPCHK(hipMemsetD32Async((hipDeviceptr_t)&s->st->word_bits, 0x208, 1, st));  // the solve in progress: ranked
+  }
+  u64 nl_f = 0, nl_b = 0;
+  rank_kind_dispatch(d, [&](auto KC) {
+    constexpr int KIND = decltype(KC)::value;
+    for (int k = std::max(first, 0); k < std::min(stop, T); k++) {
+      const uint32_t L = (uint32_t)k;
+      const u64 n = (s->rlvitems[L] + 63) & ~63ull;
+      hipLaunchKernelGGL((k_rk_forward<KIND>), dim3(rank_grid(s, n)), dim3(256), 0, st, d, g, L, s->rlvstart[L],
+                         s->rlvoff[L], n, s->rlvitems[L], s->bcount, s->st);
+      nl_f++;
+    }
+  });
+  HIPCHK(hipEventRecord(ev[1], st));
+  rank_kind_dispatch(d, [&](auto KC) {
+    constexpr int KIND = decltype(KC)::value;
+    for (int k = std::max(first, T); k < stop; k++) {
+      const uint32_t L = (uint32_t)(2 * T - 1 - k);
+      const u64 n = s->rlvitems[L];
+      hipLaunchKernelGGL((k_rk_backward<KIND>), dim3(rank_grid(s, n)), dim3(256), 0, st, d, g, L, s->rlvstart[L],
+                         s->rlvoff[L], n, s->bcount, s->st);
+      nl_b++;
+    }
+  });
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(ev[2], st));
+  if (stop < 2 * T) {
+    HIPCHK(hipStreamSynchronize(st));
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    out->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    out->word_bits = 8;
+    return GM_PARTIAL;
+  }
+  hipLaunchKernelGGL(k_rk_finish, dim3(1), dim3(1024), 0, st, g, s->rlvstart[0], s->st, (const BlockCount*)s->bcount);
+  HIPCHK(hipGetLastError());
+  u64 red[5];
+  HIPCHK(hipMemcpyAsync(red, s->st->red, sizeof red, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipEventRecord(ev[3], st));
+  HIPCHK(hipStreamSynchronize(st));
+  float f = 0, b = 0;
+  HIPCHK(hipEventElapsedTime(&f, ev[0], ev[1]));
+  HIPCHK(hipEventElapsedTime(&b, ev[1], ev[2]));
+  for (auto& e : ev) (void)hipEventDestroy(e);
+  out->ms_forward = f;
+  out->ms_backward = b;
+  out->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (timing) {
+    out->ms_expand_kernels = f;
+    out->ms_resolve_kernels = b;
+    out->n_expand_launches = nl_f;
+    out->n_resolve_launches = nl_b;
+  }
+  out->positions = red[0];
+  out->edges = red[1];
+  out->primitives = red[2];
+  out->levels = (uint32_t)T;
+  out->max_level_width = 0;
+  out->word_bits = 8;
+  out->kernels = RK_RANKED;
+  const uint32_t word = red[3] ? (uint32_t)(red[3] - 1) : NO_WORD;
+  out->root_word = word;
+  if (red[4]) return fail(GM_ECORRUPT, "solve failed:%s", err_text((uint32_t)red[4]).c_str());
+  if (word == NO_WORD) return fail(GM_ECORRUPT, "root unresolved");
+  out->root_value = (int32_t)(word & 3u);
+  out->root_remoteness = word >> 2;
+  return 0;
+}
+
+static int rank_query(gm_solver* s, const uint64_t* keys_dev, uint64_t n, uint32_t* words_dev) {
+  const int grid = (int)std::min<u64>((n + kBlock - 1) / kBlock, (u64)s->grid);
+  hipLaunchKernelGGL(k_rk_query, dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->rg, (const u64*)keys_dev, n,
+                     words_dev);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s->stream));
+  return 0;
+}
+
+static int rank_scan(gm_solver* s, bool ck, u64* keys_dev, u64 cap, u64* acc) {
+  const RankGeom& g = s->rg;
+  const u64 nwords = g.nslots / 64;
+  if (ck)
+    hipLaunchKernelGGL((k_rk_scan<true>), dim3(s->grid), dim3(256), 0, s->stream, s->d, g, (const u64*)s->rlv_dev, g.T,
+                       nwords, (u64*)nullptr, (u64)0, (u64*)nullptr, acc);
+  else
+    hipLaunchKernelGGL((k_rk_scan<false>), dim3(s->grid), dim3(256), 0, s->stream, s->d, g, (const u64*)s->rlv_dev, g.T,
+                       nwords, keys_dev, cap, &s->st->cursor_back, (u64*)nullptr);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s->stream));
+  return 0;
+}
+
+static int rank_positions(gm_solver* s, uint64_t* keys_dev, uint64_t cap, uint64_t* n) {
+  u64 cnt = 0;
+  HIPCHK(hipStreamSynchronize(s->stream));
+  HIPCHK(hipMemcpy(&cnt, &s->st->cursor_front, sizeof cnt, hipMemcpyDeviceToHost));
+  *n = cnt;
+  if (cnt > cap || !keys_dev) return cap < cnt ? fail(GM_EFULL, "need %llu slots", (unsigned long long)cnt) : 0;
+  HIPCHK(hipMemsetAsync(&s->st->cursor_back, 0, sizeof(u64), s->stream));
+  return rank_scan(s, false, (u64*)keys_dev, cap, nullptr);
+}
+
+}  // extern "C++"

@@ -308,6 +308,14 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out);
 static int plane_query(gm_solver* s, const uint64_t* keys_dev, uint64_t n, uint32_t* words_dev);
 static int plane_positions(gm_solver* s, uint64_t* keys_dev, uint64_t cap, uint64_t* n);
 static void plane_checksum_launch(gm_solver* s, u64* acc);
+static bool rank_wanted(const Desc* d, uint32_t flags);
+static bool rank_ok(const Desc* d);
+static int plan_ranked(const Desc* d, uint64_t max_table_bytes, gm_plan_t* out, bool* fits);
+static int rank_setup(gm_solver* s, const gm_buffers* buf);
+static int run_ranked(gm_solver* s, gm_result* out);
+static int rank_query(gm_solver* s, const uint64_t* keys_dev, uint64_t n, uint32_t* words_dev);
+static int rank_positions(gm_solver* s, uint64_t* keys_dev, uint64_t cap, uint64_t* n);
+static int rank_scan(gm_solver* s, bool ck, u64* keys_dev, u64 cap, u64* acc);
 
 static const Desc* get_game(int id) {
   std::lock_guard<std::mutex> lk(g_mu);
@@ -890,6 +898,22 @@ __global__ __launch_bounds__(256) void k_checksum_dense(Desc d, DenseView v, con
 // gm_buffers): nothing later -- no environment variable, no flag change --
 // can hand a table a kernel of another word width.  The codes are reported
 // in gm_result.kernels (resolve | pull << 16).
+// RANKED layout geometry (gm_ranked.h): toot-and-otto positions at computed
+// indices
+constexpr int kRankMaxCols = 8;
+struct RankGeom {
+  uint32_t C, H, R, A;     // columns, rows, height radix H + 1, cells
+  uint32_t T;              // levels (pieces 0 .. A)
+  uint32_t stride[kRankMaxCols];  // hvcode stride of column x: R^x
+  u64 nslots;
+  uint8_t* words;          // [nslots]
+  uint32_t* reach;         // [nslots / 32] reached
+  uint32_t* expd;          // [nslots / 32] reached and not primitive
+  const u64* base;         // [R^C] hvcode -> first slot of its block
+  const uint32_t* lvhv;    // hvcodes level by level
+  const uint32_t* lvph;    // the same, heights packed 4 bits per column
+};
+
 enum DenseResolveKind : uint32_t {
   RK_NONE = 0,
   RK_OCT_LIST = 1,   // k_dense_resolve8p: world 1, 16-bit table, live-group lists
@@ -901,6 +925,7 @@ enum DenseResolveKind : uint32_t {
   RK_HEX_LIST = 7,   // k_dense_resolve16p: world 1, 8-bit table, live-group lists
   RK_PLANE = 8,      // k_plane_resolve: PLANES layout (gm_plane.h), one plane per half-wave
   RK_PLANE_X2 = 9,   // k_plane_resolve_x2: two planes per half-wave, packed 16-bit lanes
+  RK_RANKED = 10,    // k_rk_backward: RANKED layout (gm_ranked.h)
 };
 enum DensePullKind : uint32_t { PK_NONE = 0, PK_WORDS = 1, PK_LANE = 2, PK_PLANE = 3 };
 
@@ -1014,6 +1039,11 @@ struct gm_solver {
   uint32_t pstage_k = 0, pkeys = 0, prows = 0;
   ncclComm_t comm2 = nullptr;        // second communicator (ncclCommSplit): the other halo direction
   hipStream_t cstream2 = nullptr;    // receive stream of the staged exchange
+  // RANKED (gm_ranked.h)
+  RankGeom rg{};
+  std::vector<uint32_t> rlvoff;        // per level: first entry of its block list
+  std::vector<u64> rlvstart, rlvitems;  // per level: first slot, slots
+  u64* rlv_dev = nullptr;              // device: rlvstart then rlvoff (k_rk_scan)
 };
 
 static const int kBlock = 256;
@@ -1669,6 +1699,15 @@ int gm_plan(int game, uint64_t positions, uint32_t flags, uint64_t max_table_byt
     out->max_levels = (uint32_t)d->max_levels;
     out->scratch_bytes = scratch_bytes_for(d->max_levels);
   }
+  if (rank_wanted(d, flags)) {  // toot-and-otto: positions at computed indices (gm_ranked.h)
+    bool fits = false;
+    int rc = plan_ranked(d, max_table_bytes, out, &fits);
+    if (rc) return rc;
+    if (fits) return 0;
+    memset(out, 0, sizeof *out);
+    out->max_levels = (uint32_t)d->max_levels;
+    out->scratch_bytes = scratch_bytes_for(d->max_levels);
+  }
   if (positions == 0) {
     gm_game_info(game, &positions, nullptr, nullptr);
     if (positions == 0) return fail(GM_EINVAL, "no known position bound for this board; pass an estimate");
@@ -1837,6 +1876,9 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
   } else if (buf->mode == GM_MODE_PLANES) {
     if (!d->dense_ok || !plane_ok(d)) return fail(GM_EINVAL, "game has no planes layout");
     if (world > 1 && (rank < 0 || rank >= world)) return fail(GM_EINVAL, "bad shard %d/%d", rank, world);
+  } else if (buf->mode == GM_MODE_RANKED) {
+    if (world != 1) return fail(GM_EINVAL, "ranked tables are one-GPU (shard keyed games by md5: gm_plan_keyed_shard)");
+    if (!rank_ok(d)) return fail(GM_EINVAL, "game has no ranked layout");
   } else if (buf->mode == GM_MODE_BUCKETED) {
     if (world < 1 || rank < 0 || rank >= world) return fail(GM_EINVAL, "bad shard %d/%d", rank, world);
     if (world > 8) return fail(GM_EINVAL, "md5-sharded bucketed levels support up to 8 ranks");
@@ -2061,6 +2103,13 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
       return rc;
     }
   }
+  if (s->mode == GM_MODE_RANKED) {
+    int rc = rank_setup(s, buf);
+    if (rc) {
+      gm_solver_destroy(s);
+      return rc;
+    }
+  }
   *out = s;
   return 0;
 }
@@ -2175,6 +2224,7 @@ void gm_solver_destroy(gm_solver* s) {
   if (s->comm) (void)ncclCommDestroy(s->comm);
   if (s->errg) (void)hipFree(s->errg);
   if (s->xdev) (void)hipFree(s->xdev);
+  if (s->rlv_dev) (void)hipFree(s->rlv_dev);
   if (s->own_stream) (void)hipStreamDestroy(s->stream);
   delete s;
 }
@@ -2188,6 +2238,7 @@ int gm_solver_solve(gm_solver* s, gm_result* out) {
   memset(out, 0, sizeof *out);
   if (s->mode == GM_MODE_DENSE) return solve_dense(s, out);
   if (s->mode == GM_MODE_PLANES) return run_planes({s}, out);
+  if (s->mode == GM_MODE_RANKED) return run_ranked(s, out);
   if (s->mode == GM_MODE_BUCKETED) return s->world > 1 ? run_bucketed_shards({s}, out) : solve_bucketed(s, out);
   if (s->world > 1) return fail(GM_EINVAL, "keyed-table shard %d/%d: drive it with gm_ks_* (md5 exchange)", s->rank, s->world);
   const int T = s->d.max_levels;
@@ -2445,6 +2496,7 @@ static int xfer_ranges(gm_solver* s, const std::vector<HostRange>& out, int sp, 
 }
 
 #include "gm_plane_run.h"
+#include "gm_ranked.h"
 
 int gm_plane_halo_plan(int game, int rank, int world, uint32_t flags, uint64_t* out, uint32_t levels) {
   const Desc* d = get_game(game);
@@ -3605,6 +3657,10 @@ int gm_solve_group(gm_solver** shards, int n, gm_result* out) {
     if (!s) return fail(GM_EINVAL, "null shard");
   if (ss[0]->mode == GM_MODE_PLANES) return run_planes(ss, out);
   if (ss[0]->mode == GM_MODE_BUCKETED) return run_bucketed_shards(ss, out);
+  if (ss[0]->mode == GM_MODE_RANKED) {
+    if (n != 1) return fail(GM_EINVAL, "ranked tables are one-GPU");
+    return run_ranked(ss[0], out);
+  }
   return run_dense(ss, out);
 }
 
@@ -3612,6 +3668,7 @@ int gm_solver_query(gm_solver* s, const uint64_t* keys_dev, uint64_t n, uint32_t
   if (!s || (n && (!keys_dev || !words_dev))) return fail(GM_EINVAL, "bad argument");
   if (!n) return 0;
   if (s->mode == GM_MODE_PLANES) return plane_query(s, keys_dev, n, words_dev);
+  if (s->mode == GM_MODE_RANKED) return rank_query(s, keys_dev, n, words_dev);
   int grid = (int)std::min<u64>((n + kBlock - 1) / kBlock, (u64)s->grid);
   if (s->mode == GM_MODE_DENSE)
     hipLaunchKernelGGL(k_dense_query, dim3(grid), dim3(kBlock), 0, s->stream, s->d, s->view, s->words, s->bits,
@@ -3630,6 +3687,7 @@ int gm_solver_query(gm_solver* s, const uint64_t* keys_dev, uint64_t n, uint32_t
 int gm_solver_positions(gm_solver* s, uint64_t* keys_dev, uint64_t cap, uint64_t* n) {
   if (!s || !n) return fail(GM_EINVAL, "bad argument");
   if (s->mode == GM_MODE_PLANES) return plane_positions(s, keys_dev, cap, n);
+  if (s->mode == GM_MODE_RANKED) return rank_positions(s, keys_dev, cap, n);
   if (s->mode == GM_MODE_BUCKETED) {  // every level's keys, contiguous
     u64 tot = 0;
     for (const BkLevel& x : s->lvh) tot += x.n;
@@ -3666,6 +3724,10 @@ int gm_solver_checksum(gm_solver* s, uint64_t out[6]) {
   HIPCHK(hipMemsetAsync(acc, 0, 6 * sizeof(u64), s->stream));
   if (s->mode == GM_MODE_PLANES)
     plane_checksum_launch(s, acc);
+  else if (s->mode == GM_MODE_RANKED) {
+    int rc = rank_scan(s, true, nullptr, 0, acc);
+    if (rc) return rc;
+  }
   else if (s->mode == GM_MODE_DENSE)
     hipLaunchKernelGGL(k_checksum_dense, dim3(s->grid), dim3(kBlock), 0, s->stream, s->d, s->view, s->words, s->bits,
                        (u64)s->d.max_levels, s->wbits(), acc);

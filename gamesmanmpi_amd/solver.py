@@ -50,12 +50,13 @@ class Solver:
                  layout="auto", max_table_bytes=0, rank=0, world=1,
                  stream=None, flags=0):
         """layout: "auto" (planes, else the level-major dense table, when
-        the descriptor supports it and the table fits max_table_bytes; else
-        bucketed levels when every move advances one level; else the keyed
-        hash table), "planes" (sum games whose first two heaps hold 32
-        values: natural rank order, gm_plane.h), "dense" (the level-major
-        dense table), "bucketed" or "hashed" (the open-addressing hash
-        table).
+        the descriptor supports it and the table fits max_table_bytes; the
+        ranked table for toot-and-otto; else bucketed levels when every move
+        advances one level; else the keyed hash table), "planes" (sum games
+        whose first two heaps hold 32 values: natural rank order,
+        gm_plane.h), "dense" (the level-major dense table), "ranked"
+        (toot-and-otto positions at computed indices, gm_ranked.h),
+        "bucketed" or "hashed" (the open-addressing hash table).
         flags: kernel-family flags (_lib.GM_F_WORDS32 / GM_F_RESOLVE_SCALAR /
         GM_F_SHARD_INORDER, A/B runs), fixed for this solver's lifetime.
         rank/world > 1: this object is one shard of a dense / planes multi-
@@ -71,8 +72,8 @@ class Solver:
         self.spec = spec if isinstance(spec, GameSpec) else GameSpec(*spec)
         self.device = torch.device(device if device is not None else "cuda")
         self.kernel_timing = kernel_timing
-        if layout not in ("auto", "planes", "dense", "hashed", "bucketed"):
-            raise ValueError("layout must be auto, planes, dense, bucketed or hashed")
+        if layout not in ("auto", "planes", "dense", "hashed", "bucketed", "ranked"):
+            raise ValueError("layout must be auto, planes, dense, ranked, bucketed or hashed")
         self.layout = layout
         self.max_table_bytes = int(max_table_bytes)
         self.rank, self.world = int(rank), int(world)
@@ -115,6 +116,9 @@ class Solver:
         if self.layout == "planes" and plan.mode != _lib.GM_MODE_PLANES:
             raise ValueError("%r has no planes layout (heaps 0 and 1 of 32 "
                              "values), or it does not fit" % (self.spec,))
+        if self.layout == "ranked" and plan.mode != _lib.GM_MODE_RANKED:
+            raise ValueError("%r has no ranked layout (toot-and-otto boards), or it "
+                             "does not fit" % (self.spec,))
         if self.layout == "bucketed" and plan.mode != _lib.GM_MODE_BUCKETED:
             raise ValueError("%r: bucketed levels need every move to advance "
                              "one level" % (self.spec,))

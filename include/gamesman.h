@@ -79,6 +79,16 @@ typedef struct gm_slot {
  * or uneven splits); their table buffer also holds the halo send / receive
  * areas. */
 #define GM_MODE_PLANES 3u
+/* RANKED (toot_and_otto_bitstring; the default for it on one GPU): no keys
+ * and no dedup -- every position at a computed index.  A position is its
+ * column stacks (heights and letters: gravity boards) plus the first
+ * player's T count; the level's height vectors are blocks of 8 x 2^L slots
+ * [T count][stack bits], levels one after another.  One byte of word per
+ * slot (value | remoteness << 2) + a reach and an expandable bit; a move is
+ * index arithmetic (gamesmanmpi_amd/csrc/gm_ranked.h).  table_slots = slots;
+ * the levels buffer is unused.  GM_F_FORCE_HASHED / GM_F_HASH_TABLE keep
+ * the keyed layouts. */
+#define GM_MODE_RANKED 4u
 
 /* Sizes the caller must allocate for a solve (see gm_plan). */
 typedef struct gm_plan_t {

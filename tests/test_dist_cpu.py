@@ -144,7 +144,9 @@ def test_plan_multi_keyed_shards_fit_together(n):
     from gamesmanmpi_amd.games import GameSpec
     spec = GameSpec("toot_and_otto_bitstring", "length=6,height=4")
     plans = gdist.plan_multi(spec, n)
-    one = gdist.plan_multi(spec, 1)[0]
+    one = gdist.plan_multi(spec, 1, flags=_lib.GM_F_FORCE_HASHED)[0]  # the one-table keyed plan
+    assert int(one.mode) == _lib.GM_MODE_BUCKETED
+    assert int(gdist.plan_multi(spec, 1)[0].mode) == _lib.GM_MODE_RANKED  # one GPU: computed indices
     assert {int(p.mode) for p in plans} == {_lib.GM_MODE_BUCKETED}
     total = sum(int(p.table_bytes) + 8 * int(p.level_capacity) for p in plans)
     single = int(one.table_bytes) + 8 * int(one.level_capacity)

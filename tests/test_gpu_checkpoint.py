@@ -22,6 +22,7 @@ CASES = [
     ("tic_tac_toe_np", "", "bucketed", {}),
     ("othello_bit_new", "length=4,height=4", "bucketed", {}),
     ("toot_and_otto_bitstring", "length=4,height=3", "bucketed", {}),
+    ("toot_and_otto_bitstring", "length=4,height=3", "ranked", {}),
     ("sum_four_to_one", "heaps=15:15:15:15", "dense", {}),                # 8-bit words
     ("sum_four_to_one", "heaps=15:15:15:15", "dense", {"flags": 64}),     # GM_F_WORDS16
     ("sum_four_to_one", "heaps=15:15:15:15", "dense", {"flags": 4}),  # GM_F_WORDS32

@@ -79,3 +79,24 @@ def test_keyed_edge_shape_matches_oracle(name, params, layout, flags):
     assert len(keys) == sol.count
     for k, v, m in zip(keys.tolist(), val.tolist(), rem.tolist()):
         assert (v, m) == tuple(sol.lookup(spec.decode(k))), (k, v, m)
+
+
+@pytest.mark.parametrize("name,params", [x for x in KEYED_SHAPES if x[0] == "toot_and_otto_bitstring"])
+def test_ranked_edge_shape_matches_oracle(name, params):
+    """toot-and-otto's RANKED layout (gm_ranked.h) on degenerate boards: one
+    column, one row, boards that fill before a word forms -- every position
+    against the oracle."""
+    from gamesmanmpi_amd.games import GameSpec
+    from gamesmanmpi_amd.solver import Solver
+    from oracle.oracle import Game  # checker only
+    spec = GameSpec(name, params)
+    sol = Game(name, params).solve(1 << 22)
+    s = Solver(spec, layout="ranked")
+    r = s.solve()
+    assert r.extra["layout"] == "ranked"
+    assert (r.positions, r.edges, r.primitives, r.root_line) == (sol.count, sol.edges, sol.stats["primitives"],
+                                                                  sol.root_line)
+    keys, val, rem = s.dump()
+    assert len(keys) == sol.count
+    for k, v, m in zip(keys.tolist(), val.tolist(), rem.tolist()):
+        assert (v, m) == tuple(sol.lookup(spec.decode(k))), (k, v, m)

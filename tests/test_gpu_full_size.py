@@ -62,14 +62,21 @@ def test_gpu_sum_15x5_checksum_both_layouts():
 
 
 def test_gpu_toot_5x4_checksum():
-    s, r = _check("toot_5x4")
+    s, r = _check("toot_5x4", layout="bucketed")
     assert r.extra["layout"] == "bucketed"
+
+
+def test_gpu_toot_5x4_checksum_ranked():
+    """The RANKED layout (the default for toot on one GPU): positions at
+    computed indices, no keys, no dedup (gm_ranked.h)."""
+    s, r = _check("toot_5x4")
+    assert r.extra["layout"] == "ranked"
 
 
 def test_gpu_toot_5x4_checksum_counted_partitions():
     """GM_F_BK_EXACT: every level counted first (the form a level falls back
     to when a provisioned partition overflows)."""
-    s, r = _check("toot_5x4", flags=128)
+    s, r = _check("toot_5x4", layout="bucketed", flags=128)
     assert r.extra["layout"] == "bucketed"
 
 
@@ -80,8 +87,14 @@ def test_gpu_toot_5x4_checksum_hash_table():
 
 def test_gpu_toot_6x4_checksum():
     """BASELINE config 3 as shipped: parity unpinned by reference fixtures
-    beyond 4x4 (see module docstring)."""
-    _check("toot_6x4")
+    beyond 4x4 (see module docstring).  The default layout, RANKED."""
+    s, r = _check("toot_6x4")
+    assert r.extra["layout"] == "ranked"
+
+
+def test_gpu_toot_6x4_checksum_bucketed():
+    s, r = _check("toot_6x4", layout="bucketed")
+    assert r.extra["layout"] == "bucketed"
 
 
 def test_gpu_sum_31x6_checksum():

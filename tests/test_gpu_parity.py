@@ -22,7 +22,8 @@ def _solve(stem, params, positions=0, layout="auto"):
 DENSE_GAMES = ("four_to_one", "sum_four_to_one")
 GOLDEN_RUNS = [(n, "hashed") for n in sorted(CASES)] + [
     (n, "dense") for n in sorted(CASES) if CASES[n][0] in DENSE_GAMES] + [
-    (n, "bucketed") for n in sorted(CASES) if CASES[n][0] not in DENSE_GAMES]
+    (n, "bucketed") for n in sorted(CASES) if CASES[n][0] not in DENSE_GAMES] + [
+    (n, "ranked") for n in sorted(CASES) if CASES[n][0] == "toot_and_otto_bitstring"]
 
 
 @pytest.mark.parametrize("name,layout", GOLDEN_RUNS)
