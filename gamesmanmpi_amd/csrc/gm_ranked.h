@@ -11,12 +11,15 @@
 //   * per column x: its height h_x in [0, H] and the letters of its stack,
 //     bit y = 1 for T (gravity: do_move fills the lowest blank cell,
 //     toot_and_otto_bitstring.py:106-116, so a column is a contiguous stack);
-//   * a = how many T's the first player has placed, in [0, 6].
+//   * a = how many T's the first mover has placed, in [0, 6].
 // Everything else in the key follows: pieces on the board L = sum h_x (the
-// level; the first player moves at even L), the T's on the board nT (the
+// level; the first mover moves at even L), the T's on the board nT (the
 // popcount of the stacks), hence every hand (6 each at the start, :38-40:
-// first player T = 6 - a, O = 6 - (ceil(L/2) - a); second player T =
-// 6 - (nT - a), O = 6 - (floor(L/2) - (nT - a))) and the turn bit.
+// first mover T = 6 - a, O = 6 - (ceil(L/2) - a); second mover T =
+// 6 - (nT - a), O = 6 - (floor(L/2) - (nT - a))) and the turn bit.  The
+// first mover is the reference's player 2: is_player1_turn reads board[-1]
+// (:218-222), a padding bit that starts 0 (the key's turn bit, gm_games.h;
+// the root's, gm_solver.hip), so player 2's hands (key bits 2A+6..) go first.
 //
 // Index space: the height vectors (h_0 .. h_{C-1}) of one level in ascending
 // code order (hvcode = sum h_x (H+1)^x), each a BLOCK of 8 x 2^L slots
@@ -60,8 +63,8 @@ __device__ __forceinline__ void rk_unpack(const RankGeom& g, uint32_t ph, RankPo
     o += p.h[x];
   }
 }
-// every hand count in [0, 6]: the first player's T's used = a; O's = ceil(L/2) - a;
-// the second player's T's = nT - a, O's = floor(L/2) - (nT - a)
+// pieces used from each hand, all in [0, 6]: the first mover's T's = a, O's =
+// ceil(L/2) - a; the second mover's T's = nT - a, O's = floor(L/2) - (nT - a)
 struct RankHands {
   int t1, o1, t2, o2;
 };
@@ -90,10 +93,12 @@ __device__ __forceinline__ u64 rk_key(const RankGeom& g, const RankPos& p, uint3
       else o |= cell;
     }
   }
+  // key hands: player 1 (the second mover) at 2A, 2A+3; player 2 (the first
+  // mover) at 2A+6, 2A+9; turn bit 1 = player 1 to move = odd levels
   const uint32_t A = g.A;
-  return t | (o << A) | ((u64)(kRankHand - u.t1) << (2 * A)) | ((u64)(kRankHand - u.o1) << (2 * A + 3)) |
-         ((u64)(kRankHand - u.t2) << (2 * A + 6)) | ((u64)(kRankHand - u.o2) << (2 * A + 9)) |
-         ((u64)((L & 1u) == 0) << (2 * A + 12));
+  return t | (o << A) | ((u64)(kRankHand - u.t2) << (2 * A)) | ((u64)(kRankHand - u.o2) << (2 * A + 3)) |
+         ((u64)(kRankHand - u.t1) << (2 * A + 6)) | ((u64)(kRankHand - u.o1) << (2 * A + 9)) |
+         ((u64)(L & 1u) << (2 * A + 12));
 }
 // key -> slot (false: not a gravity board with consistent hands)
 __device__ __forceinline__ bool rk_slot_of(const RankGeom& g, u64 key, u64* slot, uint32_t* level) {
@@ -113,14 +118,15 @@ __device__ __forceinline__ bool rk_slot_of(const RankGeom& g, u64 key, u64* slot
     L += h;
   }
   const uint32_t nT = __builtin_popcount(pat);
-  const uint32_t h1t = (uint32_t)((key >> (2 * A)) & 7), h1o = (uint32_t)((key >> (2 * A + 3)) & 7);
-  const uint32_t h2t = (uint32_t)((key >> (2 * A + 6)) & 7), h2o = (uint32_t)((key >> (2 * A + 9)) & 7);
+  // second mover (player 1) at 2A, first mover (player 2) at 2A+6 (rk_key)
+  const uint32_t sT = (uint32_t)((key >> (2 * A)) & 7), sO = (uint32_t)((key >> (2 * A + 3)) & 7);
+  const uint32_t fT = (uint32_t)((key >> (2 * A + 6)) & 7), fO = (uint32_t)((key >> (2 * A + 9)) & 7);
   const uint32_t turn = (uint32_t)((key >> (2 * A + 12)) & 1);
-  if (h1t > kRankHand) return false;
-  const uint32_t a = kRankHand - h1t;
+  if (fT > kRankHand) return false;
+  const uint32_t a = kRankHand - fT;
   const RankHands u = rk_hands(L, nT, a);
-  if (!rk_valid(u) || kRankHand - u.o1 != h1o || kRankHand - u.t2 != h2t || kRankHand - u.o2 != h2o ||
-      turn != ((L & 1u) == 0))
+  if (!rk_valid(u) || kRankHand - u.o1 != fO || kRankHand - u.t2 != sT || kRankHand - u.o2 != sO ||
+      turn != (L & 1u))
     return false;
   *slot = g.base[hv] + ((u64)a << L) + pat;
   *level = L;
@@ -151,7 +157,7 @@ __global__ __launch_bounds__(256) void k_rk_forward(Desc d, RankGeom g, uint32_t
       const RankHands u = rk_hands(L, (uint32_t)__builtin_popcount(pat), a);
       if (rk_valid(u)) {
         if (L == 0) {
-          reach = true;  // the root (hands 6 / 6 / 6 / 6, first player to move)
+          reach = true;  // the root (hands 6 / 6 / 6 / 6, the first mover to move)
         } else {
           const bool p1moved = ((L - 1) & 1u) == 0;  // the move into level L was the first player's
 #pragma unroll

@@ -94,8 +94,7 @@ def test_ranked_edge_shape_matches_oracle(name, params):
     s = Solver(spec, layout="ranked")
     r = s.solve()
     assert r.extra["layout"] == "ranked"
-    assert (r.positions, r.edges, r.primitives, r.root_line) == (sol.count, sol.edges, sol.stats["primitives"],
-                                                                  sol.root_line)
+    assert (r.positions, r.edges, r.root_line) == (sol.count, sol.edges, sol.root_line)
     keys, val, rem = s.dump()
     assert len(keys) == sol.count
     for k, v, m in zip(keys.tolist(), val.tolist(), rem.tolist()):

@@ -43,9 +43,9 @@ def test_ranked_query_of_non_positions():
     A = 16
     bad = [
         k ^ (1 << (2 * A + 12)),           # turn bit flipped
-        k ^ (1 << (2 * A)),                # first player's T count changed
+        k ^ (1 << (2 * A + 6)),            # the first mover's T count changed
         k | (1 << 63),                     # stray high bit
-        (1 << 12) | (6 << 32) | (6 << 35) | (6 << 38) | (6 << 41) | (1 << 44),  # a T floating on row 3
+        (1 << 12) | (6 << 32) | (6 << 35) | (5 << 38) | (6 << 41) | (1 << 44),  # a T floating on row 3
     ]
     w = s.query(np.array(bad, np.uint64))
     assert (w == 0xFFFFFFFF).all(), w
