@@ -135,13 +135,130 @@ __device__ __forceinline__ bool rk_slot_of(const RankGeom& g, u64 key, u64* slot
 
 // The level's slots as one index space: item i of level L = slot lvstart + i,
 // block i >> (L + 3) of the level's list (lvoff + that), a = (i >> L) & 7,
-// stack bits = i & (2^L - 1).  A wave's 64 items are one aligned 64-bit word
-// of each bitmap (levels start 64-aligned).
+// stack bits = i & (2^L - 1).  Levels start 512-aligned, so a level's boards
+// (the a = 0 view: board lvstart / 8 + (i >> (L + 3) << L) + bits) start
+// 64-aligned and every 64-slot / 64-board word belongs to one level.
+
+// F0: every board of level L (its stacks; the hands do not enter the rule):
+// the reference's primitive value (toot_prim) or UNDECIDED in bstat, and the
+// primitive bit in pbits.  One thread per board; a wave = one pbits word.
+template <int KIND>
+__global__ __launch_bounds__(256) void k_rk_boards(Desc d, RankGeom g, uint32_t L, u64 bstart, uint32_t lvoff,
+                                                   u64 nboards, u64 nreal) {
+  const uint32_t lane = threadIdx.x & 63;
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  const RankHands none{0, 0, 0, 0};
+  for (u64 i0 = (u64)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); i0 < nboards; i0 += stride) {
+    const u64 i = i0 + lane;
+    bool prim = false;
+    if (i < nreal) {
+      const u64 blk = i >> L;
+      const uint32_t pat = (uint32_t)(i & ((1ull << L) - 1));
+      RankPos p;
+      rk_unpack(g, g.lvph[lvoff + blk], p);
+      const int pr = Game<KIND>::prim(d, rk_key(g, p, pat, L, none));
+      g.bstat[bstart + i] = (uint8_t)pr;
+      prim = pr != UNDECIDED;
+    }
+    const u64 bp = __ballot(prim);
+    if (lane == 0) reinterpret_cast<u64*>(g.pbits)[(bstart + i0) >> 6] = bp;
+  }
+}
+
+// bits j of a 64-slot word (consecutive stack bits p0 + j, p0 a multiple of
+// 64) whose hands are valid: nT = popc(p0) + popc(j) in [lo, hi]
+__device__ __forceinline__ u64 rk_valid_mask(const RankGeom& g, uint32_t L, uint32_t a, uint32_t p0) {
+  if (a > kRankHand) return 0;
+  const int o1 = (int)((L + 1) / 2) - (int)a;
+  if (o1 < 0 || o1 > (int)kRankHand) return 0;
+  const int half = (int)(L / 2);
+  const int lo = (int)a + max(0, half - (int)kRankHand) - __builtin_popcount(p0);
+  const int hi = (int)a + min((int)kRankHand, half) - __builtin_popcount(p0);
+  if (hi < 0 || lo > 6) return 0;
+  const u64 up = hi >= 6 ? ~0ull : g.le[hi];
+  const u64 dn = lo <= 0 ? 0ull : g.le[lo - 1];
+  return up & ~dn;
+}
+// 32 bits -> 64: insert a 0 at bit q of every index (runs of 2^q bits, each
+// followed by a gap of 2^q)
+__device__ __forceinline__ u64 rk_spread(uint32_t e, uint32_t q) {
+  u64 x = e;
+  if (q <= 4) x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
+  if (q <= 3) x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+  if (q <= 2) x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+  if (q <= 1) x = (x | (x << 2)) & 0x3333333333333333ull;
+  if (q == 0) x = (x | (x << 1)) & 0x5555555555555555ull;
+  return x;
+}
+
+// F1 (levels L >= 6): reach and expandable bits 64 slots at a time -- a slot
+// is reached iff its hands are valid and a parent (its stacks with one
+// column's top piece removed, the first mover's T count one lower if it
+// placed that T) is expandable.  For a column whose top sits at bit q >= 6 of
+// the stacks the 64 slots' parents are 64 consecutive slots (one word); for
+// q < 6 the children with letter l at bit q have 32 consecutive parents, half
+// a word, spread back to the child bits (rk_spread).  expandable = reached
+// and not a primitive board (pbits).
+// (nwords: the level's 512-slot padded extent in words -- every bitmap word
+// of the level is written, the padding's as 0; nreal: its slots)
+__global__ __launch_bounds__(256) void k_rk_reach(RankGeom g, uint32_t L, u64 lvstart, uint32_t lvoff, u64 nwords,
+                                                  u64 nreal, BlockCount* bc, DevState* st) {
+  u64 npos = 0, prims = 0;
+  const bool fmoved = ((L - 1) & 1u) == 0;  // the move into level L was the first mover's
+  for (u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += (u64)gridDim.x * blockDim.x) {
+    const u64 i0 = w << 6, blk = i0 >> (L + 3);
+    if (i0 >= nreal) {  // padding
+      reinterpret_cast<u64*>(g.reach)[(lvstart + i0) >> 6] = 0;
+      reinterpret_cast<u64*>(g.expd)[(lvstart + i0) >> 6] = 0;
+      continue;
+    }
+    const uint32_t a = (uint32_t)((i0 >> L) & 7u), p0 = (uint32_t)(i0 & ((1ull << L) - 1));
+    const uint32_t hvc = g.lvhv[lvoff + blk];
+    RankPos p;
+    rk_unpack(g, g.lvph[lvoff + blk], p);
+    const u64 valid = rk_valid_mask(g, L, a, p0);
+    u64 r = 0;
+    if (valid) {
+#pragma unroll
+      for (int x = 0; x < kRankMaxCols; x++) {
+        if (x >= (int)g.C || p.h[x] == 0) continue;
+        const uint32_t q = p.off[x] + p.h[x] - 1;
+        const u64 pb = g.base[hvc - g.stride[x]];
+        if (q >= 6) {
+          const uint32_t l = (p0 >> q) & 1u;
+          if (fmoved && l && a == 0) continue;
+          const uint32_t pa = a - (fmoved && l ? 1u : 0u);
+          const uint32_t pp0 = (p0 & ((1u << q) - 1u)) | ((p0 >> (q + 1)) << q);
+          r |= reinterpret_cast<const u64*>(g.expd)[(pb + ((u64)pa << (L - 1)) + pp0) >> 6];
+        } else {
+          // children j with bit q = l: parents (p0 >> 1) + compress_q(j), 32 in a row
+#pragma unroll
+          for (uint32_t l = 0; l < 2; l++) {
+            if (fmoved && l && a == 0) continue;
+            const uint32_t pa = a - (fmoved && l ? 1u : 0u);
+            const u64 ps0 = pb + ((u64)pa << (L - 1)) + (p0 >> 1);  // a multiple of 32
+            const uint32_t e = g.expd[ps0 >> 5];
+            r |= rk_spread(e, q) << (l << q);
+          }
+        }
+      }
+      r &= valid;
+    }
+    const u64 pm = reinterpret_cast<const u64*>(g.pbits)[((lvstart >> 3) + (blk << L) + p0) >> 6];
+    reinterpret_cast<u64*>(g.reach)[(lvstart + i0) >> 6] = r;
+    reinterpret_cast<u64*>(g.expd)[(lvstart + i0) >> 6] = r & ~pm;
+    npos += (u64)__builtin_popcountll(r);
+    prims += (u64)__builtin_popcountll(r & pm);
+  }
+  block_count(bc, npos, 0);
+  block_add(&st->prims, prims);
+}
+
+// F1 for levels L < 6 (blocks narrower than a word): one thread per slot
 // (nitems: the level's slots rounded up to 64, so every bitmap word of the
 // level is written -- no clearing -- nreal: its slots)
-template <int KIND>
-__global__ __launch_bounds__(256) void k_rk_forward(Desc d, RankGeom g, uint32_t L, u64 lvstart, uint32_t lvoff,
-                                                    u64 nitems, u64 nreal, BlockCount* bc, DevState* st) {
+__global__ __launch_bounds__(256) void k_rk_forward(RankGeom g, uint32_t L, u64 lvstart, uint32_t lvoff, u64 nitems,
+                                                    u64 nreal, BlockCount* bc, DevState* st) {
   u64 npos = 0, prims = 0;
   const uint32_t lane = threadIdx.x & 63;
   const u64 stride = (u64)gridDim.x * blockDim.x;
@@ -159,14 +276,14 @@ __global__ __launch_bounds__(256) void k_rk_forward(Desc d, RankGeom g, uint32_t
         if (L == 0) {
           reach = true;  // the root (hands 6 / 6 / 6 / 6, the first mover to move)
         } else {
-          const bool p1moved = ((L - 1) & 1u) == 0;  // the move into level L was the first player's
+          const bool fmoved = ((L - 1) & 1u) == 0;
 #pragma unroll
           for (int x = 0; x < kRankMaxCols; x++) {
             if (x >= (int)g.C || p.h[x] == 0) continue;
             const uint32_t q = p.off[x] + p.h[x] - 1, l = (pat >> q) & 1u;
-            if (p1moved && l && a == 0) continue;
+            if (fmoved && l && a == 0) continue;
             const uint32_t pp = (pat & ((1u << q) - 1u)) | ((pat >> (q + 1)) << q);
-            const uint32_t pa = a - (p1moved && l ? 1u : 0u);
+            const uint32_t pa = a - (fmoved && l ? 1u : 0u);
             const u64 ps = g.base[hvc - g.stride[x]] + ((u64)pa << (L - 1)) + pp;
             if ((g.expd[ps >> 5] >> (ps & 31)) & 1u) {
               reach = true;
@@ -175,7 +292,7 @@ __global__ __launch_bounds__(256) void k_rk_forward(Desc d, RankGeom g, uint32_t
           }
         }
         if (reach) {
-          const int pr = Game<KIND>::prim(d, rk_key(g, p, pat, L, u));
+          const int pr = g.bstat[(lvstart >> 3) + (blk << L) + pat];
           ex = pr == UNDECIDED;
           prims += !ex;
           npos++;
@@ -193,58 +310,89 @@ __global__ __launch_bounds__(256) void k_rk_forward(Desc d, RankGeom g, uint32_t
   block_add(&st->prims, prims);
 }
 
-template <int KIND>
-__global__ __launch_bounds__(256) void k_rk_backward(Desc d, RankGeom g, uint32_t L, u64 lvstart, uint32_t lvoff,
-                                                     u64 nitems, BlockCount* bc, DevState* st) {
+// B: the reached slots of level L gather their children's words.  A
+// workgroup takes a tile of 256 x 64 slots: each thread reads one reach word,
+// the workgroup lays the reached slots' offsets out in LDS (exclusive scan of
+// the words' popcounts), then every thread resolves list entries -- waves
+// carry reached slots only (about 1 in 6 of all slots on toot 6x4), and a
+// primitive's value comes from bstat.
+constexpr uint32_t kRkTile = 256 * 64;
+__global__ __launch_bounds__(256) void k_rk_backward(RankGeom g, uint32_t L, u64 lvstart, uint32_t lvoff,
+                                                     u64 nwords, BlockCount* bc, DevState* st) {
+  __shared__ uint16_t list[kRkTile];
+  __shared__ uint32_t wsum[4];
   u64 edges = 0;
   uint32_t err = 0;
-  const u64 stride = (u64)gridDim.x * blockDim.x;
-  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < nitems; i += stride) {
-    const u64 slot = lvstart + i;
-    if (!((g.reach[slot >> 5] >> (slot & 31)) & 1u)) continue;
-    const u64 blk = i >> (L + 3);
-    const uint32_t a = (uint32_t)((i >> L) & 7u), pat = (uint32_t)(i & ((1ull << L) - 1));
-    const uint32_t hvc = g.lvhv[lvoff + blk];
-    RankPos p;
-    rk_unpack(g, g.lvph[lvoff + blk], p);
-    const RankHands u = rk_hands(L, (uint32_t)__builtin_popcount(pat), a);
-    const int pr = Game<KIND>::prim(d, rk_key(g, p, pat, L, u));
-    uint32_t word;
-    if (pr != UNDECIDED) {
-      word = make_word(pr, 0);  // process.py:120-123
-    } else {
-      const bool p1 = (L & 1u) == 0;  // the first player moves at even levels
-      const bool hasT = p1 ? u.t1 < (int)kRankHand : u.t2 < (int)kRankHand;
-      const bool hasO = p1 ? u.o1 < (int)kRankHand : u.o2 < (int)kRankHand;
-      const uint32_t at = a + (p1 ? 1u : 0u);
-      bool any_loss = false, any_tie = false, any_draw = false;
-      uint32_t min_loss = 0xFFFFFFFFu, max_all = 0, nch = 0;
-      auto take = [&](uint32_t w) {
-        const uint32_t v = w & 3u, r = w >> 2;
-        if (v == LOSS) {
-          any_loss = true;
-          min_loss = min(min_loss, r);
-        }
-        any_tie |= v == TIE;
-        any_draw |= v == DRAW;
-        max_all = max(max_all, r);
-        nch++;
-      };
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const bool fmoves = (L & 1u) == 0;  // the first mover moves at even levels
+  for (u64 t0 = (u64)blockIdx.x * 256; t0 < nwords; t0 += (u64)gridDim.x * 256) {
+    const u64 wi = t0 + threadIdx.x;
+    const u64 m = wi < nwords ? reinterpret_cast<const u64*>(g.reach)[(lvstart >> 6) + wi] : 0ull;
+    // exclusive scan of the popcounts over the workgroup
+    const uint32_t c = (uint32_t)__builtin_popcountll(m);
+    uint32_t incl = c;
 #pragma unroll
-      for (int x = 0; x < kRankMaxCols; x++) {
-        if (x >= (int)g.C || p.h[x] >= g.H) continue;
-        const uint32_t q = p.off[x] + p.h[x];
-        const uint32_t lo = pat & ((1u << q) - 1u), hi = (pat >> q) << (q + 1);
-        const u64 cb = g.base[hvc + g.stride[x]];
-        if (hasT) take(g.words[cb + ((u64)at << (L + 1)) + (lo | (1u << q) | hi)]);
-        if (hasO) take(g.words[cb + ((u64)a << (L + 1)) + (lo | hi)]);
-      }
-      if (nch == 0) err |= ERR_NO_MOVES;
-      edges += nch;
-      // reference-canonical _res_red / _remote_red
-      word = any_loss ? make_word(WIN, min_loss + 1) : make_word(any_tie ? TIE : any_draw ? DRAW : LOSS, max_all + 1);
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(incl, o);
+      if (lane >= (uint32_t)o) incl += y;
     }
-    g.words[slot] = (uint8_t)word;
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+    for (uint32_t k = 0; k < 4; k++) {
+      if (k < wv) before += wsum[k];
+      total += wsum[k];
+    }
+    uint32_t at = before + incl - c;
+    for (u64 mm = m; mm; mm &= mm - 1) list[at++] = (uint16_t)(threadIdx.x * 64 + __builtin_ctzll(mm));
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < total; e += 256) {
+      const u64 i = (t0 << 6) + list[e];
+      const u64 slot = lvstart + i;
+      const u64 blk = i >> (L + 3);
+      const uint32_t a = (uint32_t)((i >> L) & 7u), pat = (uint32_t)(i & ((1ull << L) - 1));
+      const int pr = g.bstat[(lvstart >> 3) + (blk << L) + pat];
+      uint32_t word;
+      if (pr != UNDECIDED) {
+        word = make_word(pr, 0);  // process.py:120-123
+      } else {
+        const uint32_t hvc = g.lvhv[lvoff + blk];
+        RankPos p;
+        rk_unpack(g, g.lvph[lvoff + blk], p);
+        const RankHands u = rk_hands(L, (uint32_t)__builtin_popcount(pat), a);
+        const bool hasT = fmoves ? u.t1 < (int)kRankHand : u.t2 < (int)kRankHand;
+        const bool hasO = fmoves ? u.o1 < (int)kRankHand : u.o2 < (int)kRankHand;
+        const uint32_t at_ = a + (fmoves ? 1u : 0u);
+        bool any_loss = false, any_tie = false, any_draw = false;
+        uint32_t min_loss = 0xFFFFFFFFu, max_all = 0, nch = 0;
+        auto take = [&](uint32_t w) {
+          const uint32_t v = w & 3u, r = w >> 2;
+          if (v == LOSS) {
+            any_loss = true;
+            min_loss = min(min_loss, r);
+          }
+          any_tie |= v == TIE;
+          any_draw |= v == DRAW;
+          max_all = max(max_all, r);
+          nch++;
+        };
+#pragma unroll
+        for (int x = 0; x < kRankMaxCols; x++) {
+          if (x >= (int)g.C || p.h[x] >= g.H) continue;
+          const uint32_t q = p.off[x] + p.h[x];
+          const uint32_t lo = pat & ((1u << q) - 1u), hi = (pat >> q) << (q + 1);
+          const u64 cb = g.base[hvc + g.stride[x]];
+          if (hasT) take(g.words[cb + ((u64)at_ << (L + 1)) + (lo | (1u << q) | hi)]);
+          if (hasO) take(g.words[cb + ((u64)a << (L + 1)) + (lo | hi)]);
+        }
+        if (nch == 0) err |= ERR_NO_MOVES;
+        edges += nch;
+        // reference-canonical _res_red / _remote_red
+        word = any_loss ? make_word(WIN, min_loss + 1) : make_word(any_tie ? TIE : any_draw ? DRAW : LOSS, max_all + 1);
+      }
+      g.words[slot] = (uint8_t)word;
+    }
+    __syncthreads();  // the list is rewritten by the next tile
   }
   if (err) atomicOr(&st->err, err);
   block_count(bc, 0, edges);
@@ -318,7 +466,7 @@ struct RankShape {
   std::vector<uint32_t> lvhv, lvph;     // hvcodes level by level, packed heights
   std::vector<uint32_t> lvoff;          // per level: first entry in lvhv (T + 1)
   std::vector<u64> lvstart, lvitems;    // per level: first slot, slots
-  u64 words_off, reach_off, expd_off, base_off, lvhv_off, lvph_off, table_bytes;
+  u64 words_off, reach_off, expd_off, bstat_off, pbits_off, base_off, lvhv_off, lvph_off, table_bytes;
 };
 
 static int rank_shape(const Desc* d, RankShape* rs) {
@@ -366,7 +514,7 @@ static int rank_shape(const Desc* d, RankShape* rs) {
       rs->lvph.push_back(ph);
     }
     rs->lvitems[L] = (u64)byl[L].size() * nb;
-    at += (rs->lvitems[L] + 63) & ~63ull;
+    at += (rs->lvitems[L] + 511) & ~511ull;  // boards (slots / 8) 64-aligned
   }
   rs->lvoff[g.T] = (uint32_t)rs->lvhv.size();
   rs->lvstart[g.T] = at;
@@ -374,7 +522,9 @@ static int rank_shape(const Desc* d, RankShape* rs) {
   rs->words_off = 0;
   rs->reach_off = rup256(at);
   rs->expd_off = rs->reach_off + rup256(at / 8);
-  rs->base_off = rs->expd_off + rup256(at / 8);
+  rs->bstat_off = rs->expd_off + rup256(at / 8);
+  rs->pbits_off = rs->bstat_off + rup256(at / 8);
+  rs->base_off = rs->pbits_off + rup256(at / 64);
   rs->lvhv_off = rs->base_off + rup256((u64)nhv * 8);
   rs->lvph_off = rs->lvhv_off + rup256((u64)nhv * 4);
   rs->table_bytes = rs->lvph_off + rup256((u64)nhv * 4);
@@ -409,6 +559,14 @@ static int rank_setup(gm_solver* s, const gm_buffers* buf) {
   rs.g.base = (const u64*)(t + rs.base_off);
   rs.g.lvhv = (const uint32_t*)(t + rs.lvhv_off);
   rs.g.lvph = (const uint32_t*)(t + rs.lvph_off);
+  rs.g.bstat = (uint8_t*)(t + rs.bstat_off);
+  rs.g.pbits = (u64*)(t + rs.pbits_off);
+  for (int c = 0; c < 7; c++) {
+    u64 m = 0;
+    for (int j = 0; j < 64; j++)
+      if (__builtin_popcount((unsigned)j) <= c) m |= 1ull << j;
+    rs.g.le[c] = m;
+  }
   HIPCHK(hipMemcpy((void*)rs.g.base, rs.base.data(), rs.base.size() * 8, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy((void*)rs.g.lvhv, rs.lvhv.data(), rs.lvhv.size() * 4, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy((void*)rs.g.lvph, rs.lvph.data(), rs.lvph.size() * 4, hipMemcpyHostToDevice));
@@ -470,23 +628,27 @@ static int run_ranked(gm_solver* s, gm_result* out) {
     constexpr int KIND = decltype(KC)::value;
     for (int k = std::max(first, 0); k < std::min(stop, T); k++) {
       const uint32_t L = (uint32_t)k;
-      const u64 n = (s->rlvitems[L] + 63) & ~63ull;
-      hipLaunchKernelGGL((k_rk_forward<KIND>), dim3(rank_grid(s, n)), dim3(256), 0, st, d, g, L, s->rlvstart[L],
-                         s->rlvoff[L], n, s->rlvitems[L], s->bcount, s->st);
-      nl_f++;
+      const u64 nreal = s->rlvitems[L] >> 3, nb = (s->rlvstart[L + 1] - s->rlvstart[L]) >> 3;  // boards
+      hipLaunchKernelGGL((k_rk_boards<KIND>), dim3(rank_grid(s, nb)), dim3(256), 0, st, d, g, L, s->rlvstart[L] >> 3,
+                         s->rlvoff[L], nb, nreal);
+      const u64 n = s->rlvstart[L + 1] - s->rlvstart[L];  // 512-padded: every bitmap word written
+      if (L >= 6)
+        hipLaunchKernelGGL(k_rk_reach, dim3(rank_grid(s, n / 64)), dim3(256), 0, st, g, L, s->rlvstart[L],
+                           s->rlvoff[L], n / 64, s->rlvitems[L], s->bcount, s->st);
+      else
+        hipLaunchKernelGGL(k_rk_forward, dim3(rank_grid(s, n)), dim3(256), 0, st, g, L, s->rlvstart[L], s->rlvoff[L],
+                           n, s->rlvitems[L], s->bcount, s->st);
+      nl_f += 2;
     }
   });
   HIPCHK(hipEventRecord(ev[1], st));
-  rank_kind_dispatch(d, [&](auto KC) {
-    constexpr int KIND = decltype(KC)::value;
-    for (int k = std::max(first, T); k < stop; k++) {
-      const uint32_t L = (uint32_t)(2 * T - 1 - k);
-      const u64 n = s->rlvitems[L];
-      hipLaunchKernelGGL((k_rk_backward<KIND>), dim3(rank_grid(s, n)), dim3(256), 0, st, d, g, L, s->rlvstart[L],
-                         s->rlvoff[L], n, s->bcount, s->st);
-      nl_b++;
-    }
-  });
+  for (int k = std::max(first, T); k < stop; k++) {
+    const uint32_t L = (uint32_t)(2 * T - 1 - k);
+    const u64 nw = (s->rlvitems[L] + 63) / 64;
+    hipLaunchKernelGGL(k_rk_backward, dim3(rank_grid(s, nw)), dim3(256), 0, st, g, L, s->rlvstart[L],
+                       s->rlvoff[L], nw, s->bcount, s->st);
+    nl_b++;
+  }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ev[2], st));
   if (stop < 2 * T) {

@@ -912,6 +912,9 @@ struct RankGeom {
   const u64* base;         // [R^C] hvcode -> first slot of its block
   const uint32_t* lvhv;    // hvcodes level by level
   const uint32_t* lvph;    // the same, heights packed 4 bits per column
+  uint8_t* bstat;          // [nslots / 8] per board (stacks): primitive value or UNDECIDED
+  u64* pbits;              // [nslots / 512] per board: primitive
+  u64 le[7];               // bits j < 64 with popcount(j) <= c
 };
 
 enum DenseResolveKind : uint32_t {

@@ -165,13 +165,13 @@ def test_plan_sizes():
     t = GameSpec("toot_and_otto_bitstring", "length=4,height=4")
     _lib.check(_lib.load().gm_plan(t.id, 0, 0, 0, ctypes.byref(p)))
     # toot: positions at computed indices -- per level, its height vectors'
-    # blocks of 8 x 2^L slots, levels padded to 64 (gm_ranked.h)
+    # blocks of 8 x 2^L slots, levels padded to 512 (gm_ranked.h)
     assert p.mode == _lib.GM_MODE_RANKED
     import itertools
     per = [0] * 17
     for hv in itertools.product(range(5), repeat=4):
         per[sum(hv)] += 8 << sum(hv)
-    slots = sum((n + 63) // 64 * 64 for n in per)
+    slots = sum((n + 511) // 512 * 512 for n in per)
     assert slots >= 8 * 31 ** 4 and p.table_slots == slots
     assert p.table_bytes >= slots + 2 * slots // 8
     _lib.check(_lib.load().gm_plan(t.id, 0, _lib.GM_F_FORCE_HASHED, 0, ctypes.byref(p)))
