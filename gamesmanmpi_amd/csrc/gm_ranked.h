@@ -316,9 +316,19 @@ __global__ __launch_bounds__(256) void k_rk_forward(RankGeom g, uint32_t L, u64 
 // the words' popcounts), then every thread resolves list entries -- waves
 // carry reached slots only (about 1 in 6 of all slots on toot 6x4), and a
 // primitive's value comes from bstat.
+// The children's words come through a buffer resource over level L + 1 (< 4
+// GB: every level of a supported board): a move that is not legal reads
+// offset 0xFFFFFFFF, out of range, i.e. 0 = WIN in 0, neutral in the
+// reduction -- so all 2C loads issue back to back with no branches.  CC / HH:
+// the board at compile time (0: from g).
 constexpr uint32_t kRkTile = 256 * 64;
+template <int CC, int HH>
 __global__ __launch_bounds__(256) void k_rk_backward(RankGeom g, uint32_t L, u64 lvstart, uint32_t lvoff,
-                                                     u64 nwords, BlockCount* bc, DevState* st) {
+                                                     u64 nwords, u64 cstart, u64 csize, BlockCount* bc, DevState* st) {
+  constexpr int NC = CC > 0 ? CC : kRankMaxCols;
+  const uint32_t C = CC > 0 ? (uint32_t)CC : g.C, H = HH > 0 ? (uint32_t)HH : g.H;
+  const __amdgpu_buffer_rsrc_t rw =
+      __builtin_amdgcn_make_buffer_rsrc(g.words + cstart, 0, (int)(uint32_t)csize, 0x00020000);
   __shared__ uint16_t list[kRkTile];
   __shared__ uint32_t wsum[4];
   u64 edges = 0;
@@ -356,38 +366,41 @@ __global__ __launch_bounds__(256) void k_rk_backward(RankGeom g, uint32_t L, u64
       if (pr != UNDECIDED) {
         word = make_word(pr, 0);  // process.py:120-123
       } else {
-        const uint32_t hvc = g.lvhv[lvoff + blk];
-        RankPos p;
-        rk_unpack(g, g.lvph[lvoff + blk], p);
+        const uint32_t hvc = g.lvhv[lvoff + blk], ph = g.lvph[lvoff + blk];
         const RankHands u = rk_hands(L, (uint32_t)__builtin_popcount(pat), a);
         const bool hasT = fmoves ? u.t1 < (int)kRankHand : u.t2 < (int)kRankHand;
         const bool hasO = fmoves ? u.o1 < (int)kRankHand : u.o2 < (int)kRankHand;
-        const uint32_t at_ = a + (fmoves ? 1u : 0u);
+        const uint32_t rowT = (a + (fmoves ? 1u : 0u)) << (L + 1), rowO = a << (L + 1);
+        uint32_t w[2 * NC], nch = 0, off = 0;
+#pragma unroll
+        for (int x = 0; x < NC; x++) {
+          const uint32_t h = (ph >> (4 * x)) & 15u;
+          const bool col = (CC > 0 || (uint32_t)x < C) && h < H;
+          const uint32_t q = off + h;
+          off += h;
+          const uint32_t lo = pat & ((1u << q) - 1u), hi = (pat >> q) << (q + 1);
+          const uint32_t cb = (uint32_t)(g.base[col ? hvc + g.stride[x] : hvc] - cstart);
+          const bool vT = col && hasT, vO = col && hasO;
+          w[2 * x] = __builtin_amdgcn_raw_buffer_load_b8(rw, vT ? cb + rowT + (lo | (1u << q) | hi) : 0xFFFFFFFFu, 0, 0);
+          w[2 * x + 1] = __builtin_amdgcn_raw_buffer_load_b8(rw, vO ? cb + rowO + (lo | hi) : 0xFFFFFFFFu, 0, 0);
+          nch += (uint32_t)vT + (uint32_t)vO;
+        }
+        // reference-canonical _res_red / _remote_red over the children (an
+        // absent child reads 0: WIN in 0, changes none of the four)
         bool any_loss = false, any_tie = false, any_draw = false;
-        uint32_t min_loss = 0xFFFFFFFFu, max_all = 0, nch = 0;
-        auto take = [&](uint32_t w) {
-          const uint32_t v = w & 3u, r = w >> 2;
-          if (v == LOSS) {
-            any_loss = true;
-            min_loss = min(min_loss, r);
-          }
+        uint32_t min_loss = 0xFFFFFFFFu, max_all = 0;
+#pragma unroll
+        for (int k = 0; k < 2 * NC; k++) {
+          const uint32_t v = w[k] & 3u, r = w[k] >> 2;
+          any_loss |= v == LOSS;
+          min_loss = v == LOSS ? min(min_loss, r) : min_loss;
           any_tie |= v == TIE;
           any_draw |= v == DRAW;
           max_all = max(max_all, r);
-          nch++;
-        };
-#pragma unroll
-        for (int x = 0; x < kRankMaxCols; x++) {
-          if (x >= (int)g.C || p.h[x] >= g.H) continue;
-          const uint32_t q = p.off[x] + p.h[x];
-          const uint32_t lo = pat & ((1u << q) - 1u), hi = (pat >> q) << (q + 1);
-          const u64 cb = g.base[hvc + g.stride[x]];
-          if (hasT) take(g.words[cb + ((u64)at_ << (L + 1)) + (lo | (1u << q) | hi)]);
-          if (hasO) take(g.words[cb + ((u64)a << (L + 1)) + (lo | hi)]);
         }
         if (nch == 0) err |= ERR_NO_MOVES;
         edges += nch;
-        // reference-canonical _res_red / _remote_red
+        // 
         word = any_loss ? make_word(WIN, min_loss + 1) : make_word(any_tie ? TIE : any_draw ? DRAW : LOSS, max_all + 1);
       }
       g.words[slot] = (uint8_t)word;
@@ -449,16 +462,6 @@ __global__ __launch_bounds__(256) void k_rk_scan(Desc d, RankGeom g, const u64* 
 // ---------------------------------------------------------------------------
 // host
 // ---------------------------------------------------------------------------
-static bool rank_ok(const Desc* d) {
-  if (d->kind != K_TOOT || d->L < 1 || d->L > kRankMaxCols || d->H < 1 || d->H > 7) return false;
-  if (d->max_levels > 64 || (int)d->max_levels != d->L * d->H + 1) return false;  // remoteness in 6 bits
-  double n = 8;
-  for (int x = 0; x < d->L; x++) n *= (double)((2u << d->H) - 1);
-  return n <= (double)(1ull << 36);
-}
-static bool rank_wanted(const Desc* d, uint32_t flags) {
-  return rank_ok(d) && !(flags & (GM_F_FORCE_HASHED | GM_F_HASH_TABLE));
-}
 
 struct RankShape {
   RankGeom g;
@@ -529,6 +532,23 @@ static int rank_shape(const Desc* d, RankShape* rs) {
   rs->lvph_off = rs->lvhv_off + rup256((u64)nhv * 4);
   rs->table_bytes = rs->lvph_off + rup256((u64)nhv * 4);
   return 0;
+}
+
+static bool rank_ok(const Desc* d) {
+  if (d->kind != K_TOOT || d->L < 1 || d->L > kRankMaxCols || d->H < 1 || d->H > 7) return false;
+  if (d->max_levels > 64 || (int)d->max_levels != d->L * d->H + 1) return false;  // remoteness in 6 bits
+  double n = 8;
+  for (int x = 0; x < d->L; x++) n *= (double)((2u << d->H) - 1);
+  if (n > (double)(1ull << 36)) return false;
+  // every level's slots addressable by one 32-bit buffer offset (k_rk_backward)
+  RankShape rs;
+  if (rank_shape(d, &rs)) return false;
+  for (uint32_t L = 0; L < rs.g.T; L++)
+    if (rs.lvstart[L + 1] - rs.lvstart[L] >= 0xFFFFFFFFull) return false;
+  return true;
+}
+static bool rank_wanted(const Desc* d, uint32_t flags) {
+  return rank_ok(d) && !(flags & (GM_F_FORCE_HASHED | GM_F_HASH_TABLE));
 }
 
 static int plan_ranked(const Desc* d, uint64_t max_table_bytes, gm_plan_t* out, bool* fits) {
@@ -645,8 +665,18 @@ static int run_ranked(gm_solver* s, gm_result* out) {
   for (int k = std::max(first, T); k < stop; k++) {
     const uint32_t L = (uint32_t)(2 * T - 1 - k);
     const u64 nw = (s->rlvitems[L] + 63) / 64;
-    hipLaunchKernelGGL(k_rk_backward, dim3(rank_grid(s, nw)), dim3(256), 0, st, g, L, s->rlvstart[L],
-                       s->rlvoff[L], nw, s->bcount, s->st);
+    // level L + 1's slots (the last level has no children: an empty range)
+    const u64 cs = s->rlvstart[std::min<uint32_t>(L + 1, (uint32_t)T)];
+    const u64 cn = L + 1 < (uint32_t)T ? s->rlvstart[L + 2] - cs : 0;
+    auto go = [&](auto CH) {
+      constexpr int CC = decltype(CH)::value / 16, HH = decltype(CH)::value % 16;
+      hipLaunchKernelGGL((k_rk_backward<CC, HH>), dim3(rank_grid(s, nw)), dim3(256), 0, st, g, L, s->rlvstart[L],
+                         s->rlvoff[L], nw, cs, cn, s->bcount, s->st);
+    };
+    if (g.C == 6 && g.H == 4) go(std::integral_constant<int, 6 * 16 + 4>());
+    else if (g.C == 5 && g.H == 4) go(std::integral_constant<int, 5 * 16 + 4>());
+    else if (g.C == 4 && g.H == 4) go(std::integral_constant<int, 4 * 16 + 4>());
+    else go(std::integral_constant<int, 0>());
     nl_b++;
   }
   HIPCHK(hipGetLastError());
