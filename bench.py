@@ -22,8 +22,11 @@ Prints ONE JSON line (rank 0).  Fields beyond the driver contract:
                 profiles/pmc_traffic.json) and frac_per_edge_model (one child
                 word read per edge, the round-1 figure) -- DESIGN.md §5
   keyed         BASELINE config 3 as shipped (toot 6x4, 1.19e9 positions) on
-                the keyed-table path: solve time, positions/s, per-kernel
-                §8d rooflines, fingerprint parity vs the CPU restatement
+                the layout the planner picks (RANKED: positions at computed
+                indices) and, as "bucketed", on the keyed BUCKETED levels:
+                solve time, positions/s, per-pass bytes and rates (the
+                layout's compulsory bytes; §8d's keyed-table model),
+                fingerprint parity vs the CPU restatement
   cpu_baseline  the multi-threaded CPU restatement (oracle/oracle_mt.c row
                 solver, all host threads) on the SAME workload
 """
@@ -265,16 +268,20 @@ def keyed_atomics():
                               "ms": v.get("kernel_ms")} for k, v in top[:6]}}
 
 
-def keyed_record(device):
-    """BASELINE config 3 as shipped: toot_and_otto_bitstring 6x4 on the
-    keyed path the planner picks (BUCKETED levels; one warm-up solve, one
-    timed, one with kernel timing), fingerprint vs
-    tests/golden/checksums.json."""
+def ranked_bytes(nslots, positions, edges):
+    """Compulsory bytes of the RANKED layout (gm_ranked.h): forward -- the
+    per-board primitive byte and the reach + expandable bits of every slot
+    written; backward -- the reach bits read, per reached position its board
+    byte read and its word written, per edge the child's word read."""
+    return nslots // 8 * 3, nslots // 8 + 2 * positions + edges
+
+
+def _keyed_solve(device, layout):
     from gamesmanmpi_amd.games import GameSpec
     from gamesmanmpi_amd.solver import Solver
     import torch
     params = "length=6,height=4"
-    s = Solver(GameSpec("toot_and_otto_bitstring", params), device=device)
+    s = Solver(GameSpec("toot_and_otto_bitstring", params), device=device, layout=layout)
     s.solve()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -284,25 +291,32 @@ def keyed_record(device):
     s.set_kernel_timing(True)
     tr = s.solve()
     s.set_kernel_timing(False)
+    lay = r.extra["layout"]
     fwd_b, bwd_b = keyed_bytes(r.positions, r.edges)
     out = {"workload": "toot_and_otto_bitstring " + params,
-           "layout": r.extra["layout"],
+           "layout": lay,
            "positions": r.positions, "edges": r.edges, "root": r.root_line,
            "solve_ms": wall * 1e3, "positions_per_s": r.positions / wall,
            "ms_forward": r.ms_forward, "ms_backward": r.ms_backward,
            "kernels": {}}
-    # HASHED: the expand / resolve kernels; BUCKETED: every kernel of the
-    # forward / backward passes (gm_bucketed.h F0-F5 / B3-B5)
-    names = ("expand", "resolve") if r.extra["layout"] == "hashed" else ("forward", "backward")
-    for name, b, ms, n in ((names[0], fwd_b, tr.ms_expand_kernels, tr.n_expand_launches),
-                           (names[1], bwd_b, tr.ms_resolve_kernels, tr.n_resolve_launches)):
+    # the bytes each pass must move: SURVEY §8d's keyed-table model, or for
+    # RANKED the layout's own compulsory bytes (no keys, no dedup)
+    if lay == "ranked":
+        fb, bb = ranked_bytes(int(s.plan.table_slots), r.positions, r.edges)
+        model = "ranked_bytes"
+    else:
+        fb, bb, model = fwd_b, bwd_b, "model_8d_bytes"
+    names = ("expand", "resolve") if lay == "hashed" else ("forward", "backward")
+    for name, b, ms, n in ((names[0], fb, tr.ms_expand_kernels, tr.n_expand_launches),
+                           (names[1], bb, tr.ms_resolve_kernels, tr.n_resolve_launches)):
         if n and ms > 0:
-            out["kernels"][name] = {"launches": n, "ms_total": ms,
-                                    "model_8d_bytes": b,
+            out["kernels"][name] = {"launches": n, "ms_total": ms, model: b,
                                     "achieved_GBps": b / (ms / 1e3) / 1e9,
                                     "frac": b / (ms / 1e3) / 1e9 / HBM_PEAK_GBS}
+    # SURVEY §8d's keyed bytes over the whole solve: for RANKED a rate of
+    # the keyed-table work it does NOT do (no keys moved) -- comparable across
+    # layouts as "keyed-table bytes per second", not a roofline fraction
     out["model_8d_frac_whole_solve"] = (fwd_b + bwd_b) / wall / 1e9 / HBM_PEAK_GBS
-    out["atomics"] = keyed_atomics()
     e = golden("toot_6x4")
     if e is not None:
         ck = s.checksum()
@@ -312,6 +326,22 @@ def keyed_record(device):
                                 and r.edges == e["edges"] and r.root_line == e["root_line"])}
     del s
     torch.cuda.empty_cache()
+    return out
+
+
+def keyed_record(device):
+    """BASELINE config 3 as shipped: toot_and_otto_bitstring 6x4 on the
+    layout the planner picks (RANKED: positions at computed indices), and on
+    the keyed BUCKETED levels (what every keyed game without a rank function
+    runs, othello included) as a sub-record; each: one warm-up solve, one
+    timed, one with kernel timing, fingerprint vs tests/golden/checksums.json."""
+    out = _keyed_solve(device, "auto")
+    if out["layout"] != "bucketed":
+        b = _keyed_solve(device, "bucketed")
+        b["atomics"] = keyed_atomics()
+        out["bucketed"] = b
+    else:
+        out["atomics"] = keyed_atomics()
     return out
 
 
