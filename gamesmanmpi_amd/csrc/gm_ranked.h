@@ -139,24 +139,64 @@ __device__ __forceinline__ bool rk_slot_of(const RankGeom& g, u64 key, u64* slot
 // (the a = 0 view: board lvstart / 8 + (i >> (L + 3) << L) + bits) start
 // 64-aligned and every 64-slot / 64-board word belongs to one level.
 
+// The t / o planes of a board from its stacks.  C > H: a column's h <= H
+// bits land on cells x + C y by one multiply (bit y times 2^((C-1) y) sits at
+// C y; no two products meet), else a loop.
+template <int CC, int HH>
+__device__ __forceinline__ u64 rk_board_key(const RankGeom& g, uint32_t ph, uint32_t pat, uint32_t L) {
+  u64 t = 0, o = 0;
+  uint32_t off = 0;
+  if constexpr (CC > HH && CC * HH <= 32) {
+    constexpr uint32_t mul = [] {
+      uint32_t m = 0;
+      for (int y = 0; y < HH; y++) m |= 1u << ((CC - 1) * y);
+      return m;
+    }();
+    constexpr uint32_t msk = [] {
+      uint32_t m = 0;
+      for (int y = 0; y < HH; y++) m |= 1u << (CC * y);
+      return m;
+    }();
+    uint32_t t32 = 0, o32 = 0;
+#pragma unroll
+    for (int x = 0; x < CC; x++) {
+      const uint32_t h = (ph >> (4 * x)) & 15u, full = (1u << h) - 1u;
+      const uint32_t col = (pat >> off) & full;
+      off += h;
+      t32 |= ((col * mul) & msk) << x;
+      o32 |= (((~col & full) * mul) & msk) << x;
+    }
+    t = t32;
+    o = o32;
+  } else {
+    for (uint32_t x = 0; x < g.C; x++) {
+      const uint32_t h = (ph >> (4 * x)) & 15u, col = (pat >> off) & ((1u << h) - 1u);
+      off += h;
+      for (uint32_t y = 0; y < h; y++) {
+        const u64 cell = 1ull << (g.C * y + x);
+        if ((col >> y) & 1u) t |= cell;
+        else o |= cell;
+      }
+    }
+  }
+  return t | (o << g.A) | ((u64)(L & 1u) << (2 * g.A + 12));  // hands: unread by the rule
+}
+
 // F0: every board of level L (its stacks; the hands do not enter the rule):
 // the reference's primitive value (toot_prim) or UNDECIDED in bstat, and the
 // primitive bit in pbits.  One thread per board; a wave = one pbits word.
-template <int KIND>
+template <int KIND, int CC, int HH>
 __global__ __launch_bounds__(256) void k_rk_boards(Desc d, RankGeom g, uint32_t L, u64 bstart, uint32_t lvoff,
                                                    u64 nboards, u64 nreal) {
   const uint32_t lane = threadIdx.x & 63;
   const u64 stride = (u64)gridDim.x * blockDim.x;
-  const RankHands none{0, 0, 0, 0};
   for (u64 i0 = (u64)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); i0 < nboards; i0 += stride) {
     const u64 i = i0 + lane;
     bool prim = false;
     if (i < nreal) {
       const u64 blk = i >> L;
       const uint32_t pat = (uint32_t)(i & ((1ull << L) - 1));
-      RankPos p;
-      rk_unpack(g, g.lvph[lvoff + blk], p);
-      const int pr = Game<KIND>::prim(d, rk_key(g, p, pat, L, none));
+      const int pr = Game<KIND>::prim(d, rk_board_key<CC, HH>(g, g.lvph[lvoff + blk], pat, L));
       g.bstat[bstart + i] = (uint8_t)pr;
       prim = pr != UNDECIDED;
     }
@@ -366,7 +406,14 @@ __global__ __launch_bounds__(256) void k_rk_backward(RankGeom g, uint32_t L, u64
       if (pr != UNDECIDED) {
         word = make_word(pr, 0);  // process.py:120-123
       } else {
-        const uint32_t hvc = g.lvhv[lvoff + blk], ph = g.lvph[lvoff + blk];
+        const uint32_t ph = g.lvph[lvoff + blk];
+        uint32_t cho[kRankMaxCols];
+        {
+          const uint4* cp = reinterpret_cast<const uint4*>(g.lvch + (u64)(lvoff + blk) * kRankMaxCols);
+          const uint4 c0 = cp[0], c1 = cp[1];
+          cho[0] = c0.x, cho[1] = c0.y, cho[2] = c0.z, cho[3] = c0.w;
+          cho[4] = c1.x, cho[5] = c1.y, cho[6] = c1.z, cho[7] = c1.w;
+        }
         const RankHands u = rk_hands(L, (uint32_t)__builtin_popcount(pat), a);
         const bool hasT = fmoves ? u.t1 < (int)kRankHand : u.t2 < (int)kRankHand;
         const bool hasO = fmoves ? u.o1 < (int)kRankHand : u.o2 < (int)kRankHand;
@@ -379,7 +426,7 @@ __global__ __launch_bounds__(256) void k_rk_backward(RankGeom g, uint32_t L, u64
           const uint32_t q = off + h;
           off += h;
           const uint32_t lo = pat & ((1u << q) - 1u), hi = (pat >> q) << (q + 1);
-          const uint32_t cb = (uint32_t)(g.base[col ? hvc + g.stride[x] : hvc] - cstart);
+          const uint32_t cb = cho[x];
           const bool vT = col && hasT, vO = col && hasO;
           w[2 * x] = __builtin_amdgcn_raw_buffer_load_b8(rw, vT ? cb + rowT + (lo | (1u << q) | hi) : 0xFFFFFFFFu, 0, 0);
           w[2 * x + 1] = __builtin_amdgcn_raw_buffer_load_b8(rw, vO ? cb + rowO + (lo | hi) : 0xFFFFFFFFu, 0, 0);
@@ -467,9 +514,10 @@ struct RankShape {
   RankGeom g;
   std::vector<u64> base;                // per hvcode
   std::vector<uint32_t> lvhv, lvph;     // hvcodes level by level, packed heights
+  std::vector<uint32_t> lvch;           // per entry: child block offsets in the next level (RankGeom::lvch)
   std::vector<uint32_t> lvoff;          // per level: first entry in lvhv (T + 1)
   std::vector<u64> lvstart, lvitems;    // per level: first slot, slots
-  u64 words_off, reach_off, expd_off, bstat_off, pbits_off, base_off, lvhv_off, lvph_off, table_bytes;
+  u64 words_off, reach_off, expd_off, bstat_off, pbits_off, base_off, lvhv_off, lvph_off, lvch_off, table_bytes;
 };
 
 static int rank_shape(const Desc* d, RankShape* rs) {
@@ -521,6 +569,12 @@ static int rank_shape(const Desc* d, RankShape* rs) {
   }
   rs->lvoff[g.T] = (uint32_t)rs->lvhv.size();
   rs->lvstart[g.T] = at;
+  rs->lvch.assign(rs->lvhv.size() * kRankMaxCols, 0xFFFFFFFFu);
+  for (uint32_t L = 0; L < g.T; L++)
+    for (uint32_t j = rs->lvoff[L]; j < rs->lvoff[L + 1]; j++)
+      for (uint32_t x = 0; x < g.C; x++)
+        if (((rs->lvph[j] >> (4 * x)) & 15u) < g.H)
+          rs->lvch[(size_t)j * kRankMaxCols + x] = (uint32_t)(rs->base[rs->lvhv[j] + g.stride[x]] - rs->lvstart[L + 1]);
   g.nslots = at;
   rs->words_off = 0;
   rs->reach_off = rup256(at);
@@ -530,7 +584,8 @@ static int rank_shape(const Desc* d, RankShape* rs) {
   rs->base_off = rs->pbits_off + rup256(at / 64);
   rs->lvhv_off = rs->base_off + rup256((u64)nhv * 8);
   rs->lvph_off = rs->lvhv_off + rup256((u64)nhv * 4);
-  rs->table_bytes = rs->lvph_off + rup256((u64)nhv * 4);
+  rs->lvch_off = rs->lvph_off + rup256((u64)nhv * 4);
+  rs->table_bytes = rs->lvch_off + rup256((u64)nhv * 4 * kRankMaxCols);
   return 0;
 }
 
@@ -579,6 +634,7 @@ static int rank_setup(gm_solver* s, const gm_buffers* buf) {
   rs.g.base = (const u64*)(t + rs.base_off);
   rs.g.lvhv = (const uint32_t*)(t + rs.lvhv_off);
   rs.g.lvph = (const uint32_t*)(t + rs.lvph_off);
+  rs.g.lvch = (const uint32_t*)(t + rs.lvch_off);
   rs.g.bstat = (uint8_t*)(t + rs.bstat_off);
   rs.g.pbits = (u64*)(t + rs.pbits_off);
   for (int c = 0; c < 7; c++) {
@@ -590,6 +646,7 @@ static int rank_setup(gm_solver* s, const gm_buffers* buf) {
   HIPCHK(hipMemcpy((void*)rs.g.base, rs.base.data(), rs.base.size() * 8, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy((void*)rs.g.lvhv, rs.lvhv.data(), rs.lvhv.size() * 4, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy((void*)rs.g.lvph, rs.lvph.data(), rs.lvph.size() * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy((void*)rs.g.lvch, rs.lvch.data(), rs.lvch.size() * 4, hipMemcpyHostToDevice));
   s->rg = rs.g;
   s->rlvoff = rs.lvoff;
   s->rlvstart = rs.lvstart;
@@ -649,8 +706,14 @@ static int run_ranked(gm_solver* s, gm_result* out) {
     for (int k = std::max(first, 0); k < std::min(stop, T); k++) {
       const uint32_t L = (uint32_t)k;
       const u64 nreal = s->rlvitems[L] >> 3, nb = (s->rlvstart[L + 1] - s->rlvstart[L]) >> 3;  // boards
-      hipLaunchKernelGGL((k_rk_boards<KIND>), dim3(rank_grid(s, nb)), dim3(256), 0, st, d, g, L, s->rlvstart[L] >> 3,
-                         s->rlvoff[L], nb, nreal);
+      auto boards = [&](auto CH) {
+        constexpr int CC = decltype(CH)::value / 16, HH = decltype(CH)::value % 16;
+        hipLaunchKernelGGL((k_rk_boards<KIND, CC, HH>), dim3(rank_grid(s, nb)), dim3(256), 0, st, d, g, L,
+                           s->rlvstart[L] >> 3, s->rlvoff[L], nb, nreal);
+      };
+      if (g.C == 6 && g.H == 4) boards(std::integral_constant<int, 6 * 16 + 4>());
+      else if (g.C == 5 && g.H == 4) boards(std::integral_constant<int, 5 * 16 + 4>());
+      else boards(std::integral_constant<int, 0>());
       const u64 n = s->rlvstart[L + 1] - s->rlvstart[L];  // 512-padded: every bitmap word written
       if (L >= 6)
         hipLaunchKernelGGL(k_rk_reach, dim3(rank_grid(s, n / 64)), dim3(256), 0, st, g, L, s->rlvstart[L],

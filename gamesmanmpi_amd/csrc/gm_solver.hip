@@ -912,6 +912,8 @@ struct RankGeom {
   const u64* base;         // [R^C] hvcode -> first slot of its block
   const uint32_t* lvhv;    // hvcodes level by level
   const uint32_t* lvph;    // the same, heights packed 4 bits per column
+  const uint32_t* lvch;    // per block entry, kRankMaxCols u32: child block x's first slot - its level's
+                           // first slot (0xFFFFFFFF: column x full)
   uint8_t* bstat;          // [nslots / 8] per board (stacks): primitive value or UNDECIDED
   u64* pbits;              // [nslots / 512] per board: primitive
   u64 le[7];               // bits j < 64 with popcount(j) <= c
