@@ -377,7 +377,16 @@ __global__ __launch_bounds__(256) void k_rk_backward(RankGeom g, uint32_t L, u64
   const bool fmoves = (L & 1u) == 0;  // the first mover moves at even levels
   for (u64 t0 = (u64)blockIdx.x * 256; t0 < nwords; t0 += (u64)gridDim.x * 256) {
     const u64 wi = t0 + threadIdx.x;
-    const u64 m = wi < nwords ? reinterpret_cast<const u64*>(g.reach)[(lvstart >> 6) + wi] : 0ull;
+    // the list holds the EXPANDABLE slots (reached, not primitive: one kind of
+    // work per lane); the reached primitives take their board's value below
+    const u64 m = wi < nwords ? reinterpret_cast<const u64*>(g.expd)[(lvstart >> 6) + wi] : 0ull;
+    const u64 mp = wi < nwords ? reinterpret_cast<const u64*>(g.reach)[(lvstart >> 6) + wi] & ~m : 0ull;
+    for (u64 pm = mp; pm; pm &= pm - 1) {
+      const u64 i = (wi << 6) + (u64)__builtin_ctzll(pm);
+      const u64 blk = i >> (L + 3);
+      const uint32_t pat = (uint32_t)(i & ((1ull << L) - 1));
+      g.words[lvstart + i] = (uint8_t)make_word(g.bstat[(lvstart >> 3) + (blk << L) + pat], 0);  // process.py:120-123
+    }
     // exclusive scan of the popcounts over the workgroup
     const uint32_t c = (uint32_t)__builtin_popcountll(m);
     uint32_t incl = c;
@@ -401,11 +410,8 @@ __global__ __launch_bounds__(256) void k_rk_backward(RankGeom g, uint32_t L, u64
       const u64 slot = lvstart + i;
       const u64 blk = i >> (L + 3);
       const uint32_t a = (uint32_t)((i >> L) & 7u), pat = (uint32_t)(i & ((1ull << L) - 1));
-      const int pr = g.bstat[(lvstart >> 3) + (blk << L) + pat];
       uint32_t word;
-      if (pr != UNDECIDED) {
-        word = make_word(pr, 0);  // process.py:120-123
-      } else {
+      {
         const uint32_t ph = g.lvph[lvoff + blk];
         uint32_t cho[kRankMaxCols];
         {
