@@ -405,13 +405,20 @@ __global__ __launch_bounds__(256) void k_rk_backward(RankGeom g, uint32_t L, u64
     uint32_t at = before + incl - c;
     for (u64 mm = m; mm; mm &= mm - 1) list[at++] = (uint16_t)(threadIdx.x * 64 + __builtin_ctzll(mm));
     __syncthreads();
-    for (uint32_t e = threadIdx.x; e < total; e += 256) {
-      const u64 i = (t0 << 6) + list[e];
-      const u64 slot = lvstart + i;
-      const u64 blk = i >> (L + 3);
-      const uint32_t a = (uint32_t)((i >> L) & 7u), pat = (uint32_t)(i & ((1ull << L) - 1));
-      uint32_t word;
-      {
+    // two entries per pass (e, e + 256): 4C child loads in flight per lane
+    // before any reduction or store
+    for (uint32_t e0 = threadIdx.x; e0 < total; e0 += 512) {
+      uint32_t off2[2][2 * NC], nch2[2];
+      u64 slot2[2];
+      bool live2[2];
+#pragma unroll
+      for (int u = 0; u < 2; u++) {
+        const uint32_t e = e0 + 256u * (uint32_t)u;
+        live2[u] = e < total;
+        const u64 i = (t0 << 6) + list[live2[u] ? e : e0];
+        slot2[u] = lvstart + i;
+        const u64 blk = i >> (L + 3);
+        const uint32_t a = (uint32_t)((i >> L) & 7u), pat = (uint32_t)(i & ((1ull << L) - 1));
         const uint32_t ph = g.lvph[lvoff + blk];
         uint32_t cho[kRankMaxCols];
         {
@@ -420,11 +427,11 @@ __global__ __launch_bounds__(256) void k_rk_backward(RankGeom g, uint32_t L, u64
           cho[0] = c0.x, cho[1] = c0.y, cho[2] = c0.z, cho[3] = c0.w;
           cho[4] = c1.x, cho[5] = c1.y, cho[6] = c1.z, cho[7] = c1.w;
         }
-        const RankHands u = rk_hands(L, (uint32_t)__builtin_popcount(pat), a);
-        const bool hasT = fmoves ? u.t1 < (int)kRankHand : u.t2 < (int)kRankHand;
-        const bool hasO = fmoves ? u.o1 < (int)kRankHand : u.o2 < (int)kRankHand;
+        const RankHands h_ = rk_hands(L, (uint32_t)__builtin_popcount(pat), a);
+        const bool hasT = live2[u] && (fmoves ? h_.t1 < (int)kRankHand : h_.t2 < (int)kRankHand);
+        const bool hasO = live2[u] && (fmoves ? h_.o1 < (int)kRankHand : h_.o2 < (int)kRankHand);
         const uint32_t rowT = (a + (fmoves ? 1u : 0u)) << (L + 1), rowO = a << (L + 1);
-        uint32_t w[2 * NC], nch = 0, off = 0;
+        uint32_t nch = 0, off = 0;
 #pragma unroll
         for (int x = 0; x < NC; x++) {
           const uint32_t h = (ph >> (4 * x)) & 15u;
@@ -432,31 +439,41 @@ __global__ __launch_bounds__(256) void k_rk_backward(RankGeom g, uint32_t L, u64
           const uint32_t q = off + h;
           off += h;
           const uint32_t lo = pat & ((1u << q) - 1u), hi = (pat >> q) << (q + 1);
-          const uint32_t cb = cho[x];
           const bool vT = col && hasT, vO = col && hasO;
-          w[2 * x] = __builtin_amdgcn_raw_buffer_load_b8(rw, vT ? cb + rowT + (lo | (1u << q) | hi) : 0xFFFFFFFFu, 0, 0);
-          w[2 * x + 1] = __builtin_amdgcn_raw_buffer_load_b8(rw, vO ? cb + rowO + (lo | hi) : 0xFFFFFFFFu, 0, 0);
+          off2[u][2 * x] = vT ? cho[x] + rowT + (lo | (1u << q) | hi) : 0xFFFFFFFFu;
+          off2[u][2 * x + 1] = vO ? cho[x] + rowO + (lo | hi) : 0xFFFFFFFFu;
           nch += (uint32_t)vT + (uint32_t)vO;
         }
+        nch2[u] = nch;
+      }
+      uint32_t w2[2][2 * NC];
+#pragma unroll
+      for (int u = 0; u < 2; u++)
+#pragma unroll
+        for (int k = 0; k < 2 * NC; k++) w2[u][k] = __builtin_amdgcn_raw_buffer_load_b8(rw, off2[u][k], 0, 0);
+#pragma unroll
+      for (int u = 0; u < 2; u++) {
         // reference-canonical _res_red / _remote_red over the children (an
-        // absent child reads 0: WIN in 0, changes none of the four)
+        // absent child reads 0: WIN in 0, changes none of the four;
+        // SURVEY §8a A8/A9)
         bool any_loss = false, any_tie = false, any_draw = false;
         uint32_t min_loss = 0xFFFFFFFFu, max_all = 0;
 #pragma unroll
         for (int k = 0; k < 2 * NC; k++) {
-          const uint32_t v = w[k] & 3u, r = w[k] >> 2;
+          const uint32_t v = w2[u][k] & 3u, r = w2[u][k] >> 2;
           any_loss |= v == LOSS;
           min_loss = v == LOSS ? min(min_loss, r) : min_loss;
           any_tie |= v == TIE;
           any_draw |= v == DRAW;
           max_all = max(max_all, r);
         }
-        if (nch == 0) err |= ERR_NO_MOVES;
-        edges += nch;
-        // 
-        word = any_loss ? make_word(WIN, min_loss + 1) : make_word(any_tie ? TIE : any_draw ? DRAW : LOSS, max_all + 1);
+        if (!live2[u]) continue;
+        if (nch2[u] == 0) err |= ERR_NO_MOVES;
+        edges += nch2[u];
+        const uint32_t word =
+            any_loss ? make_word(WIN, min_loss + 1) : make_word(any_tie ? TIE : any_draw ? DRAW : LOSS, max_all + 1);
+        g.words[slot2[u]] = (uint8_t)word;
       }
-      g.words[slot] = (uint8_t)word;
     }
     __syncthreads();  // the list is rewritten by the next tile
   }
