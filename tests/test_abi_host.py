@@ -2,6 +2,7 @@
 header declares, and its HOST-side entry points (codec, the product's own
 descriptors run on the host, md5 owners) agree with the reference's golden
 vectors.  No kernel is launched here."""
+import ctypes
 import json
 import os
 import re
@@ -182,3 +183,42 @@ def test_plan_sizes():
     # step-2 games (sums) never take the bucketed layout
     _lib.check(_lib.load().gm_plan(s.id, 0, _lib.GM_F_FORCE_HASHED, 0, ctypes.byref(p)))
     assert p.mode == _lib.GM_MODE_HASHED
+
+
+@pytest.mark.parametrize("outer,bytes_per_word", [
+    (191, 1),   # root digit sum 253: absolute 8-bit words
+    (192, 1),   # 254: relative 8-bit words (gm_plane.h, word form 3)
+    (443, 1),   # 505 = kPlaneRelMaxSum: the last relative one
+    (444, 2),   # 506: 16-bit words
+])
+def test_planes_word_width_by_root_sum(outer, bytes_per_word):
+    """PLANES words: 8-bit up to root digit sum 505 (absolute forms to 253,
+    relative ones above), 16-bit beyond; GM_F_WORDS16 forces 16-bit."""
+    from gamesmanmpi_amd import _lib
+    from gamesmanmpi_amd.games import GameSpec
+    s = GameSpec("sum_four_to_one", "heaps=31:31:%d" % outer)
+    p = _lib.gm_plan_t()
+    _lib.check(_lib.load().gm_plan(s.id, 0, 0, 0, ctypes.byref(p)))
+    n = 1024 * (outer + 1)
+    assert p.mode == _lib.GM_MODE_PLANES and p.table_slots == n
+    rup = lambda x: (x + 255) // 256 * 256  # noqa: E731
+    assert p.table_bytes == rup(bytes_per_word * n) + rup(n // 8)
+    _lib.check(_lib.load().gm_plan(s.id, 0, _lib.GM_F_WORDS16, 0, ctypes.byref(p)))
+    assert p.table_bytes == rup(2 * n) + rup(n // 8)
+
+
+@pytest.mark.parametrize("world,heaps", [(4, "31:31:31:31:31:127"), (8, "31:31:31:31:31:255")])
+def test_planes_bench_shards_plan_8bit_words(world, heaps):
+    """The 4- and 8-GPU bench shapes (root digit sums 281 / 409) plan 8-bit
+    relative words: a 2^30-position shard's words are 1 GiB, not 2."""
+    from gamesmanmpi_amd import _lib
+    from gamesmanmpi_amd.games import GameSpec
+    s = GameSpec("sum_four_to_one", "heaps=" + heaps)
+    for r in range(world):
+        p = _lib.gm_plan_t()
+        _lib.check(_lib.load().gm_plan_shard(s.id, r, world, 0, 0, ctypes.byref(p)))
+        assert p.mode == _lib.GM_MODE_PLANES and p.table_slots == 1 << 30
+        # 1 GiB of words + 128 MiB of reach bits + the halo slices (2 x 2^15
+        # planes each way, 8-bit): 16-bit words alone would be 2 GiB
+        halo = (1 << 25) * ((r > 0) + (r + 1 < world))
+        assert p.table_bytes == (1 << 30) + (1 << 27) + 2 * halo
