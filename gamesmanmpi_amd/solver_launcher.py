@@ -76,7 +76,7 @@ def build_parser():
                    help="location to store statistics about game",
                    action="store")
     # additions
-    p.add_argument("--layout", choices=["auto", "dense", "bucketed", "hashed", "graph"],
+    p.add_argument("--layout", choices=["auto", "dense", "ranked", "bucketed", "hashed", "graph"],
                    default="auto",
                    help="table layout (DESIGN.md §Layout); graph = host-"
                         "enumerated positions, for files without a descriptor")
@@ -104,12 +104,30 @@ def build_parser():
 DENSE_STEMS = ("four_to_one", "sum_four_to_one")  # rank-indexable descriptors
 
 
-def write_stats(statsdir, rank, spec, solver, result):
-    """<statsdir>/stats/<rank>/solution.npz (+ meta.json)."""
+def ranked_fits(spec, local):
+    """The game has a RANKED plan (toot-and-otto) that fits this GPU's free
+    memory with a margin."""
+    import ctypes
+    from gamesmanmpi_amd import _lib
+    p = _lib.gm_plan_t()
+    if _lib.load().gm_plan(spec.id, 0, 0, 0, ctypes.byref(p)) != 0 or p.mode != _lib.GM_MODE_RANKED:
+        return False
+    import torch
+    free, _ = torch.cuda.mem_get_info(local)
+    return p.table_bytes + p.scratch_bytes < 0.8 * free
+
+
+def write_stats(statsdir, rank, spec, solver, result, world=1):
+    """<statsdir>/stats/<rank>/solution.npz (+ meta.json).  world > 1 with a
+    replicated table (every rank solved the whole game): this rank writes the
+    positions the reference's md5 partition gives it (src/game_state.py:22-30)."""
     import numpy as np
     d = os.path.join(statsdir, "stats", str(rank))
     os.makedirs(d, exist_ok=True)
     keys, val, rem = solver.dump()
+    if world > 1 and getattr(solver, "replicated", False):
+        own = spec.owners_host(keys, world) == rank
+        keys, val, rem = keys[own], val[own], rem[own]
     canon, lens = spec.decode_batch(keys, stride=32)
     np.savez_compressed(os.path.join(d, "solution.npz"), keys=keys,
                         canon=canon, clen=lens, value=val, remoteness=rem)
@@ -215,6 +233,16 @@ def main(argv=None):
             from gamesmanmpi_amd.dist import ShardedSolver
             solver = ShardedSolver(spec, rank, world, device="cuda:%d" % local)
             result = solver.solve()
+        elif args.layout in ("auto", "ranked") and ranked_fits(spec, local):
+            # toot-and-otto: the whole RANKED table fits one GPU (toot 6x4:
+            # 8.9 GB, 17.5 ms) -- every rank solves it and writes the md5
+            # share the reference's partition gives it; sharding it would
+            # exchange every level
+            from gamesmanmpi_amd.solver import Solver
+            solver = Solver(spec, positions=args.positions, device="cuda:%d" % local, layout="ranked")
+            solver.replicated = True
+            result = solver.solve()
+            result.extra.update({"partition": "replicated", "world": world})
         else:
             # the reference's md5 partition, all-to-all per level (keyed.py)
             from gamesmanmpi_amd.keyed import dist_keyed_solve
@@ -255,7 +283,7 @@ def main(argv=None):
                               "layout": result.extra.get("layout"),
                               "ranks": world}), flush=True)
     if args.statsdir:
-        write_stats(args.statsdir, rank, spec, solver, result)
+        write_stats(args.statsdir, rank, spec, solver, result, world)
     if world > 1:
         import torch.distributed as dist
         dist.barrier()

@@ -250,3 +250,31 @@ def test_checkpoint_save_reuses_a_crashed_tmp(tmp_path, monkeypatch):
     with pytest.raises(ck.NotACheckpoint):
         ck.save(solver, d, 3)
     assert (tmp / "notes.txt").read_text() == "mine"
+
+
+def test_replicated_table_writes_each_ranks_md5_share(tmp_path):
+    """Under torchrun a game whose RANKED table fits one GPU is solved whole
+    on every rank; -sd then writes, per rank, the positions the reference's
+    md5 partition gives that rank (src/game_state.py:22-30): the shares are
+    disjoint and cover every position."""
+    import types
+    import numpy as np
+    from gamesmanmpi_amd import solver_launcher as sl
+    from gamesmanmpi_amd.games import GameSpec
+    from oracle.oracle import Game  # checker only
+    params = "length=3,height=3"
+    spec = GameSpec("toot_and_otto_bitstring", params)
+    sol = Game("toot_and_otto_bitstring", params).solve(1 << 20)
+    canon, clen, val, rem = sol.dump(stride=24)
+    keys = spec.encode_batch(canon, clen)
+    fake = types.SimpleNamespace(replicated=True, dump=lambda: (keys, val, rem))
+    res = types.SimpleNamespace(root_line=sol.root_line)
+    world = 3
+    seen = []
+    for r in range(world):
+        sl.write_stats(str(tmp_path), r, spec, fake, res, world)
+        z = np.load(tmp_path / "stats" / str(r) / "solution.npz")
+        assert (spec.owners_host(z["keys"], world) == r).all()
+        seen.append(z["keys"])
+    allk = np.concatenate(seen)
+    assert len(allk) == len(keys) and len(np.unique(allk)) == len(keys)
