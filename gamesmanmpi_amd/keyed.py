@@ -412,12 +412,13 @@ def group_keyed_solve(spec, world, device=None, layout="auto", flags=0, streams=
 
 
 def dist_keyed_solve(spec, device=None, positions=0, stage=None,
-                     layout="auto"):
+                     layout="auto", flags=0):
     """This process's shard of an md5-sharded job over the initialised
     torch.distributed default group; `positions`: bound for the whole job
     (0: the game's own); stage="cpu": collectives through host memory
-    (several ranks sharing one GPU in tests).  Returns (SolveResult,
-    shard)."""
+    (several ranks sharing one GPU in tests); flags: kernel-family flags of
+    the BUCKETED shards (e.g. _lib.GM_F_BKS_LOCAL: every level in the
+    local-dedup form).  Returns (SolveResult, shard)."""
     import torch.distributed as dist
     spec = spec if isinstance(spec, GameSpec) else GameSpec(*spec)
     world = dist.get_world_size()
@@ -425,7 +426,7 @@ def dist_keyed_solve(spec, device=None, positions=0, stage=None,
         from .dist import ShardedSolver
         shard = ShardedSolver(spec, dist.get_rank(), world, device=device,
                               transport="host" if stage == "cpu" else "rccl",
-                              layout="bucketed",
+                              layout="bucketed", flags=flags,
                               positions=_shard_bound(spec, world, positions))
         res = shard.solve()
         res.extra.update({"partition": "md5", "world": world})

@@ -134,7 +134,7 @@ def test_gpu_keyed_shard_refuses_whole_solve():
         sh.solver.solve()
 
 
-def _dist_worker(rank, world, port, q, name):
+def _dist_worker(rank, world, port, q, name, flags=0):
     import os
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
@@ -143,7 +143,7 @@ def _dist_worker(rank, world, port, q, name):
         from gamesmanmpi_amd.games import GameSpec
         from gamesmanmpi_amd.keyed import dist_keyed_solve
         spec = GameSpec(*CASES[name])
-        r, shard = dist_keyed_solve(spec, device="cuda:0", stage="cpu")
+        r, shard = dist_keyed_solve(spec, device="cuda:0", stage="cpu", flags=flags)
         keys, val, rem = shard.dump()
         q.put((rank, (r.positions, r.edges, r.primitives, r.root_line),
                keys, val, rem))
@@ -151,8 +151,8 @@ def _dist_worker(rank, world, port, q, name):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name", ["othello_4x4", "toot_4x3"])
-def test_gpu_keyed_two_processes_torch_exchange(name, golden_summary):
+@pytest.mark.parametrize("name,flags", [("othello_4x4", 0), ("toot_4x3", 0), ("toot_4x3", LOCAL)])
+def test_gpu_keyed_two_processes_torch_exchange(name, flags, golden_summary):
     """The one-process-per-rank path (the code the launcher runs under
     torchrun): md5-sharded BUCKETED shards (ShardedSolver; the library's
     level loop with the host-staged transport over gloo here, RCCL send /
@@ -166,7 +166,7 @@ def test_gpu_keyed_two_processes_torch_exchange(name, golden_summary):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_dist_worker, args=(r, 2, port, q, name)) for r in range(2)]
+    procs = [ctx.Process(target=_dist_worker, args=(r, 2, port, q, name, flags)) for r in range(2)]
     for p in procs:
         p.start()
     out = collect_workers(q, procs, 2, limit=150)
