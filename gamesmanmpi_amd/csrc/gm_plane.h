@@ -418,6 +418,190 @@ __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
   return __builtin_amdgcn_perm(hi, lo, sel);
 }
 
+// One visit: planes ex / ey resolved by one wave (the lower / upper half
+// wave each holds one plane's 32 rows).  A function of its own, not a
+// lambda inside the list loop: the lambda form cost the NO = 4 kernel 12
+// VGPRs (119 -> 131, one wave per SIMD less).
+template <int WB, int NO, bool SH, int RS_, bool UNR = true>
+__device__ __forceinline__ void plane_x2_visit(typename PlaneWord<WB>::T* __restrict__ tab, const PlaneGeom& g,
+                                               const uint4* __restrict__ zero,
+                                               const typename PlaneWord<WB>::T* __restrict__ recv,
+                                               typename PlaneWord<WB>::T* __restrict__ send, const PlaneEntry ex,
+                                               const PlaneEntry ey, const bool livex, const bool livey) {
+  typedef PlaneWord<WB> W;
+  typedef typename W::T T;
+  constexpr int DW = W::DW, NQ = DW / 4;
+  constexpr bool B8 = DW == 8, REL = WB == 3;
+  const uint32_t L = threadIdx.x & 31;
+  constexpr int B0 = (4 - RS_) & 3;  // relative: row bytes j = B0 mod 4 are parents with d % 4 == 0
+  uint32_t dx[NO > 0 ? NO : 1], dy[NO > 0 ? NO : 1];
+  plane_digits<NO>(g, ex.p, dx);
+  plane_digits<NO>(g, ey.p, dy);
+  const size_t ox = (size_t)ex.p * 1024u + L * 32u, oy = (size_t)ey.p * 1024u + L * 32u;
+  // E rows of both planes (8-bit: odd bytes exact in Ehi, even bytes in
+  // the high bytes of Elo; 16-bit: Ehi exact)
+  uint32_t Xh[DW], Xl[B8 ? DW : 1], Yh[DW], Yl[B8 ? DW : 1];
+#pragma unroll
+  for (int d = 0; d < DW; d++) {
+    Xh[d] = Yh[d] = 0;
+    if (B8) Xl[d] = Yl[d] = 0;
+  }
+  auto nb = [&](const PlaneEntry& e, const uint32_t* dig, size_t off, int j, int k) -> const uint4* {
+    if (SH && j == NO - 1) {
+      const uint32_t w = k == 1 ? e.top1 : e.top2;
+      return w == kPlaneAbsent ? zero
+             : w == kPlaneLocal ? (const uint4*)(tab + off - (size_t)k * g.Z * 1024u)
+                                : (const uint4*)(recv + (size_t)w * 1024u + L * 32u);
+    }
+    return dig[j] >= (uint32_t)k ? (const uint4*)(tab + off - (size_t)k * g.stride[j] * 1024u) : zero;
+  };
+  auto fold = [&](int j, int k) {
+    const uint4* sx = nb(ex, dx, ox, j, k);
+    const uint4* sy = nb(ey, dy, oy, j, k);
+    uint4 vx[NQ], vy[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; q++) {
+      vx[q] = sx[q];
+      vy[q] = sy[q];
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; q++) {
+      const uint32_t a[4] = {vx[q].x, vx[q].y, vx[q].z, vx[q].w};
+      const uint32_t b[4] = {vy[q].x, vy[q].y, vy[q].z, vy[q].w};
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        Xh[4 * q + c] = pk_max16(Xh[4 * q + c], a[c]);
+        Yh[4 * q + c] = pk_max16(Yh[4 * q + c], b[c]);
+        if (B8) {
+          Xl[4 * q + c] = pk_max16(Xl[4 * q + c], pk_shl8(a[c]));
+          Yl[4 * q + c] = pk_max16(Yl[4 * q + c], pk_shl8(b[c]));
+        }
+      }
+    }
+  };
+  if constexpr (REL) {
+    // children at d - 2 first, then their frame shift -- ONCE on the
+    // folded maxima (the shift is monotone: it commutes with max), on the
+    // one split array whose high bytes hold row bytes B0 mod 4 (Xh: odd
+    // bytes, Xl: even ones), half B0 / 2 of every dword -- then the
+    // children at d - 1
+#pragma unroll
+    for (int j = 0; j < NO; j++) fold(j, 2);
+#pragma unroll
+    for (int d = 0; d < DW; d++) {
+      if (B0 & 1) {
+        Xh[d] = rel_shift_byte<2 * (B0 >> 1) + 1>(Xh[d]);
+        Yh[d] = rel_shift_byte<2 * (B0 >> 1) + 1>(Yh[d]);
+      } else {
+        Xl[d] = rel_shift_byte<2 * (B0 >> 1) + 1>(Xl[d]);
+        Yl[d] = rel_shift_byte<2 * (B0 >> 1) + 1>(Yl[d]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NO; j++) fold(j, 1);
+  } else {
+#pragma unroll
+    for (int j = 0; j < NO; j++) {
+#pragma unroll
+      for (int k = 1; k <= 2; k++) fold(j, k);
+    }
+  }
+  const uint32_t primv =
+      (g.rank == 0 && L == 0) ? ((ex.p == 0 ? W::kPrim : 0u) | (ey.p == 0 ? W::kPrim << 16 : 0u)) : 0u;
+  // step q's results of both planes stay packed [X | Y] in op[q] (OR of
+  // the two phases: an idle lane contributes 0) and are unpacked into the
+  // two rows once, after the wavefront
+  // The step chain (lean form, round 4: backward 1.624 -> 1.540 ms per
+  // 2^30 in tools/plane_lab, bit-exact): the children that are ready a
+  // step early -- the E byte, this row's h0 - 2 result, the h1 - 2 row's
+  // -- are folded off the chain, so cur -> (lane below) -> max -> parent
+  // -> active mask is the whole dependency per step.  No lane-32 masks:
+  // the upper pair's row 0 (lane 32) reads lane 31 (the lower pair's row
+  // 31) only at steps <= 31, where row 31 is still idle and holds 0, and
+  // row 1 reads lane 31's u1 of step <= 30, also 0.  Active rows: bit q of
+  // A, one bit extract per step (phase 0: rows 0..q; phase 1: q+1..31).
+  uint32_t cur = 0, prev = 0, u1p = 0;
+  uint32_t op[32];
+  const uint32_t A0 = ~0u << L;  // bit q set: row L is active at step q of phase 0
+  // both phases unrolled (phase 0 assigns op[q], phase 1 ORs into it):
+  // 1.549 -> 1.512 ms per 2^30 backward in tools/plane_lab (var 30), 98
+  // VGPRs in the lab form against 119 for a rolled phase loop
+  // (UNR false, the per-visit RS dispatch: a rolled phase loop, so the
+  // kernel's four visit bodies stay within the instruction cache)
+  auto phase = [&](auto PHc) {
+    const int PH = PHc;  // a constant when unrolled
+    const uint32_t A = PH ? ~A0 : A0;
+#pragma unroll
+    for (int q = 0; q < 32; q++) {
+      uint32_t a;
+      if (B8) {
+        // byte q of X's and Y's E rows -> [X, 0, Y, 0]
+        const int d = q >> 2, b = q & 3;
+        const uint32_t bx = (b & 1) ? (uint32_t)b : (uint32_t)b + 1;  // byte inside the split dword
+        const uint32_t sel = 0x0C000C00u | ((4u + bx) << 16) | bx;     // hi = Y (bytes 4-7), lo = X
+        a = (b & 1) ? perm(Yh[d], Xh[d], sel) : perm(Yl[d], Xl[d], sel);
+      } else {
+        const int d = q >> 1, h = q & 1;
+        const uint32_t b0 = 2 * h;
+        const uint32_t sel = ((5u + b0) << 24) | ((4u + b0) << 16) | ((1u + b0) << 8) | b0;
+        a = perm(Yh[d], Xh[d], sel);
+      }
+      const uint32_t u2r = from_lane_below(u1p);
+      const int dcls = (RS_ + q) & 3;  // relative forms: d % 4 of this step's positions (32 = 0 mod 4)
+      const uint32_t pre = REL && dcls == 0 ? pk_max16(a, rel_shift_pk(pk_max16(prev, u2r)))
+                                            : pk_max16(pk_max16(a, prev), u2r);
+      const uint32_t u1r = from_lane_below(cur);
+      const uint32_t m = pk_max16(pk_max16(pre, cur), u1r);
+      uint32_t f = (REL && dcls == 3 ? parent_rel_up(m) : parent_x2<WB == 2 ? 2 : 1>(m)) &
+                   (uint32_t)__builtin_amdgcn_sbfe((int)A, q, 1);
+      if (q == 0) f = pk_max16(f, PH ? 0u : primv);
+      if (UNR && PH == 0) op[q] = f;
+      else op[q] |= f;
+      prev = cur;
+      cur = f;
+      u1p = u1r;
+    }
+  };
+  if constexpr (UNR) {
+    phase(std::integral_constant<int, 0>());
+    phase(std::integral_constant<int, 1>());
+  } else {
+#pragma unroll
+    for (int q = 0; q < 32; q++) op[q] = 0;
+#pragma unroll 1
+    for (int ph = 0; ph < 2; ph++) phase(ph);
+  }
+  uint32_t ox_[DW], oy_[DW];
+  if (B8) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t t1 = perm(op[4 * k + 1], op[4 * k], 0x06020400u);      // [X0 X1 Y0 Y1]
+      const uint32_t t2 = perm(op[4 * k + 3], op[4 * k + 2], 0x06020400u);  // [X2 X3 Y2 Y3]
+      ox_[k] = perm(t2, t1, 0x05040100u);
+      oy_[k] = perm(t2, t1, 0x07060302u);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      ox_[k] = perm(op[2 * k + 1], op[2 * k], 0x05040100u);
+      oy_[k] = perm(op[2 * k + 1], op[2 * k], 0x07060302u);
+    }
+  }
+  auto store = [&](T* dst, const uint32_t* o) {
+    uint4* p = (uint4*)dst;
+#pragma unroll
+    for (int q = 0; q < NQ; q++) p[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+  };
+  if (livex) {
+    store(tab + ox, ox_);
+    if (SH && ex.send != kPlaneAbsent) store(send + (size_t)ex.send * 1024u + L * 32u, ox_);
+  }
+  if (livey) {
+    store(tab + oy, oy_);
+    if (SH && ey.send != kPlaneAbsent) store(send + (size_t)ey.send * 1024u + L * 32u, oy_);
+  }
+}
+
 // (RS: with WB = 3, the launch's outer digit sum s mod 4; -1: per wave
 // visit, from its first plane -- the list deals every four consecutive
 // entries one s mod 4, padding with kPlaneAbsent entries)
@@ -427,11 +611,7 @@ __device__ __forceinline__ void plane_x2_range(typename PlaneWord<WB>::T* __rest
                                                const PlaneGeom& g, const uint4* __restrict__ zero,
                                                const typename PlaneWord<WB>::T* __restrict__ recv,
                                                typename PlaneWord<WB>::T* __restrict__ send) {
-  typedef PlaneWord<WB> W;
-  typedef typename W::T T;
-  constexpr int DW = W::DW, NQ = DW / 4;
-  constexpr bool B8 = DW == 8, REL = WB == 3;
-  const uint32_t lane = threadIdx.x & 63, L = lane & 31;
+  const uint32_t lane = threadIdx.x & 63;
   for (uint32_t i0 = sh.first; i0 < sh.end; i0 += sh.stride) {
     const uint32_t ix = i0 + 2 * (lane >> 5), iy = ix + 1;
     bool livex = ix < sh.end, livey = iy < sh.end;
@@ -448,175 +628,18 @@ __device__ __forceinline__ void plane_x2_range(typename PlaneWord<WB>::T* __rest
       ex.p = ((const uint32_t*)list)[livex ? ix : i0];
       ey.p = ((const uint32_t*)list)[livey ? iy : i0];
     }
-    auto visit = [&](auto RSc) {
-    constexpr int RS_ = decltype(RSc)::value;
-    constexpr int B0 = (4 - RS_) & 3;  // relative: row bytes j = B0 mod 4 are parents with d % 4 == 0
-    uint32_t dx[NO > 0 ? NO : 1], dy[NO > 0 ? NO : 1];
-    plane_digits<NO>(g, ex.p, dx);
-    plane_digits<NO>(g, ey.p, dy);
-    const size_t ox = (size_t)ex.p * 1024u + L * 32u, oy = (size_t)ey.p * 1024u + L * 32u;
-    // E rows of both planes (8-bit: odd bytes exact in Ehi, even bytes in
-    // the high bytes of Elo; 16-bit: Ehi exact)
-    uint32_t Xh[DW], Xl[B8 ? DW : 1], Yh[DW], Yl[B8 ? DW : 1];
-#pragma unroll
-    for (int d = 0; d < DW; d++) {
-      Xh[d] = Yh[d] = 0;
-      if (B8) Xl[d] = Yl[d] = 0;
-    }
-    auto nb = [&](const PlaneEntry& e, const uint32_t* dig, size_t off, int j, int k) -> const uint4* {
-      if (SH && j == NO - 1) {
-        const uint32_t w = k == 1 ? e.top1 : e.top2;
-        return w == kPlaneAbsent ? zero
-               : w == kPlaneLocal ? (const uint4*)(tab + off - (size_t)k * g.Z * 1024u)
-                                  : (const uint4*)(recv + (size_t)w * 1024u + L * 32u);
-      }
-      return dig[j] >= (uint32_t)k ? (const uint4*)(tab + off - (size_t)k * g.stride[j] * 1024u) : zero;
-    };
-    auto fold = [&](int j, int k) {
-      const uint4* sx = nb(ex, dx, ox, j, k);
-      const uint4* sy = nb(ey, dy, oy, j, k);
-      uint4 vx[NQ], vy[NQ];
-#pragma unroll
-      for (int q = 0; q < NQ; q++) {
-        vx[q] = sx[q];
-        vy[q] = sy[q];
-      }
-#pragma unroll
-      for (int q = 0; q < NQ; q++) {
-        const uint32_t a[4] = {vx[q].x, vx[q].y, vx[q].z, vx[q].w};
-        const uint32_t b[4] = {vy[q].x, vy[q].y, vy[q].z, vy[q].w};
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-          Xh[4 * q + c] = pk_max16(Xh[4 * q + c], a[c]);
-          Yh[4 * q + c] = pk_max16(Yh[4 * q + c], b[c]);
-          if (B8) {
-            Xl[4 * q + c] = pk_max16(Xl[4 * q + c], pk_shl8(a[c]));
-            Yl[4 * q + c] = pk_max16(Yl[4 * q + c], pk_shl8(b[c]));
-          }
-        }
-      }
-    };
-    if constexpr (REL) {
-      // children at d - 2 first, then their frame shift -- ONCE on the
-      // folded maxima (the shift is monotone: it commutes with max), on the
-      // one split array whose high bytes hold row bytes B0 mod 4 (Xh: odd
-      // bytes, Xl: even ones), half B0 / 2 of every dword -- then the
-      // children at d - 1
-#pragma unroll
-      for (int j = 0; j < NO; j++) fold(j, 2);
-#pragma unroll
-      for (int d = 0; d < DW; d++) {
-        if (B0 & 1) {
-          Xh[d] = rel_shift_byte<2 * (B0 >> 1) + 1>(Xh[d]);
-          Yh[d] = rel_shift_byte<2 * (B0 >> 1) + 1>(Yh[d]);
-        } else {
-          Xl[d] = rel_shift_byte<2 * (B0 >> 1) + 1>(Xl[d]);
-          Yl[d] = rel_shift_byte<2 * (B0 >> 1) + 1>(Yl[d]);
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < NO; j++) fold(j, 1);
-    } else {
-#pragma unroll
-      for (int j = 0; j < NO; j++) {
-#pragma unroll
-        for (int k = 1; k <= 2; k++) fold(j, k);
-      }
-    }
-    const uint32_t primv =
-        (g.rank == 0 && L == 0) ? ((ex.p == 0 ? W::kPrim : 0u) | (ey.p == 0 ? W::kPrim << 16 : 0u)) : 0u;
-    // step q's results of both planes stay packed [X | Y] in op[q] (OR of
-    // the two phases: an idle lane contributes 0) and are unpacked into the
-    // two rows once, after the wavefront
-    // The step chain (lean form, round 4: backward 1.624 -> 1.540 ms per
-    // 2^30 in tools/plane_lab, bit-exact): the children that are ready a
-    // step early -- the E byte, this row's h0 - 2 result, the h1 - 2 row's
-    // -- are folded off the chain, so cur -> (lane below) -> max -> parent
-    // -> active mask is the whole dependency per step.  No lane-32 masks:
-    // the upper pair's row 0 (lane 32) reads lane 31 (the lower pair's row
-    // 31) only at steps <= 31, where row 31 is still idle and holds 0, and
-    // row 1 reads lane 31's u1 of step <= 30, also 0.  Active rows: bit q of
-    // A, one bit extract per step (phase 0: rows 0..q; phase 1: q+1..31).
-    uint32_t cur = 0, prev = 0, u1p = 0;
-    uint32_t op[32];
-#pragma unroll
-    for (int q = 0; q < 32; q++) op[q] = 0;
-    const uint32_t A0 = ~0u << L;  // bit q set: row L is active at step q of phase 0
-#pragma unroll 1
-    for (uint32_t ph = 0; ph < 2; ph++) {
-      const uint32_t A = ph ? ~A0 : A0;
-#pragma unroll
-      for (int q = 0; q < 32; q++) {
-        uint32_t a;
-        if (B8) {
-          // byte q of X's and Y's E rows -> [X, 0, Y, 0]
-          const int d = q >> 2, b = q & 3;
-          const uint32_t bx = (b & 1) ? (uint32_t)b : (uint32_t)b + 1;  // byte inside the split dword
-          const uint32_t sel = 0x0C000C00u | ((4u + bx) << 16) | bx;     // hi = Y (bytes 4-7), lo = X
-          a = (b & 1) ? perm(Yh[d], Xh[d], sel) : perm(Yl[d], Xl[d], sel);
-        } else {
-          const int d = q >> 1, h = q & 1;
-          const uint32_t b0 = 2 * h;
-          const uint32_t sel = ((5u + b0) << 24) | ((4u + b0) << 16) | ((1u + b0) << 8) | b0;
-          a = perm(Yh[d], Xh[d], sel);
-        }
-        const uint32_t u2r = from_lane_below(u1p);
-        const int dcls = (RS_ + q) & 3;  // relative forms: d % 4 of this step's positions
-        const uint32_t pre = REL && dcls == 0 ? pk_max16(a, rel_shift_pk(pk_max16(prev, u2r)))
-                                              : pk_max16(pk_max16(a, prev), u2r);
-        const uint32_t u1r = from_lane_below(cur);
-        const uint32_t m = pk_max16(pk_max16(pre, cur), u1r);
-        const uint32_t keep = (uint32_t)__builtin_amdgcn_sbfe((int)A, q, 1);
-        uint32_t f = (REL && dcls == 3 ? parent_rel_up(m) : parent_x2<WB == 2 ? 2 : 1>(m)) & keep;
-        if (q == 0) f = pk_max16(f, ph ? 0u : primv);
-        op[q] |= f;
-        prev = cur;
-        cur = f;
-        u1p = u1r;
-      }
-    }
-    uint32_t ox_[DW], oy_[DW];
-    if (B8) {
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const uint32_t t1 = perm(op[4 * k + 1], op[4 * k], 0x06020400u);      // [X0 X1 Y0 Y1]
-        const uint32_t t2 = perm(op[4 * k + 3], op[4 * k + 2], 0x06020400u);  // [X2 X3 Y2 Y3]
-        ox_[k] = perm(t2, t1, 0x05040100u);
-        oy_[k] = perm(t2, t1, 0x07060302u);
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < 16; k++) {
-        ox_[k] = perm(op[2 * k + 1], op[2 * k], 0x05040100u);
-        oy_[k] = perm(op[2 * k + 1], op[2 * k], 0x07060302u);
-      }
-    }
-    auto store = [&](T* dst, const uint32_t* o) {
-      uint4* p = (uint4*)dst;
-#pragma unroll
-      for (int q = 0; q < NQ; q++) p[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
-    };
-    if (livex) {
-      store(tab + ox, ox_);
-      if (SH && ex.send != kPlaneAbsent) store(send + (size_t)ex.send * 1024u + L * 32u, ox_);
-    }
-    if (livey) {
-      store(tab + oy, oy_);
-      if (SH && ey.send != kPlaneAbsent) store(send + (size_t)ey.send * 1024u + L * 32u, oy_);
-    }
-    };
     if constexpr (RS >= 0) {
-      visit(std::integral_constant<int, RS>());
+      plane_x2_visit<WB, NO, SH, RS>(tab, g, zero, recv, send, ex, ey, livex, livey);
     } else {  // the visit's outer digit sum (global digits) mod 4, wave-uniform
       uint32_t dg[NO > 0 ? NO : 1], sum = 0;
       plane_global_digits<NO>(g, ex.p, dg);
 #pragma unroll
       for (int j = 0; j < NO; j++) sum += dg[j];
       switch (__builtin_amdgcn_readfirstlane(sum) & 3u) {
-        case 0: visit(std::integral_constant<int, 0>()); break;
-        case 1: visit(std::integral_constant<int, 1>()); break;
-        case 2: visit(std::integral_constant<int, 2>()); break;
-        default: visit(std::integral_constant<int, 3>()); break;
+        case 0: plane_x2_visit<WB, NO, SH, 0, false>(tab, g, zero, recv, send, ex, ey, livex, livey); break;
+        case 1: plane_x2_visit<WB, NO, SH, 1, false>(tab, g, zero, recv, send, ex, ey, livex, livey); break;
+        case 2: plane_x2_visit<WB, NO, SH, 2, false>(tab, g, zero, recv, send, ex, ey, livex, livey); break;
+        default: plane_x2_visit<WB, NO, SH, 3, false>(tab, g, zero, recv, send, ex, ey, livex, livey); break;
       }
     }
   }

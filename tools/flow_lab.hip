@@ -56,7 +56,9 @@ constexpr uint32_t kSpinLimit = 1u << 21;  // passes of ~0.1 us: a stuck wave gi
 
 // ST: 1 write-through (sc1) stores; 0 plain stores (timing only: not a
 // valid hand-off).  TR: s_memtime stamps of each wave's first 16 items.
-template <int NO, int LD, int ST = 1, bool TR = false>
+// LEVEL: one launch per plane level instead (items = the level's planes in
+// groups of 4, dealt by plane_share as the product does; no flags).
+template <int NO, int LD, int ST = 1, bool TR = false, bool LEVEL = false>
 __global__ __launch_bounds__(256) void k_flow(uint8_t* __restrict__ tab, const uint32_t* __restrict__ items,
                                               uint32_t nitems, uint32_t W, uint32_t* __restrict__ flags,
                                               uint32_t* __restrict__ tmo, PlaneGeom g, const uint4* __restrict__ zero,
@@ -68,14 +70,15 @@ __global__ __launch_bounds__(256) void k_flow(uint8_t* __restrict__ tab, const u
   const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(tab, 0, tabbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc((void*)zero, 0, 4096, 0x00020000);
   constexpr int AUX = LD == 1 ? 16 : LD == 2 ? 17 : 0;
-  for (uint32_t it = w; it < nitems; it += W, nit++) {
+  const PlaneShare shr = plane_share(nitems, 1);
+  for (uint32_t it = LEVEL ? shr.first : w; it < (LEVEL ? shr.end : nitems); it += LEVEL ? shr.stride : W, nit++) {
     if (TR) t0 = __builtin_amdgcn_s_memtime();
     const uint32_t* ip = items + (size_t)it * 4;
     // the wave's four planes: [X0, Y0] on lanes 0-31, [X1, Y1] on 32-63
     const uint32_t px = ip[2 * (lane >> 5)], py = ip[2 * (lane >> 5) + 1];
     const bool livex = px != kNone, livey = py != kNone;
     // dependency wait: lane l < 8 NO polls neighbour (l % (2 NO)) of plane l / (2 NO)
-    {
+    if constexpr (!LEVEL) {
       uint32_t nbp = kNone;
       if (lane < 8 * NO) {
         const uint32_t pq = ip[lane / (2 * NO)], n = lane % (2 * NO), j = n >> 1, k = (n & 1) + 1;
@@ -182,7 +185,7 @@ __global__ __launch_bounds__(256) void k_flow(uint8_t* __restrict__ tab, const u
     }
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
     if (TR) t3 = __builtin_amdgcn_s_memtime() + (ox_[0] & oy_[7] & 0 ? 1 : 0);
-    constexpr int SAUX = ST == 1 ? 16 : 0;
+    constexpr int SAUX = ST == 1 ? 16 : ST == 2 ? 2 : 0;
     if (livex) {
       __builtin_amdgcn_raw_buffer_store_b128((v4u){ox_[0], ox_[1], ox_[2], ox_[3]}, rt, ox, 0, SAUX);
       __builtin_amdgcn_raw_buffer_store_b128((v4u){ox_[4], ox_[5], ox_[6], ox_[7]}, rt, ox + 16, 0, SAUX);
@@ -191,6 +194,7 @@ __global__ __launch_bounds__(256) void k_flow(uint8_t* __restrict__ tab, const u
       __builtin_amdgcn_raw_buffer_store_b128((v4u){oy_[0], oy_[1], oy_[2], oy_[3]}, rt, oy, 0, SAUX);
       __builtin_amdgcn_raw_buffer_store_b128((v4u){oy_[4], oy_[5], oy_[6], oy_[7]}, rt, oy + 16, 0, SAUX);
     }
+    if (LEVEL) continue;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every lane's rows written through before any flag
     if (TR && nit < 16 && lane == 0) {
       const uint64_t t4 = __builtin_amdgcn_s_memtime();
@@ -318,6 +322,26 @@ int main(int argc, char** argv) {
       }
     }
   };
+  auto run_level_lab = [&](int v) {  // per-level launches of the lab body: 6 plain, 7 sc1, 8 nt stores
+    for (int s = 0; s <= S; s++) {
+      const uint32_t ng = (off[s + 1] - off[s]) / 4;
+      uint32_t b = (ng + 3) / 4;
+      b = std::min<uint32_t>((b + 7) / 8 * 8, (uint32_t)cus * 32);
+      const uint32_t* l = dlist + off[s];
+      auto go = [&](auto NOc) {
+        constexpr int NO = decltype(NOc)::value;
+        if (v == 6) hipLaunchKernelGGL((k_flow<NO, 3, 0, false, true>), dim3(b), dim3(256), 0, st, tab, l, ng, 0u, flags, tmo, g, (const uint4*)zero, (uint32_t)tbytes, (uint64_t*)nullptr);
+        else if (v == 7) hipLaunchKernelGGL((k_flow<NO, 3, 1, false, true>), dim3(b), dim3(256), 0, st, tab, l, ng, 0u, flags, tmo, g, (const uint4*)zero, (uint32_t)tbytes, (uint64_t*)nullptr);
+        else hipLaunchKernelGGL((k_flow<NO, 3, 2, false, true>), dim3(b), dim3(256), 0, st, tab, l, ng, 0u, flags, tmo, g, (const uint4*)zero, (uint32_t)tbytes, (uint64_t*)nullptr);
+      };
+      switch (K) {
+        case 3: go(std::integral_constant<int, 1>()); break;
+        case 4: go(std::integral_constant<int, 2>()); break;
+        case 5: go(std::integral_constant<int, 3>()); break;
+        default: go(std::integral_constant<int, 4>()); break;
+      }
+    }
+  };
   auto run_flow = [&](int v) {
     CK(hipMemsetAsync(flags, 0, np * 4 + 256, st));
     auto go = [&](auto NOc) {
@@ -348,6 +372,9 @@ int main(int argc, char** argv) {
     if (var == 0) {
       CK(hipEventRecord(e0, st));
       run_levels();
+    } else if (var >= 6) {
+      CK(hipEventRecord(e0, st));
+      run_level_lab(var);
     } else {
       CK(hipMemsetAsync(flags, 0, np * 4 + 256, st));
       CK(hipEventRecord(e0, st));
@@ -359,7 +386,7 @@ int main(int argc, char** argv) {
     float ms;
     CK(hipEventElapsedTime(&ms, e0, e1));
     if (r) ts.push_back(ms);
-    if (var != 0) {
+    if (var != 0 && var < 6) {
       uint32_t t = 0;
       CK(hipMemcpy(&t, tmo, 4, hipMemcpyDeviceToHost));
       if (t) {

@@ -228,6 +228,111 @@ __global__ __launch_bounds__(256, MINW) void lab_x2(uint8_t* __restrict__ tab, c
   }
 }
 
+// Lab form with both phases unrolled (MODE 0: the lean chain, phase 0
+// assigns op[q] instead of OR-ing into it) and (MODE 1) the active-row mask
+// as ONE v_cndmask per step against a per-step constant lane mask in SGPRs
+// instead of a per-lane bit extract + and.
+template <int NO, int MODE>
+__global__ __launch_bounds__(256) void lab_x2u(uint8_t* __restrict__ tab, const uint32_t* __restrict__ list, uint32_t n,
+                                               PlaneGeom g, const uint4* __restrict__ zero) {
+  const PlaneShare sh = plane_share(n, 4);
+  const uint32_t lane = threadIdx.x & 63, L = lane & 31;
+  for (uint32_t i0 = sh.first; i0 < sh.end; i0 += sh.stride) {
+    const uint32_t ix = i0 + 2 * (lane >> 5), iy = ix + 1;
+    const bool livex = ix < sh.end, livey = iy < sh.end;
+    const uint32_t px = list[livex ? ix : i0], py = list[livey ? iy : i0];
+    uint32_t dx[NO], dy[NO];
+    plane_digits<NO>(g, px, dx);
+    plane_digits<NO>(g, py, dy);
+    const size_t ox = (size_t)px * 1024u + L * 32u, oy = (size_t)py * 1024u + L * 32u;
+    uint32_t Xh[8], Xl[8], Yh[8], Yl[8];
+#pragma unroll
+    for (int d = 0; d < 8; d++) Xh[d] = Yh[d] = Xl[d] = Yl[d] = 0;
+#pragma unroll
+    for (int j = 0; j < NO; j++) {
+#pragma unroll
+      for (int k = 1; k <= 2; k++) {
+        const uint4* sx = dx[j] >= (uint32_t)k ? (const uint4*)(tab + ox - (size_t)k * g.stride[j] * 1024u) : zero;
+        const uint4* sy = dy[j] >= (uint32_t)k ? (const uint4*)(tab + oy - (size_t)k * g.stride[j] * 1024u) : zero;
+        uint4 vx[2], vy[2];
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+          vx[q] = sx[q];
+          vy[q] = sy[q];
+        }
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+          const uint32_t a[4] = {vx[q].x, vx[q].y, vx[q].z, vx[q].w};
+          const uint32_t b[4] = {vy[q].x, vy[q].y, vy[q].z, vy[q].w};
+#pragma unroll
+          for (int c = 0; c < 4; c++) {
+            Xh[4 * q + c] = pk_max16(Xh[4 * q + c], a[c]);
+            Yh[4 * q + c] = pk_max16(Yh[4 * q + c], b[c]);
+            Xl[4 * q + c] = pk_max16(Xl[4 * q + c], pk_shl8(a[c]));
+            Yl[4 * q + c] = pk_max16(Yl[4 * q + c], pk_shl8(b[c]));
+          }
+        }
+      }
+    }
+    const uint32_t primv = L == 0 ? ((px == 0 ? 0xFFu : 0u) | (py == 0 ? 0xFFu << 16 : 0u)) : 0u;
+    uint32_t cur = 0, prev = 0, u1p = 0;
+    uint32_t op[32];
+    const uint32_t A0 = ~0u << L;
+    auto phase = [&](auto PHc) {
+      constexpr int PH = decltype(PHc)::value;
+      const uint32_t A = PH ? ~A0 : A0;
+#pragma unroll
+      for (int q = 0; q < 32; q++) {
+        const int d = q >> 2, b = q & 3;
+        const uint32_t bx = (b & 1) ? (uint32_t)b : (uint32_t)b + 1;
+        const uint32_t sel = 0x0C000C00u | ((4u + bx) << 16) | bx;
+        const uint32_t a = (b & 1) ? perm(Yh[d], Xh[d], sel) : perm(Yl[d], Xl[d], sel);
+        const uint32_t u2r = from_lane_below(u1p);
+        const uint32_t pre = pk_max16(pk_max16(a, prev), u2r);
+        const uint32_t u1r = from_lane_below(cur);
+        const uint32_t m = pk_max16(pk_max16(pre, cur), u1r);
+        uint32_t f = parent_x2<1>(m);
+        if (MODE == 1) {
+          // lanes active at step q: phase 0 rows 0..q, phase 1 rows q+1..31, in both halves
+          const uint32_t m32 = q == 31 ? 0xFFFFFFFFu : ((2u << q) - 1u);
+          const uint64_t mk = PH ? ~(((uint64_t)m32 << 32) | m32) : (((uint64_t)m32 << 32) | m32);
+          uint32_t fo;
+          asm("v_cndmask_b32 %0, 0, %1, %2" : "=v"(fo) : "v"(f), "s"(mk));
+          f = fo;
+        } else {
+          f &= (uint32_t)__builtin_amdgcn_sbfe((int)A, q, 1);
+        }
+        if (q == 0 && PH == 0) f = pk_max16(f, primv);
+        if (PH == 0) op[q] = f;
+        else op[q] |= f;
+        prev = cur;
+        cur = f;
+        u1p = u1r;
+      }
+    };
+    phase(std::integral_constant<int, 0>());
+    phase(std::integral_constant<int, 1>());
+    uint32_t ox_[8], oy_[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t t1 = perm(op[4 * k + 1], op[4 * k], 0x06020400u);
+      const uint32_t t2 = perm(op[4 * k + 3], op[4 * k + 2], 0x06020400u);
+      ox_[k] = perm(t2, t1, 0x05040100u);
+      oy_[k] = perm(t2, t1, 0x07060302u);
+    }
+    if (livex) {
+      uint4* p = (uint4*)(tab + ox);
+      p[0] = make_uint4(ox_[0], ox_[1], ox_[2], ox_[3]);
+      p[1] = make_uint4(ox_[4], ox_[5], ox_[6], ox_[7]);
+    }
+    if (livey) {
+      uint4* p = (uint4*)(tab + oy);
+      p[0] = make_uint4(oy_[0], oy_[1], oy_[2], oy_[3]);
+      p[1] = make_uint4(oy_[4], oy_[5], oy_[6], oy_[7]);
+    }
+  }
+}
+
 static int g_grid_blocks = 2048;
 static uint64_t* g_stamps = nullptr;  // variant 15: per-wave s_memtime stamps of the level being traced
 
@@ -240,7 +345,7 @@ static void launch(int var, uint8_t* tab, const uint32_t* list, uint32_t n, cons
   const dim3 G(blocks), B(256);
   switch (var) {
     case 0:
-      hipLaunchKernelGGL((k_plane_resolve_x2<1, NO, false>), G, B, 0, st, tab, (const void*)list, n, g, zero,
+      hipLaunchKernelGGL((k_plane_resolve_x2<1, NO, false, 0>), G, B, 0, st, tab, (const void*)list, n, g, zero,
                          (const uint8_t*)nullptr, (uint8_t*)nullptr, (const uint32_t*)nullptr, 0u);
       break;
     case 1: hipLaunchKernelGGL((lab_x2<NO, 0, true>), G, B, 0, st, tab, list, n, g, zero); break;
@@ -260,6 +365,8 @@ static void launch(int var, uint8_t* tab, const uint32_t* list, uint32_t n, cons
     case 7: hipLaunchKernelGGL((lab_x2<NO, 0, true, false, 1, false, true>), G, B, 0, st, tab, list, n, g, zero); break;
     case 8: hipLaunchKernelGGL((lab_x2<NO, 0, true, false, 1, true, true>), G, B, 0, st, tab, list, n, g, zero); break;
     case 9: hipLaunchKernelGGL((lab_x2<NO, 0, true, false, 1, false, false, true>), G, B, 0, st, tab, list, n, g, zero); break;
+    case 30: hipLaunchKernelGGL((lab_x2u<NO, 0>), G, B, 0, st, tab, list, n, g, zero); break;
+    case 31: hipLaunchKernelGGL((lab_x2u<NO, 1>), G, B, 0, st, tab, list, n, g, zero); break;
     default: fprintf(stderr, "unknown variant %d\n", var); exit(1);
   }
 }
