@@ -422,6 +422,9 @@ __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
 // wave each holds one plane's 32 rows).  A function of its own, not a
 // lambda inside the list loop: the lambda form cost the NO = 4 kernel 12
 // VGPRs (119 -> 131, one wave per SIMD less).
+#ifndef GM_PLANE_RSV_UNR
+#define GM_PLANE_RSV_UNR false
+#endif
 template <int WB, int NO, bool SH, int RS_, bool UNR = true>
 __device__ __forceinline__ void plane_x2_visit(typename PlaneWord<WB>::T* __restrict__ tab, const PlaneGeom& g,
                                                const uint4* __restrict__ zero,
@@ -636,10 +639,10 @@ __device__ __forceinline__ void plane_x2_range(typename PlaneWord<WB>::T* __rest
 #pragma unroll
       for (int j = 0; j < NO; j++) sum += dg[j];
       switch (__builtin_amdgcn_readfirstlane(sum) & 3u) {
-        case 0: plane_x2_visit<WB, NO, SH, 0, false>(tab, g, zero, recv, send, ex, ey, livex, livey); break;
-        case 1: plane_x2_visit<WB, NO, SH, 1, false>(tab, g, zero, recv, send, ex, ey, livex, livey); break;
-        case 2: plane_x2_visit<WB, NO, SH, 2, false>(tab, g, zero, recv, send, ex, ey, livex, livey); break;
-        default: plane_x2_visit<WB, NO, SH, 3, false>(tab, g, zero, recv, send, ex, ey, livex, livey); break;
+        case 0: plane_x2_visit<WB, NO, SH, 0, GM_PLANE_RSV_UNR>(tab, g, zero, recv, send, ex, ey, livex, livey); break;
+        case 1: plane_x2_visit<WB, NO, SH, 1, GM_PLANE_RSV_UNR>(tab, g, zero, recv, send, ex, ey, livex, livey); break;
+        case 2: plane_x2_visit<WB, NO, SH, 2, GM_PLANE_RSV_UNR>(tab, g, zero, recv, send, ex, ey, livex, livey); break;
+        default: plane_x2_visit<WB, NO, SH, 3, GM_PLANE_RSV_UNR>(tab, g, zero, recv, send, ex, ey, livex, livey); break;
       }
     }
   }

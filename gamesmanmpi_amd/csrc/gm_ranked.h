@@ -362,7 +362,10 @@ __global__ __launch_bounds__(256) void k_rk_forward(RankGeom g, uint32_t L, u64 
 // reduction -- so all 2C loads issue back to back with no branches.  CC / HH:
 // the board at compile time (0: from g).
 constexpr uint32_t kRkTile = 256 * 64;
-template <int CC, int HH>
+// (U: list entries per lane per pass -- U x 2C child loads in flight before
+// any reduction; a tile inside one height-vector block (L >= 11) reads its
+// block's stacks / child bases once, wave-uniform)
+template <int CC, int HH, int U>
 __global__ __launch_bounds__(256) void k_rk_backward(RankGeom g, uint32_t L, u64 lvstart, uint32_t lvoff,
                                                      u64 nwords, u64 cstart, u64 csize, BlockCount* bc, DevState* st) {
   constexpr int NC = CC > 0 ? CC : kRankMaxCols;
@@ -404,32 +407,47 @@ __global__ __launch_bounds__(256) void k_rk_backward(RankGeom g, uint32_t L, u64
     }
     uint32_t at = before + incl - c;
     for (u64 mm = m; mm; mm &= mm - 1) list[at++] = (uint16_t)(threadIdx.x * 64 + __builtin_ctzll(mm));
+    // one block for the whole tile: its stacks and child bases, read once
+    const u64 tb0 = (t0 << 6) >> (L + 3);
+    const bool oneblk = ((((t0 + 255) << 6) + 63) >> (L + 3)) == tb0;
+    uint32_t tph = 0, tcho[kRankMaxCols] = {};
+    if (oneblk) {
+      tph = g.lvph[lvoff + tb0];
+      const uint4* cp = reinterpret_cast<const uint4*>(g.lvch + (u64)(lvoff + tb0) * kRankMaxCols);
+      const uint4 c0 = cp[0], c1 = cp[1];
+      tcho[0] = c0.x, tcho[1] = c0.y, tcho[2] = c0.z, tcho[3] = c0.w;
+      tcho[4] = c1.x, tcho[5] = c1.y, tcho[6] = c1.z, tcho[7] = c1.w;
+    }
     __syncthreads();
-    // two entries per pass (e, e + 256): 4C child loads in flight per lane
-    // before any reduction or store
-    for (uint32_t e0 = threadIdx.x; e0 < total; e0 += 512) {
-      uint32_t off2[2][2 * NC], nch2[2];
-      u64 slot2[2];
-      bool live2[2];
+    // U entries per pass (e, e + 256, ...): U x 2C child loads in flight per
+    // lane before any reduction or store
+    for (uint32_t e0 = threadIdx.x; e0 < total; e0 += 256u * U) {
+      uint32_t offu[U][2 * NC], nchu[U];
+      u64 slotu[U];
+      bool liveu[U];
 #pragma unroll
-      for (int u = 0; u < 2; u++) {
+      for (int u = 0; u < U; u++) {
         const uint32_t e = e0 + 256u * (uint32_t)u;
-        live2[u] = e < total;
-        const u64 i = (t0 << 6) + list[live2[u] ? e : e0];
-        slot2[u] = lvstart + i;
+        liveu[u] = e < total;
+        const u64 i = (t0 << 6) + list[liveu[u] ? e : e0];
+        slotu[u] = lvstart + i;
         const u64 blk = i >> (L + 3);
         const uint32_t a = (uint32_t)((i >> L) & 7u), pat = (uint32_t)(i & ((1ull << L) - 1));
-        const uint32_t ph = g.lvph[lvoff + blk];
-        uint32_t cho[kRankMaxCols];
-        {
+        uint32_t ph, cho[kRankMaxCols];
+        if (oneblk) {
+          ph = tph;
+#pragma unroll
+          for (int x = 0; x < kRankMaxCols; x++) cho[x] = tcho[x];
+        } else {
+          ph = g.lvph[lvoff + blk];
           const uint4* cp = reinterpret_cast<const uint4*>(g.lvch + (u64)(lvoff + blk) * kRankMaxCols);
           const uint4 c0 = cp[0], c1 = cp[1];
           cho[0] = c0.x, cho[1] = c0.y, cho[2] = c0.z, cho[3] = c0.w;
           cho[4] = c1.x, cho[5] = c1.y, cho[6] = c1.z, cho[7] = c1.w;
         }
         const RankHands h_ = rk_hands(L, (uint32_t)__builtin_popcount(pat), a);
-        const bool hasT = live2[u] && (fmoves ? h_.t1 < (int)kRankHand : h_.t2 < (int)kRankHand);
-        const bool hasO = live2[u] && (fmoves ? h_.o1 < (int)kRankHand : h_.o2 < (int)kRankHand);
+        const bool hasT = liveu[u] && (fmoves ? h_.t1 < (int)kRankHand : h_.t2 < (int)kRankHand);
+        const bool hasO = liveu[u] && (fmoves ? h_.o1 < (int)kRankHand : h_.o2 < (int)kRankHand);
         const uint32_t rowT = (a + (fmoves ? 1u : 0u)) << (L + 1), rowO = a << (L + 1);
         uint32_t nch = 0, off = 0;
 #pragma unroll
@@ -440,19 +458,19 @@ __global__ __launch_bounds__(256) void k_rk_backward(RankGeom g, uint32_t L, u64
           off += h;
           const uint32_t lo = pat & ((1u << q) - 1u), hi = (pat >> q) << (q + 1);
           const bool vT = col && hasT, vO = col && hasO;
-          off2[u][2 * x] = vT ? cho[x] + rowT + (lo | (1u << q) | hi) : 0xFFFFFFFFu;
-          off2[u][2 * x + 1] = vO ? cho[x] + rowO + (lo | hi) : 0xFFFFFFFFu;
+          offu[u][2 * x] = vT ? cho[x] + rowT + (lo | (1u << q) | hi) : 0xFFFFFFFFu;
+          offu[u][2 * x + 1] = vO ? cho[x] + rowO + (lo | hi) : 0xFFFFFFFFu;
           nch += (uint32_t)vT + (uint32_t)vO;
         }
-        nch2[u] = nch;
+        nchu[u] = nch;
       }
-      uint32_t w2[2][2 * NC];
+      uint32_t wu[U][2 * NC];
 #pragma unroll
-      for (int u = 0; u < 2; u++)
+      for (int u = 0; u < U; u++)
 #pragma unroll
-        for (int k = 0; k < 2 * NC; k++) w2[u][k] = __builtin_amdgcn_raw_buffer_load_b8(rw, off2[u][k], 0, 0);
+        for (int k = 0; k < 2 * NC; k++) wu[u][k] = __builtin_amdgcn_raw_buffer_load_b8(rw, offu[u][k], 0, 0);
 #pragma unroll
-      for (int u = 0; u < 2; u++) {
+      for (int u = 0; u < U; u++) {
         // reference-canonical _res_red / _remote_red over the children (an
         // absent child reads 0: WIN in 0, changes none of the four;
         // SURVEY §8a A8/A9)
@@ -460,19 +478,19 @@ __global__ __launch_bounds__(256) void k_rk_backward(RankGeom g, uint32_t L, u64
         uint32_t min_loss = 0xFFFFFFFFu, max_all = 0;
 #pragma unroll
         for (int k = 0; k < 2 * NC; k++) {
-          const uint32_t v = w2[u][k] & 3u, r = w2[u][k] >> 2;
+          const uint32_t v = wu[u][k] & 3u, r = wu[u][k] >> 2;
           any_loss |= v == LOSS;
           min_loss = v == LOSS ? min(min_loss, r) : min_loss;
           any_tie |= v == TIE;
           any_draw |= v == DRAW;
           max_all = max(max_all, r);
         }
-        if (!live2[u]) continue;
-        if (nch2[u] == 0) err |= ERR_NO_MOVES;
-        edges += nch2[u];
+        if (!liveu[u]) continue;
+        if (nchu[u] == 0) err |= ERR_NO_MOVES;
+        edges += nchu[u];
         const uint32_t word =
             any_loss ? make_word(WIN, min_loss + 1) : make_word(any_tie ? TIE : any_draw ? DRAW : LOSS, max_all + 1);
-        g.words[slot2[u]] = (uint8_t)word;
+        g.words[slotu[u]] = (uint8_t)word;
       }
     }
     __syncthreads();  // the list is rewritten by the next tile
@@ -695,6 +713,17 @@ static void rank_kind_dispatch(const Desc& d, F&& f) {
   }
 }
 
+// entries per lane per backward pass: 2, or GM_RK_UNROLL=4 for A/B runs (toot
+// 6x4 backward 12.27 ms at 2 against 13.07 at 4: more loads in flight do not
+// pay, the scattered byte gathers are bound by lines per load, not latency)
+static int rk_unroll() {
+  static const int u = [] {
+    const char* e = getenv("GM_RK_UNROLL");
+    return e && atoi(e) == 4 ? 4 : 2;
+  }();
+  return u;
+}
+
 static int rank_grid(const gm_solver* s, u64 nitems) {
   return (int)std::max<u64>(1, std::min<u64>((nitems + 255) / 256, (u64)std::min(s->grid * 2, kCountSlots)));
 }
@@ -756,8 +785,12 @@ static int run_ranked(gm_solver* s, gm_result* out) {
     const u64 cn = L + 1 < (uint32_t)T ? s->rlvstart[L + 2] - cs : 0;
     auto go = [&](auto CH) {
       constexpr int CC = decltype(CH)::value / 16, HH = decltype(CH)::value % 16;
-      hipLaunchKernelGGL((k_rk_backward<CC, HH>), dim3(rank_grid(s, nw)), dim3(256), 0, st, g, L, s->rlvstart[L],
-                         s->rlvoff[L], nw, cs, cn, s->bcount, s->st);
+      if (rk_unroll() == 2)
+        hipLaunchKernelGGL((k_rk_backward<CC, HH, 2>), dim3(rank_grid(s, nw)), dim3(256), 0, st, g, L,
+                           s->rlvstart[L], s->rlvoff[L], nw, cs, cn, s->bcount, s->st);
+      else
+        hipLaunchKernelGGL((k_rk_backward<CC, HH, 4>), dim3(rank_grid(s, nw)), dim3(256), 0, st, g, L,
+                           s->rlvstart[L], s->rlvoff[L], nw, cs, cn, s->bcount, s->st);
     };
     if (g.C == 6 && g.H == 4) go(std::integral_constant<int, 6 * 16 + 4>());
     else if (g.C == 5 && g.H == 4) go(std::integral_constant<int, 5 * 16 + 4>());
