@@ -168,6 +168,24 @@ __device__ __forceinline__ uint32_t pk_max16(uint32_t a, uint32_t b) {
   u16x2 x = __builtin_bit_cast(u16x2, a), y = __builtin_bit_cast(u16x2, b);
   return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(x, y));
 }
+// max of three packed step values.  The 8-bit word forms keep every step
+// value in [0, 0xFF] per 16-bit half (words in the low byte, the high byte 0:
+// the E byte extract, the parent forms and the frame shift all map [0, 0xFF]
+// into itself), and there the f16 bit patterns are +0 and positive
+// subnormals, ordered as the integers are: gfx950's v_pk_maximum3_f16 is an
+// exact three-input packed u16 max, one instruction for two v_pk_max_u16
+// (the kernels run with f16 denormals preserved, float_denorm_mode_16_64 = 3;
+// no NaN pattern can arise).  16-bit words: two integer maxes.
+template <bool B8V>
+__device__ __forceinline__ uint32_t pk_max3w(uint32_t a, uint32_t b, uint32_t c) {
+  if constexpr (B8V) {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const h2 x = __builtin_bit_cast(h2, a), y = __builtin_bit_cast(h2, b), z = __builtin_bit_cast(h2, c);
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_maximum(__builtin_elementwise_maximum(x, y), z));
+  } else {
+    return pk_max16(pk_max16(a, b), c);
+  }
+}
 __device__ __forceinline__ uint32_t pk_shl8(uint32_t a) {
   u16x2 x = __builtin_bit_cast(u16x2, a);
   return __builtin_bit_cast(uint32_t, (u16x2)(x << (unsigned short)8));
@@ -422,6 +440,9 @@ __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
 // wave each holds one plane's 32 rows).  A function of its own, not a
 // lambda inside the list loop: the lambda form cost the NO = 4 kernel 12
 // VGPRs (119 -> 131, one wave per SIMD less).
+#ifndef GM_PLANE_MAX3  // 0: the step's maxima as v_pk_max_u16 pairs (A/B)
+#define GM_PLANE_MAX3 1
+#endif
 #ifndef GM_PLANE_RSV_UNR
 #define GM_PLANE_RSV_UNR false
 #endif
@@ -552,14 +573,23 @@ __device__ __forceinline__ void plane_x2_visit(typename PlaneWord<WB>::T* __rest
       const uint32_t u2r = from_lane_below(u1p);
       const int dcls = (RS_ + q) & 3;  // relative forms: d % 4 of this step's positions (32 = 0 mod 4)
       const uint32_t pre = REL && dcls == 0 ? pk_max16(a, rel_shift_pk(pk_max16(prev, u2r)))
-                                            : pk_max16(pk_max16(a, prev), u2r);
+                                            : pk_max3w<GM_PLANE_MAX3 && B8>(a, prev, u2r);
       const uint32_t u1r = from_lane_below(cur);
-      const uint32_t m = pk_max16(pk_max16(pre, cur), u1r);
-      uint32_t f = (REL && dcls == 3 ? parent_rel_up(m) : parent_x2<WB == 2 ? 2 : 1>(m)) &
-                   (uint32_t)__builtin_amdgcn_sbfe((int)A, q, 1);
-      if (q == 0) f = pk_max16(f, PH ? 0u : primv);
-      if (UNR && PH == 0) op[q] = f;
-      else op[q] |= f;
+      const uint32_t m = pk_max3w<GM_PLANE_MAX3 && B8>(pre, cur, u1r);
+      uint32_t f = REL && dcls == 3 ? parent_rel_up(m) : parent_x2<WB == 2 ? 2 : 1>(m);
+      if (UNR && PH == 1) {
+        // phase 1: a finished row's value is never read by an active row
+        // (row L, active at steps q < L, reads rows L - 1 / L - 2 at steps
+        // q - 1 / q - 2, when they were active too), so it needs no zeroing:
+        // the mask only merges the step into the row's output, one
+        // v_cndmask in place of and + or
+        op[q] = __builtin_amdgcn_sbfe((int)A, q, 1) ? f : op[q];
+      } else {
+        f &= (uint32_t)__builtin_amdgcn_sbfe((int)A, q, 1);
+        if (q == 0) f = pk_max16(f, PH ? 0u : primv);
+        if (UNR && PH == 0) op[q] = f;
+        else op[q] |= f;
+      }
       prev = cur;
       cur = f;
       u1p = u1r;
