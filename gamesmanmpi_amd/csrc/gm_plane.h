@@ -443,6 +443,9 @@ __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
 #ifndef GM_PLANE_MAX3  // 0: the step's maxima as v_pk_max_u16 pairs (A/B)
 #define GM_PLANE_MAX3 1
 #endif
+#ifndef GM_PLANE_OFFMASK  // 0: phase 0 masks f on the chain (A/B)
+#define GM_PLANE_OFFMASK 1
+#endif
 #ifndef GM_PLANE_RSV_UNR
 #define GM_PLANE_RSV_UNR false
 #endif
@@ -575,9 +578,20 @@ __device__ __forceinline__ void plane_x2_visit(typename PlaneWord<WB>::T* __rest
       const uint32_t pre = REL && dcls == 0 ? pk_max16(a, rel_shift_pk(pk_max16(prev, u2r)))
                                             : pk_max3w<GM_PLANE_MAX3 && B8>(a, prev, u2r);
       const uint32_t u1r = from_lane_below(cur);
-      const uint32_t m = pk_max3w<GM_PLANE_MAX3 && B8>(pre, cur, u1r);
+      // phase 0, 8-bit forms: a row that has not started takes pre = the word
+      // whose parent is 0 (0xFF; 0xFE for the relative up form) -- its cur
+      // and the row below's are still 0, so m = pre and f = 0 with no mask
+      // on the chain (cur -> DPP -> max3 -> parent -> cur, five operations)
+      const bool offm = GM_PLANE_OFFMASK && UNR && B8 && PH == 0;
+      const uint32_t pre_ =
+          offm ? ((__builtin_amdgcn_sbfe((int)A, q, 1) != 0) ? pre : (REL && dcls == 3 ? 0x00FE00FEu : 0x00FF00FFu))
+               : pre;
+      const uint32_t m = pk_max3w<GM_PLANE_MAX3 && B8>(pre_, cur, u1r);
       uint32_t f = REL && dcls == 3 ? parent_rel_up(m) : parent_x2<WB == 2 ? 2 : 1>(m);
-      if (UNR && PH == 1) {
+      if (offm) {
+        if (q == 0) f = pk_max16(f, primv);
+        op[q] = f;
+      } else if (UNR && PH == 1) {
         // phase 1: a finished row's value is never read by an active row
         // (row L, active at steps q < L, reads rows L - 1 / L - 2 at steps
         // q - 1 / q - 2, when they were active too), so it needs no zeroing:
