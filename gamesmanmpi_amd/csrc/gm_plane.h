@@ -446,6 +446,9 @@ __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
 #ifndef GM_PLANE_OFFMASK  // 0: phase 0 masks f on the chain (A/B)
 #define GM_PLANE_OFFMASK 1
 #endif
+#ifndef GM_PLANE_FOLD3  // 0: even bytes folded as shift + max (A/B)
+#define GM_PLANE_FOLD3 1
+#endif
 #ifndef GM_PLANE_RSV_UNR
 #define GM_PLANE_RSV_UNR false
 #endif
@@ -482,26 +485,58 @@ __device__ __forceinline__ void plane_x2_visit(typename PlaneWord<WB>::T* __rest
     }
     return dig[j] >= (uint32_t)k ? (const uint4*)(tab + off - (size_t)k * g.stride[j] * 1024u) : zero;
   };
-  auto fold = [&](int j, int k) {
-    const uint4* sx = nb(ex, dx, ox, j, k);
-    const uint4* sy = nb(ey, dy, oy, j, k);
-    uint4 vx[NQ], vy[NQ];
+  // FL3 (8-bit forms): the even bytes fold in LOW-byte form (masked with
+  // 0x00FF00FF, two neighbours per v_pk_maximum3_f16, exact on [0, 0xFF] as
+  // in the step), the odd ones raw in the high bytes (one v_pk_max_u16 each):
+  // 2.5 operations per neighbour dword and plane instead of 3 (shift + max)
+  constexpr bool FL3 = GM_PLANE_FOLD3 && B8;
+  auto lowb = [](uint32_t v) { return FL3 ? (v & 0x00FF00FFu) : pk_shl8(v); };
+  auto fold2 = [&](int j1, int k1, int j2, int k2) {  // j2 < 0: one neighbour
+    const bool two = j2 >= 0;
+    const uint4* sx1 = nb(ex, dx, ox, j1, k1);
+    const uint4* sy1 = nb(ey, dy, oy, j1, k1);
+    const uint4* sx2 = two ? nb(ex, dx, ox, j2, k2) : sx1;
+    const uint4* sy2 = two ? nb(ey, dy, oy, j2, k2) : sy1;
+    uint4 vx1[NQ], vy1[NQ], vx2[NQ], vy2[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; q++) {
-      vx[q] = sx[q];
-      vy[q] = sy[q];
+      vx1[q] = sx1[q];
+      vy1[q] = sy1[q];
+      if (two) {
+        vx2[q] = sx2[q];
+        vy2[q] = sy2[q];
+      }
     }
 #pragma unroll
     for (int q = 0; q < NQ; q++) {
-      const uint32_t a[4] = {vx[q].x, vx[q].y, vx[q].z, vx[q].w};
-      const uint32_t b[4] = {vy[q].x, vy[q].y, vy[q].z, vy[q].w};
+      const uint32_t a1[4] = {vx1[q].x, vx1[q].y, vx1[q].z, vx1[q].w};
+      const uint32_t b1[4] = {vy1[q].x, vy1[q].y, vy1[q].z, vy1[q].w};
+      uint32_t a2[4] = {0, 0, 0, 0}, b2[4] = {0, 0, 0, 0};
+      if (two) {
+        a2[0] = vx2[q].x, a2[1] = vx2[q].y, a2[2] = vx2[q].z, a2[3] = vx2[q].w;
+        b2[0] = vy2[q].x, b2[1] = vy2[q].y, b2[2] = vy2[q].z, b2[3] = vy2[q].w;
+      }
 #pragma unroll
       for (int c = 0; c < 4; c++) {
-        Xh[4 * q + c] = pk_max16(Xh[4 * q + c], a[c]);
-        Yh[4 * q + c] = pk_max16(Yh[4 * q + c], b[c]);
+        const int d = 4 * q + c;
+        Xh[d] = pk_max16(Xh[d], a1[c]);
+        Yh[d] = pk_max16(Yh[d], b1[c]);
+        if (two) {
+          Xh[d] = pk_max16(Xh[d], a2[c]);
+          Yh[d] = pk_max16(Yh[d], b2[c]);
+        }
         if (B8) {
-          Xl[4 * q + c] = pk_max16(Xl[4 * q + c], pk_shl8(a[c]));
-          Yl[4 * q + c] = pk_max16(Yl[4 * q + c], pk_shl8(b[c]));
+          if (FL3 && two) {
+            Xl[d] = pk_max3w<true>(Xl[d], lowb(a1[c]), lowb(a2[c]));
+            Yl[d] = pk_max3w<true>(Yl[d], lowb(b1[c]), lowb(b2[c]));
+          } else {
+            Xl[d] = pk_max16(Xl[d], lowb(a1[c]));
+            Yl[d] = pk_max16(Yl[d], lowb(b1[c]));
+            if (two) {
+              Xl[d] = pk_max16(Xl[d], lowb(a2[c]));
+              Yl[d] = pk_max16(Yl[d], lowb(b2[c]));
+            }
+          }
         }
       }
     }
@@ -509,29 +544,26 @@ __device__ __forceinline__ void plane_x2_visit(typename PlaneWord<WB>::T* __rest
   if constexpr (REL) {
     // children at d - 2 first, then their frame shift -- ONCE on the
     // folded maxima (the shift is monotone: it commutes with max), on the
-    // one split array whose high bytes hold row bytes B0 mod 4 (Xh: odd
-    // bytes, Xl: even ones), half B0 / 2 of every dword -- then the
-    // children at d - 1
+    // one split array that holds row bytes B0 mod 4 (Xh: odd bytes, high in
+    // their halves; Xl: even ones, low with FL3), half B0 / 2 of every
+    // dword -- then the children at d - 1
 #pragma unroll
-    for (int j = 0; j < NO; j++) fold(j, 2);
+    for (int j = 0; j < NO; j += 2) fold2(j, 2, j + 1 < NO ? j + 1 : -1, 2);
 #pragma unroll
     for (int d = 0; d < DW; d++) {
       if (B0 & 1) {
         Xh[d] = rel_shift_byte<2 * (B0 >> 1) + 1>(Xh[d]);
         Yh[d] = rel_shift_byte<2 * (B0 >> 1) + 1>(Yh[d]);
       } else {
-        Xl[d] = rel_shift_byte<2 * (B0 >> 1) + 1>(Xl[d]);
-        Yl[d] = rel_shift_byte<2 * (B0 >> 1) + 1>(Yl[d]);
+        Xl[d] = rel_shift_byte<2 * (B0 >> 1) + (FL3 ? 0 : 1)>(Xl[d]);
+        Yl[d] = rel_shift_byte<2 * (B0 >> 1) + (FL3 ? 0 : 1)>(Yl[d]);
       }
     }
 #pragma unroll
-    for (int j = 0; j < NO; j++) fold(j, 1);
+    for (int j = 0; j < NO; j += 2) fold2(j, 1, j + 1 < NO ? j + 1 : -1, 1);
   } else {
 #pragma unroll
-    for (int j = 0; j < NO; j++) {
-#pragma unroll
-      for (int k = 1; k <= 2; k++) fold(j, k);
-    }
+    for (int j = 0; j < NO; j++) fold2(j, 1, j, 2);
   }
   const uint32_t primv =
       (g.rank == 0 && L == 0) ? ((ex.p == 0 ? W::kPrim : 0u) | (ey.p == 0 ? W::kPrim << 16 : 0u)) : 0u;
@@ -564,7 +596,7 @@ __device__ __forceinline__ void plane_x2_visit(typename PlaneWord<WB>::T* __rest
       if (B8) {
         // byte q of X's and Y's E rows -> [X, 0, Y, 0]
         const int d = q >> 2, b = q & 3;
-        const uint32_t bx = (b & 1) ? (uint32_t)b : (uint32_t)b + 1;  // byte inside the split dword
+        const uint32_t bx = (b & 1) || FL3 ? (uint32_t)b : (uint32_t)b + 1;  // byte inside the split dword
         const uint32_t sel = 0x0C000C00u | ((4u + bx) << 16) | bx;     // hi = Y (bytes 4-7), lo = X
         a = (b & 1) ? perm(Yh[d], Xh[d], sel) : perm(Yl[d], Xl[d], sel);
       } else {
