@@ -205,6 +205,156 @@ __global__ __launch_bounds__(256) void k_rk_boards(Desc d, RankGeom g, uint32_t 
   }
 }
 
+// F0, bit-sliced (boards of <= 32 cells with <= 31 windows: the BASELINE 6x4
+// and the 5x4 / 4x4 test boards; levels L >= 5): a thread takes 32 boards of
+// one block -- stack patterns pat0 + b, b = 0..31 -- as bit b of 32-bit words.
+// Cell (x, y) holds stack bit j = off_x + y, and across the 32 boards that
+// bit is the constant 0xAAAAAAAA, 0xCCCCCCCC, .. for j < 5 and all-zero / all-
+// one from pat0 above; a window's TOOT (OTTO) bits are the AND of its four
+// cells' T / O words, the counts are a Harley-Seal carry-save sum of the
+// window words (v_bitop3: one instruction per sum, one per carry), and the
+// comparison is a 5-bit bit-sliced one.  bstat bytes and pbits words come
+// out as k_rk_boards writes them (tests/test_gpu_ranked.py: word for word
+// against BUCKETED; the 5x4 / 6x4 goldens).  ~15 operations a board where
+// the per-board kernel issues ~150.
+template <int CC, int HH>
+struct RkWindows {
+  static constexpr int NC = CC * HH;
+  int n = 0, c[64] = {}, s[64] = {};
+  constexpr RkWindows() {
+    const int dxs[4] = {1, 0, 1, 1}, dys[4] = {0, 1, 1, -1};
+    for (int i = 0; i < 4; i++)
+      for (int y = 0; y < HH; y++)
+        for (int x = 0; x < CC; x++) {
+          const int ex = x + 3 * dxs[i], ey = y + 3 * dys[i];
+          if (ex >= 0 && ex < CC && ey >= 0 && ey < HH) {
+            c[n] = CC * y + x;
+            s[n] = dxs[i] + CC * dys[i];
+            n++;
+          }
+        }
+  }
+};
+// v_bitop3_b32 truth tables over (a, b, c) = (0xF0, 0xCC, 0xAA)
+__device__ __forceinline__ uint32_t rk_xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t rk_maj(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+}
+__device__ __forceinline__ uint32_t rk_and3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x80);
+}
+// Harley-Seal: the 5-bit bit-sliced count of up to 32 window words (zeros fold away)
+__device__ __forceinline__ void rk_count32(const uint32_t (&x)[32], uint32_t (&cnt)[5]) {
+  uint32_t ones = 0, twos = 0, fours = 0, eights = 0, sixteens = 0;
+#pragma unroll
+  for (int i = 0; i < 32; i += 16) {
+    uint32_t twosA, twosB, foursA, foursB, eightsA, eightsB, t;
+    auto csa = [](uint32_t& h, uint32_t& l, uint32_t a, uint32_t b, uint32_t c) {
+      h = rk_maj(a, b, c);
+      l = rk_xor3(a, b, c);
+    };
+    csa(twosA, ones, ones, x[i + 0], x[i + 1]);
+    csa(twosB, ones, ones, x[i + 2], x[i + 3]);
+    csa(foursA, twos, twos, twosA, twosB);
+    csa(twosA, ones, ones, x[i + 4], x[i + 5]);
+    csa(twosB, ones, ones, x[i + 6], x[i + 7]);
+    csa(foursB, twos, twos, twosA, twosB);
+    csa(eightsA, fours, fours, foursA, foursB);
+    csa(twosA, ones, ones, x[i + 8], x[i + 9]);
+    csa(twosB, ones, ones, x[i + 10], x[i + 11]);
+    csa(foursA, twos, twos, twosA, twosB);
+    csa(twosA, ones, ones, x[i + 12], x[i + 13]);
+    csa(twosB, ones, ones, x[i + 14], x[i + 15]);
+    csa(foursB, twos, twos, twosA, twosB);
+    csa(eightsB, fours, fours, foursA, foursB);
+    csa(t, eights, eights, eightsA, eightsB);
+    sixteens |= t;  // the total is <= 31: one sixteen at most
+  }
+  cnt[0] = ones, cnt[1] = twos, cnt[2] = fours, cnt[3] = eights, cnt[4] = sixteens;
+}
+template <int CC, int HH>
+__global__ __launch_bounds__(256) void k_rk_boards_sl(RankGeom g, uint32_t L, u64 bstart, uint32_t lvoff,
+                                                      u64 nslices, u64 nreal) {
+  constexpr RkWindows<CC, HH> W{};
+  static_assert(CC * HH <= 32 && W.n <= 31, "bit-sliced boards: <= 32 cells, <= 31 windows");
+  constexpr int NCELL = CC * HH;
+  // stack bit j's word over the 32 boards for j < 5 (0 above: pat0 gives those)
+  __shared__ uint32_t kLow[32];
+  if (threadIdx.x < 32) {
+    const uint32_t j = threadIdx.x;
+    kLow[j] = j == 0 ? 0xAAAAAAAAu : j == 1 ? 0xCCCCCCCCu : j == 2 ? 0xF0F0F0F0u : j == 3 ? 0xFF00FF00u
+              : j == 4 ? 0xFFFF0000u : 0u;
+  }
+  __syncthreads();
+  const bool p1 = (L & 1u) != 0, full = L == (uint32_t)NCELL;
+  const uint32_t eqv = full ? 1u : 2u;  // eq -> TIE (2) on a full board, else UNDECIDED (4)
+  for (u64 sl = (u64)blockIdx.x * blockDim.x + threadIdx.x; sl < nslices; sl += (u64)gridDim.x * blockDim.x) {
+    const u64 ib0 = sl << 5;
+    uint32_t pm = 0;
+    if (ib0 < nreal) {
+      const u64 blk = ib0 >> L;
+      const uint32_t pat0 = (uint32_t)(ib0 & ((1ull << L) - 1));
+      const uint32_t ph = g.lvph[lvoff + blk];
+      uint32_t Tm[NCELL], Om[NCELL];
+      uint32_t off = 0;
+#pragma unroll
+      for (int x = 0; x < CC; x++) {
+        const uint32_t h = (ph >> (4 * x)) & 15u, hm = (1u << h) - 1u;
+#pragma unroll
+        for (int y = 0; y < HH; y++) {
+          const uint32_t j = (off + (uint32_t)y) & 31u;
+          // bits >= 5 of the stacks: pat0's, the same for all 32 (all 0 / all 1)
+          const uint32_t S = kLow[j] | (uint32_t)__builtin_amdgcn_sbfe((int)pat0, j, 1);
+          const uint32_t vm = (uint32_t)__builtin_amdgcn_sbfe((int)hm, y, 1);  // cell (x, y) occupied
+          Tm[CC * y + x] = S & vm;
+          Om[CC * y + x] = ~S & vm;
+        }
+        off += h;
+      }
+      uint32_t xt[32], xo[32];
+#pragma unroll
+      for (int w = 0; w < 32; w++) {
+        if (w < W.n) {
+          const int c = W.c[w], st = W.s[w];
+          xt[w] = rk_and3(Tm[c], Om[c + st], Om[c + 2 * st]) & Tm[c + 3 * st];
+          xo[w] = rk_and3(Om[c], Tm[c + st], Tm[c + 2 * st]) & Om[c + 3 * st];
+        } else {
+          xt[w] = xo[w] = 0;
+        }
+      }
+      uint32_t ct[5], co[5];
+      rk_count32(xt, ct);
+      rk_count32(xo, co);
+      // bit-sliced compare, least significant bit first
+      uint32_t gt = ct[0] & ~co[0], eq = ~(ct[0] ^ co[0]);
+#pragma unroll
+      for (int k = 1; k < 5; k++) {
+        // gt' = t & ~o | ~(t ^ o) & gt over (t, o, gt): table 0xB2; eq' = eq & ~(t ^ o) over (eq, t, o): 0x90
+        gt = __builtin_amdgcn_bitop3_b32(ct[k], co[k], gt, 0xB2);
+        eq = __builtin_amdgcn_bitop3_b32(eq, ct[k], co[k], 0x90);
+      }
+      // toot_prim: equal counts -> TIE on a full board, else UNDECIDED;
+      // otherwise LOSS iff (toot > otto) != p1, else WIN (gm_games.h)
+      const uint32_t loss = ~eq & (p1 ? ~gt : gt);
+      pm = full ? ~0u : ~eq;
+      uint32_t by[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const uint32_t e4 = (eq >> (4 * k)) & 15u, l4 = (loss >> (4 * k)) & 15u;
+        const uint32_t es = (e4 * 0x00204081u) & 0x01010101u;
+        const uint32_t ls = (l4 * 0x00204081u) & 0x01010101u;
+        by[k] = (es << eqv) | ls;  // WIN 0 / LOSS 1 / TIE 2 / UNDECIDED 4
+      }
+      uint4* bp = reinterpret_cast<uint4*>(g.bstat + bstart + ib0);
+      bp[0] = make_uint4(by[0], by[1], by[2], by[3]);
+      bp[1] = make_uint4(by[4], by[5], by[6], by[7]);
+    }
+    reinterpret_cast<uint32_t*>(g.pbits)[(bstart + ib0) >> 5] = pm;
+  }
+}
+
 // bits j of a 64-slot word (consecutive stack bits p0 + j, p0 a multiple of
 // 64) whose hands are valid: nT = popc(p0) + popc(j) in [lo, hi]
 __device__ __forceinline__ u64 rk_valid_mask(const RankGeom& g, uint32_t L, uint32_t a, uint32_t p0) {
@@ -425,45 +575,53 @@ __global__ __launch_bounds__(256) void k_rk_backward(RankGeom g, uint32_t L, u64
       uint32_t offu[U][2 * NC], nchu[U];
       u64 slotu[U];
       bool liveu[U];
+      // the children's offsets: lo | hi (the stacks with a 0 inserted at bit
+      // q = the column's top) is pat + (pat & ~(2^q - 1)), the T child adds
+      // 2^q and, if the first mover placed it, one a-row (2^(L+1)); a tile
+      // inside one block runs a copy of this with the block's stacks and
+      // child bases uniform, so q, the masks and the bases stay scalar
+      auto entries = [&](const uint32_t phu, const uint32_t* chou, bool uni) {
 #pragma unroll
-      for (int u = 0; u < U; u++) {
-        const uint32_t e = e0 + 256u * (uint32_t)u;
-        liveu[u] = e < total;
-        const u64 i = (t0 << 6) + list[liveu[u] ? e : e0];
-        slotu[u] = lvstart + i;
-        const u64 blk = i >> (L + 3);
-        const uint32_t a = (uint32_t)((i >> L) & 7u), pat = (uint32_t)(i & ((1ull << L) - 1));
-        uint32_t ph, cho[kRankMaxCols];
-        if (oneblk) {
-          ph = tph;
+        for (int u = 0; u < U; u++) {
+          const uint32_t e = e0 + 256u * (uint32_t)u;
+          liveu[u] = e < total;
+          const u64 i = (t0 << 6) + list[liveu[u] ? e : e0];
+          slotu[u] = lvstart + i;
+          const u64 blk = i >> (L + 3);
+          const uint32_t a = (uint32_t)((i >> L) & 7u), pat = (uint32_t)(i & ((1ull << L) - 1));
+          uint32_t ph = phu, cho[kRankMaxCols];
+          if (uni) {
 #pragma unroll
-          for (int x = 0; x < kRankMaxCols; x++) cho[x] = tcho[x];
-        } else {
-          ph = g.lvph[lvoff + blk];
-          const uint4* cp = reinterpret_cast<const uint4*>(g.lvch + (u64)(lvoff + blk) * kRankMaxCols);
-          const uint4 c0 = cp[0], c1 = cp[1];
-          cho[0] = c0.x, cho[1] = c0.y, cho[2] = c0.z, cho[3] = c0.w;
-          cho[4] = c1.x, cho[5] = c1.y, cho[6] = c1.z, cho[7] = c1.w;
+            for (int x = 0; x < kRankMaxCols; x++) cho[x] = chou[x];
+          } else {
+            ph = g.lvph[lvoff + blk];
+            const uint4* cp = reinterpret_cast<const uint4*>(g.lvch + (u64)(lvoff + blk) * kRankMaxCols);
+            const uint4 c0 = cp[0], c1 = cp[1];
+            cho[0] = c0.x, cho[1] = c0.y, cho[2] = c0.z, cho[3] = c0.w;
+            cho[4] = c1.x, cho[5] = c1.y, cho[6] = c1.z, cho[7] = c1.w;
+          }
+          const RankHands h_ = rk_hands(L, (uint32_t)__builtin_popcount(pat), a);
+          const bool hasT = liveu[u] && (fmoves ? h_.t1 < (int)kRankHand : h_.t2 < (int)kRankHand);
+          const bool hasO = liveu[u] && (fmoves ? h_.o1 < (int)kRankHand : h_.o2 < (int)kRankHand);
+          const uint32_t rp = (a << (L + 1)) + pat, dT = fmoves ? (1u << (L + 1)) : 0u;
+          uint32_t nch = 0, off = 0;
+#pragma unroll
+          for (int x = 0; x < NC; x++) {
+            const uint32_t h = (ph >> (4 * x)) & 15u;
+            const bool col = (CC > 0 || (uint32_t)x < C) && h < H;
+            const uint32_t q = off + h;
+            off += h;
+            const uint32_t oO = cho[x] + rp + (pat & (0xFFFFFFFFu << q)), oT = oO + dT + (1u << q);
+            const bool vT = col && hasT, vO = col && hasO;
+            offu[u][2 * x] = vT ? oT : 0xFFFFFFFFu;
+            offu[u][2 * x + 1] = vO ? oO : 0xFFFFFFFFu;
+            nch += (uint32_t)vT + (uint32_t)vO;
+          }
+          nchu[u] = nch;
         }
-        const RankHands h_ = rk_hands(L, (uint32_t)__builtin_popcount(pat), a);
-        const bool hasT = liveu[u] && (fmoves ? h_.t1 < (int)kRankHand : h_.t2 < (int)kRankHand);
-        const bool hasO = liveu[u] && (fmoves ? h_.o1 < (int)kRankHand : h_.o2 < (int)kRankHand);
-        const uint32_t rowT = (a + (fmoves ? 1u : 0u)) << (L + 1), rowO = a << (L + 1);
-        uint32_t nch = 0, off = 0;
-#pragma unroll
-        for (int x = 0; x < NC; x++) {
-          const uint32_t h = (ph >> (4 * x)) & 15u;
-          const bool col = (CC > 0 || (uint32_t)x < C) && h < H;
-          const uint32_t q = off + h;
-          off += h;
-          const uint32_t lo = pat & ((1u << q) - 1u), hi = (pat >> q) << (q + 1);
-          const bool vT = col && hasT, vO = col && hasO;
-          offu[u][2 * x] = vT ? cho[x] + rowT + (lo | (1u << q) | hi) : 0xFFFFFFFFu;
-          offu[u][2 * x + 1] = vO ? cho[x] + rowO + (lo | hi) : 0xFFFFFFFFu;
-          nch += (uint32_t)vT + (uint32_t)vO;
-        }
-        nchu[u] = nch;
-      }
+      };
+      if (oneblk) entries(tph, tcho, true);
+      else entries(0u, tcho, false);
       uint32_t wu[U][2 * NC];
 #pragma unroll
       for (int u = 0; u < U; u++)
@@ -724,6 +882,16 @@ static int rk_unroll() {
   return u;
 }
 
+// the bit-sliced board kernel (k_rk_boards_sl) where it applies; GM_RK_SLICED=0
+// keeps the per-board one (A/B runs)
+static bool rk_sliced() {
+  static const bool on = [] {
+    const char* e = getenv("GM_RK_SLICED");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 static int rank_grid(const gm_solver* s, u64 nitems) {
   return (int)std::max<u64>(1, std::min<u64>((nitems + 255) / 256, (u64)std::min(s->grid * 2, kCountSlots)));
 }
@@ -763,9 +931,23 @@ static int run_ranked(gm_solver* s, gm_result* out) {
         hipLaunchKernelGGL((k_rk_boards<KIND, CC, HH>), dim3(rank_grid(s, nb)), dim3(256), 0, st, d, g, L,
                            s->rlvstart[L] >> 3, s->rlvoff[L], nb, nreal);
       };
-      if (g.C == 6 && g.H == 4) boards(std::integral_constant<int, 6 * 16 + 4>());
-      else if (g.C == 5 && g.H == 4) boards(std::integral_constant<int, 5 * 16 + 4>());
-      else boards(std::integral_constant<int, 0>());
+      auto boards_sl = [&](auto CH) {
+        constexpr int CC = decltype(CH)::value / 16, HH = decltype(CH)::value % 16;
+        hipLaunchKernelGGL((k_rk_boards_sl<CC, HH>), dim3(rank_grid(s, nb / 32)), dim3(256), 0, st, g, L,
+                           s->rlvstart[L] >> 3, s->rlvoff[L], nb / 32, nreal);
+      };
+      const bool sliced = L >= 5 && rk_sliced();
+      if (g.C == 6 && g.H == 4) {
+        if (sliced) boards_sl(std::integral_constant<int, 6 * 16 + 4>());
+        else boards(std::integral_constant<int, 6 * 16 + 4>());
+      } else if (g.C == 5 && g.H == 4) {
+        if (sliced) boards_sl(std::integral_constant<int, 5 * 16 + 4>());
+        else boards(std::integral_constant<int, 5 * 16 + 4>());
+      } else if (g.C == 4 && g.H == 4 && sliced) {
+        boards_sl(std::integral_constant<int, 4 * 16 + 4>());
+      } else {
+        boards(std::integral_constant<int, 0>());
+      }
       const u64 n = s->rlvstart[L + 1] - s->rlvstart[L];  // 512-padded: every bitmap word written
       if (L >= 6)
         hipLaunchKernelGGL(k_rk_reach, dim3(rank_grid(s, n / 64)), dim3(256), 0, st, g, L, s->rlvstart[L],
