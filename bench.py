@@ -189,6 +189,17 @@ def pmc_traffic_total(kernel, workload):
     return row["bytes_per_launch"], row.get("launches", 0)
 
 
+def planes_traffic(kernel, workload):
+    """PLANES backward HBM bytes per launch: the PMC bytes of `kernel` and of
+    the one-workgroup runs (k_plane_run) over all their launches in the PMC
+    pass -- a launch-weighted mean, whatever number of solves the pass held --
+    or None."""
+    rows = [r for r in (pmc_traffic_total(k, workload) for k in (kernel, "k_plane_run")) if r[0] and r[1]]
+    if not rows:
+        return None
+    return sum(b * n for b, n in rows) / sum(n for _, n in rows)
+
+
 def golden(name):
     try:
         with open(os.path.join(ROOT, "tests", "golden", "checksums.json")) as fh:
@@ -453,9 +464,10 @@ def main():
     traffic, traffic_src = pmc_traffic(kname, workload)
     if layout == "planes" and traffic is not None:
         # the backward's launches are this kernel plus the one-workgroup runs
-        # of narrow levels (k_plane_run): their PMC bytes over all of them
-        per_solve = sum(b * n for b, n in (pmc_traffic_total(k, workload) for k in (kname, "k_plane_run")) if b)
-        traffic = per_solve / world / kn if per_solve else traffic
+        # of narrow levels (k_plane_run): their PMC bytes over all of them,
+        # per launch (the PMC pass may hold several solves: weight by its own
+        # launch counts, not by this solve's)
+        traffic = planes_traffic(kname, workload) or traffic
     roof = {"bound": "hbm", "kernel": kname,
             "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

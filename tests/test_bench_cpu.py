@@ -75,3 +75,16 @@ def test_kernel_names_come_from_the_library():
     from gamesmanmpi_amd import _lib
     assert _lib.RESOLVE_KERNELS[1] == "k_dense_resolve8p"
     assert _lib.PULL_KERNELS[1] == "k_dense_pull_words"
+
+
+def test_planes_traffic_is_a_launch_weighted_mean(monkeypatch):
+    """The PMC pass may hold several solves: the bench's PLANES traffic is
+    bytes per launch over the pass's own launches, not scaled by them."""
+    import bench
+    rows = {"k_plane_resolve_x2": (36.0e6, 234.0), "k_plane_run": (0.13e6, 4.0)}
+    monkeypatch.setattr(bench, "pmc_traffic_total", lambda k, w: rows.get(k, (None, 0)))
+    t = bench.planes_traffic("k_plane_resolve_x2", "w")
+    assert abs(t - (36.0e6 * 234 + 0.13e6 * 4) / 238) < 1.0
+    assert 0.13e6 < t < 36.0e6
+    monkeypatch.setattr(bench, "pmc_traffic_total", lambda k, w: (None, 0))
+    assert bench.planes_traffic("k_plane_resolve_x2", "w") is None
