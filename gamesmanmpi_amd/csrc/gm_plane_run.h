@@ -200,7 +200,11 @@ struct PlaneShape {
 // (8-bit relative words, profiles/r04j/): 2.32 / 2.89 / 3.51 / 4.01 ms (N = 4)
 // and 2.35 / 2.92 / 3.54 / 4.03 ms (N = 8) at k = 2 / 3 / 4 / 5 -- every key
 // costs ~4.5 us beyond its planes, while the trail is B - 1 keys whatever k
-// is (narrower keys only shorten each of them) -- so k = 2.  A
+// is (narrower keys only shorten each of them) -- so k = 2; at N = 2, k = 1
+// (profiles/r04zn/: a shard's sweep and its widest window of B keys -- the
+// trail each rank adds -- from kernel traces: 2.24 + 0.83 ms at k = 1 against
+// 3.12 + 0.54 ms at k = 2 under the profiler; equal at N = 4, k = 2 ahead at
+// N = 8).  A
 // key's planes have outer digit sums s = rB + o + c = rB + key - (k - 1) c of
 // several residues mod 4: with the relative word forms the staged lists deal
 // each key's planes by s mod 4 in whole wave visits (padded) and the kernel
@@ -211,7 +215,7 @@ static uint32_t plane_stage_k(int world) {
     const int k = atoi(e);
     if (k >= 1 && k <= 64) return (uint32_t)k;
   }
-  return 2u;
+  return world == 2 ? 1u : 2u;
 }
 // list padding of the relative forms' staged deal: at most 3 entries per
 // (key, s mod 4) class
