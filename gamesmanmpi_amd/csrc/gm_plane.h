@@ -7,10 +7,19 @@
 // distribute -> resolve with _res_red/_remote_red) by a sweep over PLANES:
 //
 //   position (h0, h1, P), P = mixed-radix index of the outer heaps
-//   h2..h(K-1) ("plane"), stored at
-//       word[P * 1024 + h1 * 32 + ((h0 + h1) & 31)]
-//   i.e. planes of 32 x 32 positions, rows of 32, each row ROTATED left by
-//   its row number.  A plane is 1 KiB (8-bit words) or 2 KiB (16-bit).
+//   h2..h(K-1) ("plane"): planes of 32 x 32 positions, rows of 32, each row
+//   ROTATED left by its row number -- byte b = (h0 + h1) & 31 of row h1 --
+//   and every row cut into 16-B PIECES, piece c of all 32 rows side by side:
+//       byte  P * 1024 + c * 512 + h1 * 16 + (b & 15),  c = b >> 4  (8-bit)
+//       word  P * 1024 + c * 256 + h1 * 8 + (b & 7),    c = b >> 3  (16-bit)
+//   (plane_word_index).  A plane is 1 KiB (8-bit words) or 2 KiB (16-bit).
+//   Lane h1 still loads and stores its row as 16-B pieces, but a half-wave's
+//   32 pieces of one instruction are now 512 CONTIGUOUS bytes: four whole
+//   128-B lines.  With rows contiguous instead (round 4), each store
+//   instruction wrote half of 8 lines, and the L2 filled every line from
+//   memory before the second half arrived: +1 KiB of fetch per plane written
+//   (FETCH_SIZE 4.26 -> 3.70 GB per 2^30 backward in tools/stream_lab.hip
+//   var 14 vs 19), a third of the fabric reads of the wide plane levels.
 //
 // One move lowers ONE heap by 1 or 2 (test_games/four_to_one.py:7-22), so a
 // position's children lie in its own plane (h0 / h1 lowered) or at the same
@@ -117,6 +126,19 @@ struct PlaneEntry {
   uint32_t top2;   // neighbour at top value - 2: the same
   uint32_t send;   // halo plane index in the send buffer (boundary slices), or kPlaneAbsent
 };
+
+// element index of byte / word b (rotated row position) of row h1 of plane
+// P (T = 8- or 16-bit words)
+__host__ __device__ inline uint64_t plane_word_index(uint64_t P, uint32_t h1, uint32_t b, uint32_t wb) {
+  return wb == 2 ? P * 1024u + (uint64_t)(b >> 3) * 256u + h1 * 8u + (b & 7u)
+                 : P * 1024u + (uint64_t)(b >> 4) * 512u + h1 * 16u + (b & 15u);
+}
+// in elements of T: a lane's first piece in its plane, and the piece stride
+template <typename T>
+__host__ __device__ constexpr uint32_t plane_row0(uint32_t h1) { return h1 * (16u / (uint32_t)sizeof(T)); }
+template <typename T>
+__host__ __device__ constexpr uint32_t plane_piece() { return 512u / (uint32_t)sizeof(T); }
+constexpr int kPieceU4 = 32;  // piece stride in uint4 (512 B)
 
 template <int WB>
 struct PlaneWord;
@@ -274,7 +296,7 @@ __device__ __forceinline__ void plane_x1_range(typename PlaneWord<WB>::T* __rest
     const uint32_t P = e.p;
     uint32_t dig[NO > 0 ? NO : 1];
     plane_digits<NO>(g, P, dig);
-    const size_t rowoff = (size_t)P * 1024u + L * 32u;  // in words
+    const size_t rowoff = (size_t)P * 1024u + plane_row0<typename W::T>(L);  // in words: the row's first piece
     // external children: rows of the neighbour planes, folded into E
     uint32_t Ehi[DW], Elo[WB == 1 ? DW : 1];
 #pragma unroll
@@ -291,13 +313,13 @@ __device__ __forceinline__ void plane_x1_range(typename PlaneWord<WB>::T* __rest
           const uint32_t w = k == 1 ? e.top1 : e.top2;
           src = w == kPlaneAbsent ? zero
                 : w == kPlaneLocal ? (const uint4*)(tab + rowoff - (size_t)k * g.Z * 1024u)
-                                   : (const uint4*)(recv + (size_t)w * 1024u + L * 32u);
+                                   : (const uint4*)(recv + (size_t)w * 1024u + plane_row0<typename W::T>(L));
         } else {
           src = dig[j] >= (uint32_t)k ? (const uint4*)(tab + rowoff - (size_t)k * g.stride[j] * 1024u) : zero;
         }
         uint4 v[NQ];
 #pragma unroll
-        for (int q = 0; q < NQ; q++) v[q] = src[q];
+        for (int q = 0; q < NQ; q++) v[q] = src[q * kPieceU4];
 #pragma unroll
         for (int q = 0; q < NQ; q++) {
           const uint32_t x[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
@@ -351,11 +373,13 @@ __device__ __forceinline__ void plane_x1_range(typename PlaneWord<WB>::T* __rest
     if (live) {
       uint4* dst = (uint4*)(tab + rowoff);
 #pragma unroll
-      for (int q = 0; q < NQ; q++) dst[q] = make_uint4(out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]);
+      for (int q = 0; q < NQ; q++)
+        dst[q * kPieceU4] = make_uint4(out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]);
       if (SH && e.send != kPlaneAbsent) {  // a boundary slice: also into the send buffer
-        uint4* sd = (uint4*)(send + (size_t)e.send * 1024u + L * 32u);
+        uint4* sd = (uint4*)(send + (size_t)e.send * 1024u + plane_row0<typename W::T>(L));
 #pragma unroll
-        for (int q = 0; q < NQ; q++) sd[q] = make_uint4(out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]);
+        for (int q = 0; q < NQ; q++)
+          sd[q * kPieceU4] = make_uint4(out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]);
       }
     }
   }
@@ -467,7 +491,7 @@ __device__ __forceinline__ void plane_x2_visit(typename PlaneWord<WB>::T* __rest
   uint32_t dx[NO > 0 ? NO : 1], dy[NO > 0 ? NO : 1];
   plane_digits<NO>(g, ex.p, dx);
   plane_digits<NO>(g, ey.p, dy);
-  const size_t ox = (size_t)ex.p * 1024u + L * 32u, oy = (size_t)ey.p * 1024u + L * 32u;
+  const size_t ox = (size_t)ex.p * 1024u + plane_row0<T>(L), oy = (size_t)ey.p * 1024u + plane_row0<T>(L);
   // E rows of both planes (8-bit: odd bytes exact in Ehi, even bytes in
   // the high bytes of Elo; 16-bit: Ehi exact)
   uint32_t Xh[DW], Xl[B8 ? DW : 1], Yh[DW], Yl[B8 ? DW : 1];
@@ -481,7 +505,7 @@ __device__ __forceinline__ void plane_x2_visit(typename PlaneWord<WB>::T* __rest
       const uint32_t w = k == 1 ? e.top1 : e.top2;
       return w == kPlaneAbsent ? zero
              : w == kPlaneLocal ? (const uint4*)(tab + off - (size_t)k * g.Z * 1024u)
-                                : (const uint4*)(recv + (size_t)w * 1024u + L * 32u);
+                                : (const uint4*)(recv + (size_t)w * 1024u + plane_row0<T>(L));
     }
     return dig[j] >= (uint32_t)k ? (const uint4*)(tab + off - (size_t)k * g.stride[j] * 1024u) : zero;
   };
@@ -500,11 +524,11 @@ __device__ __forceinline__ void plane_x2_visit(typename PlaneWord<WB>::T* __rest
     uint4 vx1[NQ], vy1[NQ], vx2[NQ], vy2[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; q++) {
-      vx1[q] = sx1[q];
-      vy1[q] = sy1[q];
+      vx1[q] = sx1[q * kPieceU4];
+      vy1[q] = sy1[q * kPieceU4];
       if (two) {
-        vx2[q] = sx2[q];
-        vy2[q] = sy2[q];
+        vx2[q] = sx2[q * kPieceU4];
+        vy2[q] = sy2[q * kPieceU4];
       }
     }
 #pragma unroll
@@ -669,15 +693,15 @@ __device__ __forceinline__ void plane_x2_visit(typename PlaneWord<WB>::T* __rest
   auto store = [&](T* dst, const uint32_t* o) {
     uint4* p = (uint4*)dst;
 #pragma unroll
-    for (int q = 0; q < NQ; q++) p[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+    for (int q = 0; q < NQ; q++) p[q * kPieceU4] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
   };
   if (livex) {
     store(tab + ox, ox_);
-    if (SH && ex.send != kPlaneAbsent) store(send + (size_t)ex.send * 1024u + L * 32u, ox_);
+    if (SH && ex.send != kPlaneAbsent) store(send + (size_t)ex.send * 1024u + plane_row0<T>(L), ox_);
   }
   if (livey) {
     store(tab + oy, oy_);
-    if (SH && ey.send != kPlaneAbsent) store(send + (size_t)ey.send * 1024u + L * 32u, oy_);
+    if (SH && ey.send != kPlaneAbsent) store(send + (size_t)ey.send * 1024u + plane_row0<T>(L), oy_);
   }
 }
 

@@ -33,7 +33,7 @@ __global__ __launch_bounds__(256) void k_plane_reach(uint32_t* bits, PlaneGeom g
 // the position's digit sum (all heaps; read by the relative forms only)
 template <int WB>
 __device__ __forceinline__ uint32_t plane_vr(const void* tab, u64 P, uint32_t h0, uint32_t h1, uint32_t e) {
-  const u64 i = P * 1024u + h1 * 32u + ((h0 + h1) & 31u);
+  const u64 i = plane_word_index(P, h1, (h0 + h1) & 31u, WB == 2 ? 2u : 1u);
   const uint32_t w = WB == 2 ? ((const uint16_t*)tab)[i] : ((const uint8_t*)tab)[i];
   return WB == 3 ? plane_rel_to_vr(w, e) : plane_word_to_vr(w, WB);
 }
@@ -929,6 +929,42 @@ static int plane_check_stage(std::vector<gm_solver*>& ss, int mode, hipStream_t 
   return 0;
 }
 
+// Fault injection for the failure tests only: GM_FAULT_STAGED="rank:key"
+// makes shard `rank` fail at key `key` of the staged backward as a DEFERRED
+// error (below); "rank:key:early" returns at once instead -- the path that
+// solve_multi's communicator abort has to bound.  Unset: no effect.
+struct StagedFault {
+  int rank = -1;
+  uint32_t key = 0;
+  bool early = false;
+};
+static StagedFault staged_fault() {
+  StagedFault f;
+  const char* e = getenv("GM_FAULT_STAGED");
+  if (!e || !*e) return f;
+  unsigned r = 0, k = 0;
+  char tail[16] = {0};
+  const int n = sscanf(e, "%u:%u:%15s", &r, &k, tail);
+  if (n >= 2) {
+    f.rank = (int)r;
+    f.key = k;
+    f.early = n == 3 && strcmp(tail, "early") == 0;
+  }
+  return f;
+}
+__global__ void k_err_or(DevState* st, uint32_t e) {
+  if (threadIdx.x == 0) st->err |= e;
+}
+// a deferred failure (herr, already reported through fail()): remembered on
+// the shard, and ERR_SHARD_FAILED set in its error word for the reduction
+static int staged_defer(gm_solver* s, int herr, hipStream_t st) {
+  if (!herr) return 0;
+  s->defer_rc = herr;
+  s->defer_msg = gm_last_error();
+  hipLaunchKernelGGL(k_err_or, dim3(1), dim3(64), 0, st, s->st, (uint32_t)ERR_SHARD_FAILED);
+  return 0;
+}
+
 // The staged backward (see plane_stage_k): every rank walks its keys; row s
 // of the halo is waited for before key k s and sent after key B - 1 + k s.
 //  mode 2 (in-process group, one stream): shard after shard, rows copied to
@@ -946,6 +982,13 @@ static int plane_check_stage(std::vector<gm_solver*>& ss, int mode, hipStream_t 
 //    copy on the receiver's receive stream in place of each ncclSend /
 //    ncclRecv pair.  What only RCCL itself exercises: ncclCommSplit, the
 //    send / receive matching on the two communicators, RCCL's own progress.
+// Failures of a rank's own work (a stream / event call, a launch) are
+// DEFERRED in modes 1, 3 and 4: the rank stops computing but keeps posting
+// every halo send and receive of its schedule, so its peers finish their
+// keys instead of waiting forever in a receive, marks ERR_SHARD_FAILED in its
+// error word, which the end-of-solve reduction hands to every rank, and
+// reports its own error there (s->defer_rc).  Only a failed transfer call
+// returns at once: the exchange itself is then broken.
 static int plane_backward_staged(std::vector<gm_solver*>& ss, int mode, hipStream_t st, u64* nlaunch) {
   gm_solver* s0 = ss[0];
   const uint32_t k = s0->pstage_k, K = s0->pkeys, R = s0->prows, B = s0->pg.B;
@@ -1002,8 +1045,14 @@ static int plane_backward_staged(std::vector<gm_solver*>& ss, int mode, hipStrea
     const bool rx = rank > 0, tx = rank + 1 < W;
     auto rbuf = [&](uint32_t r, u64* n) { return (void*)((char*)s->precv + seg(s->prcv_off, r, n) * pb); };
     auto sbuf = [&](uint32_t r, u64* n) { return (void*)((char*)s->psend + seg(s->psnd_off, r, n) * pb); };
+    const StagedFault fault = staged_fault();
+    int herr = 0;  // deferred failure (see above)
     for (uint32_t key = 0; key < K; key++) {
       uint32_t r;
+      if (!herr && fault.rank == rank && fault.key == key) {
+        herr = fail(GM_EHIP, "injected fault: shard %d at key %u", rank, key);
+        if (fault.early) return herr;
+      }
       if (rx && row_need(key, &r)) {
         bat.flush();
         u64 n;
@@ -1013,7 +1062,7 @@ static int plane_backward_staged(std::vector<gm_solver*>& ss, int mode, hipStrea
         int rc = xfer_ranges(s, out, -1, in, rank - 1, st);
         if (rc) return rc;
       }
-      launch_key(bat, key);
+      if (!herr) launch_key(bat, key);
       if (tx && row_done(key, &r)) {
         bat.flush();
         u64 n;
@@ -1026,18 +1075,21 @@ static int plane_backward_staged(std::vector<gm_solver*>& ss, int mode, hipStrea
     }
     bat.flush();
     *nlaunch = bat.launches;
-    return 0;
+    return staged_defer(s, herr, st);
   }
   // mode 1 (RCCL) and mode 4 (its one-GPU rehearsal): the same key loop,
   // receive window, streams, events and joins per shard; only the two
   // transfer calls differ.  Per shard: compute stream s->stream, send
   // stream ts, receive stream rs; RE[r] row r received, SE[r] row r final
   // here, XS[r] row r handed to the send stream's transfer.
+  const StagedFault fault = staged_fault();
   auto staged_rank = [&](gm_solver* s, auto&& recv_op, auto&& send_op) -> int {
     PlaneBatcher bat(s);
     const int rank = s->rank;
     const bool rx = rank > 0, tx = rank + 1 < W;
     hipStream_t cst = s->stream;
+    // set-up (before any transfer of this rank: a failure here is returned
+    // at once, as a mode-1 peer's matching calls have not been posted either)
     if (!s->cstream) HIPCHK(hipStreamCreateWithFlags(&s->cstream, hipStreamNonBlocking));
     if (!s->cstream2) HIPCHK(hipStreamCreateWithFlags(&s->cstream2, hipStreamNonBlocking));
     while (s->pev.size() < 3 * (size_t)R + 3) {
@@ -1050,9 +1102,13 @@ static int plane_backward_staged(std::vector<gm_solver*>& ss, int mode, hipStrea
     hipEvent_t* XS = SE + R;             // row r's send issued on the send stream
     hipEvent_t* XE = XS + R;             // [0] start, [1] sends done, [2] receives done
     hipStream_t ts = s->cstream, rs = s->cstream2;
-    HIPCHK(hipEventRecord(XE[0], cst));
-    HIPCHK(hipStreamWaitEvent(ts, XE[0], 0));
-    HIPCHK(hipStreamWaitEvent(rs, XE[0], 0));
+    int herr = 0;  // deferred failure: compute stops, the transfers go on
+    auto dchk = [&](hipError_t e, const char* what) {
+      if (e != hipSuccess && !herr) herr = fail(GM_EHIP, "%s: %s", what, hipGetErrorString(e));
+    };
+    dchk(hipEventRecord(XE[0], cst), "hipEventRecord");
+    dchk(hipStreamWaitEvent(ts, XE[0], 0), "hipStreamWaitEvent");
+    dchk(hipStreamWaitEvent(rs, XE[0], 0), "hipStreamWaitEvent");
     constexpr uint32_t kAhead = 8;  // rows whose receives are posted ahead of the key that reads them
     uint32_t posted = 0;            // rows [0, posted) have their receive posted
     auto post_to = [&](uint32_t lim) -> int {
@@ -1061,39 +1117,43 @@ static int plane_backward_staged(std::vector<gm_solver*>& ss, int mode, hipStrea
         void* b = (void*)((char*)s->precv + seg(s->prcv_off, posted, &n) * pb);
         int rc = recv_op(s, posted, b, n, rs);
         if (rc) return rc;
-        HIPCHK(hipEventRecord(RE[posted], rs));
+        dchk(hipEventRecord(RE[posted], rs), "hipEventRecord");
       }
       return 0;
     };
     for (uint32_t key = 0; key < K; key++) {
       uint32_t r;
+      if (!herr && fault.rank == rank && fault.key == key) {
+        herr = fail(GM_EHIP, "injected fault: shard %d at key %u", rank, key);
+        if (fault.early) return herr;
+      }
       if (rx && row_need(key, &r)) {
         bat.flush();
         int rc = post_to(r + 1 + kAhead);
         if (rc) return rc;
-        HIPCHK(hipStreamWaitEvent(cst, RE[r], 0));
+        dchk(hipStreamWaitEvent(cst, RE[r], 0), "hipStreamWaitEvent");
       }
-      launch_key(bat, key);
+      if (!herr) launch_key(bat, key);
       if (tx && row_done(key, &r)) {
         bat.flush();
-        HIPCHK(hipEventRecord(SE[r], cst));
-        HIPCHK(hipStreamWaitEvent(ts, SE[r], 0));
+        dchk(hipEventRecord(SE[r], cst), "hipEventRecord");
+        dchk(hipStreamWaitEvent(ts, SE[r], 0), "hipStreamWaitEvent");
         u64 n;
         void* b = (void*)((char*)s->psend + seg(s->psnd_off, r, &n) * pb);
         int rc = send_op(s, r, b, n, ts);
         if (rc) return rc;
-        HIPCHK(hipEventRecord(XS[r], ts));
+        dchk(hipEventRecord(XS[r], ts), "hipEventRecord");
       }
     }
     bat.flush();
     if (rank == 0 || mode == 1) *nlaunch = bat.launches;
     int rc = post_to(R);
     if (rc) return rc;
-    HIPCHK(hipEventRecord(XE[1], ts));
-    HIPCHK(hipEventRecord(XE[2], rs));
-    HIPCHK(hipStreamWaitEvent(cst, XE[1], 0));
-    HIPCHK(hipStreamWaitEvent(cst, XE[2], 0));
-    return 0;
+    dchk(hipEventRecord(XE[1], ts), "hipEventRecord");
+    dchk(hipEventRecord(XE[2], rs), "hipEventRecord");
+    dchk(hipStreamWaitEvent(cst, XE[1], 0), "hipStreamWaitEvent");
+    dchk(hipStreamWaitEvent(cst, XE[2], 0), "hipStreamWaitEvent");
+    return staged_defer(s, herr, cst);
   };
   if (mode == 4) {
     // the ranks' host loops in pipeline order (a row's XS event exists before
@@ -1182,6 +1242,10 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
                   s0->pform == 3 ? " relative" : "");
   }
   const bool staged = mode != 0 && s0->pstage_k;
+  for (gm_solver* s : ss) {
+    s->defer_rc = 0;
+    s->defer_msg.clear();
+  }
   if (mode != 0 && !s0->halo_ok) {
     int rc = staged ? plane_check_stage(ss, mode, st) : plane_check_plan(ss, mode, st);
     if (rc) return rc;
@@ -1340,7 +1404,14 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
   bat0.flush();  // a stop inside a run
   if (!staged) nlaunch = mode == 0 && !per_level ? bat0.launches : (u64)(S + 1) * (pipe ? 2 : 1);
   if (last_x >= 0) HIPCHK(hipStreamWaitEvent(st, PE[S + 1 + last_x], 0));  // join the comm stream
-  HIPCHK(hipGetLastError());
+  {
+    const hipError_t e = hipGetLastError();  // (a failed launch of the backward)
+    if (e != hipSuccess) {
+      if (!staged || mode == 2) return fail(GM_EHIP, "plane backward: %s", hipGetErrorString(e));
+      // staged shards: deferred, so the end-of-solve reduction is still entered
+      if (!s0->defer_rc) staged_defer(s0, fail(GM_EHIP, "plane backward: %s", hipGetErrorString(e)), st);
+    }
+  }
   if (join()) return GM_EHIP;
   HIPCHK(hipEventRecord(e2, st));
   if (overlap) HIPCHK(hipStreamWaitEvent(st, e1, 0));  // the counts and state resets before the finish
@@ -1421,7 +1492,11 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
   out->kernels = (plane_x1(s0) ? RK_PLANE : RK_PLANE_X2) | (PK_PLANE << 16);
   const uint32_t word = red[3] ? (uint32_t)(red[3] - 1) : NO_WORD;
   out->root_word = word;
-  if (red[4]) return fail(GM_ECORRUPT, "solve failed:%s", err_text((uint32_t)red[4]).c_str());
+  if (red[4]) {
+    for (gm_solver* s : ss)  // this process's shard failed: its own error
+      if (s->defer_rc) return fail(s->defer_rc, "shard %d/%d: %s", s->rank, s->world, s->defer_msg.c_str());
+    return fail(GM_ECORRUPT, "solve failed:%s", err_text((uint32_t)red[4]).c_str());
+  }
   if (word == NO_WORD) return fail(GM_ECORRUPT, "root unresolved");
   out->root_value = (int32_t)(word & 3u);
   out->root_remoteness = word >> 2;

@@ -85,6 +85,10 @@ enum : uint32_t {
   ERR_CHILD_UNRESOLVED = 16u,
   ERR_NO_MOVES = 32u,
   ERR_SELF_MISSING = 64u,
+  // a shard failed on its host side (a deferred error: it kept serving its
+  // halo transfers so that its peers finished, then reported through the
+  // end-of-solve reduction; gm_plane_run.h plane_backward_staged)
+  ERR_SHARD_FAILED = 512u,
 };
 
 // ---------------------------------------------------------------------------
@@ -1043,6 +1047,8 @@ struct gm_solver {
   // per key / per row; k = key skew, K keys, rows 0..smax
   uint32_t pstage_k = 0, pkeys = 0, prows = 0;
   ncclComm_t comm2 = nullptr;        // second communicator (ncclCommSplit): the other halo direction
+  int defer_rc = 0;                  // a deferred failure of this shard's last solve (0: none)
+  std::string defer_msg;
   hipStream_t cstream2 = nullptr;    // receive stream of the staged exchange
   // RANKED (gm_ranked.h)
   RankGeom rg{};
@@ -1347,6 +1353,7 @@ static std::string err_text(uint32_t e) {
   if (e & ERR_SELF_MISSING) s += " self-missing";
   if (e & ERR_BUCKET_FULL) s += " hash-bucket-over-capacity";
   if (e & ERR_EDGE_COUNT) s += " edge-count-mismatch";
+  if (e & ERR_SHARD_FAILED) s += " shard-failed";
   return s;
 }
 
@@ -3779,6 +3786,13 @@ static void multi_destroy(MultiSolve& m) {
   (void)hipSetDevice(cur);
 }
 
+// Failure in bounded time: every early return goes through bail (shards and
+// communicators freed, the caller's device restored).  A shard whose solve
+// fails on its own side defers the error to the end-of-solve reduction (the
+// staged PLANES backward, the md5 BUCKETED levels), so its peers finish; a
+// shard whose solve returns while its peers may still wait in an RCCL call
+// (an early return) aborts EVERY communicator of the group (ncclCommAbort:
+// the peers' pending calls return with an error), so join() always returns.
 static int solve_multi(int game, int ngpus, const gm_buffers* buf, gm_result* out) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
@@ -3792,15 +3806,17 @@ static int solve_multi(int game, int ngpus, const gm_buffers* buf, gm_result* ou
   std::vector<ncclComm_t> comms((size_t)ngpus, nullptr);
   std::vector<int> devs((size_t)ngpus);
   for (int i = 0; i < ngpus; i++) devs[(size_t)i] = i;
+  bool aborted = false;  // every communicator aborted (and detached from its shard)
   auto bail = [&](int rc) {
-    for (size_t i = 0; i < comms.size(); i++)
-      if (comms[i] && !(m.ss[i] && m.ss[i]->comm == comms[i])) (void)ncclCommDestroy(comms[i]);
+    if (!aborted)
+      for (size_t i = 0; i < comms.size(); i++)
+        if (comms[i] && !(m.ss[i] && m.ss[i]->comm == comms[i])) (void)ncclCommDestroy(comms[i]);
     multi_destroy(m);
     (void)hipSetDevice(cur);
     return rc;
   };
   for (int i = 0; i < ngpus; i++) {
-    HIPCHK(hipSetDevice(i));
+    if (hipSetDevice(i) != hipSuccess) return bail(fail(GM_EHIP, "hipSetDevice(%d)", i));
     const int rc = gm_solver_create_shard(game, i, ngpus, &buf[i], &m.ss[(size_t)i]);
     if (rc) return bail(fail(rc, "shard %d: %s", i, gm_last_error()));
   }
@@ -3809,26 +3825,48 @@ static int solve_multi(int game, int ngpus, const gm_buffers* buf, gm_result* ou
   for (int i = 0; i < ngpus; i++) {
     gm_solver* sh = m.ss[(size_t)i];
     sh->comm = comms[(size_t)i];
-    HIPCHK(hipSetDevice(i));
+    if (hipSetDevice(i) != hipSuccess) return bail(fail(GM_EHIP, "hipSetDevice(%d)", i));
     if (!sh->errg && hipMalloc((void**)&sh->errg, (size_t)ngpus * sizeof(u64)) != hipSuccess)
       return bail(fail(GM_EHIP, "error-mask gather buffer"));
   }
   std::vector<gm_result> res((size_t)ngpus);
   std::vector<int> rcs((size_t)ngpus, 0);
   std::vector<std::string> msg((size_t)ngpus);
+  std::mutex abort_mu;  // one abort of the whole group, by the first thread that fails
+  auto abort_all = [&]() {
+    std::lock_guard<std::mutex> lk(abort_mu);
+    if (aborted) return;
+    aborted = true;
+    for (size_t i = 0; i < comms.size(); i++)
+      if (comms[i]) (void)ncclCommAbort(comms[i]);
+    // (the second communicators of the staged deal are split from these and
+    // are aborted with the shards' own below, after the join)
+  };
   std::vector<std::thread> th;
   for (int i = 0; i < ngpus; i++)
     th.emplace_back([&, i]() {
       if (hipSetDevice(i) != hipSuccess) {
         rcs[(size_t)i] = GM_EHIP;
         msg[(size_t)i] = "hipSetDevice";
+        abort_all();
         return;
       }
       rcs[(size_t)i] = gm_solver_solve(m.ss[(size_t)i], &res[(size_t)i]);
-      if (rcs[(size_t)i]) msg[(size_t)i] = gm_last_error();
+      if (rcs[(size_t)i]) {
+        msg[(size_t)i] = gm_last_error();
+        // a deferred failure has already taken every peer through the
+        // reduction; any other failure may leave them waiting: abort
+        if (!m.ss[(size_t)i]->defer_rc) abort_all();
+      }
     });
   for (auto& t : th) t.join();
   (void)hipSetDevice(cur);
+  if (aborted)  // the aborted communicators are not destroyed again with the shards
+    for (gm_solver* sh : m.ss)
+      if (sh) {
+        if (sh->comm2) (void)ncclCommAbort(sh->comm2);
+        sh->comm = sh->comm2 = nullptr;
+      }
   for (int i = 0; i < ngpus; i++)
     if (rcs[(size_t)i]) return bail(fail(rcs[(size_t)i], "shard %d: %s", i, msg[(size_t)i].c_str()));
   *out = res[0];
