@@ -152,12 +152,26 @@ def _kernel_sources_sha16():
         sys.path.pop(0)
 
 
+def _kernel_code_sha16(kernel):
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    try:
+        from codeobj import kernel_code_sha16
+        return kernel_code_sha16(os.path.join(ROOT, "gamesmanmpi_amd", "libgamesman_hip.so"), kernel)
+    except ImportError:
+        return None
+    finally:
+        sys.path.pop(0)
+
+
 def _pmc_row(kernel, workload):
     """The committed PMC summary's row for `kernel` (profiles/pmc_traffic.json,
     tools/pmc_summary.py --traffic over separate rocprofv3 --pmc passes of
     this bench) and a note: None when no pass of this workload and kernel is
-    recorded, or when the kernel sources changed since the passes ran (the
-    counters describe other code: rerun tools/gpu_session.sh TAG pmc)."""
+    recorded, or when the kernel's machine code changed since the passes ran
+    (the counters describe other code: rerun tools/gpu_session.sh TAG pmc).
+    The key is the measured kernel's own gfx950 code (tools/codeobj.py), so
+    host-side edits and other kernels leave the figure valid; rows written
+    before that key existed fall back to the kernel-source hash."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as fh:
@@ -166,6 +180,12 @@ def _pmc_row(kernel, workload):
         return None, None
     if not row or row.get("workload") != workload:
         return None, None
+    if "kernel_code_sha16" in row:
+        now = _kernel_code_sha16(kernel)
+        if not now or row["kernel_code_sha16"] != now:
+            return None, "stale: profiles/pmc_traffic.json (%s) measured %s code %s, this library's is %s" % (
+                row.get("source", "?"), kernel, row["kernel_code_sha16"], now)
+        return row, "profiles/pmc_traffic.json (%s, %s code %s)" % (row.get("source", "?"), kernel, now)
     now = _kernel_sources_sha16()
     if row.get("kernel_sources_sha16") != now:
         return None, "stale: profiles/pmc_traffic.json (%s) measured kernel sources %s, these are %s" % (

@@ -476,7 +476,7 @@ __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
 #ifndef GM_PLANE_RSV_UNR
 #define GM_PLANE_RSV_UNR false
 #endif
-template <int WB, int NO, bool SH, int RS_, bool UNR = true>
+template <int WB, int NO, bool SH, int RS_, bool UNR = true, bool WT = false>
 __device__ __forceinline__ void plane_x2_visit(typename PlaneWord<WB>::T* __restrict__ tab, const PlaneGeom& g,
                                                const uint4* __restrict__ zero,
                                                const typename PlaneWord<WB>::T* __restrict__ recv,
@@ -690,10 +690,25 @@ __device__ __forceinline__ void plane_x2_visit(typename PlaneWord<WB>::T* __rest
       oy_[k] = perm(op[2 * k + 1], op[2 * k], 0x07060302u);
     }
   }
+  // WT (the per-level grid launches): write-through (sc1) vector stores --
+  // the next level is a new launch whose readers find nothing of this one in
+  // their L2 anyway, and the lines leave while the kernel still runs instead
+  // of in the write-back at its end: 1.342 -> 1.283-1.292 ms per 2^30
+  // backward (tools/stream_lab.hip, GM_PLANE_STORE_POLICY builds; nt stores
+  // 1.42 ms).  (An inline-asm store the compiler does not count in vmcnt only
+  // makes its later waits stricter: it is the youngest operation.)
   auto store = [&](T* dst, const uint32_t* o) {
     uint4* p = (uint4*)dst;
 #pragma unroll
-    for (int q = 0; q < NQ; q++) p[q * kPieceU4] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+    for (int q = 0; q < NQ; q++) {
+      if constexpr (WT) {
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        const v4u v = {o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]};
+        asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p + q * kPieceU4), "v"(v) : "memory");
+      } else {
+        p[q * kPieceU4] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+      }
+    }
   };
   if (livex) {
     store(tab + ox, ox_);
@@ -708,7 +723,7 @@ __device__ __forceinline__ void plane_x2_visit(typename PlaneWord<WB>::T* __rest
 // (RS: with WB = 3, the launch's outer digit sum s mod 4; -1: per wave
 // visit, from its first plane -- the list deals every four consecutive
 // entries one s mod 4, padding with kPlaneAbsent entries)
-template <int WB, int NO, bool SH, int RS = 0>
+template <int WB, int NO, bool SH, int RS = 0, bool WT = false>
 __device__ __forceinline__ void plane_x2_range(typename PlaneWord<WB>::T* __restrict__ tab,
                                                const void* __restrict__ list, const PlaneShare sh,
                                                const PlaneGeom& g, const uint4* __restrict__ zero,
@@ -732,17 +747,17 @@ __device__ __forceinline__ void plane_x2_range(typename PlaneWord<WB>::T* __rest
       ey.p = ((const uint32_t*)list)[livey ? iy : i0];
     }
     if constexpr (RS >= 0) {
-      plane_x2_visit<WB, NO, SH, RS>(tab, g, zero, recv, send, ex, ey, livex, livey);
+      plane_x2_visit<WB, NO, SH, RS, true, WT>(tab, g, zero, recv, send, ex, ey, livex, livey);
     } else {  // the visit's outer digit sum (global digits) mod 4, wave-uniform
       uint32_t dg[NO > 0 ? NO : 1], sum = 0;
       plane_global_digits<NO>(g, ex.p, dg);
 #pragma unroll
       for (int j = 0; j < NO; j++) sum += dg[j];
       switch (__builtin_amdgcn_readfirstlane(sum) & 3u) {
-        case 0: plane_x2_visit<WB, NO, SH, 0, GM_PLANE_RSV_UNR>(tab, g, zero, recv, send, ex, ey, livex, livey); break;
-        case 1: plane_x2_visit<WB, NO, SH, 1, GM_PLANE_RSV_UNR>(tab, g, zero, recv, send, ex, ey, livex, livey); break;
-        case 2: plane_x2_visit<WB, NO, SH, 2, GM_PLANE_RSV_UNR>(tab, g, zero, recv, send, ex, ey, livex, livey); break;
-        default: plane_x2_visit<WB, NO, SH, 3, GM_PLANE_RSV_UNR>(tab, g, zero, recv, send, ex, ey, livex, livey); break;
+        case 0: plane_x2_visit<WB, NO, SH, 0, GM_PLANE_RSV_UNR, WT>(tab, g, zero, recv, send, ex, ey, livex, livey); break;
+        case 1: plane_x2_visit<WB, NO, SH, 1, GM_PLANE_RSV_UNR, WT>(tab, g, zero, recv, send, ex, ey, livex, livey); break;
+        case 2: plane_x2_visit<WB, NO, SH, 2, GM_PLANE_RSV_UNR, WT>(tab, g, zero, recv, send, ex, ey, livex, livey); break;
+        default: plane_x2_visit<WB, NO, SH, 3, GM_PLANE_RSV_UNR, WT>(tab, g, zero, recv, send, ex, ey, livex, livey); break;
       }
     }
   }
@@ -756,7 +771,7 @@ __global__ __launch_bounds__(256) void k_plane_resolve_x2(typename PlaneWord<WB>
                                                           typename PlaneWord<WB>::T* __restrict__ send,
                                                           const uint32_t* __restrict__ pf, uint32_t pflines) {
   const uint32_t v = plane_prefetch(pf, pflines);
-  plane_x2_range<WB, NO, SH, RS>(tab, list, plane_share(n, 4), g, zero, recv, send);
+  plane_x2_range<WB, NO, SH, RS, true>(tab, list, plane_share(n, 4), g, zero, recv, send);
   plane_keep(v);
 }
 

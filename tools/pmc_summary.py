@@ -50,7 +50,11 @@ def kernel_sources_sha16(root_dir):
 def traffic(workload, out_path, root):
     per, launches = load(root)
     res = {}
-    src_sha = kernel_sources_sha16(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src_sha = kernel_sources_sha16(repo)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from codeobj import kernel_code_sha16
+    so = os.path.join(repo, "gamesmanmpi_amd", "libgamesman_hip.so")
     for name, ctr in per.items():
         if "FETCH_SIZE" not in ctr or "WRITE_SIZE" not in ctr:
             continue
@@ -60,7 +64,9 @@ def traffic(workload, out_path, root):
         w = ctr["WRITE_SIZE"] * 1024 / n
         row = {"workload": workload, "bytes_per_launch": f + w,
                "fetch_bytes_per_launch": f, "write_bytes_per_launch": w,
-               "launches": n, "source": root, "kernel_sources_sha16": src_sha}
+               "launches": n, "source": root, "kernel_sources_sha16": src_sha,
+               # the key bench.py checks: the measured kernel's own gfx950 code
+               "kernel_code_sha16": kernel_code_sha16(so, short)}
         if "TCC_HIT_sum" in ctr:
             row["l2_hit_rate"] = ctr["TCC_HIT_sum"] / max(1.0, ctr["TCC_HIT_sum"] + ctr["TCC_MISS_sum"])
         res[short] = row
