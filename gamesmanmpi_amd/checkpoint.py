@@ -215,6 +215,11 @@ def restore(directory, device=None):
         # checkpoint was planned with (older checkpoints: from its plan mode)
         resolved = meta.get("layout_resolved") or _lib.MODE_NAMES.get(int(meta["plan"]["mode"]))
         if resolved:
+            # free the first table before the second is allocated: both at
+            # once would peak at, e.g., toot 6x4's RANKED plus BUCKETED tables
+            solver._free()
+            del solver
+            torch.cuda.empty_cache()
             solver = make(resolved)
     if _plan_dict(solver) != meta["plan"]:
         raise ValueError("checkpoint plan %r does not match this build's %r"

@@ -34,6 +34,10 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "gm_solver.hip is written for gfx950 (MI355X) only: v_bitop3_b32, v_pk_maximum3_f16 on f16 subnormals"
+#endif
+
 #include <algorithm>
 #include <chrono>
 #include <cstdarg>

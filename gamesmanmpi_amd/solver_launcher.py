@@ -117,6 +117,29 @@ def ranked_fits(spec, local):
     return p.table_bytes + p.scratch_bytes < 0.8 * free
 
 
+def agreed_ranked(spec, layout, local):
+    """Under torchrun: do ALL ranks take the replicated RANKED path?  Each
+    rank's own answer (ranked_fits: its GPU's free memory) is combined with a
+    MIN all-reduce, so every rank branches the same way and the collectives
+    of the path they take match (a rank alone on the md5 keyed path would
+    wait in its all-to-all for peers that never enter it).  An explicit
+    --layout ranked that does not fit on every rank is an error, not a silent
+    switch to the keyed path."""
+    import torch
+    import torch.distributed as dist
+    if layout not in ("auto", "ranked"):
+        return False
+    mine = bool(ranked_fits(spec, local))
+    dev = torch.device("cuda", local) if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([1 if mine else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    every = bool(int(t.item()))
+    if layout == "ranked" and not every:
+        raise SystemExit("--layout ranked: the RANKED table of %s does not fit on every rank's GPU "
+                         "(this rank: %s)" % (spec.name, "fits" if mine else "does not fit"))
+    return every
+
+
 def write_stats(statsdir, rank, spec, solver, result, world=1):
     """<statsdir>/stats/<rank>/solution.npz (+ meta.json).  world > 1 with a
     replicated table (every rank solved the whole game): this rank writes the
@@ -233,7 +256,7 @@ def main(argv=None):
             from gamesmanmpi_amd.dist import ShardedSolver
             solver = ShardedSolver(spec, rank, world, device="cuda:%d" % local)
             result = solver.solve()
-        elif args.layout in ("auto", "ranked") and ranked_fits(spec, local):
+        elif agreed_ranked(spec, args.layout, local):
             # toot-and-otto: the whole RANKED table fits one GPU (toot 6x4:
             # 8.9 GB, 17.5 ms) -- every rank solves it and writes the md5
             # share the reference's partition gives it; sharding it would

@@ -97,6 +97,9 @@ def test_checkpoint_restore_uses_the_resolved_layout(monkeypatch, tmp_path):
             self.buffers = ()
             self.device = device
 
+        def _free(self):  # the first table goes before the second is made
+            made.append("free")
+
     monkeypatch.setattr(checkpoint, "Solver", FakeSolver)
     monkeypatch.setattr(checkpoint, "GameSpec", lambda g, p: (g, p))
     monkeypatch.setattr(checkpoint, "latest", lambda d: d)
@@ -108,5 +111,5 @@ def test_checkpoint_restore_uses_the_resolved_layout(monkeypatch, tmp_path):
                     positions_hint=0, max_table_bytes=0, flags=0, plan=plan, step=4, steps=6, **meta_layout)
         monkeypatch.setattr(checkpoint, "read_meta", lambda d, m=meta: m)
         s, step = checkpoint.restore(str(tmp_path))
-        assert made == ["auto", "dense"] and step == 4
+        assert made == ["auto", "free", "dense"] and step == 4
         assert int(s.plan.mode) == _lib.GM_MODE_DENSE
