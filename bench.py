@@ -6,10 +6,12 @@ A "step" is one complete strong solve from the root: state reset, forward
 expansion of every level, retrograde pass of every level, root word back on
 the host.  N=1 workload: heaps 31^6 = 2^30 = 1,073,741,824 positions,
 187 levels, 12,280,922,112 edges.  For N>1 (one process per GPU, launched by
-torch.distributed.run) the heaps are 31^5 x (32N-1): 2^30 positions per
-GPU; the ranks split the last heap's values into blocks of 8 dealt round
-robin and exchange two boundary slices per block and level over RCCL
-(DESIGN.md §6).  Every step's counts, root value AND root remoteness are
+torch.distributed.run) the heaps are 31 x (32N-1) x 31^4: 2^30 positions per
+GPU (the game is symmetric in its heaps: the same state space as
+31^5 x (32N-1) with the long heap second); rank r holds heap-1 values
+[32r, 32r + 32) of every plane -- the one-GPU table's planes and levels -- and
+streams each level's last two rows to rank r + 1 over RCCL, which needs them
+for that level only (the row deal).  Every step's counts, root value AND root remoteness are
 checked: counts and value by closed forms, the remoteness against the
 CPU restatement's solve of the same workload (tests/golden/checksums.json,
 or this run's cpu_baseline).
@@ -43,15 +45,16 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
 
 
 def heaps_for(world):
-    """Weak scaling, 2^30 positions per GPU: heaps 31^5 x (32N - 1).  N=1 is
-    SURVEY §8d's 31^6 (2^30 positions, 187 levels, b = 11.4375).  The ranks
-    split the last heap into blocks of 8 values dealt round robin, four per
-    rank (round robin keeps the ranks' per-level work within
-    1.11 / 1.19 / 1.41x of the mean at N = 2 / 4 / 8; one contiguous block
-    of 32 per rank would give 1.51 / 2.53 / 4.58x)."""
+    """Weak scaling, 2^30 positions per GPU: heaps 31 x (32N - 1) x 31^4.  N=1
+    is SURVEY §8d's 31^6 (2^30 positions, 187 levels, b = 11.4375).  The long
+    heap is heap 1, the planes' row axis: rank r owns its values
+    [32r, 32r + 32), i.e. a 32 x 32 slab of every plane -- each rank's table
+    is the one-GPU table -- and the only cross-rank edge is rows 0, 1 reading
+    rank r - 1's rows 30, 31 of the same plane (round 4 split
+    the LAST heap in blocks of 32 and trailed by a block of keys per rank)."""
     if world not in (1, 2, 4, 8):
         raise SystemExit("--gpus must be 1, 2, 4 or 8")
-    return [31] * 5 + [32 * world - 1]
+    return [31] * 6 if world == 1 else [31, 32 * world - 1] + [31] * 4
 
 
 def expected(heaps):
@@ -464,10 +467,14 @@ def main():
     workload = "sum_four_to_one heaps=%s" % ":".join(map(str, heaps))
     if layout == "planes":
         m = plane_bytes(heaps, word_bits // 8)
-        model = {"resolve_compulsory": m["resolve_compulsory"] / world,
-                 "pull_compulsory": m["pull_compulsory"] / world,
-                 "resolve_per_edge": m["resolve_requested"] / world,
-                 "pull_per_edge": m["pull_requested"] / world}
+        # plane_bytes counts 32 x 32 planes over the outer heaps: per rank
+        # already when heap 1 is the dealt one (the row deal), the whole job
+        # when the last heap is
+        div = world if heaps[1] == 31 else 1
+        model = {"resolve_compulsory": m["resolve_compulsory"] / div,
+                 "pull_compulsory": m["pull_compulsory"] / div,
+                 "resolve_per_edge": m["resolve_requested"] / div,
+                 "pull_per_edge": m["pull_requested"] / div}
         resolve_k, pull_k = tr.extra.get("resolve_kernel", "?"), tr.extra.get("pull_kernel", "?")
     elif layout == "dense":
         model = dense_bytes(heaps if world == 1 else heaps[:-1] + [(heaps[-1] + 1) // world - 1],
@@ -557,7 +564,9 @@ def main():
                    "positions_per_gpu": P // world, "edges_per_gpu": E // world,
                    "levels": r.levels, "root": r.root_line, "root_checked_against": root_src,
                    "layout": layout,
-                   "parallelism": ((("staged pipeline: one block of the top heap per rank x%d, halo rows "
+                   "parallelism": ((("row deal: heap 1 in 32-row slabs x%d, each level's last two rows per plane "
+                                     "streamed to the next rank" if layout == "planes" and heaps[1] != 31 else
+                                     "staged pipeline: one block of the top heap per rank x%d, halo rows "
                                      "streamed to the next rank" if layout == "planes" else
                                      "round-robin top-heap blocks x%d, one halo exchange per level") % world
                                     + ", %s" % ("host-staged (gloo, all ranks on one GPU: rehearsal, not a "

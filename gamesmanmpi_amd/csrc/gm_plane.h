@@ -90,6 +90,9 @@ struct PlaneGeom {
   uint32_t nplanes;  // planes of this table (local)
   uint32_t world, rank, B, Z;  // shards (world 1: B = Z = 0)
   uint32_t spread;  // shards: the link-spreading deal (plane_owner), else round robin
+  // the row deal (shards of heap 1, plane_shape): this shard's rows are heap-1
+  // values [h1off, h1off + 32); the outer digits are the whole table's
+  uint32_t rowdeal, h1off;
   uint32_t base[kPlaneMaxOuter];
   uint32_t shift[kPlaneMaxOuter];   // log2(stride[j]) when pow2
   uint32_t stride[kPlaneMaxOuter];  // global plane-index stride of outer digit j
@@ -244,7 +247,7 @@ __device__ __forceinline__ void plane_digits(const PlaneGeom& g, uint32_t P, uin
 template <int NO>
 __device__ __forceinline__ void plane_global_digits(const PlaneGeom& g, uint32_t P, uint32_t* dig) {
   plane_digits<NO>(g, P, dig);
-  if (g.world > 1 && NO > 0) {
+  if (g.B && NO > 0) {  // the top-heap deals (the row deal's outer digits are global)
     const uint32_t u = P / g.Z, j = u / g.B, o = u - j * g.B;
     dig[NO - 1] = plane_gblock(g, j) * g.B + o;
   }
@@ -476,7 +479,7 @@ __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
 #ifndef GM_PLANE_RSV_UNR
 #define GM_PLANE_RSV_UNR false
 #endif
-template <int WB, int NO, bool SH, int RS_, bool UNR = true, bool WT = false>
+template <int WB, int NO, bool SH, int RS_, bool UNR = true, bool WT = false, bool HR = false>
 __device__ __forceinline__ void plane_x2_visit(typename PlaneWord<WB>::T* __restrict__ tab, const PlaneGeom& g,
                                                const uint4* __restrict__ zero,
                                                const typename PlaneWord<WB>::T* __restrict__ recv,
@@ -515,22 +518,8 @@ __device__ __forceinline__ void plane_x2_visit(typename PlaneWord<WB>::T* __rest
   // 2.5 operations per neighbour dword and plane instead of 3 (shift + max)
   constexpr bool FL3 = GM_PLANE_FOLD3 && B8;
   auto lowb = [](uint32_t v) { return FL3 ? (v & 0x00FF00FFu) : pk_shl8(v); };
-  auto fold2 = [&](int j1, int k1, int j2, int k2) {  // j2 < 0: one neighbour
-    const bool two = j2 >= 0;
-    const uint4* sx1 = nb(ex, dx, ox, j1, k1);
-    const uint4* sy1 = nb(ey, dy, oy, j1, k1);
-    const uint4* sx2 = two ? nb(ex, dx, ox, j2, k2) : sx1;
-    const uint4* sy2 = two ? nb(ey, dy, oy, j2, k2) : sy1;
-    uint4 vx1[NQ], vy1[NQ], vx2[NQ], vy2[NQ];
-#pragma unroll
-    for (int q = 0; q < NQ; q++) {
-      vx1[q] = sx1[q * kPieceU4];
-      vy1[q] = sy1[q * kPieceU4];
-      if (two) {
-        vx2[q] = sx2[q * kPieceU4];
-        vy2[q] = sy2[q * kPieceU4];
-      }
-    }
+  // the neighbour rows' values (v*2: when `two`) into the E rows
+  auto foldv = [&](const uint4* vx1, const uint4* vy1, const uint4* vx2, const uint4* vy2, const bool two) {
 #pragma unroll
     for (int q = 0; q < NQ; q++) {
       const uint32_t a1[4] = {vx1[q].x, vx1[q].y, vx1[q].z, vx1[q].w};
@@ -565,6 +554,58 @@ __device__ __forceinline__ void plane_x2_visit(typename PlaneWord<WB>::T* __rest
       }
     }
   };
+  auto fold2 = [&](int j1, int k1, int j2, int k2) {  // j2 < 0: one neighbour
+    const bool two = j2 >= 0;
+    const uint4* sx1 = nb(ex, dx, ox, j1, k1);
+    const uint4* sy1 = nb(ey, dy, oy, j1, k1);
+    const uint4* sx2 = two ? nb(ex, dx, ox, j2, k2) : sx1;
+    const uint4* sy2 = two ? nb(ey, dy, oy, j2, k2) : sy1;
+    uint4 vx1[NQ], vy1[NQ], vx2[NQ], vy2[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; q++) {
+      vx1[q] = sx1[q * kPieceU4];
+      vy1[q] = sy1[q * kPieceU4];
+      if (two) {
+        vx2[q] = sx2[q * kPieceU4];
+        vy2[q] = sy2[q * kPieceU4];
+      }
+    }
+    foldv(vx1, vy1, vx2, vy2, two);
+  };
+  // HR (the row deal, shards of heap 1): the first two rows' neighbours below
+  // the shard -- heap-1 values h1off - 1 and h1off - 2 -- are the previous
+  // shard's rows 31 and 30, from the halo buffer (recv: per list entry
+  // [row 30 | row 31] as that shard stored them, each rotated by its own row).
+  // Row L's neighbour at h1 - k (L < k) is halo row L - k + 2, and in row L's
+  // rotation its byte j is their byte j - k: every other lane reads zeros.
+  auto hrow = [&](const PlaneEntry& e, int k, uint4* v) {
+    const bool has = HR && e.top1 != kPlaneAbsent && L < (uint32_t)k;
+    const uint4* src = has ? (const uint4*)(recv + (size_t)e.top1 * 64u + (L + 2u - (uint32_t)k) * 32u) : zero;
+    uint32_t x[DW], y[DW];
+#pragma unroll
+    for (int q = 0; q < NQ; q++) {
+      const uint4 t = src[q];
+      x[4 * q] = t.x, x[4 * q + 1] = t.y, x[4 * q + 2] = t.z, x[4 * q + 3] = t.w;
+    }
+#pragma unroll
+    for (int d = 0; d < DW; d++) {
+      const uint32_t lo = x[(d + DW - 1) % DW];
+      y[d] = B8 ? __builtin_amdgcn_alignbit(x[d], lo, 32u - 8u * (uint32_t)k)
+                : (k == 2 ? lo : __builtin_amdgcn_alignbit(x[d], lo, 16u));
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; q++) v[q] = make_uint4(y[4 * q], y[4 * q + 1], y[4 * q + 2], y[4 * q + 3]);
+  };
+  auto hfold = [&](int k1, int k2) {  // k2 = 0: one neighbour row
+    uint4 x1[NQ], y1[NQ], x2[NQ], y2[NQ];
+    hrow(ex, k1, x1);
+    hrow(ey, k1, y1);
+    if (k2) {
+      hrow(ex, k2, x2);
+      hrow(ey, k2, y2);
+    }
+    foldv(x1, y1, x2, y2, k2 != 0);
+  };
   if constexpr (REL) {
     // children at d - 2 first, then their frame shift -- ONCE on the
     // folded maxima (the shift is monotone: it commutes with max), on the
@@ -573,6 +614,7 @@ __device__ __forceinline__ void plane_x2_visit(typename PlaneWord<WB>::T* __rest
     // dword -- then the children at d - 1
 #pragma unroll
     for (int j = 0; j < NO; j += 2) fold2(j, 2, j + 1 < NO ? j + 1 : -1, 2);
+    if constexpr (HR) hfold(2, 0);
 #pragma unroll
     for (int d = 0; d < DW; d++) {
       if (B0 & 1) {
@@ -585,9 +627,11 @@ __device__ __forceinline__ void plane_x2_visit(typename PlaneWord<WB>::T* __rest
     }
 #pragma unroll
     for (int j = 0; j < NO; j += 2) fold2(j, 1, j + 1 < NO ? j + 1 : -1, 1);
+    if constexpr (HR) hfold(1, 0);
   } else {
 #pragma unroll
     for (int j = 0; j < NO; j++) fold2(j, 1, j, 2);
+    if constexpr (HR) hfold(1, 2);
   }
   const uint32_t primv =
       (g.rank == 0 && L == 0) ? ((ex.p == 0 ? W::kPrim : 0u) | (ey.p == 0 ? W::kPrim << 16 : 0u)) : 0u;
@@ -710,20 +754,29 @@ __device__ __forceinline__ void plane_x2_visit(typename PlaneWord<WB>::T* __rest
       }
     }
   };
+  // HR: rows 30 and 31 also go to the next shard's halo, one entry per plane
+  auto hstore = [&](const PlaneEntry& e, const uint32_t* o) {
+    if (!HR || e.send == kPlaneAbsent || L < 30) return;
+    uint4* p = (uint4*)(send + (size_t)e.send * 64u + (L - 30u) * 32u);
+#pragma unroll
+    for (int q = 0; q < NQ; q++) p[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+  };
   if (livex) {
     store(tab + ox, ox_);
     if (SH && ex.send != kPlaneAbsent) store(send + (size_t)ex.send * 1024u + plane_row0<T>(L), ox_);
+    hstore(ex, ox_);
   }
   if (livey) {
     store(tab + oy, oy_);
     if (SH && ey.send != kPlaneAbsent) store(send + (size_t)ey.send * 1024u + plane_row0<T>(L), oy_);
+    hstore(ey, oy_);
   }
 }
 
 // (RS: with WB = 3, the launch's outer digit sum s mod 4; -1: per wave
 // visit, from its first plane -- the list deals every four consecutive
 // entries one s mod 4, padding with kPlaneAbsent entries)
-template <int WB, int NO, bool SH, int RS = 0, bool WT = false>
+template <int WB, int NO, bool SH, int RS = 0, bool WT = false, bool HR = false>
 __device__ __forceinline__ void plane_x2_range(typename PlaneWord<WB>::T* __restrict__ tab,
                                                const void* __restrict__ list, const PlaneShare sh,
                                                const PlaneGeom& g, const uint4* __restrict__ zero,
@@ -743,11 +796,18 @@ __device__ __forceinline__ void plane_x2_range(typename PlaneWord<WB>::T* __rest
         if (ey.p == kPlaneAbsent) ey = e0, livey = false;
       }
     } else {
-      ex.p = ((const uint32_t*)list)[livex ? ix : i0];
-      ey.p = ((const uint32_t*)list)[livey ? iy : i0];
+      const uint32_t jx = livex ? ix : i0, jy = livey ? iy : i0;
+      ex.p = ((const uint32_t*)list)[jx];
+      ey.p = ((const uint32_t*)list)[jy];
+      if (HR) {  // the row deal: halo entries in list order
+        ex.top1 = recv ? jx : kPlaneAbsent;
+        ey.top1 = recv ? jy : kPlaneAbsent;
+        ex.send = send ? jx : kPlaneAbsent;
+        ey.send = send ? jy : kPlaneAbsent;
+      }
     }
     if constexpr (RS >= 0) {
-      plane_x2_visit<WB, NO, SH, RS, true, WT>(tab, g, zero, recv, send, ex, ey, livex, livey);
+      plane_x2_visit<WB, NO, SH, RS, true, WT, HR>(tab, g, zero, recv, send, ex, ey, livex, livey);
     } else {  // the visit's outer digit sum (global digits) mod 4, wave-uniform
       uint32_t dg[NO > 0 ? NO : 1], sum = 0;
       plane_global_digits<NO>(g, ex.p, dg);
@@ -763,7 +823,7 @@ __device__ __forceinline__ void plane_x2_range(typename PlaneWord<WB>::T* __rest
   }
 }
 
-template <int WB, int NO, bool SH, int RS>
+template <int WB, int NO, bool SH, int RS, bool HR = false>
 __global__ __launch_bounds__(256) void k_plane_resolve_x2(typename PlaneWord<WB>::T* __restrict__ tab,
                                                           const void* __restrict__ list, uint32_t n, PlaneGeom g,
                                                           const uint4* __restrict__ zero,
@@ -771,7 +831,7 @@ __global__ __launch_bounds__(256) void k_plane_resolve_x2(typename PlaneWord<WB>
                                                           typename PlaneWord<WB>::T* __restrict__ send,
                                                           const uint32_t* __restrict__ pf, uint32_t pflines) {
   const uint32_t v = plane_prefetch(pf, pflines);
-  plane_x2_range<WB, NO, SH, RS, true>(tab, list, plane_share(n, 4), g, zero, recv, send);
+  plane_x2_range<WB, NO, SH, RS, true, HR>(tab, list, plane_share(n, 4), g, zero, recv, send);
   plane_keep(v);
 }
 
@@ -855,7 +915,7 @@ __device__ __forceinline__ void plane_reach_body(uint32_t* __restrict__ bits, co
     uint32_t w[4];
 #pragma unroll
     for (uint32_t k = 0; k < 4; k++) {
-      const uint32_t h1 = h1b + k;
+      const uint32_t h1 = h1b + k + g.h1off;  // heap 1's value (the row deal: this shard's rows)
       const bool ink = in && h1 <= g.rlim[1];
       w[k] = ink ? full : 0u;
       if (ink) {

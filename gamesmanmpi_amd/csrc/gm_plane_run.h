@@ -55,7 +55,11 @@ __device__ __forceinline__ bool plane_locate(const Desc& d, const PlaneGeom& g, 
   *h1 = dig[1];
   u64 p = 0;
   const int no = d.nheaps - 2;
-  if (g.world > 1) {
+  if (g.rowdeal) {  // this shard holds heap-1 values [h1off, h1off + 32)
+    if (dig[1] < g.h1off || dig[1] >= g.h1off + 32u) return false;
+    *h1 = dig[1] - g.h1off;
+    for (int j = 0; j < no; j++) p += (u64)dig[2 + j] * g.stride[j];
+  } else if (g.world > 1) {
     const uint32_t t = dig[d.nheaps - 1], blk = t / g.B, o = t - blk * g.B;
     if (plane_owner(g, blk) != g.rank) return false;
     for (int j = 0; j + 1 < no; j++) p += (u64)dig[2 + j] * g.stride[j];
@@ -102,7 +106,7 @@ __device__ __forceinline__ u64 plane_key(const Desc& d, const PlaneGeom& g, uint
                                          uint32_t* osum = nullptr) {
   uint32_t dig[NO > 0 ? NO : 1];
   plane_global_digits<NO>(g, P, dig);
-  u64 k = (u64)h0 + (u64)h1 * d.stride[1];
+  u64 k = (u64)h0 + (u64)(h1 + g.h1off) * d.stride[1];
   uint32_t t = 0;
 #pragma unroll
   for (int j = 0; j < NO; j++) {
@@ -139,7 +143,7 @@ __global__ __launch_bounds__(256) void k_plane_checksum(Desc d, PlaneGeom g, con
     const u64 base = plane_key<NO>(d, g, P, 0, h1, &os);
     for (; w; w &= w - 1) {
       const uint32_t h0 = (uint32_t)__builtin_ctz(w);
-      ck_add(d, base + h0, plane_vr<WB>(tab, P, h0, h1, os + h0 + h1), a);
+      ck_add(d, base + h0, plane_vr<WB>(tab, P, h0, h1, os + h0 + h1 + g.h1off), a);
     }
   }
   ck_block_add(acc, a);
@@ -151,9 +155,17 @@ __global__ __launch_bounds__(256) void k_plane_checksum(Desc d, PlaneGeom g, con
 // PLANES applies to sum_four_to_one whose heaps 0 and 1 hold 32 values (a
 // plane is 32 x 32), with at most kPlaneMaxOuter further heaps and every
 // remoteness below 2^15 (16-bit order forms).
-static bool plane_ok(const Desc* d) {
+static uint32_t plane_form(const Desc* d, uint32_t flags);
+// The row deal (shards of heap 1): heap 1 holds 32 values per rank, each rank
+// a 32-row slab of every plane (plane_shape); 8-bit words only (the packed
+// kernels carry its halo rows)
+static bool plane_row_deal(const Desc* d, int world) {
+  return world > 1 && d->nheaps >= 3 && d->heap[0] == 31 && d->heap[1] + 1 == 32u * (uint32_t)world &&
+         plane_form(d, 0) != 2;
+}
+static bool plane_ok(const Desc* d, int world) {
   if (d->kind != K_SUM || d->variant != 0 || d->nheaps < 2 || d->nheaps - 2 > kPlaneMaxOuter) return false;
-  if (d->heap[0] != 31 || d->heap[1] != 31 || d->root_sum >= 0x7FFF) return false;
+  if (d->heap[0] != 31 || (d->heap[1] != 31 && !plane_row_deal(d, world)) || d->root_sum >= 0x7FFF) return false;
   u64 np = 1;
   for (int i = 2; i < d->nheaps; i++) np *= d->base[i];
   return np <= 0xFFFFFFF0ull;
@@ -166,8 +178,9 @@ static uint32_t plane_form(const Desc* d, uint32_t flags) {
   if (flags & GM_F_WORDS16) return 2u;
   return d->root_sum <= 253 ? 1u : d->root_sum <= kPlaneRelMaxSum ? 3u : 2u;
 }
-static bool plane_wanted(const Desc* d, uint32_t flags) {
-  return plane_ok(d) && !(flags & (GM_F_LEVEL_MAJOR | GM_F_FORCE_HASHED | GM_F_WORDS32 | GM_F_RESOLVE_SCALAR));
+static bool plane_wanted(const Desc* d, uint32_t flags, int world) {
+  if (plane_row_deal(d, world) && (flags & (GM_F_WORDS16 | GM_F_PLANE_X1))) return false;
+  return plane_ok(d, world) && !(flags & (GM_F_LEVEL_MAJOR | GM_F_FORCE_HASHED | GM_F_WORDS32 | GM_F_RESOLVE_SCALAR));
 }
 
 struct PlaneShape {
@@ -219,7 +232,7 @@ static uint32_t plane_stage_k(int world) {
 }
 // list padding of the relative forms' staged deal: at most 3 entries per
 // (key, s mod 4) class
-static u64 plane_stage_pad(const PlaneShape* ps) { return ps->form == 3 ? 12ull * ps->nkeys : 0ull; }
+static u64 plane_stage_pad(const PlaneShape* ps) { return ps->form == 3 && !ps->g.rowdeal ? 12ull * ps->nkeys : 0ull; }
 
 static u64 rup256(u64 x) { return (x + 255) & ~255ull; }
 
@@ -265,9 +278,28 @@ static int plane_shape(const Desc* d, int rank, int world, uint32_t flags, Plane
   ps->wb = ps->form == 2 ? 2u : 1u;
   ps->S = 0;
   for (int i = 2; i < d->nheaps; i++) ps->S += d->heap[i];
+  const bool rows = plane_row_deal(d, world);
+  if (rows && (ps->form == 2 || (flags & GM_F_PLANE_X1)))
+    return fail(GM_EINVAL, "the row deal runs the packed 8-bit kernels only");
   if (world <= 1) {
     g.nplanes = (uint32_t)np;
     ps->nlocal = np;
+  } else if (rows) {
+    // The row deal: every rank holds all 2^(5 * outer) planes, rows = heap-1
+    // values [32 r, 32 r + 32).  Plane levels are the one-table levels; a
+    // plane's rows 0 and 1 read the previous rank's rows 30 and 31 of the
+    // SAME plane (heap 1 - 1, - 2), so rank r's level l waits only for rank
+    // r - 1's level l: the pipeline trails by one level (+ its transfer)
+    // instead of B keys.  As staged keys: key = row = level, both with lag 0.
+    if (rank < 0 || rank >= world) return fail(GM_EINVAL, "bad shard %d/%d", rank, world);
+    g.rowdeal = 1;
+    g.h1off = 32u * (uint32_t)rank;
+    g.nplanes = (uint32_t)np;
+    ps->nlocal = np;
+    ps->stage_k = 1;
+    ps->nkeys = ps->nrows = ps->S + 1;
+    ps->nrecv = rank > 0 ? np : 0;          // halo entries: two rows per plane
+    ps->nsend = rank + 1 < world ? np : 0;
   } else {
     if (g.no < 1) return fail(GM_EINVAL, "sharded planes need at least 3 heaps");
     if (rank < 0 || rank >= world) return fail(GM_EINVAL, "bad shard %d/%d", rank, world);
@@ -298,15 +330,16 @@ static int plane_shape(const Desc* d, int rank, int world, uint32_t flags, Plane
       if (gb + 1 < ps->nblocks) ps->nsend += 2 * Z;
     }
   }
-  const u64 pb = 1024ull * ps->wb;
+  const u64 pb = 1024ull * ps->wb, hb = g.rowdeal ? 64ull * ps->wb : pb;  // halo entry: plane / two rows
   ps->words_off = 0;
   ps->bits_off = rup256(ps->nlocal * pb);
   ps->recv_off = ps->bits_off + rup256(ps->nlocal * 128);
-  ps->send_off = ps->recv_off + rup256(ps->nrecv * pb);
-  ps->table_bytes = ps->send_off + rup256(ps->nsend * pb);
+  ps->send_off = ps->recv_off + rup256(ps->nrecv * hb);
+  ps->table_bytes = ps->send_off + rup256(ps->nsend * hb);
   ps->zero_off = rup256(scratch_bytes_for(d->max_levels));
   ps->list_off = ps->zero_off + 4096;
-  ps->scratch_bytes = ps->list_off + rup256((ps->nlocal + plane_stage_pad(ps)) * (world > 1 ? sizeof(PlaneEntry) : 4));
+  ps->scratch_bytes =
+      ps->list_off + rup256((ps->nlocal + plane_stage_pad(ps)) * (world > 1 && !g.rowdeal ? sizeof(PlaneEntry) : 4));
   return 0;
 }
 
@@ -417,7 +450,7 @@ static int plane_lists(gm_solver* s, const PlaneShape& ps, std::vector<uint8_t>&
     return t;
   };
   s->ploff.assign((size_t)S + 2, 0);
-  if (g.world <= 1) {
+  if (g.world <= 1 || g.rowdeal) {
     std::vector<uint32_t> lev(ps.nlocal);
     for (u64 P = 0; P < ps.nlocal; P++) {
       lev[P] = digsum(P, g.no);
@@ -457,6 +490,13 @@ static int plane_lists(gm_solver* s, const PlaneShape& ps, std::vector<uint8_t>&
         std::sort(tmp.begin(), tmp.end());
         for (u64 i = a; i < b; i++) L[i] = tmp[i - a].second;
       }
+    }
+    if (g.rowdeal) {  // halo row r = level r's entries, in list order, both ways
+      s->prcv_off.assign((size_t)S + 2, 0);
+      s->psnd_off.assign((size_t)S + 2, 0);
+      if (g.rank > 0) s->prcv_off = s->ploff;
+      if (g.rank + 1 < g.world) s->psnd_off = s->ploff;
+      s->pbnd.clear();
     }
     return 0;
   }
@@ -614,8 +654,21 @@ static void plane_launch_t(gm_solver* s, u64 a, u64 n, u64 pa, u64 pn, uint32_t 
   typedef typename PlaneWord<WB>::T T;
   const void* list = (const char*)s->plist + a * (SH ? sizeof(PlaneEntry) : 4);
   const dim3 grid((uint32_t)blocks), blk(256);
+  // the row deal: uint32 lists, halo rows from rank - 1 / to rank + 1, one
+  // entry (two rows) per list entry: the kernel indexes them from the launch's
+  // first entry, a
+  const bool hr = !SH && s->pg.rowdeal;
+  const T* hrecv = hr && s->rank > 0 ? (const T*)s->precv + a * 64u : nullptr;
+  T* hsend = hr && s->rank + 1 < s->world ? (T*)s->psend + a * 64u : nullptr;
   if constexpr (WB == 3) {
     auto go = [&](auto RS) {
+      if constexpr (!SH) {
+        if (hr) {
+          hipLaunchKernelGGL((k_plane_resolve_x2<3, NO, false, decltype(RS)::value, true>), grid, blk, 0, s->stream,
+                             (T*)s->ptab, list, (uint32_t)n, s->pg, s->pzero, hrecv, hsend, pf, pfl);
+          return;
+        }
+      }
       hipLaunchKernelGGL((k_plane_resolve_x2<3, NO, SH, decltype(RS)::value>), grid, blk, 0, s->stream, (T*)s->ptab,
                          list, (uint32_t)n, s->pg, s->pzero, (const T*)s->precv, (T*)s->psend, pf, pfl);
     };
@@ -633,6 +686,13 @@ static void plane_launch_t(gm_solver* s, u64 a, u64 n, u64 pa, u64 pn, uint32_t 
     hipLaunchKernelGGL((k_plane_resolve<WB, NO, SH>), grid, blk, 0, s->stream, (T*)s->ptab, list, (uint32_t)n, s->pg,
                        s->pzero, (const T*)s->precv, (T*)s->psend, pf, pfl);
   } else {
+    if constexpr (!SH && WB == 1) {
+      if (hr) {
+        hipLaunchKernelGGL((k_plane_resolve_x2<1, NO, false, 0, true>), grid, blk, 0, s->stream, (T*)s->ptab, list,
+                           (uint32_t)n, s->pg, s->pzero, hrecv, hsend, pf, pfl);
+        return;
+      }
+    }
     hipLaunchKernelGGL((k_plane_resolve_x2<WB, NO, SH, 0>), grid, blk, 0, s->stream, (T*)s->ptab, list, (uint32_t)n,
                        s->pg, s->pzero, (const T*)s->precv, (T*)s->psend, pf, pfl);
   }
@@ -652,7 +712,7 @@ static void plane_launch_w(gm_solver* s, u64 a, u64 n, u64 pa, u64 pn, uint32_t 
 // the solver's word form and shard flag as template arguments
 template <class F>
 static void plane_form_dispatch(const gm_solver* s, F&& f) {
-  const bool sh = s->world > 1;
+  const bool sh = s->world > 1 && !s->pg.rowdeal;  // PlaneEntry lists (the top-heap deals)
   auto w = [&](auto WB) {
     if (sh) f(WB, std::true_type());
     else f(WB, std::false_type());
@@ -706,7 +766,7 @@ struct PlaneBatcher {
   u64 launches = 0;  // grid launches + runs issued
   explicit PlaneBatcher(gm_solver* sv) : s(sv) {
     // one pass of the run's waves: one CU beats a grid launch up to about there
-    narrow = (s->flags & GM_F_PLANE_NO_RUNS)
+    narrow = (s->flags & GM_F_PLANE_NO_RUNS) || s->pg.rowdeal  // (k_plane_run carries no halo rows)
                  ? 0
                  : (u64)((double)(kPlaneRunThreads / 64) * (plane_x1(s) ? 2 : 4) * GM_PLANE_RUN_PASSES);
     run.n = 0;
@@ -895,6 +955,7 @@ static u64 plane_stage_sig(const gm_solver* s) {
   mix(s->prows);
   mix(s->pg.B);
   mix(s->pg.Z);
+  mix(s->pg.rowdeal);
   mix(s->world);
   const std::vector<u64>& rows = s->rank > 0 ? s->prcv_off : s->psnd_off;
   for (u64 v : rows) mix(v);
@@ -991,9 +1052,12 @@ static int staged_defer(gm_solver* s, int herr, hipStream_t st) {
 // returns at once: the exchange itself is then broken.
 static int plane_backward_staged(std::vector<gm_solver*>& ss, int mode, hipStream_t st, u64* nlaunch) {
   gm_solver* s0 = ss[0];
-  const uint32_t k = s0->pstage_k, K = s0->pkeys, R = s0->prows, B = s0->pg.B;
+  // (the row deal: key = row = plane level, each final after its own key --
+  // a lag of B - 1 = 0 -- and two rows per plane in the halo)
+  const bool rowdeal = s0->pg.rowdeal != 0;
+  const uint32_t k = s0->pstage_k, K = s0->pkeys, R = s0->prows, B = rowdeal ? 1u : s0->pg.B;
   const int W = s0->world;
-  const u64 pb = 1024ull * s0->pwb;
+  const u64 pb = (rowdeal ? 64ull : 1024ull) * s0->pwb;
   auto row_done = [&](uint32_t key, uint32_t* r) {  // key completes row *r (its last slice)
     if (key + 1 < B || (key - (B - 1)) % k) return false;
     *r = (key - (B - 1)) / k;
@@ -1008,10 +1072,11 @@ static int plane_backward_staged(std::vector<gm_solver*>& ss, int mode, hipStrea
     *n = off[r + 1] - off[r];
     return off[r];
   };
-  auto launch_key = [K, B](PlaneBatcher& pb_, uint32_t key) {
+  auto launch_key = [K, rowdeal](PlaneBatcher& pb_, uint32_t key) {
     const std::vector<u64>& o = pb_.s->ploff;
-    (void)B;  // relative forms: s mod 4 per wave visit (plane_lists_staged)
-    const uint32_t rs = kPlaneRsVisit;
+    // relative forms: s mod 4 per wave visit (plane_lists_staged); the row
+    // deal's keys are plane levels, of one s each
+    const uint32_t rs = rowdeal ? key & 3u : kPlaneRsVisit;
     pb_.add(o[key], o[(size_t)key + 1], rs, key + 1 < K ? o[(size_t)key + 2] - o[(size_t)key + 1] : 0);
   };
   if (mode == 2) {

@@ -307,8 +307,8 @@ static u64 dense_bits_bytes(const Desc* d, const DenseGeom& g) {
 
 struct gm_solver;
 struct PlaneShape;
-static bool plane_ok(const Desc* d);
-static bool plane_wanted(const Desc* d, uint32_t flags);
+static bool plane_ok(const Desc* d, int world);
+static bool plane_wanted(const Desc* d, uint32_t flags, int world);
 static int plan_planes(const Desc* d, int rank, int world, uint32_t flags, uint64_t max_table_bytes, gm_plan_t* out,
                        bool* fits);
 static int plane_setup(gm_solver* s, const gm_buffers* buf);
@@ -1600,7 +1600,7 @@ int gm_plan_shard(int game, int rank, int world, uint32_t flags, uint64_t max_ta
   out->scratch_bytes = scratch_bytes_for(d->max_levels);
   if (!d->dense_ok || (flags & GM_F_FORCE_HASHED))
     return fail(GM_EINVAL, "only DENSE layouts shard by prefix blocks; keyed tables shard by md5 owner");
-  if (plane_wanted(d, flags)) {
+  if (plane_wanted(d, flags, world)) {
     bool fits = false;
     int rc = plan_planes(d, rank, world, flags, max_table_bytes, out, &fits);
     if (rc) return rc;
@@ -1696,7 +1696,7 @@ int gm_plan(int game, uint64_t positions, uint32_t flags, uint64_t max_table_byt
   memset(out, 0, sizeof *out);
   out->max_levels = (uint32_t)d->max_levels;
   out->scratch_bytes = scratch_bytes_for(d->max_levels);
-  if (d->dense_ok && plane_wanted(d, flags)) {
+  if (d->dense_ok && plane_wanted(d, flags, 1)) {
     bool fits = false;
     int rc = plan_planes(d, 0, 1, flags, max_table_bytes, out, &fits);
     if (rc) return rc;
@@ -1890,7 +1890,7 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
       return fail(GM_EINVAL, "dense table of %llu bytes, these flags need %llu (plan with the flags the solver is "
                              "created with)", (unsigned long long)buf->table_bytes, (unsigned long long)need);
   } else if (buf->mode == GM_MODE_PLANES) {
-    if (!d->dense_ok || !plane_ok(d)) return fail(GM_EINVAL, "game has no planes layout");
+    if (!d->dense_ok || !plane_ok(d, world)) return fail(GM_EINVAL, "game has no planes layout");
     if (world > 1 && (rank < 0 || rank >= world)) return fail(GM_EINVAL, "bad shard %d/%d", rank, world);
   } else if (buf->mode == GM_MODE_RANKED) {
     if (world != 1) return fail(GM_EINVAL, "ranked tables are one-GPU (shard keyed games by md5: gm_plan_keyed_shard)");
@@ -2517,7 +2517,7 @@ static int xfer_ranges(gm_solver* s, const std::vector<HostRange>& out, int sp, 
 int gm_plane_halo_plan(int game, int rank, int world, uint32_t flags, uint64_t* out, uint32_t levels) {
   const Desc* d = get_game(game);
   if (!d || !out || world < 2 || rank < 0 || rank >= world) return fail(GM_EINVAL, "bad argument");
-  if (!plane_ok(d)) return fail(GM_EINVAL, "game has no planes layout");
+  if (!plane_ok(d, world)) return fail(GM_EINVAL, "game has no planes layout");
   PlaneShape ps;
   int rc = plane_shape(d, rank, world, flags, &ps);
   if (rc) return rc;

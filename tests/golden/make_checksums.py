@@ -43,6 +43,12 @@ CASES = {
     "sum_31x5_63": ("sum_four_to_one", "heaps=31:31:31:31:31:63", "rows"),
     "sum_31x5_127": ("sum_four_to_one", "heaps=31:31:31:31:31:127", "rows"),
     "sum_31x5_255": ("sum_four_to_one", "heaps=31:31:31:31:31:255", "rows"),
+    # the same shapes with the long heap second (heap 1): the row deal's
+    # bench shapes -- the game is symmetric in its heaps, so
+    # counts and root lines equal the ones above, the key-order checksum not
+    "sum_31_63_31x4": ("sum_four_to_one", "heaps=31:63:31:31:31:31", "rows"),
+    "sum_31_127_31x4": ("sum_four_to_one", "heaps=31:127:31:31:31:31", "rows"),
+    "sum_31_255_31x4": ("sum_four_to_one", "heaps=31:255:31:31:31:31", "rows"),
 }
 
 

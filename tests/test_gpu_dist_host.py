@@ -25,6 +25,8 @@ CASES = {  # (layout, world, deal) -> (params, flags)
     ("planes", 2, "staged"): ("heaps=31:31:3:15", 0),
     ("planes", 3, "staged"): ("heaps=31:31:3:23", 0),
     ("planes", 4, "staged"): ("heaps=31:31:2:7:15", 0),
+    ("planes", 2, "rows"): ("heaps=31:63:3:15", 0),     # the row deal (heap 1 split in 32-row slabs)
+    ("planes", 3, "rows"): ("heaps=31:95:3:7", 0),
     ("planes", 2, "level-sync"): ("heaps=31:31:3:15", LEVEL_SYNC),
     ("planes", 3, "level-sync"): ("heaps=31:31:3:23", LEVEL_SYNC),
     ("dense", 2, ""): ("heaps=15:15:15:15:31", 0),

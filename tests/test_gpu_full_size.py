@@ -179,6 +179,19 @@ def test_gpu_toot_6x4_two_md5_shards_checksum():
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("name,world,streams", [("sum_31_63_31x4", 2, "one"), ("sum_31_63_31x4", 2, "own"),
+                                                ("sum_31_127_31x4", 4, "own"), ("sum_31_255_31x4", 8, "one"),
+                                                ("sum_31_255_31x4", 8, "own")])
+def test_gpu_row_deal_bench_shapes_checksum(name, world, streams):
+    """bench.py --gpus N workloads (31 x (32N - 1) x 31^4, 2^30 positions per
+    shard, the row deal): all shards in this process, on one stream or on
+    streams of their own (the RCCL schedule's rehearsal); fingerprints summed
+    against the oracle_mt golden."""
+    import torch
+    _check_group(name, world, streams=streams)
+    torch.cuda.empty_cache()
+
+
 # The one-GPU rehearsal of the RCCL staged schedule (gm_plane_run.h mode 4):
 # every shard on a stream of its own with mode 1's send / receive streams,
 # receives posted ahead, SE / RE events and end-of-solve joins; a device copy

@@ -329,3 +329,39 @@ def test_planes_relative_group_matches_oracle(world, params, flags, streams):
         assert (got[own] == 0xFFFFFFFF).all()
         got[own] = w[own]
     np.testing.assert_array_equal(got, want)
+
+
+ROW_GROUP_CASES = [  # the row deal: heap 1 holds 32 values per rank
+    (2, "heaps=31:63:3:15", "one"),
+    (2, "heaps=31:63:3:15", "own"),
+    (2, "heaps=31:63:7", "own"),          # one outer heap
+    (3, "heaps=31:95:2:7", "own"),
+    (4, "heaps=31:127:31:31", "one"),     # 4.2e6 positions, two outer heaps of 32
+    (8, "heaps=31:255:3:3", "own"),       # root digit sum 292: relative words
+    (8, "heaps=31:255:1:1:1", "one"),     # relative words, three outer heaps
+]
+
+
+@pytest.mark.parametrize("world,params,streams", ROW_GROUP_CASES)
+def test_planes_row_deal_group_matches_oracle(world, params, streams):
+    """The row deal (gm_plane_run.h plane_shape): rank r owns heap-1 values
+    [32r, 32r + 32) of every plane and streams each level's rows 30, 31 to
+    rank r + 1.  One stream (halo copies in order) and own streams (mode 4,
+    the RCCL schedule's rehearsal): every position's word, answered by its
+    one owner, equals the oracle's."""
+    from gamesmanmpi_amd.dist import group_solve
+    from gamesmanmpi_amd.games import GameSpec
+    rg, shards = group_solve(GameSpec("sum_four_to_one", params), world, streams=streams)
+    sol = _oracle(params)
+    assert rg.extra["layout"] == "planes"
+    assert (rg.positions, rg.edges, rg.primitives, rg.root_line) == (sol.count, sol.edges, sol.stats["primitives"],
+                                                                     sol.root_line)
+    keys = np.arange(sol.count, dtype=np.uint64)
+    want = _oracle_words(sol, sol.count)
+    got = np.full(sol.count, 0xFFFFFFFF, np.uint32)
+    for sh in shards:
+        w = sh.query(keys)
+        own = w != 0xFFFFFFFF
+        assert (got[own] == 0xFFFFFFFF).all()
+        got[own] = w[own]
+    np.testing.assert_array_equal(got, want)

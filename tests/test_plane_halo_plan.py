@@ -93,3 +93,23 @@ def test_staged_only_where_blocks_divide():
     assert all(not p[4:].any() for p in plans)
     plans = _plans("heaps=31:31:3:63", 3)  # 64 values: not divisible by 3
     assert any(p[4:].any() for p in plans)
+
+
+@pytest.mark.parametrize("params,world", [("heaps=31:63:3:15", 2), ("heaps=31:95:2:7", 3),
+                                          ("heaps=31:127:31:31:31:31", 4), ("heaps=31:255:31:31:31:31", 8)])
+def test_row_deal_plans(params, world):
+    """The row deal (heap 1 in 32-row slabs): step = plane level, every
+    level's planes travel from rank r to rank r + 1 only (two rows each: the
+    unit is a list entry), rank 0 receives and the last rank sends nothing,
+    and a level carries exactly its plane count."""
+    plans = _plans(params, world)
+    outer = [int(h) + 1 for h in params.split("=")[1].split(":")[2:]]
+    n = np.ones(1, np.int64)
+    for b in outer:
+        n = np.convolve(n, np.ones(b, np.int64))
+    for r in range(world):
+        assert _peers(plans[r]) == ([r + 1] if r + 1 < world else [])
+        if r + 1 < world:
+            np.testing.assert_array_equal(plans[r][:len(n), r + 1, 0], n)
+            assert not plans[r][len(n):, :, :].any()
+    assert not plans[0][:, :, 1].any()

@@ -3,7 +3,7 @@
 # the PLANES PMC passes, and kernel traces of the staged shard groups on ONE
 # stream (every key alone on the GPU: the per-key durations the pipeline model
 # takes).  Each GPU step under its own limit; the first failure ends it.
-#   bash tools/r05_session.sh TAG [what...]   what: bench prof pmc stage
+#   bash tools/r05_session.sh TAG [what...]   what: bench prof pmc stage rows
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 tag=${1:-r05g}
@@ -33,6 +33,11 @@ for w in $what; do
         set -- $wk
         GM_PLANE_STAGE_K=$2 step stage_w$1_k$2 240 rocprofv3 --kernel-trace --output-format csv \
           -d "$out/stage_w$1_k$2" -o run -- python3 tools/group_planes.py "$1" 2
+      done ;;
+    rows)  # the row deal's bench shapes (bench.heaps_for), one stream
+      for w in 2 4 8; do
+        step rows_w$w 240 rocprofv3 --kernel-trace --output-format csv -d "$out/rows_w$w" -o run -- \
+          python3 tools/group_planes.py "$w" 2
       done ;;
   esac
 done
