@@ -511,18 +511,24 @@ __global__ __launch_bounds__(256) void k_rk_forward(RankGeom g, uint32_t L, u64 
 // offset 0xFFFFFFFF, out of range, i.e. 0 = WIN in 0, neutral in the
 // reduction -- so all 2C loads issue back to back with no branches.  CC / HH:
 // the board at compile time (0: from g).
-constexpr uint32_t kRkTile = 256 * 64;
 // (U: list entries per lane per pass -- U x 2C child loads in flight before
 // any reduction; a tile inside one height-vector block (L >= 11) reads its
-// block's stacks / child bases once, wave-uniform)
-template <int CC, int HH, int U>
+// block's stacks / child bases once, wave-uniform.  SPT: slots per thread
+// and tile word, 64 or 32: a tile of 256 x 32 slots halves the LDS list
+// (16 KB), so 9 workgroups fit a CU instead of 4 and the waves in flight go
+// from 4 to 6 per SIMD (then bound by the 79 VGPRs) -- the pass waits on its
+// gathers most of the time (SQ_WAIT_ANY 59 %, profiles/r05d))
+template <int CC, int HH, int U, int SPT = 64>
 __global__ __launch_bounds__(256) void k_rk_backward(RankGeom g, uint32_t L, u64 lvstart, uint32_t lvoff,
                                                      u64 nwords, u64 cstart, u64 csize, BlockCount* bc, DevState* st) {
+  static_assert(SPT == 64 || SPT == 32, "tile words of 64 or 32 slots");
+  typedef typename std::conditional<SPT == 64, u64, uint32_t>::type MW;  // a tile word
+  constexpr int LG = SPT == 64 ? 6 : 5;
   constexpr int NC = CC > 0 ? CC : kRankMaxCols;
   const uint32_t C = CC > 0 ? (uint32_t)CC : g.C, H = HH > 0 ? (uint32_t)HH : g.H;
   const __amdgpu_buffer_rsrc_t rw =
       __builtin_amdgcn_make_buffer_rsrc(g.words + cstart, 0, (int)(uint32_t)csize, 0x00020000);
-  __shared__ uint16_t list[kRkTile];
+  __shared__ uint16_t list[256 * SPT];
   __shared__ uint32_t wsum[4];
   u64 edges = 0;
   uint32_t err = 0;
@@ -532,16 +538,16 @@ __global__ __launch_bounds__(256) void k_rk_backward(RankGeom g, uint32_t L, u64
     const u64 wi = t0 + threadIdx.x;
     // the list holds the EXPANDABLE slots (reached, not primitive: one kind of
     // work per lane); the reached primitives take their board's value below
-    const u64 m = wi < nwords ? reinterpret_cast<const u64*>(g.expd)[(lvstart >> 6) + wi] : 0ull;
-    const u64 mp = wi < nwords ? reinterpret_cast<const u64*>(g.reach)[(lvstart >> 6) + wi] & ~m : 0ull;
-    for (u64 pm = mp; pm; pm &= pm - 1) {
-      const u64 i = (wi << 6) + (u64)__builtin_ctzll(pm);
+    const MW m = wi < nwords ? reinterpret_cast<const MW*>(g.expd)[(lvstart >> LG) + wi] : (MW)0;
+    const MW mp = wi < nwords ? reinterpret_cast<const MW*>(g.reach)[(lvstart >> LG) + wi] & ~m : (MW)0;
+    for (MW pm = mp; pm; pm &= pm - 1) {
+      const u64 i = (wi << LG) + (u64)__builtin_ctzll((u64)pm);
       const u64 blk = i >> (L + 3);
       const uint32_t pat = (uint32_t)(i & ((1ull << L) - 1));
       g.words[lvstart + i] = (uint8_t)make_word(g.bstat[(lvstart >> 3) + (blk << L) + pat], 0);  // process.py:120-123
     }
     // exclusive scan of the popcounts over the workgroup
-    const uint32_t c = (uint32_t)__builtin_popcountll(m);
+    const uint32_t c = (uint32_t)__builtin_popcountll((u64)m);
     uint32_t incl = c;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -556,10 +562,10 @@ __global__ __launch_bounds__(256) void k_rk_backward(RankGeom g, uint32_t L, u64
       total += wsum[k];
     }
     uint32_t at = before + incl - c;
-    for (u64 mm = m; mm; mm &= mm - 1) list[at++] = (uint16_t)(threadIdx.x * 64 + __builtin_ctzll(mm));
+    for (MW mm = m; mm; mm &= mm - 1) list[at++] = (uint16_t)(threadIdx.x * SPT + __builtin_ctzll((u64)mm));
     // one block for the whole tile: its stacks and child bases, read once
-    const u64 tb0 = (t0 << 6) >> (L + 3);
-    const bool oneblk = ((((t0 + 255) << 6) + 63) >> (L + 3)) == tb0;
+    const u64 tb0 = (t0 << LG) >> (L + 3);
+    const bool oneblk = ((((t0 + 255) << LG) + (SPT - 1)) >> (L + 3)) == tb0;
     uint32_t tph = 0, tcho[kRankMaxCols] = {};
     if (oneblk) {
       tph = g.lvph[lvoff + tb0];
@@ -585,7 +591,7 @@ __global__ __launch_bounds__(256) void k_rk_backward(RankGeom g, uint32_t L, u64
         for (int u = 0; u < U; u++) {
           const uint32_t e = e0 + 256u * (uint32_t)u;
           liveu[u] = e < total;
-          const u64 i = (t0 << 6) + list[liveu[u] ? e : e0];
+          const u64 i = (t0 << LG) + list[liveu[u] ? e : e0];
           slotu[u] = lvstart + i;
           const u64 blk = i >> (L + 3);
           const uint32_t a = (uint32_t)((i >> L) & 7u), pat = (uint32_t)(i & ((1ull << L) - 1));
@@ -877,11 +883,20 @@ static void rank_kind_dispatch(const Desc& d, F&& f) {
 static int rk_unroll() {
   static const int u = [] {
     const char* e = getenv("GM_RK_UNROLL");
-    return e && atoi(e) == 4 ? 4 : 2;
+    return e && atoi(e) == 4 ? 4 : e && atoi(e) == 1 ? 1 : 2;
   }();
   return u;
 }
 
+// backward tile words of 64 or 32 slots (k_rk_backward SPT); GM_RK_SPT=64
+// restores the round-4 tile (A/B)
+static int rk_spt() {
+  static const int v = [] {
+    const char* e = getenv("GM_RK_SPT");
+    return e && atoi(e) == 64 ? 64 : 32;
+  }();
+  return v;
+}
 // the bit-sliced board kernel (k_rk_boards_sl) where it applies; GM_RK_SLICED=0
 // keeps the per-board one (A/B runs)
 static bool rk_sliced() {
@@ -961,13 +976,20 @@ static int run_ranked(gm_solver* s, gm_result* out) {
   HIPCHK(hipEventRecord(ev[1], st));
   for (int k = std::max(first, T); k < stop; k++) {
     const uint32_t L = (uint32_t)(2 * T - 1 - k);
-    const u64 nw = (s->rlvitems[L] + 63) / 64;
+    const int spt = rk_spt();
+    const u64 nw = (s->rlvitems[L] + spt - 1) / spt;  // tile words
     // level L + 1's slots (the last level has no children: an empty range)
     const u64 cs = s->rlvstart[std::min<uint32_t>(L + 1, (uint32_t)T)];
     const u64 cn = L + 1 < (uint32_t)T ? s->rlvstart[L + 2] - cs : 0;
     auto go = [&](auto CH) {
       constexpr int CC = decltype(CH)::value / 16, HH = decltype(CH)::value % 16;
-      if (rk_unroll() == 2)
+      if (spt == 32 && rk_unroll() == 1)
+        hipLaunchKernelGGL((k_rk_backward<CC, HH, 1, 32>), dim3(rank_grid(s, nw)), dim3(256), 0, st, g, L,
+                           s->rlvstart[L], s->rlvoff[L], nw, cs, cn, s->bcount, s->st);
+      else if (spt == 32)
+        hipLaunchKernelGGL((k_rk_backward<CC, HH, 2, 32>), dim3(rank_grid(s, nw)), dim3(256), 0, st, g, L,
+                           s->rlvstart[L], s->rlvoff[L], nw, cs, cn, s->bcount, s->st);
+      else if (rk_unroll() == 2)
         hipLaunchKernelGGL((k_rk_backward<CC, HH, 2>), dim3(rank_grid(s, nw)), dim3(256), 0, st, g, L,
                            s->rlvstart[L], s->rlvoff[L], nw, cs, cn, s->bcount, s->st);
       else
