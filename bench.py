@@ -166,7 +166,7 @@ def _kernel_code_sha16(kernel):
         sys.path.pop(0)
 
 
-def _pmc_row(kernel, workload):
+def _pmc_row(kernel, workload, path=None):
     """The committed PMC summary's row for `kernel` (profiles/pmc_traffic.json,
     tools/pmc_summary.py --traffic over separate rocprofv3 --pmc passes of
     this bench) and a note: None when no pass of this workload and kernel is
@@ -175,7 +175,7 @@ def _pmc_row(kernel, workload):
     The key is the measured kernel's own gfx950 code (tools/codeobj.py), so
     host-side edits and other kernels leave the figure valid; rows written
     before that key existed fall back to the kernel-source hash."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    path = path or os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as fh:
             row = json.load(fh).get(kernel)
@@ -183,12 +183,13 @@ def _pmc_row(kernel, workload):
         return None, None
     if not row or row.get("workload") != workload:
         return None, None
+    rel = os.path.relpath(path, ROOT)
     if "kernel_code_sha16" in row:
         now = _kernel_code_sha16(kernel)
         if not now or row["kernel_code_sha16"] != now:
-            return None, "stale: profiles/pmc_traffic.json (%s) measured %s code %s, this library's is %s" % (
-                row.get("source", "?"), kernel, row["kernel_code_sha16"], now)
-        return row, "profiles/pmc_traffic.json (%s, %s code %s)" % (row.get("source", "?"), kernel, now)
+            return None, "stale: %s (%s) measured %s code %s, this library's is %s" % (
+                rel, row.get("source", "?"), kernel, row["kernel_code_sha16"], now)
+        return row, "%s (%s, %s code %s)" % (rel, row.get("source", "?"), kernel, now)
     now = _kernel_sources_sha16()
     if row.get("kernel_sources_sha16") != now:
         return None, "stale: profiles/pmc_traffic.json (%s) measured kernel sources %s, these are %s" % (
@@ -221,6 +222,29 @@ def planes_traffic(kernel, workload):
     if not rows:
         return None
     return sum(b * n for b, n in rows) / sum(n for _, n in rows)
+
+
+def ranked_pmc(words):
+    """The RANKED kernels' counter bytes per solve from the committed PMC
+    passes of one toot 6x4 solve (profiles/pmc_ranked.json, tools/pmc_ranked.sh
+    + tools/pmc_summary.py --traffic), each only while the kernel's gfx950
+    code is the one measured; the backward's write bytes against the words it
+    produces (one byte per reached position)."""
+    path = os.path.join(ROOT, "profiles", "pmc_ranked.json")
+    res = {}
+    for k in ("k_rk_backward", "k_rk_reach", "k_rk_boards_sl"):
+        row, note = _pmc_row(k, "toot_and_otto_bitstring length=6,height=4", path)
+        if not row:
+            res[k] = {"source": note}
+            continue
+        n = row.get("launches", 0)
+        res[k] = {"fetch_bytes_per_solve": row["fetch_bytes_per_launch"] * n,
+                  "write_bytes_per_solve": row["write_bytes_per_launch"] * n,
+                  "l2_hit_rate": row.get("l2_hit_rate"), "launches": n, "source": note}
+    b = res["k_rk_backward"]
+    if "write_bytes_per_solve" in b:
+        b["write_bytes_over_words_produced"] = b["write_bytes_per_solve"] / words
+    return res
 
 
 def golden(name):
@@ -347,6 +371,8 @@ def _keyed_solve(device, layout):
             out["kernels"][name] = {"launches": n, "ms_total": ms, model: b,
                                     "achieved_GBps": b / (ms / 1e3) / 1e9,
                                     "frac": b / (ms / 1e3) / 1e9 / HBM_PEAK_GBS}
+    if lay == "ranked":
+        out["pmc"] = ranked_pmc(r.positions)
     # the whole solve against its own layout's bytes; for RANKED, SURVEY
     # §8d's keyed-table bytes (work it does NOT do: no keys are moved) only as
     # an equivalent rate comparable with the keyed layouts, never as a

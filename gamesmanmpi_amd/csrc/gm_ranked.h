@@ -518,8 +518,9 @@ __global__ __launch_bounds__(256) void k_rk_forward(RankGeom g, uint32_t L, u64 
 // (16 KB), so 9 workgroups fit a CU instead of 4 and the waves in flight go
 // from 4 to 6 per SIMD (then bound by the 79 VGPRs) -- the pass waits on its
 // gathers most of the time (SQ_WAIT_ANY 59 %, profiles/r05d))
-template <int CC, int HH, int U, int SPT = 64>
-__global__ __launch_bounds__(256) void k_rk_backward(RankGeom g, uint32_t L, u64 lvstart, uint32_t lvoff,
+template <int CC, int HH, int U, int SPT = 64, int WPE = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_rk_backward(
+    RankGeom g, uint32_t L, u64 lvstart, uint32_t lvoff,
                                                      u64 nwords, u64 cstart, u64 csize, BlockCount* bc, DevState* st) {
   static_assert(SPT == 64 || SPT == 32, "tile words of 64 or 32 slots");
   typedef typename std::conditional<SPT == 64, u64, uint32_t>::type MW;  // a tile word
@@ -747,6 +748,28 @@ static int rank_shape(const Desc* d, RankShape* rs) {
     }
     byl[s].push_back(c);
   }
+  // Block order inside a level.  A child block (hv + e_x) is read by up to C
+  // parent blocks, one per column; in ascending code order those are up to
+  // (H+1)^(C-1) codes apart, so a child block's lines are fetched again by
+  // parents far away in time.  GM_RK_ORDER=morton orders a level's blocks by
+  // the bit-interleaved height digits instead (neighbours along any column
+  // mostly close together) -- A/B
+  if (const char* e = getenv("GM_RK_ORDER")) {
+    if (!strcmp(e, "morton")) {
+      auto key = [&](uint32_t c) {
+        uint32_t dig[kRankMaxCols] = {}, v = c;
+        for (uint32_t x = 0; x < g.C; x++) {
+          dig[x] = v % g.R;
+          v /= g.R;
+        }
+        u64 k = 0;
+        for (int b = 3; b >= 0; b--)
+          for (int x = (int)g.C - 1; x >= 0; x--) k = k * 2 + ((dig[x] >> b) & 1u);
+        return k;
+      };
+      for (auto& v : byl) std::sort(v.begin(), v.end(), [&](uint32_t a, uint32_t b) { return key(a) < key(b); });
+    }
+  }
   rs->base.assign(nhv, 0);
   rs->lvhv.clear();
   rs->lvph.clear();
@@ -897,6 +920,14 @@ static int rk_spt() {
   }();
   return v;
 }
+// GM_RK_WPE=8: the backward compiled for 8 waves per SIMD (<= 64 VGPRs; A/B)
+static int rk_wpe() {
+  static const int v = [] {
+    const char* e = getenv("GM_RK_WPE");
+    return e && atoi(e) == 8 ? 8 : 1;
+  }();
+  return v;
+}
 // the bit-sliced board kernel (k_rk_boards_sl) where it applies; GM_RK_SLICED=0
 // keeps the per-board one (A/B runs)
 static bool rk_sliced() {
@@ -983,7 +1014,13 @@ static int run_ranked(gm_solver* s, gm_result* out) {
     const u64 cn = L + 1 < (uint32_t)T ? s->rlvstart[L + 2] - cs : 0;
     auto go = [&](auto CH) {
       constexpr int CC = decltype(CH)::value / 16, HH = decltype(CH)::value % 16;
-      if (spt == 32 && rk_unroll() == 1)
+      if (spt == 32 && rk_unroll() == 1 && rk_wpe() == 8)
+        hipLaunchKernelGGL((k_rk_backward<CC, HH, 1, 32, 8>), dim3(rank_grid(s, nw)), dim3(256), 0, st, g, L,
+                           s->rlvstart[L], s->rlvoff[L], nw, cs, cn, s->bcount, s->st);
+      else if (spt == 32 && rk_wpe() == 8)
+        hipLaunchKernelGGL((k_rk_backward<CC, HH, 2, 32, 8>), dim3(rank_grid(s, nw)), dim3(256), 0, st, g, L,
+                           s->rlvstart[L], s->rlvoff[L], nw, cs, cn, s->bcount, s->st);
+      else if (spt == 32 && rk_unroll() == 1)
         hipLaunchKernelGGL((k_rk_backward<CC, HH, 1, 32>), dim3(rank_grid(s, nw)), dim3(256), 0, st, g, L,
                            s->rlvstart[L], s->rlvoff[L], nw, cs, cn, s->bcount, s->st);
       else if (spt == 32)
