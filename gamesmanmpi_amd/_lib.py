@@ -32,6 +32,7 @@ GM_F_PLANE_ROUND_ROBIN = 2048  # PLANES shards A/B: round-robin blocks (one halo
 GM_F_PLANE_LEVEL_SYNC = 4096  # PLANES shards A/B: level-synchronous deal instead of the staged pipeline
 GM_F_PLANE_NO_RUNS = 8192  # PLANES A/B: no one-workgroup runs of narrow levels / keys
 GM_F_BKS_LOCAL = 16384  # md5-sharded bucketed: local dedup before hashing / sending
+GM_F_RANKED_SHARD = 32768  # gm_plan_keyed_shard: md5 shards of the RANKED layout (toot-and-otto)
 KERNEL_FLAGS = (GM_F_WORDS32 | GM_F_RESOLVE_SCALAR | GM_F_SHARD_INORDER | GM_F_WORDS16 | GM_F_BK_EXACT
                 | GM_F_GRAPH | GM_F_LEVEL_MAJOR | GM_F_PLANE_X1 | GM_F_PLANE_ROUND_ROBIN
                 | GM_F_PLANE_LEVEL_SYNC | GM_F_PLANE_NO_RUNS
@@ -119,7 +120,7 @@ EXPORTS = (
     "gm_solver_destroy", "gm_solve", "gm_plan_multi", "gm_query", "gm_release", "gm_owner", "gm_owner_host",
     "gm_plan_shard", "gm_plan_keyed_shard", "gm_solver_create_shard", "gm_comm_unique_id",
     "gm_solver_comm_init", "gm_solve_group", "gm_solver_set_flags", "gm_solver_set_steps",
-    "gm_shard_info", "gm_solver_set_transport", "gm_shard_halo_sigs", "gm_plane_halo_plan",
+    "gm_shard_info", "gm_solver_set_transport", "gm_shard_halo_sigs", "gm_plane_halo_plan", "gm_rk_shard_stats",
     "gm_ks_begin", "gm_ks_level_size", "gm_ks_expand", "gm_ks_insert",
     "gm_ks_finalize", "gm_ks_counts", "gm_ks_children", "gm_ks_reduce",
     "gm_ks_end", "gm_graph_solve",
@@ -192,6 +193,7 @@ def load():
         "gm_solver_set_transport": [c.c_void_p, XFER_FN, c.c_void_p],
         "gm_shard_halo_sigs": [c.c_int, c.c_int, c.c_int, c.c_uint32, c.c_void_p, c.c_uint32],
         "gm_plane_halo_plan": [c.c_int, c.c_int, c.c_int, c.c_uint32, c.c_void_p, c.c_uint32],
+        "gm_rk_shard_stats": [c.c_void_p, c.c_void_p],
         "gm_ks_begin": [c.c_void_p, c.c_int],
         "gm_ks_level_size": [c.c_void_p, c.c_int, P(c.c_uint64)],
         "gm_ks_expand": [c.c_void_p, c.c_int, c.c_void_p, c.c_void_p,

@@ -518,10 +518,20 @@ __global__ __launch_bounds__(256) void k_rk_forward(RankGeom g, uint32_t L, u64 
 // (16 KB), so 9 workgroups fit a CU instead of 4 and the waves in flight go
 // from 4 to 6 per SIMD (then bound by the 79 VGPRs) -- the pass waits on its
 // gathers most of the time (SQ_WAIT_ANY 59 %, profiles/r05d))
-template <int CC, int HH, int U, int SPT = 64, int WPE = 1>
+// md5 owners of 32 slots as three bit planes (gm_ranked_shard.h: ownb[w] =
+// bits 0, 1, 2 of the owners of slots 32w .. 32w + 31 in x, y, z): bit j of
+// the result = slot j's owner is v (< 8)
+__device__ __forceinline__ uint32_t rko_own_mask(const uint4 o, uint32_t v) {
+  return ((v & 1u) ? o.x : ~o.x) & ((v & 2u) ? o.y : ~o.y) & ((v & 4u) ? o.z : ~o.z);
+}
+
+// OWN (md5 shards, gm_ranked_shard.h): only the slots whose md5 owner
+// (ownb: bit planes, 16 B per 32 slots) is `orank` are resolved here; the
+// others arrive from their owners before the level above reads them
+template <int CC, int HH, int U, int SPT = 64, int WPE = 1, bool OWN = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_rk_backward(
-    RankGeom g, uint32_t L, u64 lvstart, uint32_t lvoff,
-                                                     u64 nwords, u64 cstart, u64 csize, BlockCount* bc, DevState* st) {
+    RankGeom g, uint32_t L, u64 lvstart, uint32_t lvoff, u64 nwords, u64 cstart, u64 csize, BlockCount* bc,
+    DevState* st, const uint4* __restrict__ ownb = nullptr, uint32_t orank = 0) {
   static_assert(SPT == 64 || SPT == 32, "tile words of 64 or 32 slots");
   typedef typename std::conditional<SPT == 64, u64, uint32_t>::type MW;  // a tile word
   constexpr int LG = SPT == 64 ? 6 : 5;
@@ -531,7 +541,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       __builtin_amdgcn_make_buffer_rsrc(g.words + cstart, 0, (int)(uint32_t)csize, 0x00020000);
   __shared__ uint16_t list[256 * SPT];
   __shared__ uint32_t wsum[4];
-  u64 edges = 0;
+  u64 edges = 0, resolved = 0;
   uint32_t err = 0;
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const bool fmoves = (L & 1u) == 0;  // the first mover moves at even levels
@@ -539,8 +549,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const u64 wi = t0 + threadIdx.x;
     // the list holds the EXPANDABLE slots (reached, not primitive: one kind of
     // work per lane); the reached primitives take their board's value below
-    const MW m = wi < nwords ? reinterpret_cast<const MW*>(g.expd)[(lvstart >> LG) + wi] : (MW)0;
-    const MW mp = wi < nwords ? reinterpret_cast<const MW*>(g.reach)[(lvstart >> LG) + wi] & ~m : (MW)0;
+    MW m = wi < nwords ? reinterpret_cast<const MW*>(g.expd)[(lvstart >> LG) + wi] : (MW)0;
+    MW mp = wi < nwords ? reinterpret_cast<const MW*>(g.reach)[(lvstart >> LG) + wi] & ~m : (MW)0;
+    if constexpr (OWN) {
+      static_assert(SPT == 32, "owned tiles: 32-slot words");
+      const MW om = wi < nwords ? rko_own_mask(ownb[(lvstart >> 5) + wi], orank) : (MW)0;
+      m &= om;
+      mp &= om;
+      resolved += (u64)__builtin_popcount(m | mp);
+    }
     for (MW pm = mp; pm; pm &= pm - 1) {
       const u64 i = (wi << LG) + (u64)__builtin_ctzll((u64)pm);
       const u64 blk = i >> (L + 3);
@@ -662,6 +679,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   }
   if (err) atomicOr(&st->err, err);
   block_count(bc, 0, edges);
+  if constexpr (OWN) {  // slots this shard resolved (gm_rk_shard_stats)
+    for (int o = 32; o > 0; o >>= 1) resolved += __shfl_xor(resolved, o);
+    if ((threadIdx.x & 63) == 0 && resolved) atomicAdd((unsigned long long*)&st->ks_cursor, (unsigned long long)resolved);
+  }
 }
 
 // the end of a solve: the root's word, then the counts (fill_red_body)
@@ -848,6 +869,7 @@ static int plan_ranked(const Desc* d, uint64_t max_table_bytes, gm_plan_t* out, 
   return 0;
 }
 
+static int rko_setup(gm_solver* s, const gm_buffers* buf, const RankShape& rs);  // gm_ranked_shard.h
 static int rank_setup(gm_solver* s, const gm_buffers* buf) {
   RankShape rs;
   int rc = rank_shape(&s->d, &rs);
@@ -887,6 +909,7 @@ static int rank_setup(gm_solver* s, const gm_buffers* buf) {
     tabs[rs.g.T + 1 + L] = rs.lvoff[L];
   }
   HIPCHK(hipMemcpy(s->rlv_dev, tabs.data(), tabs.size() * 8, hipMemcpyHostToDevice));
+  if (s->world > 1) return rko_setup(s, buf, rs);  // md5 shards: owners, exchange buffers
   return 0;
 }
 
@@ -942,10 +965,90 @@ static int rank_grid(const gm_solver* s, u64 nitems) {
   return (int)std::max<u64>(1, std::min<u64>((nitems + 255) / 256, (u64)std::min(s->grid * 2, kCountSlots)));
 }
 
+// one forward level of the RANKED solve: the board pass, then reach / counts
+static void rank_forward_level(gm_solver* s, hipStream_t st, uint32_t L) {
+  const Desc& d = s->d;
+  const RankGeom& g = s->rg;
+  rank_kind_dispatch(d, [&](auto KC) {
+    constexpr int KIND = decltype(KC)::value;
+    const u64 nreal = s->rlvitems[L] >> 3, nb = (s->rlvstart[L + 1] - s->rlvstart[L]) >> 3;  // boards
+    auto boards = [&](auto CH) {
+      constexpr int CC = decltype(CH)::value / 16, HH = decltype(CH)::value % 16;
+      hipLaunchKernelGGL((k_rk_boards<KIND, CC, HH>), dim3(rank_grid(s, nb)), dim3(256), 0, st, d, g, L,
+                         s->rlvstart[L] >> 3, s->rlvoff[L], nb, nreal);
+    };
+    auto boards_sl = [&](auto CH) {
+      constexpr int CC = decltype(CH)::value / 16, HH = decltype(CH)::value % 16;
+      hipLaunchKernelGGL((k_rk_boards_sl<CC, HH>), dim3(rank_grid(s, nb / 32)), dim3(256), 0, st, g, L,
+                         s->rlvstart[L] >> 3, s->rlvoff[L], nb / 32, nreal);
+    };
+    const bool sliced = L >= 5 && rk_sliced();
+    if (g.C == 6 && g.H == 4) {
+      if (sliced) boards_sl(std::integral_constant<int, 6 * 16 + 4>());
+      else boards(std::integral_constant<int, 6 * 16 + 4>());
+    } else if (g.C == 5 && g.H == 4) {
+      if (sliced) boards_sl(std::integral_constant<int, 5 * 16 + 4>());
+      else boards(std::integral_constant<int, 5 * 16 + 4>());
+    } else if (g.C == 4 && g.H == 4 && sliced) {
+      boards_sl(std::integral_constant<int, 4 * 16 + 4>());
+    } else {
+      boards(std::integral_constant<int, 0>());
+    }
+    const u64 n = s->rlvstart[L + 1] - s->rlvstart[L];  // 512-padded: every bitmap word written
+    if (L >= 6)
+      hipLaunchKernelGGL(k_rk_reach, dim3(rank_grid(s, n / 64)), dim3(256), 0, st, g, L, s->rlvstart[L],
+                         s->rlvoff[L], n / 64, s->rlvitems[L], s->bcount, s->st);
+    else
+      hipLaunchKernelGGL(k_rk_forward, dim3(rank_grid(s, n)), dim3(256), 0, st, g, L, s->rlvstart[L], s->rlvoff[L],
+                         n, s->rlvitems[L], s->bcount, s->st);
+  });
+}
+
+// one backward level (ownb: md5 shards -- only the slots `orank` owns, in
+// 32-slot tile words)
+static void rank_backward_level(gm_solver* s, hipStream_t st, uint32_t L, const uint4* ownb = nullptr,
+                                uint32_t orank = 0) {
+  const RankGeom& g = s->rg;
+  const uint32_t T = g.T;
+  const int spt = ownb ? 32 : rk_spt();
+  const u64 nw = (s->rlvitems[L] + spt - 1) / spt;  // tile words
+  // level L + 1's slots (the last level has no children: an empty range)
+  const u64 cs = s->rlvstart[std::min<uint32_t>(L + 1, T)];
+  const u64 cn = L + 1 < T ? s->rlvstart[L + 2] - cs : 0;
+  const dim3 grid(rank_grid(s, nw)), blk(256);
+  auto go = [&](auto CH) {
+    constexpr int CC = decltype(CH)::value / 16, HH = decltype(CH)::value % 16;
+    if (ownb)
+      hipLaunchKernelGGL((k_rk_backward<CC, HH, 2, 32, 1, true>), grid, blk, 0, st, g, L, s->rlvstart[L],
+                         s->rlvoff[L], nw, cs, cn, s->bcount, s->st, ownb, orank);
+    else if (spt == 32 && rk_unroll() == 1 && rk_wpe() == 8)
+      hipLaunchKernelGGL((k_rk_backward<CC, HH, 1, 32, 8>), grid, blk, 0, st, g, L, s->rlvstart[L], s->rlvoff[L], nw,
+                         cs, cn, s->bcount, s->st, nullptr, 0u);
+    else if (spt == 32 && rk_wpe() == 8)
+      hipLaunchKernelGGL((k_rk_backward<CC, HH, 2, 32, 8>), grid, blk, 0, st, g, L, s->rlvstart[L], s->rlvoff[L], nw,
+                         cs, cn, s->bcount, s->st, nullptr, 0u);
+    else if (spt == 32 && rk_unroll() == 1)
+      hipLaunchKernelGGL((k_rk_backward<CC, HH, 1, 32>), grid, blk, 0, st, g, L, s->rlvstart[L], s->rlvoff[L], nw, cs,
+                         cn, s->bcount, s->st, nullptr, 0u);
+    else if (spt == 32)
+      hipLaunchKernelGGL((k_rk_backward<CC, HH, 2, 32>), grid, blk, 0, st, g, L, s->rlvstart[L], s->rlvoff[L], nw, cs,
+                         cn, s->bcount, s->st, nullptr, 0u);
+    else if (rk_unroll() == 2)
+      hipLaunchKernelGGL((k_rk_backward<CC, HH, 2>), grid, blk, 0, st, g, L, s->rlvstart[L], s->rlvoff[L], nw, cs, cn,
+                         s->bcount, s->st, nullptr, 0u);
+    else
+      hipLaunchKernelGGL((k_rk_backward<CC, HH, 4>), grid, blk, 0, st, g, L, s->rlvstart[L], s->rlvoff[L], nw, cs, cn,
+                         s->bcount, s->st, nullptr, 0u);
+  };
+  if (g.C == 6 && g.H == 4) go(std::integral_constant<int, 6 * 16 + 4>());
+  else if (g.C == 5 && g.H == 4) go(std::integral_constant<int, 5 * 16 + 4>());
+  else if (g.C == 4 && g.H == 4) go(std::integral_constant<int, 4 * 16 + 4>());
+  else go(std::integral_constant<int, 0>());
+}
+
 // Steps (gm_solver_set_steps): forward level L is step L, backward level L
 // step 2T - 1 - L, as for the other layouts.
 static int run_ranked(gm_solver* s, gm_result* out) {
-  const Desc& d = s->d;
   const RankGeom& g = s->rg;
   const int T = (int)g.T;
   const int first = (int)s->step_first, stop = s->step_stop ? (int)s->step_stop : 2 * T;
@@ -967,76 +1070,13 @@ static int run_ranked(gm_solver* s, gm_result* out) {
     HIPCHK(hipMemsetD32Async((hipDeviceptr_t)&s->st->word_bits, 0x208, 1, st));  // the solve in progress: ranked
   }
   u64 nl_f = 0, nl_b = 0;
-  rank_kind_dispatch(d, [&](auto KC) {
-    constexpr int KIND = decltype(KC)::value;
-    for (int k = std::max(first, 0); k < std::min(stop, T); k++) {
-      const uint32_t L = (uint32_t)k;
-      const u64 nreal = s->rlvitems[L] >> 3, nb = (s->rlvstart[L + 1] - s->rlvstart[L]) >> 3;  // boards
-      auto boards = [&](auto CH) {
-        constexpr int CC = decltype(CH)::value / 16, HH = decltype(CH)::value % 16;
-        hipLaunchKernelGGL((k_rk_boards<KIND, CC, HH>), dim3(rank_grid(s, nb)), dim3(256), 0, st, d, g, L,
-                           s->rlvstart[L] >> 3, s->rlvoff[L], nb, nreal);
-      };
-      auto boards_sl = [&](auto CH) {
-        constexpr int CC = decltype(CH)::value / 16, HH = decltype(CH)::value % 16;
-        hipLaunchKernelGGL((k_rk_boards_sl<CC, HH>), dim3(rank_grid(s, nb / 32)), dim3(256), 0, st, g, L,
-                           s->rlvstart[L] >> 3, s->rlvoff[L], nb / 32, nreal);
-      };
-      const bool sliced = L >= 5 && rk_sliced();
-      if (g.C == 6 && g.H == 4) {
-        if (sliced) boards_sl(std::integral_constant<int, 6 * 16 + 4>());
-        else boards(std::integral_constant<int, 6 * 16 + 4>());
-      } else if (g.C == 5 && g.H == 4) {
-        if (sliced) boards_sl(std::integral_constant<int, 5 * 16 + 4>());
-        else boards(std::integral_constant<int, 5 * 16 + 4>());
-      } else if (g.C == 4 && g.H == 4 && sliced) {
-        boards_sl(std::integral_constant<int, 4 * 16 + 4>());
-      } else {
-        boards(std::integral_constant<int, 0>());
-      }
-      const u64 n = s->rlvstart[L + 1] - s->rlvstart[L];  // 512-padded: every bitmap word written
-      if (L >= 6)
-        hipLaunchKernelGGL(k_rk_reach, dim3(rank_grid(s, n / 64)), dim3(256), 0, st, g, L, s->rlvstart[L],
-                           s->rlvoff[L], n / 64, s->rlvitems[L], s->bcount, s->st);
-      else
-        hipLaunchKernelGGL(k_rk_forward, dim3(rank_grid(s, n)), dim3(256), 0, st, g, L, s->rlvstart[L], s->rlvoff[L],
-                           n, s->rlvitems[L], s->bcount, s->st);
-      nl_f += 2;
-    }
-  });
+  for (int k = std::max(first, 0); k < std::min(stop, T); k++) {
+    rank_forward_level(s, st, (uint32_t)k);
+    nl_f += 2;
+  }
   HIPCHK(hipEventRecord(ev[1], st));
   for (int k = std::max(first, T); k < stop; k++) {
-    const uint32_t L = (uint32_t)(2 * T - 1 - k);
-    const int spt = rk_spt();
-    const u64 nw = (s->rlvitems[L] + spt - 1) / spt;  // tile words
-    // level L + 1's slots (the last level has no children: an empty range)
-    const u64 cs = s->rlvstart[std::min<uint32_t>(L + 1, (uint32_t)T)];
-    const u64 cn = L + 1 < (uint32_t)T ? s->rlvstart[L + 2] - cs : 0;
-    auto go = [&](auto CH) {
-      constexpr int CC = decltype(CH)::value / 16, HH = decltype(CH)::value % 16;
-      if (spt == 32 && rk_unroll() == 1 && rk_wpe() == 8)
-        hipLaunchKernelGGL((k_rk_backward<CC, HH, 1, 32, 8>), dim3(rank_grid(s, nw)), dim3(256), 0, st, g, L,
-                           s->rlvstart[L], s->rlvoff[L], nw, cs, cn, s->bcount, s->st);
-      else if (spt == 32 && rk_wpe() == 8)
-        hipLaunchKernelGGL((k_rk_backward<CC, HH, 2, 32, 8>), dim3(rank_grid(s, nw)), dim3(256), 0, st, g, L,
-                           s->rlvstart[L], s->rlvoff[L], nw, cs, cn, s->bcount, s->st);
-      else if (spt == 32 && rk_unroll() == 1)
-        hipLaunchKernelGGL((k_rk_backward<CC, HH, 1, 32>), dim3(rank_grid(s, nw)), dim3(256), 0, st, g, L,
-                           s->rlvstart[L], s->rlvoff[L], nw, cs, cn, s->bcount, s->st);
-      else if (spt == 32)
-        hipLaunchKernelGGL((k_rk_backward<CC, HH, 2, 32>), dim3(rank_grid(s, nw)), dim3(256), 0, st, g, L,
-                           s->rlvstart[L], s->rlvoff[L], nw, cs, cn, s->bcount, s->st);
-      else if (rk_unroll() == 2)
-        hipLaunchKernelGGL((k_rk_backward<CC, HH, 2>), dim3(rank_grid(s, nw)), dim3(256), 0, st, g, L,
-                           s->rlvstart[L], s->rlvoff[L], nw, cs, cn, s->bcount, s->st);
-      else
-        hipLaunchKernelGGL((k_rk_backward<CC, HH, 4>), dim3(rank_grid(s, nw)), dim3(256), 0, st, g, L,
-                           s->rlvstart[L], s->rlvoff[L], nw, cs, cn, s->bcount, s->st);
-    };
-    if (g.C == 6 && g.H == 4) go(std::integral_constant<int, 6 * 16 + 4>());
-    else if (g.C == 5 && g.H == 4) go(std::integral_constant<int, 5 * 16 + 4>());
-    else if (g.C == 4 && g.H == 4) go(std::integral_constant<int, 4 * 16 + 4>());
-    else go(std::integral_constant<int, 0>());
+    rank_backward_level(s, st, (uint32_t)(2 * T - 1 - k));
     nl_b++;
   }
   HIPCHK(hipGetLastError());

@@ -320,6 +320,8 @@ static bool rank_wanted(const Desc* d, uint32_t flags);
 static bool rank_ok(const Desc* d);
 static int plan_ranked(const Desc* d, uint64_t max_table_bytes, gm_plan_t* out, bool* fits);
 static int rank_setup(gm_solver* s, const gm_buffers* buf);
+static int plan_ranked_shard(const Desc* d, int world, uint64_t max_table_bytes, gm_plan_t* out);
+static int run_ranked_shards(std::vector<gm_solver*> ss, gm_result* out);
 static int run_ranked(gm_solver* s, gm_result* out);
 static int rank_query(gm_solver* s, const uint64_t* keys_dev, uint64_t n, uint32_t* words_dev);
 static int rank_positions(gm_solver* s, uint64_t* keys_dev, uint64_t cap, uint64_t* n);
@@ -1059,6 +1061,14 @@ struct gm_solver {
   std::vector<uint32_t> rlvoff;        // per level: first entry of its block list
   std::vector<u64> rlvstart, rlvitems;  // per level: first slot, slots
   u64* rlv_dev = nullptr;              // device: rlvstart then rlvoff (k_rk_scan)
+  // md5 shards of the RANKED layout (gm_ranked_shard.h), inside the table
+  // buffer: every slot's owner, the level pack / receive buffers, per-level
+  // tile counts, their offsets and totals (device; the totals also on the host)
+  uint4* rko_own = nullptr;  // owner bit planes, 16 B per 32 slots
+  uint8_t *rko_pk = nullptr, *rko_rb = nullptr;
+  uint32_t *rko_cnt = nullptr, *rko_toff = nullptr;
+  u64* rko_tot = nullptr;
+  std::vector<u64> rko_tile0, rko_tot_h;
 };
 
 static const int kBlock = 256;
@@ -1759,6 +1769,10 @@ int gm_plan_keyed_shard(int game, int rank, int world, uint64_t positions, uint3
   const Desc* d = get_game(game);
   if (!d || !out) return fail(GM_EINVAL, "bad argument");
   if (world < 2 || world > 8 || rank < 0 || rank >= world) return fail(GM_EINVAL, "bad shard %d/%d (2..8 ranks)", rank, world);
+  if (flags & GM_F_RANKED_SHARD) {  // the RANKED index space, md5-owned slots (gm_ranked_shard.h)
+    memset(out, 0, sizeof *out);
+    return plan_ranked_shard(d, world, max_table_bytes, out);
+  }
   if (!bk_ok(d) || (flags & GM_F_HASH_TABLE))
     return fail(GM_EINVAL, "md5-sharded bucketed levels need every move to advance one level");
   memset(out, 0, sizeof *out);
@@ -1893,7 +1907,9 @@ int gm_solver_create_shard(int game, int rank, int world, const gm_buffers* buf,
     if (!d->dense_ok || !plane_ok(d, world)) return fail(GM_EINVAL, "game has no planes layout");
     if (world > 1 && (rank < 0 || rank >= world)) return fail(GM_EINVAL, "bad shard %d/%d", rank, world);
   } else if (buf->mode == GM_MODE_RANKED) {
-    if (world != 1) return fail(GM_EINVAL, "ranked tables are one-GPU (shard keyed games by md5: gm_plan_keyed_shard)");
+    if (world != 1 && !(buf->flags & GM_F_RANKED_SHARD))
+      return fail(GM_EINVAL, "ranked md5 shards are planned with GM_F_RANKED_SHARD (gm_plan_keyed_shard)");
+    if (world > 8 || rank < 0 || rank >= world) return fail(GM_EINVAL, "bad ranked shard %d/%d (2..8 ranks)", rank, world);
     if (!rank_ok(d)) return fail(GM_EINVAL, "game has no ranked layout");
   } else if (buf->mode == GM_MODE_BUCKETED) {
     if (world < 1 || rank < 0 || rank >= world) return fail(GM_EINVAL, "bad shard %d/%d", rank, world);
@@ -2203,8 +2219,9 @@ int gm_shard_halo_sigs(int game, int rank, int world, uint32_t flags, uint64_t* 
 
 int gm_solver_set_transport(gm_solver* s, gm_xfer_fn fn, void* ctx) {
   if (!s) return fail(GM_EINVAL, "bad argument");
-  if ((s->mode != GM_MODE_DENSE && s->mode != GM_MODE_PLANES && s->mode != GM_MODE_BUCKETED) || s->world <= 1)
-    return fail(GM_EINVAL, "a transport serves dense / planes / bucketed shards of a world > 1");
+  if ((s->mode != GM_MODE_DENSE && s->mode != GM_MODE_PLANES && s->mode != GM_MODE_BUCKETED &&
+       s->mode != GM_MODE_RANKED) || s->world <= 1)
+    return fail(GM_EINVAL, "a transport serves dense / planes / bucketed / ranked shards of a world > 1");
   s->xfer = fn;
   s->xfer_ctx = ctx;
   return 0;
@@ -2254,7 +2271,7 @@ int gm_solver_solve(gm_solver* s, gm_result* out) {
   memset(out, 0, sizeof *out);
   if (s->mode == GM_MODE_DENSE) return solve_dense(s, out);
   if (s->mode == GM_MODE_PLANES) return run_planes({s}, out);
-  if (s->mode == GM_MODE_RANKED) return run_ranked(s, out);
+  if (s->mode == GM_MODE_RANKED) return s->world > 1 ? run_ranked_shards({s}, out) : run_ranked(s, out);
   if (s->mode == GM_MODE_BUCKETED) return s->world > 1 ? run_bucketed_shards({s}, out) : solve_bucketed(s, out);
   if (s->world > 1) return fail(GM_EINVAL, "keyed-table shard %d/%d: drive it with gm_ks_* (md5 exchange)", s->rank, s->world);
   const int T = s->d.max_levels;
@@ -2513,6 +2530,17 @@ static int xfer_ranges(gm_solver* s, const std::vector<HostRange>& out, int sp, 
 
 #include "gm_plane_run.h"
 #include "gm_ranked.h"
+#include "gm_ranked_shard.h"
+
+int gm_rk_shard_stats(gm_solver* s, uint64_t out[2]) {
+  if (!s || !out) return fail(GM_EINVAL, "bad argument");
+  if (s->mode != GM_MODE_RANKED || s->world < 2 || !s->rko_own) return fail(GM_EINVAL, "not a ranked md5 shard");
+  HIPCHK(hipStreamSynchronize(s->stream));
+  HIPCHK(hipMemcpy(&out[0], &s->st->ks_cursor, sizeof(u64), hipMemcpyDeviceToHost));
+  out[1] = 0;
+  for (size_t L = 0; L < s->rko_tot_h.size() / (size_t)s->world; L++) out[1] += s->rko_tot_h[L * s->world + s->rank];
+  return 0;
+}
 
 int gm_plane_halo_plan(int game, int rank, int world, uint32_t flags, uint64_t* out, uint32_t levels) {
   const Desc* d = get_game(game);
@@ -3673,10 +3701,7 @@ int gm_solve_group(gm_solver** shards, int n, gm_result* out) {
     if (!s) return fail(GM_EINVAL, "null shard");
   if (ss[0]->mode == GM_MODE_PLANES) return run_planes(ss, out);
   if (ss[0]->mode == GM_MODE_BUCKETED) return run_bucketed_shards(ss, out);
-  if (ss[0]->mode == GM_MODE_RANKED) {
-    if (n != 1) return fail(GM_EINVAL, "ranked tables are one-GPU");
-    return run_ranked(ss[0], out);
-  }
+  if (ss[0]->mode == GM_MODE_RANKED) return ss[0]->world > 1 ? run_ranked_shards(ss, out) : run_ranked(ss[0], out);
   return run_dense(ss, out);
 }
 

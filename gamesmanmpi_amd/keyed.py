@@ -365,11 +365,23 @@ def _shard_bound(spec, world, positions):
     return int(int(positions or spec.positions_bound) * 1.03) // int(world) + 65536
 
 
+def ranked_shards_apply(spec, world):
+    """True when md5 shards of the RANKED index space serve this game
+    (toot-and-otto boards: gm_ranked_shard.h)."""
+    plan = _lib.gm_plan_t()
+    return _lib.load().gm_plan_keyed_shard(
+        spec.id, 0, int(world), 0, _lib.GM_F_RANKED_SHARD, 0, ctypes.byref(plan)) == 0
+
+
 def _pick(spec, world, layout):
-    if layout not in ("auto", "bucketed", "hashed"):
-        raise ValueError("layout: auto, bucketed or hashed")
+    if layout not in ("auto", "bucketed", "hashed", "ranked"):
+        raise ValueError("layout: auto, ranked, bucketed or hashed")
     if layout == "hashed":
         return "hashed"
+    if layout == "ranked":
+        if not ranked_shards_apply(spec, world):
+            raise ValueError("%r: md5-sharded RANKED tables are toot-and-otto boards only" % (spec,))
+        return "ranked"
     if bucketed_shards_apply(spec, world):
         return "bucketed"
     if layout == "bucketed":
@@ -393,9 +405,10 @@ def group_keyed_solve(spec, world, device=None, layout="auto", flags=0, streams=
     dev = torch.device(device if device is not None else "cuda")
     ss = _group_streams(dev, world, streams)
     stream = ss[0]
-    if _pick(spec, world, layout) == "bucketed":
+    pick = _pick(spec, world, layout)
+    if pick in ("bucketed", "ranked"):
         per = _shard_bound(spec, world, 0)
-        shards = [Solver(spec, positions=per, device=dev, layout="bucketed",
+        shards = [Solver(spec, positions=per, device=dev, layout=pick,
                          rank=g, world=world, stream=ss[g], flags=flags)
                   for g in range(world)]
         arr = (ctypes.c_void_p * world)(*[s.handle.value for s in shards])
@@ -422,11 +435,12 @@ def dist_keyed_solve(spec, device=None, positions=0, stage=None,
     import torch.distributed as dist
     spec = spec if isinstance(spec, GameSpec) else GameSpec(*spec)
     world = dist.get_world_size()
-    if _pick(spec, world, layout) == "bucketed":
+    pick = _pick(spec, world, layout)
+    if pick in ("bucketed", "ranked"):
         from .dist import ShardedSolver
         shard = ShardedSolver(spec, dist.get_rank(), world, device=device,
                               transport="host" if stage == "cpu" else "rccl",
-                              layout="bucketed", flags=flags,
+                              layout=pick, flags=flags,
                               positions=_shard_bound(spec, world, positions))
         res = shard.solve()
         res.extra.update({"partition": "md5", "world": world})

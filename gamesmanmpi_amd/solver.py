@@ -97,8 +97,11 @@ class Solver:
         flags = self.flags | {"hashed": _lib.GM_F_FORCE_HASHED | _lib.GM_F_HASH_TABLE,
                               "bucketed": _lib.GM_F_FORCE_HASHED,
                               "dense": _lib.GM_F_LEVEL_MAJOR}.get(self._planned_layout, 0)
-        if self.world > 1 and self.layout == "bucketed":
-            # an md5 shard of bucketed levels: `positions` bounds this shard
+        if self.world > 1 and self.layout in ("bucketed", "ranked"):
+            # an md5 shard of bucketed levels (`positions` bounds this
+            # shard), or of the RANKED index space (toot-and-otto)
+            if self.layout == "ranked":
+                flags |= _lib.GM_F_RANKED_SHARD
             _lib.check(L.gm_plan_keyed_shard(self.spec.id, self.rank,
                                              self.world, int(positions), flags,
                                              self.max_table_bytes,
@@ -166,6 +169,13 @@ class Solver:
     @property
     def handle(self):
         return self._h
+
+    def shard_stats(self):
+        """md5 shards of the RANKED layout: (slots this shard resolved in its
+        last solve, reached positions its md5 owner rule gives it)."""
+        out = (ctypes.c_uint64 * 2)()
+        _lib.check(_lib.load().gm_rk_shard_stats(self._h, out))
+        return int(out[0]), int(out[1])
 
     def set_kernel_timing(self, on):
         """Time every kernel launch with HIP events (on the solve stream)."""

@@ -85,6 +85,9 @@ def build_parser():
     p.add_argument("--no-verify", action="store_true",
                    help="skip replaying the module against its descriptor")
     p.add_argument("--verify-samples", type=int, default=200)
+    p.add_argument("--ranked-replicated", action="store_true",
+                   help="under torchrun, toot-and-otto: every rank solves the whole RANKED table "
+                        "instead of the md5-owned RANKED shards")
     p.add_argument("--json", action="store_true",
                    help="also print a JSON line with counts and timings")
     p.add_argument("--symmetries", action="store_true",
@@ -104,20 +107,25 @@ def build_parser():
 DENSE_STEMS = ("four_to_one", "sum_four_to_one")  # rank-indexable descriptors
 
 
-def ranked_fits(spec, local):
+def ranked_fits(spec, local, world=1, replicated=False):
     """The game has a RANKED plan (toot-and-otto) that fits this GPU's free
-    memory with a margin."""
+    memory with a margin: the one-table plan, or (world > 1, not replicated)
+    an md5 shard's (the table + owner bit planes + level exchange buffers)."""
     import ctypes
     from gamesmanmpi_amd import _lib
     p = _lib.gm_plan_t()
-    if _lib.load().gm_plan(spec.id, 0, 0, 0, ctypes.byref(p)) != 0 or p.mode != _lib.GM_MODE_RANKED:
+    if world > 1 and not replicated:
+        rc = _lib.load().gm_plan_keyed_shard(spec.id, 0, world, 0, _lib.GM_F_RANKED_SHARD, 0, ctypes.byref(p))
+    else:
+        rc = _lib.load().gm_plan(spec.id, 0, 0, 0, ctypes.byref(p))
+    if rc != 0 or p.mode != _lib.GM_MODE_RANKED:
         return False
     import torch
     free, _ = torch.cuda.mem_get_info(local)
     return p.table_bytes + p.scratch_bytes < 0.8 * free
 
 
-def agreed_ranked(spec, layout, local):
+def agreed_ranked(spec, layout, local, world=1, replicated=False):
     """Under torchrun: do ALL ranks take the replicated RANKED path?  Each
     rank's own answer (ranked_fits: its GPU's free memory) is combined with a
     MIN all-reduce, so every rank branches the same way and the collectives
@@ -129,7 +137,7 @@ def agreed_ranked(spec, layout, local):
     import torch.distributed as dist
     if layout not in ("auto", "ranked"):
         return False
-    mine = bool(ranked_fits(spec, local))
+    mine = bool(ranked_fits(spec, local, world, replicated))
     dev = torch.device("cuda", local) if dist.get_backend() == "nccl" else torch.device("cpu")
     t = torch.tensor([1 if mine else 0], dtype=torch.int32, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MIN)
@@ -256,22 +264,28 @@ def main(argv=None):
             from gamesmanmpi_amd.dist import ShardedSolver
             solver = ShardedSolver(spec, rank, world, device="cuda:%d" % local)
             result = solver.solve()
-        elif agreed_ranked(spec, args.layout, local):
-            # toot-and-otto: the whole RANKED table fits one GPU (toot 6x4:
-            # 8.9 GB, 17.5 ms) -- every rank solves it and writes the md5
-            # share the reference's partition gives it; sharding it would
-            # exchange every level
+        elif args.ranked_replicated and agreed_ranked(spec, args.layout, local, world, True):
+            # (--ranked-replicated) every rank solves the whole RANKED table
+            # and writes the md5 share the reference's partition gives it
             from gamesmanmpi_amd.solver import Solver
             solver = Solver(spec, positions=args.positions, device="cuda:%d" % local, layout="ranked")
             solver.replicated = True
             result = solver.solve()
             result.extra.update({"partition": "replicated", "world": world})
+        elif not args.ranked_replicated and agreed_ranked(spec, args.layout, local, world):
+            # toot-and-otto: md5 shards of the RANKED index space -- every
+            # position resolved by its md5 owner (src/game_state.py:22-30),
+            # each level's words exchanged over RCCL (gm_ranked_shard.h);
+            # every rank ends with the whole table and writes its md5 share
+            from gamesmanmpi_amd.keyed import dist_keyed_solve
+            result, solver = dist_keyed_solve(spec, device="cuda:%d" % local, layout="ranked")
+            solver.replicated = True
         else:
             # the reference's md5 partition, all-to-all per level (keyed.py)
             from gamesmanmpi_amd.keyed import dist_keyed_solve
             result, shard = dist_keyed_solve(spec, device="cuda:%d" % local,
                                              positions=args.positions)
-            solver = shard.solver
+            solver = getattr(shard, "solver", shard)  # (GpuShard wraps its Solver; a bucketed shard is one)
     elif args.checkpoint:
         from gamesmanmpi_amd import checkpoint
         from gamesmanmpi_amd.solver import Solver

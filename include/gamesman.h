@@ -155,6 +155,11 @@ typedef struct gm_buffers {
                                   children locally first and hash / send each
                                   unique child once (A/B against hashing and
                                   sending every child occurrence) */
+#define GM_F_RANKED_SHARD 32768u /* gm_plan_keyed_shard: toot-and-otto as md5
+                                  shards of the RANKED index space (every
+                                  slot resolved by its md5 owner, level words
+                                  exchanged; gm_ranked_shard.h) instead of
+                                  BUCKETED levels */
 #define GM_F_GRAPH 256u      /* dense one-table full solves: capture the
                                   forward and backward launches as HIP graphs
                                   on the first solve, replay them after
@@ -342,6 +347,12 @@ int gm_shard_halo_sigs(int game, int rank, int world, uint32_t flags, uint64_t *
  * (the game's levels always suffice), else GM_EINVAL.  Replaces the per-edge
  * message fan-out of the reference's shards (src/process.py:37-267). */
 int gm_plane_halo_plan(int game, int rank, int world, uint32_t flags, uint64_t *out, uint32_t levels);
+/* md5 shards of the RANKED layout: out[0] = the slots this shard resolved in
+ * its last solve (k_rk_backward<OWN>), out[1] = the reached positions its md5
+ * owner rule gives it (src/game_state.py:22-30).  Equal on every shard, and
+ * the out[1] add up to the positions, when every position was resolved on
+ * its owner. */
+int gm_rk_shard_stats(gm_solver *s, uint64_t out[2]);
 /* All `n` shards of one job in ONE process on one stream, halos moved by
  * device-to-device copies: the same kernels and halo geometry as the RCCL
  * path, runnable on a single GPU (parity tests). */

@@ -18,7 +18,7 @@ def _worker(rank, world, port, q, fits, layout):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from gamesmanmpi_amd import solver_launcher as sl
-        sl.ranked_fits = lambda spec, local: fits[rank]
+        sl.ranked_fits = lambda spec, local, *a: fits[rank]
         spec = types.SimpleNamespace(name="toot_and_otto_bitstring")
         try:
             q.put((rank, "ranked" if sl.agreed_ranked(spec, layout, 0) else "keyed"))
