@@ -528,7 +528,7 @@ __device__ __forceinline__ uint32_t rko_own_mask(const uint4 o, uint32_t v) {
 // OWN (md5 shards, gm_ranked_shard.h): only the slots whose md5 owner
 // (ownb: bit planes, 16 B per 32 slots) is `orank` are resolved here; the
 // others arrive from their owners before the level above reads them
-template <int CC, int HH, int U, int SPT = 64, int WPE = 1, bool OWN = false>
+template <int CC, int HH, int U, int SPT = 64, int WPE = 1, bool OWN = false, int DBG = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_rk_backward(
     RankGeom g, uint32_t L, u64 lvstart, uint32_t lvoff, u64 nwords, u64 cstart, u64 csize, BlockCount* bc,
     DevState* st, const uint4* __restrict__ ownb = nullptr, uint32_t orank = 0) {
@@ -558,11 +558,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       mp &= om;
       resolved += (u64)__builtin_popcount(m | mp);
     }
-    for (MW pm = mp; pm; pm &= pm - 1) {
-      const u64 i = (wi << LG) + (u64)__builtin_ctzll((u64)pm);
-      const u64 blk = i >> (L + 3);
-      const uint32_t pat = (uint32_t)(i & ((1ull << L) - 1));
-      g.words[lvstart + i] = (uint8_t)make_word(g.bstat[(lvstart >> 3) + (blk << L) + pat], 0);  // process.py:120-123
+    // the reached primitives take their board's value (process.py:120-123).
+    // From L = 5 on, a 32-slot word's slots are 32 consecutive boards (one
+    // block, one a): their bstat bytes come in as two 16-B loads and go out as
+    // the word row -- bstat's byte is the word (remoteness 0) -- whole: the
+    // expandable slots' bytes are rewritten by the entries below (after the
+    // barrier), the unreached ones are never read.  A loop of one dependent
+    // load and store per primitive cost 2.6 of the 10.3 ms backward
+    // (GM_RK_DBG A/B, round 5).
+    if (SPT == 32 && L >= 5) {
+      if (mp) {
+        const u64 i0 = wi << LG, blk = i0 >> (L + 3);
+        const uint32_t pat0 = (uint32_t)(i0 & ((1ull << L) - 1));
+        const uint4* src = reinterpret_cast<const uint4*>(g.bstat + (lvstart >> 3) + (blk << L) + pat0);
+        uint4* dst = reinterpret_cast<uint4*>(g.words + lvstart + i0);
+        const uint4 v0 = src[0], v1 = src[1];
+        dst[0] = v0;
+        dst[1] = v1;
+      }
+    } else {
+      for (MW pm = mp; pm; pm &= pm - 1) {
+        const u64 i = (wi << LG) + (u64)__builtin_ctzll((u64)pm);
+        const u64 blk = i >> (L + 3);
+        const uint32_t pat = (uint32_t)(i & ((1ull << L) - 1));
+        g.words[lvstart + i] = (uint8_t)make_word(g.bstat[(lvstart >> 3) + (blk << L) + pat], 0);
+      }
     }
     // exclusive scan of the popcounts over the workgroup
     const uint32_t c = (uint32_t)__builtin_popcountll((u64)m);
@@ -595,7 +615,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     __syncthreads();
     // U entries per pass (e, e + 256, ...): U x 2C child loads in flight per
     // lane before any reduction or store
-    for (uint32_t e0 = threadIdx.x; e0 < total; e0 += 256u * U) {
+    for (uint32_t e0 = threadIdx.x; e0 < (DBG == 2 ? 0u : total); e0 += 256u * U) {
       uint32_t offu[U][2 * NC], nchu[U];
       u64 slotu[U];
       bool liveu[U];
@@ -650,7 +670,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
       for (int u = 0; u < U; u++)
 #pragma unroll
-        for (int k = 0; k < 2 * NC; k++) wu[u][k] = __builtin_amdgcn_raw_buffer_load_b8(rw, offu[u][k], 0, 0);
+        for (int k = 0; k < 2 * NC; k++)
+          wu[u][k] = DBG == 1 ? (offu[u][k] & 0x7Du)  // (A/B only: no gathers, a word from the offset)
+                              : __builtin_amdgcn_raw_buffer_load_b8(rw, offu[u][k], 0, 0);
 #pragma unroll
       for (int u = 0; u < U; u++) {
         // reference-canonical _res_red / _remote_red over the children (an
@@ -943,6 +965,15 @@ static int rk_spt() {
   }();
   return v;
 }
+// GM_RK_DBG=1 / 2: the backward without its gathers / without its entries
+// (timing A/B only: the words are wrong)
+static int rk_dbg() {
+  static const int v = [] {
+    const char* e = getenv("GM_RK_DBG");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
 // GM_RK_WPE=8: the backward compiled for 8 waves per SIMD (<= 64 VGPRs; A/B)
 static int rk_wpe() {
   static const int v = [] {
@@ -1021,6 +1052,12 @@ static void rank_backward_level(gm_solver* s, hipStream_t st, uint32_t L, const 
     if (ownb)
       hipLaunchKernelGGL((k_rk_backward<CC, HH, 2, 32, 1, true>), grid, blk, 0, st, g, L, s->rlvstart[L],
                          s->rlvoff[L], nw, cs, cn, s->bcount, s->st, ownb, orank);
+    else if (rk_dbg() == 1)
+      hipLaunchKernelGGL((k_rk_backward<CC, HH, 2, 32, 1, false, 1>), grid, blk, 0, st, g, L, s->rlvstart[L],
+                         s->rlvoff[L], nw, cs, cn, s->bcount, s->st, nullptr, 0u);
+    else if (rk_dbg() == 2)
+      hipLaunchKernelGGL((k_rk_backward<CC, HH, 2, 32, 1, false, 2>), grid, blk, 0, st, g, L, s->rlvstart[L],
+                         s->rlvoff[L], nw, cs, cn, s->bcount, s->st, nullptr, 0u);
     else if (spt == 32 && rk_unroll() == 1 && rk_wpe() == 8)
       hipLaunchKernelGGL((k_rk_backward<CC, HH, 1, 32, 8>), grid, blk, 0, st, g, L, s->rlvstart[L], s->rlvoff[L], nw,
                          cs, cn, s->bcount, s->st, nullptr, 0u);
