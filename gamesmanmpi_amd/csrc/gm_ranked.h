@@ -678,17 +678,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         // reference-canonical _res_red / _remote_red over the children (an
         // absent child reads 0: WIN in 0, changes none of the four;
         // SURVEY §8a A8/A9)
-        bool any_loss = false, any_tie = false, any_draw = false;
-        uint32_t min_loss = 0xFFFFFFFFu, max_all = 0;
+        // in VALU terms: the values seen as one-hot bits (1 << v, OR), the
+        // largest word (its remoteness is the largest: r = w >> 2), and the
+        // smallest word among the LOSS children -- a word + 256 unless its
+        // value is LOSS (v = 1: (w ^ 1) & 3 == 0), so a minimum below 256 is
+        // a LOSS child's; min / max over pairs of children (v_min3 / v_max3)
+        uint32_t oh = 0, mn = 0xFFFFu, mx = 0;
 #pragma unroll
         for (int k = 0; k < 2 * NC; k++) {
-          const uint32_t v = wu[u][k] & 3u, r = wu[u][k] >> 2;
-          any_loss |= v == LOSS;
-          min_loss = v == LOSS ? min(min_loss, r) : min_loss;
-          any_tie |= v == TIE;
-          any_draw |= v == DRAW;
-          max_all = max(max_all, r);
+          const uint32_t w = wu[u][k];
+          oh |= 1u << (w & 3u);
+          mn = min(mn, w + (((w ^ 1u) & 3u) << 8));
+          mx = max(mx, w);
         }
+        const bool any_loss = (oh >> LOSS) & 1u, any_tie = (oh >> TIE) & 1u, any_draw = (oh >> DRAW) & 1u;
+        const uint32_t min_loss = mn >> 2, max_all = mx >> 2;
         if (!liveu[u]) continue;
         if (nchu[u] == 0) err |= ERR_NO_MOVES;
         edges += nchu[u];
