@@ -444,6 +444,82 @@ __global__ __launch_bounds__(256) void k_rk_reach(RankGeom g, uint32_t L, u64 lv
   block_add(&st->prims, prims);
 }
 
+// The same, four consecutive words per thread per step (L >= 6: a height-
+// vector block is >= 8 words, so an aligned group of four shares one block,
+// its metadata and its parents' bases): the four words' parent loads are in
+// flight together instead of one word's three dependent round trips (block
+// metadata -> parent base -> parent bits) after another: the toot 6x4
+// forward 2.01 -> 1.91 ms (round 5, tools/rk_anatomy.sh)
+__global__ __launch_bounds__(256) void k_rk_reach4(RankGeom g, uint32_t L, u64 lvstart, uint32_t lvoff, u64 nwords,
+                                                   u64 nreal, BlockCount* bc, DevState* st) {
+  u64 npos = 0, prims = 0;
+  const bool fmoved = ((L - 1) & 1u) == 0;  // the move into level L was the first mover's
+  for (u64 w0 = ((u64)blockIdx.x * blockDim.x + threadIdx.x) * 4; w0 < nwords; w0 += (u64)gridDim.x * blockDim.x * 4) {
+    const u64 b0 = w0 << 6;
+    u64* rout = reinterpret_cast<u64*>(g.reach) + ((lvstart + b0) >> 6);
+    u64* xout = reinterpret_cast<u64*>(g.expd) + ((lvstart + b0) >> 6);
+    if (b0 >= nreal) {  // padding (nreal: whole blocks, a multiple of four words)
+      reinterpret_cast<uint4*>(rout)[0] = reinterpret_cast<uint4*>(rout)[1] = make_uint4(0, 0, 0, 0);
+      reinterpret_cast<uint4*>(xout)[0] = reinterpret_cast<uint4*>(xout)[1] = make_uint4(0, 0, 0, 0);
+      continue;
+    }
+    const u64 blk = b0 >> (L + 3);
+    const uint32_t hvc = g.lvhv[lvoff + blk];
+    RankPos p;
+    rk_unpack(g, g.lvph[lvoff + blk], p);
+    uint32_t a[4], p0[4];
+    u64 valid[4], r[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const u64 i0 = b0 + ((u64)k << 6);
+      a[k] = (uint32_t)((i0 >> L) & 7u);
+      p0[k] = (uint32_t)(i0 & ((1ull << L) - 1));
+      valid[k] = rk_valid_mask(g, L, a[k], p0[k]);
+      r[k] = 0;
+    }
+#pragma unroll
+    for (int x = 0; x < kRankMaxCols; x++) {
+      if (x >= (int)g.C || p.h[x] == 0) continue;
+      const uint32_t q = p.off[x] + p.h[x] - 1;
+      const u64 pb = g.base[hvc - g.stride[x]];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        if (!valid[k]) continue;
+        if (q >= 6) {
+          const uint32_t l = (p0[k] >> q) & 1u;
+          if (fmoved && l && a[k] == 0) continue;
+          const uint32_t pa = a[k] - (fmoved && l ? 1u : 0u);
+          const uint32_t pp0 = (p0[k] & ((1u << q) - 1u)) | ((p0[k] >> (q + 1)) << q);
+          r[k] |= reinterpret_cast<const u64*>(g.expd)[(pb + ((u64)pa << (L - 1)) + pp0) >> 6];
+        } else {
+#pragma unroll
+          for (uint32_t l = 0; l < 2; l++) {
+            if (fmoved && l && a[k] == 0) continue;
+            const uint32_t pa = a[k] - (fmoved && l ? 1u : 0u);
+            const u64 ps0 = pb + ((u64)pa << (L - 1)) + (p0[k] >> 1);  // a multiple of 32
+            r[k] |= rk_spread(g.expd[ps0 >> 5], q) << (l << q);
+          }
+        }
+      }
+    }
+    u64 e[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      r[k] &= valid[k];
+      const u64 pm = reinterpret_cast<const u64*>(g.pbits)[((lvstart >> 3) + (blk << L) + p0[k]) >> 6];
+      e[k] = r[k] & ~pm;
+      npos += (u64)__builtin_popcountll(r[k]);
+      prims += (u64)__builtin_popcountll(r[k] & pm);
+    }
+    reinterpret_cast<uint4*>(rout)[0] = make_uint4((uint32_t)r[0], (uint32_t)(r[0] >> 32), (uint32_t)r[1], (uint32_t)(r[1] >> 32));
+    reinterpret_cast<uint4*>(rout)[1] = make_uint4((uint32_t)r[2], (uint32_t)(r[2] >> 32), (uint32_t)r[3], (uint32_t)(r[3] >> 32));
+    reinterpret_cast<uint4*>(xout)[0] = make_uint4((uint32_t)e[0], (uint32_t)(e[0] >> 32), (uint32_t)e[1], (uint32_t)(e[1] >> 32));
+    reinterpret_cast<uint4*>(xout)[1] = make_uint4((uint32_t)e[2], (uint32_t)(e[2] >> 32), (uint32_t)e[3], (uint32_t)(e[3] >> 32));
+  }
+  block_count(bc, npos, 0);
+  block_add(&st->prims, prims);
+}
+
 // F1 for levels L < 6 (blocks narrower than a word): one thread per slot
 // (nitems: the level's slots rounded up to 64, so every bitmap word of the
 // level is written -- no clearing -- nreal: its slots)
@@ -1031,7 +1107,7 @@ static void rank_forward_level(gm_solver* s, hipStream_t st, uint32_t L) {
     }
     const u64 n = s->rlvstart[L + 1] - s->rlvstart[L];  // 512-padded: every bitmap word written
     if (L >= 6)
-      hipLaunchKernelGGL(k_rk_reach, dim3(rank_grid(s, n / 64)), dim3(256), 0, st, g, L, s->rlvstart[L],
+      hipLaunchKernelGGL(k_rk_reach4, dim3(rank_grid(s, n / 256)), dim3(256), 0, st, g, L, s->rlvstart[L],
                          s->rlvoff[L], n / 64, s->rlvitems[L], s->bcount, s->st);
     else
       hipLaunchKernelGGL(k_rk_forward, dim3(rank_grid(s, n)), dim3(256), 0, st, g, L, s->rlvstart[L], s->rlvoff[L],
