@@ -232,7 +232,7 @@ def ranked_pmc(words):
     produces (one byte per reached position)."""
     path = os.path.join(ROOT, "profiles", "pmc_ranked.json")
     res = {}
-    for k in ("k_rk_backward", "k_rk_reach", "k_rk_boards_sl"):
+    for k in ("k_rk_backward", "k_rk_reach4", "k_rk_boards_sl"):
         row, note = _pmc_row(k, "toot_and_otto_bitstring length=6,height=4", path)
         if not row:
             res[k] = {"source": note}

@@ -389,67 +389,14 @@ __device__ __forceinline__ u64 rk_spread(uint32_t e, uint32_t q) {
 // q < 6 the children with letter l at bit q have 32 consecutive parents, half
 // a word, spread back to the child bits (rk_spread).  expandable = reached
 // and not a primitive board (pbits).
+// Four consecutive words per thread per step (a height-vector block is >= 8
+// words at L >= 6, so an aligned group of four shares one block, its metadata
+// and its parents' bases): the four words' parent loads are in flight
+// together instead of one word's three dependent round trips (block metadata
+// -> parent base -> parent bits) after another -- the toot 6x4 forward
+// 2.01 -> 1.91 ms against one word per thread (round 5, tools/rk_anatomy.sh).
 // (nwords: the level's 512-slot padded extent in words -- every bitmap word
 // of the level is written, the padding's as 0; nreal: its slots)
-__global__ __launch_bounds__(256) void k_rk_reach(RankGeom g, uint32_t L, u64 lvstart, uint32_t lvoff, u64 nwords,
-                                                  u64 nreal, BlockCount* bc, DevState* st) {
-  u64 npos = 0, prims = 0;
-  const bool fmoved = ((L - 1) & 1u) == 0;  // the move into level L was the first mover's
-  for (u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += (u64)gridDim.x * blockDim.x) {
-    const u64 i0 = w << 6, blk = i0 >> (L + 3);
-    if (i0 >= nreal) {  // padding
-      reinterpret_cast<u64*>(g.reach)[(lvstart + i0) >> 6] = 0;
-      reinterpret_cast<u64*>(g.expd)[(lvstart + i0) >> 6] = 0;
-      continue;
-    }
-    const uint32_t a = (uint32_t)((i0 >> L) & 7u), p0 = (uint32_t)(i0 & ((1ull << L) - 1));
-    const uint32_t hvc = g.lvhv[lvoff + blk];
-    RankPos p;
-    rk_unpack(g, g.lvph[lvoff + blk], p);
-    const u64 valid = rk_valid_mask(g, L, a, p0);
-    u64 r = 0;
-    if (valid) {
-#pragma unroll
-      for (int x = 0; x < kRankMaxCols; x++) {
-        if (x >= (int)g.C || p.h[x] == 0) continue;
-        const uint32_t q = p.off[x] + p.h[x] - 1;
-        const u64 pb = g.base[hvc - g.stride[x]];
-        if (q >= 6) {
-          const uint32_t l = (p0 >> q) & 1u;
-          if (fmoved && l && a == 0) continue;
-          const uint32_t pa = a - (fmoved && l ? 1u : 0u);
-          const uint32_t pp0 = (p0 & ((1u << q) - 1u)) | ((p0 >> (q + 1)) << q);
-          r |= reinterpret_cast<const u64*>(g.expd)[(pb + ((u64)pa << (L - 1)) + pp0) >> 6];
-        } else {
-          // children j with bit q = l: parents (p0 >> 1) + compress_q(j), 32 in a row
-#pragma unroll
-          for (uint32_t l = 0; l < 2; l++) {
-            if (fmoved && l && a == 0) continue;
-            const uint32_t pa = a - (fmoved && l ? 1u : 0u);
-            const u64 ps0 = pb + ((u64)pa << (L - 1)) + (p0 >> 1);  // a multiple of 32
-            const uint32_t e = g.expd[ps0 >> 5];
-            r |= rk_spread(e, q) << (l << q);
-          }
-        }
-      }
-      r &= valid;
-    }
-    const u64 pm = reinterpret_cast<const u64*>(g.pbits)[((lvstart >> 3) + (blk << L) + p0) >> 6];
-    reinterpret_cast<u64*>(g.reach)[(lvstart + i0) >> 6] = r;
-    reinterpret_cast<u64*>(g.expd)[(lvstart + i0) >> 6] = r & ~pm;
-    npos += (u64)__builtin_popcountll(r);
-    prims += (u64)__builtin_popcountll(r & pm);
-  }
-  block_count(bc, npos, 0);
-  block_add(&st->prims, prims);
-}
-
-// The same, four consecutive words per thread per step (L >= 6: a height-
-// vector block is >= 8 words, so an aligned group of four shares one block,
-// its metadata and its parents' bases): the four words' parent loads are in
-// flight together instead of one word's three dependent round trips (block
-// metadata -> parent base -> parent bits) after another: the toot 6x4
-// forward 2.01 -> 1.91 ms (round 5, tools/rk_anatomy.sh)
 __global__ __launch_bounds__(256) void k_rk_reach4(RankGeom g, uint32_t L, u64 lvstart, uint32_t lvoff, u64 nwords,
                                                    u64 nreal, BlockCount* bc, DevState* st) {
   u64 npos = 0, prims = 0;
@@ -577,23 +524,19 @@ __global__ __launch_bounds__(256) void k_rk_forward(RankGeom g, uint32_t L, u64 
 }
 
 // B: the reached slots of level L gather their children's words.  A
-// workgroup takes a tile of 256 x 64 slots: each thread reads one reach word,
-// the workgroup lays the reached slots' offsets out in LDS (exclusive scan of
-// the words' popcounts), then every thread resolves list entries -- waves
-// carry reached slots only (about 1 in 6 of all slots on toot 6x4), and a
-// primitive's value comes from bstat.
-// The children's words come through a buffer resource over level L + 1 (< 4
-// GB: every level of a supported board): a move that is not legal reads
-// offset 0xFFFFFFFF, out of range, i.e. 0 = WIN in 0, neutral in the
-// reduction -- so all 2C loads issue back to back with no branches.  CC / HH:
-// the board at compile time (0: from g).
-// (U: list entries per lane per pass -- U x 2C child loads in flight before
-// any reduction; a tile inside one height-vector block (L >= 11) reads its
-// block's stacks / child bases once, wave-uniform.  SPT: slots per thread
-// and tile word, 64 or 32: a tile of 256 x 32 slots halves the LDS list
-// (16 KB), so 9 workgroups fit a CU instead of 4 and the waves in flight go
-// from 4 to 6 per SIMD (then bound by the 79 VGPRs) -- the pass waits on its
-// gathers most of the time (SQ_WAIT_ANY 59 %, profiles/r05d))
+// workgroup takes a tile of 256 x 32 slots: each thread reads one 32-slot
+// reach word, the workgroup lays the reached slots' offsets out in LDS
+// (exclusive scan of the words' popcounts), then every thread resolves list
+// entries -- waves carry reached slots only (about 1 in 6 of all slots on
+// toot 6x4), and a primitive's value comes from bstat.  The 16 KB list lets
+// 9 workgroups share a CU (then bound by VGPRs); a list of 256 x 64 slots
+// (4 per CU) was slower (profiles/r05d: SQ_WAIT_ANY 59 %).
+// The children's words come through a buffer resource over level L + 1: a
+// move that is not legal reads an offset past the level's end, i.e. 0 = WIN
+// in 0, neutral in the reduction -- so all 2C loads of an entry, two entries
+// per lane, issue back to back with no branches.  CC / HH: the board at
+// compile time (0: from g).  A tile inside one height-vector block (L >= 10)
+// reads its block's stacks / child bases once, wave-uniform.
 // md5 owners of 32 slots as three bit planes (gm_ranked_shard.h: ownb[w] =
 // bits 0, 1, 2 of the owners of slots 32w .. 32w + 31 in x, y, z): bit j of
 // the result = slot j's owner is v (< 8)
@@ -601,35 +544,49 @@ __device__ __forceinline__ uint32_t rko_own_mask(const uint4 o, uint32_t v) {
   return ((v & 1u) ? o.x : ~o.x) & ((v & 2u) ? o.y : ~o.y) & ((v & 4u) ? o.z : ~o.z);
 }
 
+typedef unsigned short rk_u16x2 __attribute__((ext_vector_type(2)));
+
+// Offsets of an illegal move.  A board compiled in (CC > 0: every level
+// <= 1 GiB, rank_backward_level checks) marks a full column by a child base of
+// 2^30 and an empty hand by a slot base of 2^31: one add3 per child, and any
+// sum holding a mark lands in [2^30, 2^32), past the level's end -- then
+// clamped to 2^30, one address for every illegal move of a wave (distinct
+// out-of-range addresses cost the gathers as much as real ones: toot 6x4
+// backward 7.6 -> 8.9 ms without the clamp).  The generic kernel (levels up
+// to 4 GB) adds with unsigned saturation instead: a mark of 2^32 - 1 stays
+// there.
+constexpr uint32_t kRkColMark = 0x40000000u, kRkHandMark = 0x80000000u;
+
 // OWN (md5 shards, gm_ranked_shard.h): only the slots whose md5 owner
 // (ownb: bit planes, 16 B per 32 slots) is `orank` are resolved here; the
-// others arrive from their owners before the level above reads them
-template <int CC, int HH, int U, int SPT = 64, int WPE = 1, bool OWN = false, int DBG = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_rk_backward(
-    RankGeom g, uint32_t L, u64 lvstart, uint32_t lvoff, u64 nwords, u64 cstart, u64 csize, BlockCount* bc,
-    DevState* st, const uint4* __restrict__ ownb = nullptr, uint32_t orank = 0) {
-  static_assert(SPT == 64 || SPT == 32, "tile words of 64 or 32 slots");
-  typedef typename std::conditional<SPT == 64, u64, uint32_t>::type MW;  // a tile word
-  constexpr int LG = SPT == 64 ? 6 : 5;
+// others arrive from their owners before the level above reads them.
+// DBG (A/B timing only, the words are wrong): 1 = no gathers, 2 = no entries.
+template <int CC, int HH, bool OWN = false, int DBG = 0>
+__global__ __launch_bounds__(256) void k_rk_backward(RankGeom g, uint32_t L, u64 lvstart, uint32_t lvoff,
+                                                     u64 nwords, u64 cstart, u64 csize, BlockCount* bc, DevState* st,
+                                                     const uint4* __restrict__ ownb = nullptr, uint32_t orank = 0) {
+  constexpr int U = 2;  // entries per lane per pass: U x 2C child loads in flight before any reduction
   constexpr int NC = CC > 0 ? CC : kRankMaxCols;
+  constexpr bool NARROW = CC > 0;
   const uint32_t C = CC > 0 ? (uint32_t)CC : g.C, H = HH > 0 ? (uint32_t)HH : g.H;
+  const uint32_t colmark = NARROW ? kRkColMark : 0xFFFFFFFFu, handmark = NARROW ? kRkHandMark : 0xFFFFFFFFu;
   const __amdgpu_buffer_rsrc_t rw =
       __builtin_amdgcn_make_buffer_rsrc(g.words + cstart, 0, (int)(uint32_t)csize, 0x00020000);
-  __shared__ uint16_t list[256 * SPT];
+  __shared__ uint16_t list[256 * 32];
   __shared__ uint32_t wsum[4];
   u64 edges = 0, resolved = 0;
   uint32_t err = 0;
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const bool fmoves = (L & 1u) == 0;  // the first mover moves at even levels
+  const uint32_t dT = fmoves ? (1u << (L + 1)) : 0u;  // the first mover's T: one a-row on
   for (u64 t0 = (u64)blockIdx.x * 256; t0 < nwords; t0 += (u64)gridDim.x * 256) {
     const u64 wi = t0 + threadIdx.x;
     // the list holds the EXPANDABLE slots (reached, not primitive: one kind of
     // work per lane); the reached primitives take their board's value below
-    MW m = wi < nwords ? reinterpret_cast<const MW*>(g.expd)[(lvstart >> LG) + wi] : (MW)0;
-    MW mp = wi < nwords ? reinterpret_cast<const MW*>(g.reach)[(lvstart >> LG) + wi] & ~m : (MW)0;
+    uint32_t m = wi < nwords ? g.expd[(lvstart >> 5) + wi] : 0u;
+    uint32_t mp = wi < nwords ? g.reach[(lvstart >> 5) + wi] & ~m : 0u;
     if constexpr (OWN) {
-      static_assert(SPT == 32, "owned tiles: 32-slot words");
-      const MW om = wi < nwords ? rko_own_mask(ownb[(lvstart >> 5) + wi], orank) : (MW)0;
+      const uint32_t om = wi < nwords ? rko_own_mask(ownb[(lvstart >> 5) + wi], orank) : 0u;
       m &= om;
       mp &= om;
       resolved += (u64)__builtin_popcount(m | mp);
@@ -642,9 +599,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // barrier), the unreached ones are never read.  A loop of one dependent
     // load and store per primitive cost 2.6 of the 10.3 ms backward
     // (GM_RK_DBG A/B, round 5).
-    if (SPT == 32 && L >= 5) {
+    if (L >= 5) {
       if (mp) {
-        const u64 i0 = wi << LG, blk = i0 >> (L + 3);
+        const u64 i0 = wi << 5, blk = i0 >> (L + 3);
         const uint32_t pat0 = (uint32_t)(i0 & ((1ull << L) - 1));
         const uint4* src = reinterpret_cast<const uint4*>(g.bstat + (lvstart >> 3) + (blk << L) + pat0);
         uint4* dst = reinterpret_cast<uint4*>(g.words + lvstart + i0);
@@ -653,15 +610,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         dst[1] = v1;
       }
     } else {
-      for (MW pm = mp; pm; pm &= pm - 1) {
-        const u64 i = (wi << LG) + (u64)__builtin_ctzll((u64)pm);
+      for (uint32_t pm = mp; pm; pm &= pm - 1) {
+        const u64 i = (wi << 5) + (u64)__builtin_ctz(pm);
         const u64 blk = i >> (L + 3);
         const uint32_t pat = (uint32_t)(i & ((1ull << L) - 1));
         g.words[lvstart + i] = (uint8_t)make_word(g.bstat[(lvstart >> 3) + (blk << L) + pat], 0);
       }
     }
     // exclusive scan of the popcounts over the workgroup
-    const uint32_t c = (uint32_t)__builtin_popcountll((u64)m);
+    const uint32_t c = (uint32_t)__builtin_popcount(m);
     uint32_t incl = c;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -676,10 +633,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       total += wsum[k];
     }
     uint32_t at = before + incl - c;
-    for (MW mm = m; mm; mm &= mm - 1) list[at++] = (uint16_t)(threadIdx.x * SPT + __builtin_ctzll((u64)mm));
+    for (uint32_t mm = m; mm; mm &= mm - 1) list[at++] = (uint16_t)(threadIdx.x * 32 + __builtin_ctz(mm));
     // one block for the whole tile: its stacks and child bases, read once
-    const u64 tb0 = (t0 << LG) >> (L + 3);
-    const bool oneblk = ((((t0 + 255) << LG) + (SPT - 1)) >> (L + 3)) == tb0;
+    const u64 tb0 = (t0 << 5) >> (L + 3);
+    const bool oneblk = ((((t0 + 255) << 5) + 31) >> (L + 3)) == tb0;
     uint32_t tph = 0, tcho[kRankMaxCols] = {};
     if (oneblk) {
       tph = g.lvph[lvoff + tb0];
@@ -689,23 +646,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       tcho[4] = c1.x, tcho[5] = c1.y, tcho[6] = c1.z, tcho[7] = c1.w;
     }
     __syncthreads();
-    // U entries per pass (e, e + 256, ...): U x 2C child loads in flight per
-    // lane before any reduction or store
     for (uint32_t e0 = threadIdx.x; e0 < (DBG == 2 ? 0u : total); e0 += 256u * U) {
       uint32_t offu[U][2 * NC], nchu[U];
       u64 slotu[U];
       bool liveu[U];
       // the children's offsets: lo | hi (the stacks with a 0 inserted at bit
-      // q = the column's top) is pat + (pat & ~(2^q - 1)), the T child adds
-      // 2^q and, if the first mover placed it, one a-row (2^(L+1)); a tile
-      // inside one block runs a copy of this with the block's stacks and
-      // child bases uniform, so q, the masks and the bases stay scalar
+      // q = the column's top) is pat + (pat & ~(2^q - 1)); the T child adds
+      // 2^q and, if the first mover placed it, one a-row (dT).  Per column:
+      // its child base (or colmark when full) and 2^q; per entry: the slot's
+      // own part for the O and the T children (or handmark when that hand is
+      // empty) -- a tile inside one block runs a copy with the column terms
+      // wave-uniform (scalar)
       auto entries = [&](const uint32_t phu, const uint32_t* chou, bool uni) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
           const uint32_t e = e0 + 256u * (uint32_t)u;
           liveu[u] = e < total;
-          const u64 i = (t0 << LG) + list[liveu[u] ? e : e0];
+          const u64 i = (t0 << 5) + list[liveu[u] ? e : e0];
           slotu[u] = lvstart + i;
           const u64 blk = i >> (L + 3);
           const uint32_t a = (uint32_t)((i >> L) & 7u), pat = (uint32_t)(i & ((1ull << L) - 1));
@@ -721,23 +678,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             cho[4] = c1.x, cho[5] = c1.y, cho[6] = c1.z, cho[7] = c1.w;
           }
           const RankHands h_ = rk_hands(L, (uint32_t)__builtin_popcount(pat), a);
-          const bool hasT = liveu[u] && (fmoves ? h_.t1 < (int)kRankHand : h_.t2 < (int)kRankHand);
-          const bool hasO = liveu[u] && (fmoves ? h_.o1 < (int)kRankHand : h_.o2 < (int)kRankHand);
-          const uint32_t rp = (a << (L + 1)) + pat, dT = fmoves ? (1u << (L + 1)) : 0u;
-          uint32_t nch = 0, off = 0;
+          const bool hasT = fmoves ? h_.t1 < (int)kRankHand : h_.t2 < (int)kRankHand;
+          const bool hasO = fmoves ? h_.o1 < (int)kRankHand : h_.o2 < (int)kRankHand;
+          const uint32_t rp = (a << (L + 1)) + pat;
+          const uint32_t bO = hasO ? rp : handmark, bT = hasT ? rp + dT : handmark;
+          uint32_t ncol = 0, off = 0;
 #pragma unroll
           for (int x = 0; x < NC; x++) {
             const uint32_t h = (ph >> (4 * x)) & 15u;
             const bool col = (CC > 0 || (uint32_t)x < C) && h < H;
             const uint32_t q = off + h;
             off += h;
-            const uint32_t oO = cho[x] + rp + (pat & (0xFFFFFFFFu << q)), oT = oO + dT + (1u << q);
-            const bool vT = col && hasT, vO = col && hasO;
-            offu[u][2 * x] = vT ? oT : 0xFFFFFFFFu;
-            offu[u][2 * x + 1] = vO ? oO : 0xFFFFFFFFu;
-            nch += (uint32_t)vT + (uint32_t)vO;
+            const uint32_t base = col ? cho[x] : colmark, hi = pat & (0xFFFFFFFFu << q);
+            if constexpr (NARROW) {
+              offu[u][2 * x] = min(base + (1u << q) + hi + bT, kRkColMark);
+              offu[u][2 * x + 1] = min(base + hi + bO, kRkColMark);
+            } else {
+              const uint32_t bh = __builtin_elementwise_add_sat(base, hi);
+              offu[u][2 * x] = __builtin_elementwise_add_sat(__builtin_elementwise_add_sat(bh, 1u << q), bT);
+              offu[u][2 * x + 1] = __builtin_elementwise_add_sat(bh, bO);
+            }
+            ncol += (uint32_t)col;
           }
-          nchu[u] = nch;
+          nchu[u] = liveu[u] ? ncol * ((uint32_t)hasT + (uint32_t)hasO) : 0u;
         }
       };
       if (oneblk) entries(tph, tcho, true);
@@ -753,27 +716,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       for (int u = 0; u < U; u++) {
         // reference-canonical _res_red / _remote_red over the children (an
         // absent child reads 0: WIN in 0, changes none of the four;
-        // SURVEY §8a A8/A9)
-        // in VALU terms: the values seen as one-hot bits (1 << v, OR), the
-        // largest word (its remoteness is the largest: r = w >> 2), and the
-        // smallest word among the LOSS children -- a word + 256 unless its
-        // value is LOSS (v = 1: (w ^ 1) & 3 == 0), so a minimum below 256 is
-        // a LOSS child's; min / max over pairs of children (v_min3 / v_max3)
-        uint32_t oh = 0, mn = 0xFFFFu, mx = 0;
+        // SURVEY §8a A8/A9), a column's T and O children side by side in the
+        // 16-bit halves of one register (v_pk_min_u16 / v_pk_max_u16):
+        //   t = (v ^ 1) & 3 -- LOSS 0, WIN 1, DRAW 2, TIE 3: its maximum is
+        //       the best non-losing value (TIE over DRAW over WIN);
+        //   min of w + (t << 8): below 256 iff a child is a LOSS, then the
+        //       smallest LOSS child's word;  max of w: the largest remoteness
+        rk_u16x2 mn = {0xFFFFu, 0xFFFFu}, mx = {0, 0}, pr = {0, 0};
 #pragma unroll
-        for (int k = 0; k < 2 * NC; k++) {
-          const uint32_t w = wu[u][k];
-          oh |= 1u << (w & 3u);
-          mn = min(mn, w + (((w ^ 1u) & 3u) << 8));
-          mx = max(mx, w);
+        for (int x = 0; x < NC; x++) {
+          const uint32_t p = wu[u][2 * x] | (wu[u][2 * x + 1] << 16);
+          const uint32_t t = (p ^ 0x00010001u) & 0x00030003u;
+          mn = __builtin_elementwise_min(mn, __builtin_bit_cast(rk_u16x2, p + (t << 8)));
+          mx = __builtin_elementwise_max(mx, __builtin_bit_cast(rk_u16x2, p));
+          pr = __builtin_elementwise_max(pr, __builtin_bit_cast(rk_u16x2, t));
         }
-        const bool any_loss = (oh >> LOSS) & 1u, any_tie = (oh >> TIE) & 1u, any_draw = (oh >> DRAW) & 1u;
-        const uint32_t min_loss = mn >> 2, max_all = mx >> 2;
+        const uint32_t mn1 = min((uint32_t)mn.x, (uint32_t)mn.y), mx1 = max((uint32_t)mx.x, (uint32_t)mx.y);
+        const uint32_t pr1 = max((uint32_t)pr.x, (uint32_t)pr.y);
         if (!liveu[u]) continue;
         if (nchu[u] == 0) err |= ERR_NO_MOVES;
         edges += nchu[u];
-        const uint32_t word =
-            any_loss ? make_word(WIN, min_loss + 1) : make_word(any_tie ? TIE : any_draw ? DRAW : LOSS, max_all + 1);
+        const uint32_t word = mn1 < 256u ? make_word(WIN, (mn1 >> 2) + 1)
+                                         : make_word(pr1 == 3u ? TIE : pr1 == 2u ? DRAW : LOSS, (mx1 >> 2) + 1);
         g.words[slotu[u]] = (uint8_t)word;
       }
     }
@@ -1025,40 +989,12 @@ static void rank_kind_dispatch(const Desc& d, F&& f) {
   }
 }
 
-// entries per lane per backward pass: 2, or GM_RK_UNROLL=4 for A/B runs (toot
-// 6x4 backward 12.27 ms at 2 against 13.07 at 4: more loads in flight do not
-// pay, the scattered byte gathers are bound by lines per load, not latency)
-static int rk_unroll() {
-  static const int u = [] {
-    const char* e = getenv("GM_RK_UNROLL");
-    return e && atoi(e) == 4 ? 4 : e && atoi(e) == 1 ? 1 : 2;
-  }();
-  return u;
-}
-
-// backward tile words of 64 or 32 slots (k_rk_backward SPT); GM_RK_SPT=64
-// restores the round-4 tile (A/B)
-static int rk_spt() {
-  static const int v = [] {
-    const char* e = getenv("GM_RK_SPT");
-    return e && atoi(e) == 64 ? 64 : 32;
-  }();
-  return v;
-}
 // GM_RK_DBG=1 / 2: the backward without its gathers / without its entries
 // (timing A/B only: the words are wrong)
 static int rk_dbg() {
   static const int v = [] {
     const char* e = getenv("GM_RK_DBG");
     return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-// GM_RK_WPE=8: the backward compiled for 8 waves per SIMD (<= 64 VGPRs; A/B)
-static int rk_wpe() {
-  static const int v = [] {
-    const char* e = getenv("GM_RK_WPE");
-    return e && atoi(e) == 8 ? 8 : 1;
   }();
   return v;
 }
@@ -1121,8 +1057,7 @@ static void rank_backward_level(gm_solver* s, hipStream_t st, uint32_t L, const 
                                 uint32_t orank = 0) {
   const RankGeom& g = s->rg;
   const uint32_t T = g.T;
-  const int spt = ownb ? 32 : rk_spt();
-  const u64 nw = (s->rlvitems[L] + spt - 1) / spt;  // tile words
+  const u64 nw = (s->rlvitems[L] + 31) / 32;  // 32-slot tile words
   // level L + 1's slots (the last level has no children: an empty range)
   const u64 cs = s->rlvstart[std::min<uint32_t>(L + 1, T)];
   const u64 cn = L + 1 < T ? s->rlvstart[L + 2] - cs : 0;
@@ -1130,36 +1065,23 @@ static void rank_backward_level(gm_solver* s, hipStream_t st, uint32_t L, const 
   auto go = [&](auto CH) {
     constexpr int CC = decltype(CH)::value / 16, HH = decltype(CH)::value % 16;
     if (ownb)
-      hipLaunchKernelGGL((k_rk_backward<CC, HH, 2, 32, 1, true>), grid, blk, 0, st, g, L, s->rlvstart[L],
-                         s->rlvoff[L], nw, cs, cn, s->bcount, s->st, ownb, orank);
+      hipLaunchKernelGGL((k_rk_backward<CC, HH, true>), grid, blk, 0, st, g, L, s->rlvstart[L], s->rlvoff[L], nw, cs,
+                         cn, s->bcount, s->st, ownb, orank);
     else if (rk_dbg() == 1)
-      hipLaunchKernelGGL((k_rk_backward<CC, HH, 2, 32, 1, false, 1>), grid, blk, 0, st, g, L, s->rlvstart[L],
-                         s->rlvoff[L], nw, cs, cn, s->bcount, s->st, nullptr, 0u);
+      hipLaunchKernelGGL((k_rk_backward<CC, HH, false, 1>), grid, blk, 0, st, g, L, s->rlvstart[L], s->rlvoff[L], nw,
+                         cs, cn, s->bcount, s->st, nullptr, 0u);
     else if (rk_dbg() == 2)
-      hipLaunchKernelGGL((k_rk_backward<CC, HH, 2, 32, 1, false, 2>), grid, blk, 0, st, g, L, s->rlvstart[L],
-                         s->rlvoff[L], nw, cs, cn, s->bcount, s->st, nullptr, 0u);
-    else if (spt == 32 && rk_unroll() == 1 && rk_wpe() == 8)
-      hipLaunchKernelGGL((k_rk_backward<CC, HH, 1, 32, 8>), grid, blk, 0, st, g, L, s->rlvstart[L], s->rlvoff[L], nw,
+      hipLaunchKernelGGL((k_rk_backward<CC, HH, false, 2>), grid, blk, 0, st, g, L, s->rlvstart[L], s->rlvoff[L], nw,
                          cs, cn, s->bcount, s->st, nullptr, 0u);
-    else if (spt == 32 && rk_wpe() == 8)
-      hipLaunchKernelGGL((k_rk_backward<CC, HH, 2, 32, 8>), grid, blk, 0, st, g, L, s->rlvstart[L], s->rlvoff[L], nw,
-                         cs, cn, s->bcount, s->st, nullptr, 0u);
-    else if (spt == 32 && rk_unroll() == 1)
-      hipLaunchKernelGGL((k_rk_backward<CC, HH, 1, 32>), grid, blk, 0, st, g, L, s->rlvstart[L], s->rlvoff[L], nw, cs,
-                         cn, s->bcount, s->st, nullptr, 0u);
-    else if (spt == 32)
-      hipLaunchKernelGGL((k_rk_backward<CC, HH, 2, 32>), grid, blk, 0, st, g, L, s->rlvstart[L], s->rlvoff[L], nw, cs,
-                         cn, s->bcount, s->st, nullptr, 0u);
-    else if (rk_unroll() == 2)
-      hipLaunchKernelGGL((k_rk_backward<CC, HH, 2>), grid, blk, 0, st, g, L, s->rlvstart[L], s->rlvoff[L], nw, cs, cn,
-                         s->bcount, s->st, nullptr, 0u);
     else
-      hipLaunchKernelGGL((k_rk_backward<CC, HH, 4>), grid, blk, 0, st, g, L, s->rlvstart[L], s->rlvoff[L], nw, cs, cn,
+      hipLaunchKernelGGL((k_rk_backward<CC, HH>), grid, blk, 0, st, g, L, s->rlvstart[L], s->rlvoff[L], nw, cs, cn,
                          s->bcount, s->st, nullptr, 0u);
   };
-  if (g.C == 6 && g.H == 4) go(std::integral_constant<int, 6 * 16 + 4>());
-  else if (g.C == 5 && g.H == 4) go(std::integral_constant<int, 5 * 16 + 4>());
-  else if (g.C == 4 && g.H == 4) go(std::integral_constant<int, 4 * 16 + 4>());
+  // the compiled-in boards' marks need the child level <= 1 GiB (kRkColMark)
+  const bool narrow = cn <= kRkColMark;
+  if (narrow && g.C == 6 && g.H == 4) go(std::integral_constant<int, 6 * 16 + 4>());
+  else if (narrow && g.C == 5 && g.H == 4) go(std::integral_constant<int, 5 * 16 + 4>());
+  else if (narrow && g.C == 4 && g.H == 4) go(std::integral_constant<int, 4 * 16 + 4>());
   else go(std::integral_constant<int, 0>());
 }
 

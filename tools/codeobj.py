@@ -21,9 +21,9 @@ import sys
 MEASURED = {
     "k_plane_resolve_x2": ("k_plane_resolve_x2", "ILi1ELi4ELb0E"),
     "k_plane_run": ("k_plane_run", "ILi1ELi4ELb0ELb0E"),
-    "k_rk_backward": ("k_rk_backward", "ILi6ELi4ELi2ELi32ELi1ELb0EE"),  # toot 6x4, U = 2, 32-slot words, one table
+    "k_rk_backward": ("k_rk_backward", "ILi6ELi4ELb0ELi0EE"),  # toot 6x4, one table, no A/B knob
     "k_rk_boards_sl": ("k_rk_boards_sl",),
-    "k_rk_reach": ("k_rk_reach",),
+    "k_rk_reach4": ("k_rk_reach4",),
 }
 
 
