@@ -1272,6 +1272,42 @@ static int plane_backward_staged(std::vector<gm_solver*>& ss, int mode, hipStrea
 // The PLANES solve.  Steps (gm_solver_set_steps, one table only): 2T like
 // the other layouts; step 0 is the forward pass (reach map + counts), steps
 // 1..T-1 are empty, step T + l is plane level l (l <= S), later steps empty.
+// GM_PLANE_GRAPH=1: one-table full solves replay one HIP graph of the whole
+// solve (A/B; not the default: 1.40-1.43 vs 1.36-1.42 ms per 2^30 bench step
+// with plain launches, profiles/r05z -- the kernels and their device-side
+// boundaries, not the host's enqueueing, make the step)
+static bool plane_graph_on() {
+  static const bool on = [] {
+    const char* e = getenv("GM_PLANE_GRAPH");
+    return e && atoi(e) == 1;
+  }();
+  return on;
+}
+
+// the counts of a finished solve (red: positions, edges, primitives, root
+// word + 1, error bits) into the result
+static int plane_result(const std::vector<gm_solver*>& ss, const u64* red, gm_result* out) {
+  gm_solver* s0 = ss[0];
+  out->positions = red[0];
+  out->edges = red[1];
+  out->primitives = red[2];
+  out->levels = (uint32_t)s0->d.max_levels;
+  out->max_level_width = 0;
+  out->word_bits = 8 * s0->pwb;
+  out->kernels = (plane_x1(s0) ? RK_PLANE : RK_PLANE_X2) | (PK_PLANE << 16);
+  const uint32_t word = red[3] ? (uint32_t)(red[3] - 1) : NO_WORD;
+  out->root_word = word;
+  if (red[4]) {
+    for (gm_solver* s : ss)  // this process's shard failed: its own error
+      if (s->defer_rc) return fail(s->defer_rc, "shard %d/%d: %s", s->rank, s->world, s->defer_msg.c_str());
+    return fail(GM_ECORRUPT, "solve failed:%s", err_text((uint32_t)red[4]).c_str());
+  }
+  if (word == NO_WORD) return fail(GM_ECORRUPT, "root unresolved");
+  out->root_value = (int32_t)(word & 3u);
+  out->root_remoteness = word >> 2;
+  return 0;
+}
+
 static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
   gm_solver* s0 = ss[0];
   const Desc& d = s0->d;
@@ -1372,6 +1408,45 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
     if (!s0->cstream) HIPCHK(hipStreamCreateWithFlags(&s0->cstream, hipStreamNonBlocking));
     fs = s0->cstream;
   }
+  // One table, whole solve: ONE graph launch.  The solve is captured once
+  // (this function again, in capture mode: every launch and copy goes into
+  // the graph, the counts into pinned host memory) and replayed: the host no
+  // longer enqueues ~120 launches per solve, so the narrow first levels do
+  // not wait for it and the solve starts right after the call (A/B knob)
+  if (overlap && plane_graph_on() && !s0->pcapture) {
+    if (!s0->pgexec) {
+      if (!s0->phost) HIPCHK(hipHostMalloc((void**)&s0->phost, 8 * sizeof(u64), hipHostMallocDefault));
+      s0->pcapture = true;
+      gm_result cap{};
+      const int rc = run_planes(ss, &cap);
+      s0->pcapture = false;
+      hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+      if (hipStreamIsCapturing(st, &cst) == hipSuccess && cst != hipStreamCaptureStatusNone) {
+        hipGraph_t gr = nullptr;  // a capture that failed half-way
+        (void)hipStreamEndCapture(st, &gr);
+        if (gr) (void)hipGraphDestroy(gr);
+      }
+      if (rc) {
+        cleanup();
+        return rc;
+      }
+    }
+    auto t0 = std::chrono::steady_clock::now();
+    HIPCHK(hipEventRecord(e0, st));
+    HIPCHK(hipGraphLaunch(s0->pgexec, st));
+    HIPCHK(hipEventRecord(e2, st));
+    HIPCHK(hipStreamSynchronize(st));
+    u64 red[5];
+    for (int i = 0; i < 5; i++) red[i] = s0->phost[i];
+    float b = 0;
+    HIPCHK(hipEventElapsedTime(&b, e0, e2));
+    out->ms_forward = 0;  // inside the graph, beside the backward
+    out->ms_backward = b;
+    out->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    cleanup();
+    return plane_result(ss, red, out);
+  }
+  if (s0->pcapture) HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
   auto t0 = std::chrono::steady_clock::now();
   HIPCHK(hipEventRecord(e0, st));
   if (overlap) HIPCHK(hipStreamWaitEvent(fs, e0, 0));
@@ -1501,6 +1576,23 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
     if (r != ncclSuccess || r2 != ncclSuccess || r3 != ncclSuccess)
       return fail(GM_EHIP, "RCCL allreduce: %s", ncclGetErrorString(r != ncclSuccess ? r : r2 != ncclSuccess ? r2 : r3));
   }
+  if (s0->pcapture) {  // the end of the captured solve: counts to pinned host memory, the graph made
+    HIPCHK(hipMemcpyAsync(s0->phost, s0->st->red, 5 * sizeof(u64), hipMemcpyDeviceToHost, st));
+    hipGraph_t gr = nullptr;
+    const hipError_t e = hipStreamEndCapture(st, &gr);
+    cleanup();
+    if (e != hipSuccess) {
+      if (gr) (void)hipGraphDestroy(gr);
+      return fail(GM_EHIP, "plane graph capture: %s", hipGetErrorString(e));
+    }
+    const hipError_t ei = hipGraphInstantiate(&s0->pgexec, gr, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(gr);
+    if (ei != hipSuccess) {
+      s0->pgexec = nullptr;
+      return fail(GM_EHIP, "plane graph instantiate: %s", hipGetErrorString(ei));
+    }
+    return 0;
+  }
   u64 red[5] = {0, 0, 0, 0, 0};
   for (gm_solver* s : ss) {
     u64 r[5];
@@ -1548,24 +1640,7 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
     out->n_resolve_launches = nlaunch;
   }
   cleanup();
-  out->positions = red[0];
-  out->edges = red[1];
-  out->primitives = red[2];
-  out->levels = (uint32_t)T;
-  out->max_level_width = 0;
-  out->word_bits = 8 * s0->pwb;
-  out->kernels = (plane_x1(s0) ? RK_PLANE : RK_PLANE_X2) | (PK_PLANE << 16);
-  const uint32_t word = red[3] ? (uint32_t)(red[3] - 1) : NO_WORD;
-  out->root_word = word;
-  if (red[4]) {
-    for (gm_solver* s : ss)  // this process's shard failed: its own error
-      if (s->defer_rc) return fail(s->defer_rc, "shard %d/%d: %s", s->rank, s->world, s->defer_msg.c_str());
-    return fail(GM_ECORRUPT, "solve failed:%s", err_text((uint32_t)red[4]).c_str());
-  }
-  if (word == NO_WORD) return fail(GM_ECORRUPT, "root unresolved");
-  out->root_value = (int32_t)(word & 3u);
-  out->root_remoteness = word >> 2;
-  return 0;
+  return plane_result(ss, red, out);
 }
 
 static int plane_query(gm_solver* s, const uint64_t* keys_dev, uint64_t n, uint32_t* words_dev) {

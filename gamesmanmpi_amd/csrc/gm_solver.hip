@@ -1001,6 +1001,11 @@ struct gm_solver {
   // whole-solve HIP graphs of a one-table dense solve (run_dense): the
   // forward and the backward launches, captured on the first full solve
   hipGraphExec_t gfwd = nullptr, gbwd = nullptr;
+  // the whole one-table PLANES solve as one HIP graph (run_planes), its counts
+  // copied into pinned host memory at the end of every replay
+  hipGraphExec_t pgexec = nullptr;
+  u64* phost = nullptr;
+  bool pcapture = false;
   // BUCKETED (gm_bucketed.h): level store, words, in-edges, partition scratch
   u64* bkK = nullptr;
   uint32_t* bkW = nullptr;
@@ -2251,6 +2256,8 @@ void gm_solver_destroy(gm_solver* s) {
   for (hipEvent_t e : s->pev) (void)hipEventDestroy(e);
   if (s->gfwd) (void)hipGraphExecDestroy(s->gfwd);
   if (s->gbwd) (void)hipGraphExecDestroy(s->gbwd);
+  if (s->pgexec) (void)hipGraphExecDestroy(s->pgexec);
+  if (s->phost) (void)hipHostFree(s->phost);
   if (s->cstream) (void)hipStreamDestroy(s->cstream);
   if (s->cstream2) (void)hipStreamDestroy(s->cstream2);
   if (s->comm2) (void)ncclCommDestroy(s->comm2);

@@ -365,3 +365,29 @@ def test_planes_row_deal_group_matches_oracle(world, params, streams):
         assert (got[own] == 0xFFFFFFFF).all()
         got[own] = w[own]
     np.testing.assert_array_equal(got, want)
+
+
+def test_planes_graph_replay_equals_plain_launches():
+    """GM_PLANE_GRAPH=1 (A/B knob): the whole one-table solve captured once
+    and replayed as one HIP graph gives the plain launches' counts, root and
+    fingerprint on every replay (a child process: the knob is read once)."""
+    import subprocess
+    import sys
+    params = "heaps=31:31:9:6:3"
+    code = ("import json\n"
+            "from gamesmanmpi_amd.games import GameSpec\n"
+            "from gamesmanmpi_amd.solver import Solver\n"
+            "s = Solver(GameSpec('sum_four_to_one', %r))\n"
+            "out = []\n"
+            "for _ in range(3):\n"
+            "    r = s.solve()\n"
+            "    out.append([r.positions, r.edges, r.primitives, r.root_line, s.checksum()['checksum']])\n"
+            "print(json.dumps(out))\n" % params)
+    got = {}
+    for g in ("0", "1"):
+        env = dict(os.environ, GM_PLANE_GRAPH=g)
+        p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=180,
+                           cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        assert p.returncode == 0, p.stderr[-2000:]
+        got[g] = json.loads(p.stdout.strip().splitlines()[-1])
+    assert got["1"] == got["0"] and got["0"][0] == got["0"][2]
