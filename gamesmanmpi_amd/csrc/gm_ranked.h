@@ -573,6 +573,7 @@ __global__ __launch_bounds__(256) void k_rk_backward(RankGeom g, uint32_t L, u64
   const __amdgpu_buffer_rsrc_t rw =
       __builtin_amdgcn_make_buffer_rsrc(g.words + cstart, 0, (int)(uint32_t)csize, 0x00020000);
   __shared__ uint16_t list[256 * 32];
+  __shared__ uint4 tw[256 * 2];  // the tile's words (L >= 5): 32 B per tile word, in slot order
   __shared__ uint32_t wsum[4];
   u64 edges = 0, resolved = 0;
   uint32_t err = 0;
@@ -593,21 +594,22 @@ __global__ __launch_bounds__(256) void k_rk_backward(RankGeom g, uint32_t L, u64
     }
     // the reached primitives take their board's value (process.py:120-123).
     // From L = 5 on, a 32-slot word's slots are 32 consecutive boards (one
-    // block, one a): their bstat bytes come in as two 16-B loads and go out as
-    // the word row -- bstat's byte is the word (remoteness 0) -- whole: the
-    // expandable slots' bytes are rewritten by the entries below (after the
-    // barrier), the unreached ones are never read.  A loop of one dependent
-    // load and store per primitive cost 2.6 of the 10.3 ms backward
-    // (GM_RK_DBG A/B, round 5).
-    if (L >= 5) {
+    // block, one a): their bstat bytes -- bstat's byte is the word
+    // (remoteness 0) -- come in as two 16-B loads into the tile's LDS row,
+    // the entries below write the expandable slots' bytes into the same row,
+    // and the row goes out whole (two 16-B stores) once the tile is resolved:
+    // no byte store reaches memory, the unreached slots' bytes are never
+    // read.  A loop of one dependent load and store per primitive cost 2.6 of
+    // the 10.3 ms backward (GM_RK_DBG A/B, round 5).
+    const bool rows = L >= 5;
+    if (rows) {
       if (mp) {
         const u64 i0 = wi << 5, blk = i0 >> (L + 3);
         const uint32_t pat0 = (uint32_t)(i0 & ((1ull << L) - 1));
         const uint4* src = reinterpret_cast<const uint4*>(g.bstat + (lvstart >> 3) + (blk << L) + pat0);
-        uint4* dst = reinterpret_cast<uint4*>(g.words + lvstart + i0);
         const uint4 v0 = src[0], v1 = src[1];
-        dst[0] = v0;
-        dst[1] = v1;
+        tw[2 * threadIdx.x] = v0;
+        tw[2 * threadIdx.x + 1] = v1;
       }
     } else {
       for (uint32_t pm = mp; pm; pm &= pm - 1) {
@@ -738,10 +740,20 @@ __global__ __launch_bounds__(256) void k_rk_backward(RankGeom g, uint32_t L, u64
         edges += nchu[u];
         const uint32_t word = mn1 < 256u ? make_word(WIN, (mn1 >> 2) + 1)
                                          : make_word(pr1 == 3u ? TIE : pr1 == 2u ? DRAW : LOSS, (mx1 >> 2) + 1);
-        g.words[slotu[u]] = (uint8_t)word;
+        if (rows) reinterpret_cast<uint8_t*>(tw)[slotu[u] - lvstart - (t0 << 5)] = (uint8_t)word;
+        else g.words[slotu[u]] = (uint8_t)word;
       }
     }
-    __syncthreads();  // the list is rewritten by the next tile
+    if (rows) {  // the tile's rows with a reached slot, whole
+      __syncthreads();
+      if ((m | mp) && wi < nwords) {
+        uint4* dst = reinterpret_cast<uint4*>(g.words + lvstart + (wi << 5));
+        const uint4 v0 = tw[2 * threadIdx.x], v1 = tw[2 * threadIdx.x + 1];
+        dst[0] = v0;
+        dst[1] = v1;
+      }
+    }
+    __syncthreads();  // the list and the rows are rewritten by the next tile
   }
   if (err) atomicOr(&st->err, err);
   block_count(bc, 0, edges);
