@@ -562,7 +562,7 @@ constexpr uint32_t kRkColMark = 0x40000000u, kRkHandMark = 0x80000000u;
 // others arrive from their owners before the level above reads them.
 // DBG (A/B timing only, the words are wrong): 1 = no gathers, 2 = no entries.
 template <int CC, int HH, bool OWN = false, int DBG = 0>
-__global__ __launch_bounds__(256) void k_rk_backward(RankGeom g, uint32_t L, u64 lvstart, uint32_t lvoff,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_rk_backward(RankGeom g, uint32_t L, u64 lvstart, uint32_t lvoff,
                                                      u64 nwords, u64 cstart, u64 csize, BlockCount* bc, DevState* st,
                                                      const uint4* __restrict__ ownb = nullptr, uint32_t orank = 0) {
   constexpr int U = 2;  // entries per lane per pass: U x 2C child loads in flight before any reduction
