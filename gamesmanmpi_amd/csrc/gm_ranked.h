@@ -398,7 +398,7 @@ __device__ __forceinline__ u64 rk_spread(uint32_t e, uint32_t q) {
 // (nwords: the level's 512-slot padded extent in words -- every bitmap word
 // of the level is written, the padding's as 0; nreal: its slots)
 __global__ __launch_bounds__(256) void k_rk_reach4(RankGeom g, uint32_t L, u64 lvstart, uint32_t lvoff, u64 nwords,
-                                                   u64 nreal, BlockCount* bc, DevState* st) {
+                                                   u64 nreal, BlockCount* bc, DevState* st, u64 plvstart) {
   u64 npos = 0, prims = 0;
   const bool fmoved = ((L - 1) & 1u) == 0;  // the move into level L was the first mover's
   for (u64 w0 = ((u64)blockIdx.x * blockDim.x + threadIdx.x) * 4; w0 < nwords; w0 += (u64)gridDim.x * blockDim.x * 4) {
@@ -411,9 +411,14 @@ __global__ __launch_bounds__(256) void k_rk_reach4(RankGeom g, uint32_t L, u64 l
       continue;
     }
     const u64 blk = b0 >> (L + 3);
-    const uint32_t hvc = g.lvhv[lvoff + blk];
     RankPos p;
     rk_unpack(g, g.lvph[lvoff + blk], p);
+    // the parent blocks' offsets (lvpa), loaded beside the stacks: two
+    // dependent round trips per group (metadata, parent bits) instead of
+    // three (hvcode, parent base, parent bits)
+    const uint4* pp = reinterpret_cast<const uint4*>(g.lvpa + (u64)(lvoff + blk) * kRankMaxCols);
+    const uint4 pa0 = pp[0], pa1 = pp[1];
+    const uint32_t pao[kRankMaxCols] = {pa0.x, pa0.y, pa0.z, pa0.w, pa1.x, pa1.y, pa1.z, pa1.w};
     uint32_t a[4], p0[4];
     u64 valid[4], r[4];
 #pragma unroll
@@ -428,7 +433,7 @@ __global__ __launch_bounds__(256) void k_rk_reach4(RankGeom g, uint32_t L, u64 l
     for (int x = 0; x < kRankMaxCols; x++) {
       if (x >= (int)g.C || p.h[x] == 0) continue;
       const uint32_t q = p.off[x] + p.h[x] - 1;
-      const u64 pb = g.base[hvc - g.stride[x]];
+      const u64 pb = plvstart + pao[x];
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         if (!valid[k]) continue;
@@ -820,9 +825,10 @@ struct RankShape {
   std::vector<u64> base;                // per hvcode
   std::vector<uint32_t> lvhv, lvph;     // hvcodes level by level, packed heights
   std::vector<uint32_t> lvch;           // per entry: child block offsets in the next level (RankGeom::lvch)
+  std::vector<uint32_t> lvpa;           // per entry: parent block offsets in the level below (RankGeom::lvpa)
   std::vector<uint32_t> lvoff;          // per level: first entry in lvhv (T + 1)
   std::vector<u64> lvstart, lvitems;    // per level: first slot, slots
-  u64 words_off, reach_off, expd_off, bstat_off, pbits_off, base_off, lvhv_off, lvph_off, lvch_off, table_bytes;
+  u64 words_off, reach_off, expd_off, bstat_off, pbits_off, base_off, lvhv_off, lvph_off, lvch_off, lvpa_off, table_bytes;
 };
 
 static int rank_shape(const Desc* d, RankShape* rs) {
@@ -902,6 +908,12 @@ static int rank_shape(const Desc* d, RankShape* rs) {
       for (uint32_t x = 0; x < g.C; x++)
         if (((rs->lvph[j] >> (4 * x)) & 15u) < g.H)
           rs->lvch[(size_t)j * kRankMaxCols + x] = (uint32_t)(rs->base[rs->lvhv[j] + g.stride[x]] - rs->lvstart[L + 1]);
+  rs->lvpa.assign(rs->lvhv.size() * kRankMaxCols, 0xFFFFFFFFu);
+  for (uint32_t L = 1; L < g.T; L++)
+    for (uint32_t j = rs->lvoff[L]; j < rs->lvoff[L + 1]; j++)
+      for (uint32_t x = 0; x < g.C; x++)
+        if (((rs->lvph[j] >> (4 * x)) & 15u) > 0)
+          rs->lvpa[(size_t)j * kRankMaxCols + x] = (uint32_t)(rs->base[rs->lvhv[j] - g.stride[x]] - rs->lvstart[L - 1]);
   g.nslots = at;
   rs->words_off = 0;
   rs->reach_off = rup256(at);
@@ -912,7 +924,8 @@ static int rank_shape(const Desc* d, RankShape* rs) {
   rs->lvhv_off = rs->base_off + rup256((u64)nhv * 8);
   rs->lvph_off = rs->lvhv_off + rup256((u64)nhv * 4);
   rs->lvch_off = rs->lvph_off + rup256((u64)nhv * 4);
-  rs->table_bytes = rs->lvch_off + rup256((u64)nhv * 4 * kRankMaxCols);
+  rs->lvpa_off = rs->lvch_off + rup256((u64)nhv * 4 * kRankMaxCols);
+  rs->table_bytes = rs->lvpa_off + rup256((u64)nhv * 4 * kRankMaxCols);
   return 0;
 }
 
@@ -963,6 +976,7 @@ static int rank_setup(gm_solver* s, const gm_buffers* buf) {
   rs.g.lvhv = (const uint32_t*)(t + rs.lvhv_off);
   rs.g.lvph = (const uint32_t*)(t + rs.lvph_off);
   rs.g.lvch = (const uint32_t*)(t + rs.lvch_off);
+  rs.g.lvpa = (const uint32_t*)(t + rs.lvpa_off);
   rs.g.bstat = (uint8_t*)(t + rs.bstat_off);
   rs.g.pbits = (u64*)(t + rs.pbits_off);
   for (int c = 0; c < 7; c++) {
@@ -975,6 +989,7 @@ static int rank_setup(gm_solver* s, const gm_buffers* buf) {
   HIPCHK(hipMemcpy((void*)rs.g.lvhv, rs.lvhv.data(), rs.lvhv.size() * 4, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy((void*)rs.g.lvph, rs.lvph.data(), rs.lvph.size() * 4, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy((void*)rs.g.lvch, rs.lvch.data(), rs.lvch.size() * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy((void*)rs.g.lvpa, rs.lvpa.data(), rs.lvpa.size() * 4, hipMemcpyHostToDevice));
   s->rg = rs.g;
   s->rlvoff = rs.lvoff;
   s->rlvstart = rs.lvstart;
@@ -1056,7 +1071,7 @@ static void rank_forward_level(gm_solver* s, hipStream_t st, uint32_t L) {
     const u64 n = s->rlvstart[L + 1] - s->rlvstart[L];  // 512-padded: every bitmap word written
     if (L >= 6)
       hipLaunchKernelGGL(k_rk_reach4, dim3(rank_grid(s, n / 256)), dim3(256), 0, st, g, L, s->rlvstart[L],
-                         s->rlvoff[L], n / 64, s->rlvitems[L], s->bcount, s->st);
+                         s->rlvoff[L], n / 64, s->rlvitems[L], s->bcount, s->st, s->rlvstart[L - 1]);
     else
       hipLaunchKernelGGL(k_rk_forward, dim3(rank_grid(s, n)), dim3(256), 0, st, g, L, s->rlvstart[L], s->rlvoff[L],
                          n, s->rlvitems[L], s->bcount, s->st);

@@ -924,6 +924,8 @@ struct RankGeom {
   const uint32_t* lvph;    // the same, heights packed 4 bits per column
   const uint32_t* lvch;    // per block entry, kRankMaxCols u32: child block x's first slot - its level's
                            // first slot (0xFFFFFFFF: column x full)
+  const uint32_t* lvpa;    // per block entry, kRankMaxCols u32: parent block x (column x's top piece
+                           // removed)'s first slot - its level's first slot (0xFFFFFFFF: column x empty)
   uint8_t* bstat;          // [nslots / 8] per board (stacks): primitive value or UNDECIDED
   u64* pbits;              // [nslots / 512] per board: primitive
   u64 le[7];               // bits j < 64 with popcount(j) <= c
