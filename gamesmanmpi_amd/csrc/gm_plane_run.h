@@ -1360,8 +1360,17 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
   auto cleanup = [&]() {
     for (auto e : ev) (void)hipEventDestroy(e);
   };
+  // the solve's three timing events live with the solver (created once: a
+  // create + destroy per event per solve was host time between solves); a
+  // graph capture takes fresh ones
   hipEvent_t e0, e1, e2;
-  if (new_event(&e0) || new_event(&e1) || new_event(&e2)) return GM_EHIP;
+  if (s0->pcapture) {
+    if (new_event(&e0) || new_event(&e1) || new_event(&e2)) return GM_EHIP;
+  } else {
+    for (auto& e : s0->pse)
+      if (!e) HIPCHK(hipEventCreate(&e));
+    e0 = s0->pse[0], e1 = s0->pse[1], e2 = s0->pse[2];
+  }
   std::vector<hipEvent_t> kr;  // per-level start/stop (shard 0's launches)
   hipEvent_t kx[2];
   if (timing) {
@@ -1596,8 +1605,12 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
   u64 red[5] = {0, 0, 0, 0, 0};
   for (gm_solver* s : ss) {
     u64 r[5];
-    HIPCHK(hipMemcpyAsync(r, s->st->red, sizeof r, hipMemcpyDeviceToHost, st));
+    // (into pinned host memory: a pageable destination is staged and waited
+    // for inside the copy call)
+    if (!s->phost) HIPCHK(hipHostMalloc((void**)&s->phost, 8 * sizeof(u64), hipHostMallocDefault));
+    HIPCHK(hipMemcpyAsync(s->phost, s->st->red, sizeof r, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    memcpy(r, s->phost, sizeof r);
     if (mode == 3) {
       std::vector<u64> all((size_t)5 * s->world);
       int rc = xfer_call(s, GM_XFER_ALLGATHER, r, sizeof r, -1, all.data(), all.size() * 8, -1);

@@ -1008,6 +1008,7 @@ struct gm_solver {
   hipGraphExec_t pgexec = nullptr;
   u64* phost = nullptr;
   bool pcapture = false;
+  hipEvent_t pse[3] = {nullptr, nullptr, nullptr};  // run_planes' timing events
   // BUCKETED (gm_bucketed.h): level store, words, in-edges, partition scratch
   u64* bkK = nullptr;
   uint32_t* bkW = nullptr;
@@ -2259,6 +2260,8 @@ void gm_solver_destroy(gm_solver* s) {
   if (s->gfwd) (void)hipGraphExecDestroy(s->gfwd);
   if (s->gbwd) (void)hipGraphExecDestroy(s->gbwd);
   if (s->pgexec) (void)hipGraphExecDestroy(s->pgexec);
+  for (hipEvent_t e : s->pse)
+    if (e) (void)hipEventDestroy(e);
   if (s->phost) (void)hipHostFree(s->phost);
   if (s->cstream) (void)hipStreamDestroy(s->cstream);
   if (s->cstream2) (void)hipStreamDestroy(s->cstream2);
