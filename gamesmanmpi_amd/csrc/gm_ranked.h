@@ -653,8 +653,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
       tcho[4] = c1.x, tcho[5] = c1.y, tcho[6] = c1.z, tcho[7] = c1.w;
     }
     __syncthreads();
-    for (uint32_t e0 = threadIdx.x; e0 < (DBG == 2 ? 0u : total); e0 += 256u * U) {
-      uint32_t offu[U][2 * NC], nchu[U];
+    // A tile inside one block knows its full columns (wave-uniform): it runs
+    // a copy of the pass over its NV columns with room only, compacted in
+    // order (base cb[k], top bit cq[k]) -- no loads or reduction for a full
+    // column, whose move is illegal for every slot of the tile (at the deep
+    // levels two to three of six).  Other tiles run the NC-column pass with
+    // per-lane stacks, a full column's offsets at the mark.
+    uint32_t nv = 0, cb[NC], cq[NC];
+    {
+      uint32_t off = 0;
+#pragma unroll
+      for (int x = 0; x < NC; x++) {
+        const uint32_t h = (tph >> (4 * x)) & 15u, q = off + h;
+        off += h;
+        const bool col = (CC > 0 || (uint32_t)x < C) && h < H;
+#pragma unroll
+        for (int k = 0; k <= x; k++)
+          if (col && nv == (uint32_t)k) cb[k] = tcho[x], cq[k] = q;
+        nv += col ? 1u : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < NC; k++)
+        if ((uint32_t)k >= nv) cb[k] = colmark, cq[k] = 0u;  // (the NC-column copy's extra columns: marked)
+    }
+    auto pass = [&](auto NVc, const uint32_t e0, const bool uni) {
+      constexpr int NV = decltype(NVc)::value;
+      uint32_t offu[U][2 * NV], nchu[U];
       u64 slotu[U];
       bool liveu[U];
       // the children's offsets: lo | hi (the stacks with a 0 inserted at bit
@@ -662,36 +686,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
       // 2^q and, if the first mover placed it, one a-row (dT).  Per column:
       // its child base (or colmark when full) and 2^q; per entry: the slot's
       // own part for the O and the T children (or handmark when that hand is
-      // empty) -- a tile inside one block runs a copy with the column terms
-      // wave-uniform (scalar)
-      auto entries = [&](const uint32_t phu, const uint32_t* chou, bool uni) {
+      // empty)
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-          const uint32_t e = e0 + 256u * (uint32_t)u;
-          liveu[u] = e < total;
-          const u64 i = (t0 << 5) + list[liveu[u] ? e : e0];
-          slotu[u] = lvstart + i;
-          const u64 blk = i >> (L + 3);
-          const uint32_t a = (uint32_t)((i >> L) & 7u), pat = (uint32_t)(i & ((1ull << L) - 1));
-          uint32_t ph = phu, cho[kRankMaxCols];
-          if (uni) {
+      for (int u = 0; u < U; u++) {
+        const uint32_t e = e0 + 256u * (uint32_t)u;
+        liveu[u] = e < total;
+        const u64 i = (t0 << 5) + list[liveu[u] ? e : e0];
+        slotu[u] = lvstart + i;
+        const u64 blk = i >> (L + 3);
+        const uint32_t a = (uint32_t)((i >> L) & 7u), pat = (uint32_t)(i & ((1ull << L) - 1));
+        const RankHands h_ = rk_hands(L, (uint32_t)__builtin_popcount(pat), a);
+        const bool hasT = fmoves ? h_.t1 < (int)kRankHand : h_.t2 < (int)kRankHand;
+        const bool hasO = fmoves ? h_.o1 < (int)kRankHand : h_.o2 < (int)kRankHand;
+        const uint32_t rp = (a << (L + 1)) + pat;
+        const uint32_t bO = hasO ? rp : handmark, bT = hasT ? rp + dT : handmark;
+        uint32_t ncol = 0;
+        if (uni) {
 #pragma unroll
-            for (int x = 0; x < kRankMaxCols; x++) cho[x] = chou[x];
-          } else {
-            ph = g.lvph[lvoff + blk];
-            const uint4* cp = reinterpret_cast<const uint4*>(g.lvch + (u64)(lvoff + blk) * kRankMaxCols);
-            const uint4 c0 = cp[0], c1 = cp[1];
-            cho[0] = c0.x, cho[1] = c0.y, cho[2] = c0.z, cho[3] = c0.w;
-            cho[4] = c1.x, cho[5] = c1.y, cho[6] = c1.z, cho[7] = c1.w;
+          for (int k = 0; k < NV; k++) {
+            const uint32_t q = cq[k], base = cb[k], hi = pat & (0xFFFFFFFFu << q);
+            if constexpr (NARROW) {
+              offu[u][2 * k] = min(base + (1u << q) + hi + bT, kRkColMark);
+              offu[u][2 * k + 1] = min(base + hi + bO, kRkColMark);
+            } else {
+              const uint32_t bh = __builtin_elementwise_add_sat(base, hi);
+              offu[u][2 * k] = __builtin_elementwise_add_sat(__builtin_elementwise_add_sat(bh, 1u << q), bT);
+              offu[u][2 * k + 1] = __builtin_elementwise_add_sat(bh, bO);
+            }
           }
-          const RankHands h_ = rk_hands(L, (uint32_t)__builtin_popcount(pat), a);
-          const bool hasT = fmoves ? h_.t1 < (int)kRankHand : h_.t2 < (int)kRankHand;
-          const bool hasO = fmoves ? h_.o1 < (int)kRankHand : h_.o2 < (int)kRankHand;
-          const uint32_t rp = (a << (L + 1)) + pat;
-          const uint32_t bO = hasO ? rp : handmark, bT = hasT ? rp + dT : handmark;
-          uint32_t ncol = 0, off = 0;
+          ncol = nv;
+        } else {
+          const uint32_t ph = g.lvph[lvoff + blk];
+          const uint4* cp = reinterpret_cast<const uint4*>(g.lvch + (u64)(lvoff + blk) * kRankMaxCols);
+          const uint4 c0 = cp[0], c1 = cp[1];
+          const uint32_t cho[kRankMaxCols] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+          uint32_t off = 0;
 #pragma unroll
-          for (int x = 0; x < NC; x++) {
+          for (int x = 0; x < NV; x++) {
             const uint32_t h = (ph >> (4 * x)) & 15u;
             const bool col = (CC > 0 || (uint32_t)x < C) && h < H;
             const uint32_t q = off + h;
@@ -707,16 +738,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
             }
             ncol += (uint32_t)col;
           }
-          nchu[u] = liveu[u] ? ncol * ((uint32_t)hasT + (uint32_t)hasO) : 0u;
         }
-      };
-      if (oneblk) entries(tph, tcho, true);
-      else entries(0u, tcho, false);
-      uint32_t wu[U][2 * NC];
+        nchu[u] = liveu[u] ? ncol * ((uint32_t)hasT + (uint32_t)hasO) : 0u;
+      }
+      uint32_t wu[U][2 * NV];
 #pragma unroll
       for (int u = 0; u < U; u++)
 #pragma unroll
-        for (int k = 0; k < 2 * NC; k++)
+        for (int k = 0; k < 2 * NV; k++)
           wu[u][k] = DBG == 1 ? (offu[u][k] & 0x7Du)  // (A/B only: no gathers, a word from the offset)
                               : __builtin_amdgcn_raw_buffer_load_b8(rw, offu[u][k], 0, 0);
 #pragma unroll
@@ -731,7 +760,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
         //       smallest LOSS child's word;  max of w: the largest remoteness
         rk_u16x2 mn = {0xFFFFu, 0xFFFFu}, mx = {0, 0}, pr = {0, 0};
 #pragma unroll
-        for (int x = 0; x < NC; x++) {
+        for (int x = 0; x < NV; x++) {
           const uint32_t p = wu[u][2 * x] | (wu[u][2 * x + 1] << 16);
           const uint32_t t = (p ^ 0x00010001u) & 0x00030003u;
           mn = __builtin_elementwise_min(mn, __builtin_bit_cast(rk_u16x2, p + (t << 8)));
@@ -747,6 +776,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
                                          : make_word(pr1 == 3u ? TIE : pr1 == 2u ? DRAW : LOSS, (mx1 >> 2) + 1);
         if (rows) reinterpret_cast<uint8_t*>(tw)[slotu[u] - lvstart - (t0 << 5)] = (uint8_t)word;
         else g.words[slotu[u]] = (uint8_t)word;
+      }
+    };
+    const uint32_t nvu = __builtin_amdgcn_readfirstlane(nv);
+    for (uint32_t e0 = threadIdx.x; e0 < (DBG == 2 ? 0u : total); e0 += 256u * U) {
+      if (!oneblk || nvu == 0) {
+        pass(std::integral_constant<int, NC>(), e0, false);
+      } else if constexpr (CC > 0 && DBG == 0) {
+        // (the compiled-in boards: one copy per count of columns with room)
+        if (nvu >= (uint32_t)NC) pass(std::integral_constant<int, NC>(), e0, true);
+        else if (nvu == 1) pass(std::integral_constant<int, 1>(), e0, true);
+        else if (nvu == 2) pass(std::integral_constant<int, NC >= 2 ? 2 : 1>(), e0, true);
+        else if (nvu == 3) pass(std::integral_constant<int, NC >= 3 ? 3 : 1>(), e0, true);
+        else if (nvu == 4) pass(std::integral_constant<int, NC >= 4 ? 4 : 1>(), e0, true);
+        else if (nvu == 5) pass(std::integral_constant<int, NC >= 5 ? 5 : 1>(), e0, true);
+        else pass(std::integral_constant<int, NC>(), e0, true);
+      } else {
+        pass(std::integral_constant<int, NC>(), e0, true);
       }
     }
     if (rows) {  // the tile's rows with a reached slot, whole
