@@ -1284,6 +1284,20 @@ static bool plane_graph_on() {
   return on;
 }
 
+// The end of a one-table solve: the host polls the stream instead of
+// sleeping in hipStreamSynchronize, whose wake-up is host time between solves
+// (GM_PLANE_SPIN=0: hipStreamSynchronize)
+static hipError_t plane_wait(hipStream_t st) {
+  static const bool spin = [] {
+    const char* e = getenv("GM_PLANE_SPIN");
+    return !(e && atoi(e) == 0);
+  }();
+  if (!spin) return hipStreamSynchronize(st);
+  hipError_t e;
+  while ((e = hipStreamQuery(st)) == hipErrorNotReady) __builtin_ia32_pause();
+  return e;
+}
+
 // the counts of a finished solve (red: positions, edges, primitives, root
 // word + 1, error bits) into the result
 static int plane_result(const std::vector<gm_solver*>& ss, const u64* red, gm_result* out) {
@@ -1444,7 +1458,7 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
     HIPCHK(hipEventRecord(e0, st));
     HIPCHK(hipGraphLaunch(s0->pgexec, st));
     HIPCHK(hipEventRecord(e2, st));
-    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(plane_wait(st));
     u64 red[5];
     for (int i = 0; i < 5; i++) red[i] = s0->phost[i];
     float b = 0;
@@ -1609,7 +1623,7 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
     // for inside the copy call)
     if (!s->phost) HIPCHK(hipHostMalloc((void**)&s->phost, 8 * sizeof(u64), hipHostMallocDefault));
     HIPCHK(hipMemcpyAsync(s->phost, s->st->red, sizeof r, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(mode == 0 ? plane_wait(st) : hipStreamSynchronize(st));
     memcpy(r, s->phost, sizeof r);
     if (mode == 3) {
       std::vector<u64> all((size_t)5 * s->world);
