@@ -1298,6 +1298,16 @@ static hipError_t plane_wait(hipStream_t st) {
   return e;
 }
 
+// GM_PLANE_FWD_FIRST=1: a one-table solve enqueues its forward before the
+// backward's first launch (the order before round 5; A/B)
+static bool plane_fwd_first() {
+  static const bool on = [] {
+    const char* e = getenv("GM_PLANE_FWD_FIRST");
+    return e && atoi(e) == 1;
+  }();
+  return on;
+}
+
 // the counts of a finished solve (red: positions, edges, primitives, root
 // word + 1, error bits) into the result
 static int plane_result(const std::vector<gm_solver*>& ss, const u64* red, gm_result* out) {
@@ -1474,25 +1484,36 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
   HIPCHK(hipEventRecord(e0, st));
   if (overlap) HIPCHK(hipStreamWaitEvent(fs, e0, 0));
   if (fork()) return GM_EHIP;
-  if (first == 0) {
-    for (gm_solver* s : ss) {
-      hipStream_t ws = overlap ? fs : s->stream;
-      HIPCHK(hipMemsetAsync(s->st, 0, devstate_bytes(T), ws));
-      HIPCHK(hipMemsetAsync(s->bcount, 0, kCountSlots * sizeof(BlockCount), ws));
-      // the word width: written by k_plane_reach below (no reach: here)
-      if (stop == 0) HIPCHK(hipMemsetD32Async((hipDeviceptr_t)&s->st->word_bits, (int)s->pmark(), 1, ws));
+  auto issue_forward = [&]() -> int {
+    if (first == 0) {
+      for (gm_solver* s : ss) {
+        hipStream_t ws = overlap ? fs : s->stream;
+        HIPCHK(hipMemsetAsync(s->st, 0, devstate_bytes(T), ws));
+        HIPCHK(hipMemsetAsync(s->bcount, 0, kCountSlots * sizeof(BlockCount), ws));
+        // the word width: written by k_plane_reach below (no reach: here)
+        if (stop == 0) HIPCHK(hipMemsetD32Async((hipDeviceptr_t)&s->st->word_bits, (int)s->pmark(), 1, ws));
+      }
+      if (stop > 0) {
+        if (timing) HIPCHK(hipEventRecord(kx[0], st));
+        for (gm_solver* s : ss) plane_reach_launch(s, overlap ? fs : nullptr);
+        if (timing && join()) return GM_EHIP;
+        if (timing) HIPCHK(hipEventRecord(kx[1], st));
+      }
     }
-    if (stop > 0) {
-      if (timing) HIPCHK(hipEventRecord(kx[0], st));
-      for (gm_solver* s : ss) plane_reach_launch(s, overlap ? fs : nullptr);
-      if (timing && join()) return GM_EHIP;
-      if (timing) HIPCHK(hipEventRecord(kx[1], st));
-    }
+    HIPCHK(hipGetLastError());
+    if (join()) return GM_EHIP;
+    HIPCHK(hipEventRecord(e1, fs));  // overlap: the forward's end on its own stream
+    if (fork()) return GM_EHIP;
+    return 0;
+  };
+  // overlap: the forward (resets, reach map, counts) is enqueued on its side
+  // stream right after the backward's first launch, so the host's first
+  // enqueue is a resolve launch (the forward is read by the finish only)
+  bool fwd_pending = overlap && !plane_fwd_first();
+  if (!fwd_pending) {
+    const int rc = issue_forward();
+    if (rc) return rc;
   }
-  HIPCHK(hipGetLastError());
-  if (join()) return GM_EHIP;
-  HIPCHK(hipEventRecord(e1, fs));  // overlap: the forward's end on its own stream
-  if (fork()) return GM_EHIP;
   // kernel timing: one table -- the backward is nothing but the resolve
   // launches, so one event pair around all of them (no events between
   // launches: they would add their own gaps to what they time); shards --
@@ -1541,6 +1562,11 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
     if (mode == 0 && !per_level) {
       bat0.add(s0->ploff[l], s0->ploff[(size_t)l + 1], l, l < S ? s0->ploff[(size_t)l + 2] - s0->ploff[(size_t)l + 1] : 0);
       if (l == S) bat0.flush();
+      if (fwd_pending && bat0.launches > 0) {
+        fwd_pending = false;
+        const int rc = issue_forward();
+        if (rc) return rc;
+      }
     } else if (!pipe) {
       for (gm_solver* s : ss) plane_launch(s, l);
     } else {
@@ -1565,6 +1591,11 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
     if (per_level || (timing && l == S)) HIPCHK(hipEventRecord(kr[2 * l + 1], st));
   }
   bat0.flush();  // a stop inside a run
+  if (fwd_pending) {  // (nothing launched in the loop)
+    fwd_pending = false;
+    const int rc = issue_forward();
+    if (rc) return rc;
+  }
   if (!staged) nlaunch = mode == 0 && !per_level ? bat0.launches : (u64)(S + 1) * (pipe ? 2 : 1);
   if (last_x >= 0) HIPCHK(hipStreamWaitEvent(st, PE[S + 1 + last_x], 0));  // join the comm stream
   {
