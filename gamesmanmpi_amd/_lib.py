@@ -115,7 +115,7 @@ class gm_result(ctypes.Structure):
 EXPORTS = (
     "gm_game_lookup", "gm_game_info", "gm_root", "gm_encode", "gm_decode",
     "gm_encode_batch", "gm_decode_batch", "gm_str_utf8", "gm_host_expand", "gm_host_level", "gm_symmetry", "gm_abi_sizes", "gm_plan", "gm_solver_create",
-    "gm_solver_solve", "gm_solver_query", "gm_solver_positions",
+    "gm_solver_solve", "gm_solver_solve_async", "gm_solver_collect", "gm_solver_query", "gm_solver_positions",
     "gm_solver_checksum",
     "gm_solver_destroy", "gm_solve", "gm_plan_multi", "gm_query", "gm_release", "gm_owner", "gm_owner_host",
     "gm_plan_shard", "gm_plan_keyed_shard", "gm_solver_create_shard", "gm_comm_unique_id",
@@ -165,6 +165,8 @@ def load():
                     P(gm_plan_t)],
         "gm_solver_create": [c.c_int, P(gm_buffers), P(c.c_void_p)],
         "gm_solver_solve": [c.c_void_p, P(gm_result)],
+        "gm_solver_solve_async": [c.c_void_p, P(c.c_uint64)],
+        "gm_solver_collect": [c.c_void_p, c.c_uint64, P(gm_result)],
         "gm_solver_query": [c.c_void_p, c.c_void_p, c.c_uint64, c.c_void_p],
         "gm_solver_positions": [c.c_void_p, c.c_void_p, c.c_uint64,
                                 P(c.c_uint64)],

@@ -276,6 +276,7 @@ static int bks_alltoall(std::vector<gm_solver*>& ss, int mode, hipStream_t st, s
     HIPCHK(hipMemcpyAsync(x.rbuf + x.ro[(size_t)r] * eb, x.sbuf + x.so[(size_t)r] * eb, x.sc[(size_t)r] * eb,
                           hipMemcpyDeviceToDevice, st));
   if (mode == 1) {
+    RCCL_LIVE(s);
     ncclGroupStart();
     ncclResult_t e1 = ncclSuccess, e2 = ncclSuccess;
     for (int p = 0; p < W; p++) {
@@ -323,6 +324,7 @@ static int bks_allgather(std::vector<gm_solver*>& ss, int mode, hipStream_t st, 
     s->xdev_n = m + out.size();
   }
   u64* dev = s->xdev;
+  RCCL_LIVE(s);
   HIPCHK(hipMemcpyAsync(dev, mine[0].data(), m * 8, hipMemcpyHostToDevice, st));
   const ncclResult_t r = ncclAllGather(dev, dev + m, m, ncclUint64, s->comm, st);
   hipError_t e = hipMemcpyAsync(out.data(), dev + m, out.size() * 8, hipMemcpyDeviceToHost, st);

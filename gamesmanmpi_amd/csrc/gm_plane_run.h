@@ -224,7 +224,7 @@ struct PlaneShape {
 // picks its specialisation per visit (plane_x2_range, RS = -1).
 // GM_PLANE_STAGE_K overrides k (A/B).
 static uint32_t plane_stage_k(int world) {
-  if (const char* e = getenv("GM_PLANE_STAGE_K")) {
+  if (const char* e = lab_env("GM_PLANE_STAGE_K")) {
     const int k = atoi(e);
     if (k >= 1 && k <= 64) return (uint32_t)k;
   }
@@ -883,6 +883,7 @@ static int plane_exchange(std::vector<gm_solver*>& ss, uint32_t l, int mode, hip
   auto sbuf = [&](int p, u64* n) { return (void*)((char*)s->psend + plane_seg(s->psnd_off, l, W, p, n) * pb); };
   auto rbuf = [&](int p, u64* n) { return (void*)((char*)s->precv + plane_seg(s->prcv_off, l, W, p, n) * pb); };
   if (mode == 1) {
+    RCCL_LIVE(s);
     ncclResult_t r = ncclGroupStart();
     for (int p = 0; p < W && r == ncclSuccess; p++) {
       u64 ns, nr;
@@ -925,6 +926,7 @@ static int plane_check_plan(std::vector<gm_solver*>& ss, int mode, hipStream_t s
       int rc = xfer_call(ss[0], GM_XFER_ALLGATHER, mine.data(), m * 8, -1, all.data(), all.size() * 8, -1);
       if (rc) return rc;
     } else {
+      RCCL_LIVE(ss[0]);
       u64* dev = nullptr;
       HIPCHK(hipMalloc((void**)&dev, (m + all.size()) * 8));
       HIPCHK(hipMemcpyAsync(dev, mine.data(), m * 8, hipMemcpyHostToDevice, st));
@@ -972,6 +974,7 @@ static int plane_check_stage(std::vector<gm_solver*>& ss, int mode, hipStream_t 
       int rc = xfer_call(ss[0], GM_XFER_ALLGATHER, &mine, 8, -1, all.data(), all.size() * 8, -1);
       if (rc) return rc;
     } else {
+      RCCL_LIVE(ss[0]);
       u64* dev = nullptr;
       HIPCHK(hipMalloc((void**)&dev, (size_t)(1 + W) * 8));
       HIPCHK(hipMemcpyAsync(dev, &mine, 8, hipMemcpyHostToDevice, st));
@@ -1001,7 +1004,7 @@ struct StagedFault {
 };
 static StagedFault staged_fault() {
   StagedFault f;
-  const char* e = getenv("GM_FAULT_STAGED");
+  const char* e = lab_env("GM_FAULT_STAGED");
   if (!e || !*e) return f;
   unsigned r = 0, k = 0;
   char tail[16] = {0};
@@ -1031,7 +1034,8 @@ static int staged_defer(gm_solver* s, int herr, hipStream_t st) {
 //  mode 2 (in-process group, one stream): shard after shard, rows copied to
 //    the next shard as they complete (the next shard runs after this one).
 //  mode 1 (RCCL): transfers r -> r + 1 travel on comm when r is even and on
-//    comm2 (ncclCommSplit, made on first use) when odd, so on every rank one
+//    comm2 (ncclCommSplit: up front for an in-process group, solve_multi;
+//    on first use by a one-process-per-GPU rank) when odd, so on every rank one
 //    communicator carries only its receives and the other only its sends:
 //    receives are posted ahead (a window of rows) on the receive stream and
 //    can never hold up the sends, which follow the rank's own keys on the
@@ -1257,12 +1261,14 @@ static int plane_backward_staged(std::vector<gm_solver*>& ss, int mode, hipStrea
       s,
       [&](gm_solver* t, uint32_t, void* b, u64 n, hipStream_t rs) -> int {
         if (!n) return 0;
+        RCCL_LIVE(t);
         const ncclResult_t e = ncclRecv(b, n * pb, ncclUint8, t->rank - 1, crecv, rs);
         if (e != ncclSuccess) return fail(GM_EHIP, "RCCL halo receive: %s", ncclGetErrorString(e));
         return 0;
       },
       [&](gm_solver* t, uint32_t, void* b, u64 n, hipStream_t ts) -> int {
         if (!n) return 0;
+        RCCL_LIVE(t);
         const ncclResult_t e = ncclSend(b, n * pb, ncclUint8, t->rank + 1, csend, ts);
         if (e != ncclSuccess) return fail(GM_EHIP, "RCCL halo send: %s", ncclGetErrorString(e));
         return 0;
@@ -1272,40 +1278,22 @@ static int plane_backward_staged(std::vector<gm_solver*>& ss, int mode, hipStrea
 // The PLANES solve.  Steps (gm_solver_set_steps, one table only): 2T like
 // the other layouts; step 0 is the forward pass (reach map + counts), steps
 // 1..T-1 are empty, step T + l is plane level l (l <= S), later steps empty.
-// GM_PLANE_GRAPH=1: one-table full solves replay one HIP graph of the whole
-// solve (A/B; not the default: 1.40-1.43 vs 1.36-1.42 ms per 2^30 bench step
-// with plain launches, profiles/r05z -- the kernels and their device-side
-// boundaries, not the host's enqueueing, make the step)
-static bool plane_graph_on() {
-  static const bool on = [] {
-    const char* e = getenv("GM_PLANE_GRAPH");
-    return e && atoi(e) == 1;
-  }();
-  return on;
-}
-
-// The end of a one-table solve: the host polls the stream instead of
-// sleeping in hipStreamSynchronize, whose wake-up is host time between solves
-// (GM_PLANE_SPIN=0: hipStreamSynchronize)
+// The end of a one-table solve: the host polls the stream for a bounded
+// time (up to kPlaneSpinUs, about a narrow plane level: the solve's last
+// launches), then sleeps in hipStreamSynchronize -- a solve's wake-up is not
+// paid on every call, and no core is pinned for a long solve (round 5 spun
+// without a bound: 1.325 vs 1.329 ms per bench step, within noise).  Queued
+// solves (gm_solver_solve_async) do not wait here at all.
+constexpr double kPlaneSpinUs = 100.0;
 static hipError_t plane_wait(hipStream_t st) {
-  static const bool spin = [] {
-    const char* e = getenv("GM_PLANE_SPIN");
-    return !(e && atoi(e) == 0);
-  }();
-  if (!spin) return hipStreamSynchronize(st);
+  const auto t0 = std::chrono::steady_clock::now();
   hipError_t e;
-  while ((e = hipStreamQuery(st)) == hipErrorNotReady) __builtin_ia32_pause();
+  while ((e = hipStreamQuery(st)) == hipErrorNotReady) {
+    if (std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > kPlaneSpinUs)
+      return hipStreamSynchronize(st);
+    __builtin_ia32_pause();
+  }
   return e;
-}
-
-// GM_PLANE_FWD_FIRST=1: a one-table solve enqueues its forward before the
-// backward's first launch (the order before round 5; A/B)
-static bool plane_fwd_first() {
-  static const bool on = [] {
-    const char* e = getenv("GM_PLANE_FWD_FIRST");
-    return e && atoi(e) == 1;
-  }();
-  return on;
 }
 
 // the counts of a finished solve (red: positions, edges, primitives, root
@@ -1332,7 +1320,7 @@ static int plane_result(const std::vector<gm_solver*>& ss, const u64* red, gm_re
   return 0;
 }
 
-static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
+static int run_planes(std::vector<gm_solver*> ss, gm_result* out, bool async) {
   gm_solver* s0 = ss[0];
   const Desc& d = s0->d;
   const int T = d.max_levels;
@@ -1358,6 +1346,8 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
   const int stop = mode == 0 && s0->step_stop ? (int)s0->step_stop : 2 * T;
   s0->step_first = s0->step_stop = 0;
   const bool timing = (s0->flags & GM_F_KERNEL_TIMING) && first == 0 && stop == 2 * T;
+  if (async && (mode != 0 || first != 0 || stop != 2 * T || timing))
+    return fail(GM_EINVAL, "queued solves: one-table PLANES full solves without kernel timing only");
   hipStream_t st = s0->stream;
   if (first > 0) {
     uint32_t wb = 0;
@@ -1386,14 +1376,13 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
   };
   // the solve's three timing events live with the solver (created once: a
   // create + destroy per event per solve was host time between solves); a
-  // graph capture takes fresh ones
+  // queued solve (gm_solver_solve_async) uses its ring slot's own
   hipEvent_t e0, e1, e2;
-  if (s0->pcapture) {
-    if (new_event(&e0) || new_event(&e1) || new_event(&e2)) return GM_EHIP;
-  } else {
-    for (auto& e : s0->pse)
-      if (!e) HIPCHK(hipEventCreate(&e));
-    e0 = s0->pse[0], e1 = s0->pse[1], e2 = s0->pse[2];
+  {
+    hipEvent_t* se = async ? s0->pring[s0->pq_next % kPlaneRing].ev : s0->pse;
+    for (int i = 0; i < 3; i++)
+      if (!se[i]) HIPCHK(hipEventCreate(&se[i]));
+    e0 = se[0], e1 = se[1], e2 = se[2];
   }
   std::vector<hipEvent_t> kr;  // per-level start/stop (shard 0's launches)
   hipEvent_t kx[2];
@@ -1441,45 +1430,6 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
     if (!s0->cstream) HIPCHK(hipStreamCreateWithFlags(&s0->cstream, hipStreamNonBlocking));
     fs = s0->cstream;
   }
-  // One table, whole solve: ONE graph launch.  The solve is captured once
-  // (this function again, in capture mode: every launch and copy goes into
-  // the graph, the counts into pinned host memory) and replayed: the host no
-  // longer enqueues ~120 launches per solve, so the narrow first levels do
-  // not wait for it and the solve starts right after the call (A/B knob)
-  if (overlap && plane_graph_on() && !s0->pcapture) {
-    if (!s0->pgexec) {
-      if (!s0->phost) HIPCHK(hipHostMalloc((void**)&s0->phost, 8 * sizeof(u64), hipHostMallocDefault));
-      s0->pcapture = true;
-      gm_result cap{};
-      const int rc = run_planes(ss, &cap);
-      s0->pcapture = false;
-      hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
-      if (hipStreamIsCapturing(st, &cst) == hipSuccess && cst != hipStreamCaptureStatusNone) {
-        hipGraph_t gr = nullptr;  // a capture that failed half-way
-        (void)hipStreamEndCapture(st, &gr);
-        if (gr) (void)hipGraphDestroy(gr);
-      }
-      if (rc) {
-        cleanup();
-        return rc;
-      }
-    }
-    auto t0 = std::chrono::steady_clock::now();
-    HIPCHK(hipEventRecord(e0, st));
-    HIPCHK(hipGraphLaunch(s0->pgexec, st));
-    HIPCHK(hipEventRecord(e2, st));
-    HIPCHK(plane_wait(st));
-    u64 red[5];
-    for (int i = 0; i < 5; i++) red[i] = s0->phost[i];
-    float b = 0;
-    HIPCHK(hipEventElapsedTime(&b, e0, e2));
-    out->ms_forward = 0;  // inside the graph, beside the backward
-    out->ms_backward = b;
-    out->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    cleanup();
-    return plane_result(ss, red, out);
-  }
-  if (s0->pcapture) HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
   auto t0 = std::chrono::steady_clock::now();
   HIPCHK(hipEventRecord(e0, st));
   if (overlap) HIPCHK(hipStreamWaitEvent(fs, e0, 0));
@@ -1509,7 +1459,7 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
   // overlap: the forward (resets, reach map, counts) is enqueued on its side
   // stream right after the backward's first launch, so the host's first
   // enqueue is a resolve launch (the forward is read by the finish only)
-  bool fwd_pending = overlap && !plane_fwd_first();
+  bool fwd_pending = overlap;
   if (!fwd_pending) {
     const int rc = issue_forward();
     if (rc) return rc;
@@ -1622,30 +1572,24 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
                          (const void*)s->ptab, s->pbits, s->st, (const BlockCount*)s->bcount);
     });
   HIPCHK(hipGetLastError());
+  if (async) {  // queued: the counts into the slot's pinned memory, then its completion event
+    PlaneSlot& q = s0->pring[s0->pq_next % kPlaneRing];
+    if (!q.host) HIPCHK(hipHostMalloc((void**)&q.host, 8 * sizeof(u64), hipHostMallocDefault));
+    if (!q.ev[3]) HIPCHK(hipEventCreate(&q.ev[3]));
+    HIPCHK(hipMemcpyAsync(q.host, s0->st->red, 5 * sizeof(u64), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipEventRecord(q.ev[3], st));
+    s0->pq_next++;
+    cleanup();
+    return 0;
+  }
   if (mode == 1) {
+    RCCL_LIVE(s0);
     ncclGroupStart();
     ncclResult_t r = ncclAllReduce(s0->st->red, s0->st->red, 4, ncclUint64, ncclSum, s0->comm, st);
     ncclResult_t r2 = ncclAllGather(s0->st->red + 4, s0->errg, 1, ncclUint64, s0->comm, st);
     ncclResult_t r3 = ncclGroupEnd();
     if (r != ncclSuccess || r2 != ncclSuccess || r3 != ncclSuccess)
       return fail(GM_EHIP, "RCCL allreduce: %s", ncclGetErrorString(r != ncclSuccess ? r : r2 != ncclSuccess ? r2 : r3));
-  }
-  if (s0->pcapture) {  // the end of the captured solve: counts to pinned host memory, the graph made
-    HIPCHK(hipMemcpyAsync(s0->phost, s0->st->red, 5 * sizeof(u64), hipMemcpyDeviceToHost, st));
-    hipGraph_t gr = nullptr;
-    const hipError_t e = hipStreamEndCapture(st, &gr);
-    cleanup();
-    if (e != hipSuccess) {
-      if (gr) (void)hipGraphDestroy(gr);
-      return fail(GM_EHIP, "plane graph capture: %s", hipGetErrorString(e));
-    }
-    const hipError_t ei = hipGraphInstantiate(&s0->pgexec, gr, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(gr);
-    if (ei != hipSuccess) {
-      s0->pgexec = nullptr;
-      return fail(GM_EHIP, "plane graph instantiate: %s", hipGetErrorString(ei));
-    }
-    return 0;
   }
   u64 red[5] = {0, 0, 0, 0, 0};
   for (gm_solver* s : ss) {
@@ -1699,6 +1643,39 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out) {
   }
   cleanup();
   return plane_result(ss, red, out);
+}
+
+// A queued solve's result (gm_solver_collect): wait for its completion
+// event (bounded spin, then a blocking wait), read its counts from the slot
+static int plane_collect(gm_solver* s, u64 ticket, gm_result* out) {
+  if (ticket < s->pq_done || ticket >= s->pq_next)
+    return fail(GM_EINVAL, "ticket %llu: queued solves %llu..%llu are outstanding", (unsigned long long)ticket,
+                (unsigned long long)s->pq_done, (unsigned long long)s->pq_next);
+  if (ticket != s->pq_done) return fail(GM_EINVAL, "collect queued solves in order (next: %llu)", (unsigned long long)s->pq_done);
+  PlaneSlot& q = s->pring[ticket % kPlaneRing];
+  const auto t0 = std::chrono::steady_clock::now();
+  hipError_t e;
+  while ((e = hipEventQuery(q.ev[3])) == hipErrorNotReady) {
+    if (std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > kPlaneSpinUs) {
+      e = hipEventSynchronize(q.ev[3]);
+      break;
+    }
+    __builtin_ia32_pause();
+  }
+  s->pq_done++;
+  if (e != hipSuccess) return fail(GM_EHIP, "queued solve %llu: %s", (unsigned long long)ticket, hipGetErrorString(e));
+  u64 red[5];
+  memcpy(red, q.host, sizeof red);
+  float f = 0, b = 0, t = 0;
+  HIPCHK(hipEventElapsedTime(&f, q.ev[0], q.ev[1]));
+  HIPCHK(hipEventElapsedTime(&b, q.ev[0], q.ev[2]));
+  HIPCHK(hipEventElapsedTime(&t, q.ev[0], q.ev[3]));
+  out->ms_forward = f;
+  out->ms_backward = b;
+  out->ms_total = t;  // device span of the queued solve (its host wall overlaps other solves)
+  out->ms_expand_kernels = out->ms_resolve_kernels = 0;
+  out->n_expand_launches = out->n_resolve_launches = 0;
+  return plane_result({s}, red, out);
 }
 
 static int plane_query(gm_solver* s, const uint64_t* keys_dev, uint64_t n, uint32_t* words_dev) {

@@ -799,7 +799,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
       __syncthreads();
       if ((m | mp) && wi < nwords) {
         uint4* dst = reinterpret_cast<uint4*>(g.words + lvstart + (wi << 5));
-        const uint4 v0 = tw[2 * threadIdx.x], v1 = tw[2 * threadIdx.x + 1];
+        uint4 v0 = tw[2 * threadIdx.x], v1 = tw[2 * threadIdx.x + 1];
+        if constexpr (OWN) {
+          // md5 shards: only this shard's reached slots (m | mp, both
+          // already masked to the owned ones) are written; every other byte
+          // of the row keeps what the table holds (other owners' words come
+          // in through the level exchange, k_rko_unpack), so the backward
+          // never depends on running before the unpack
+          const uint4 o0 = dst[0], o1 = dst[1];
+          uint32_t nv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+          const uint32_t ov[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
+          const uint32_t mine = m | mp;
+#pragma unroll
+          for (int d = 0; d < 8; d++) {
+            const uint32_t nib = (mine >> (4 * d)) & 15u;
+            const uint32_t bm = ((nib & 1u) ? 0xFFu : 0u) | ((nib & 2u) ? 0xFF00u : 0u) |
+                                ((nib & 4u) ? 0xFF0000u : 0u) | ((nib & 8u) ? 0xFF000000u : 0u);
+            nv[d] = (nv[d] & bm) | (ov[d] & ~bm);
+          }
+          v0 = make_uint4(nv[0], nv[1], nv[2], nv[3]);
+          v1 = make_uint4(nv[4], nv[5], nv[6], nv[7]);
+        }
         dst[0] = v0;
         dst[1] = v1;
       }
@@ -905,7 +925,7 @@ static int rank_shape(const Desc* d, RankShape* rs) {
   // parents far away in time.  GM_RK_ORDER=morton orders a level's blocks by
   // the bit-interleaved height digits instead (neighbours along any column
   // mostly close together) -- A/B
-  if (const char* e = getenv("GM_RK_ORDER")) {
+  if (const char* e = lab_env("GM_RK_ORDER")) {
     if (!strcmp(e, "morton")) {
       auto key = [&](uint32_t c) {
         uint32_t dig[kRankMaxCols] = {}, v = c;
@@ -1066,7 +1086,7 @@ static void rank_kind_dispatch(const Desc& d, F&& f) {
 // (timing A/B only: the words are wrong)
 static int rk_dbg() {
   static const int v = [] {
-    const char* e = getenv("GM_RK_DBG");
+    const char* e = lab_env("GM_RK_DBG");
     return e ? atoi(e) : 0;
   }();
   return v;
@@ -1075,7 +1095,7 @@ static int rk_dbg() {
 // keeps the per-board one (A/B runs)
 static bool rk_sliced() {
   static const bool on = [] {
-    const char* e = getenv("GM_RK_SLICED");
+    const char* e = lab_env("GM_RK_SLICED");
     return !(e && atoi(e) == 0);
   }();
   return on;

@@ -290,13 +290,20 @@ static int run_ranked_shards(std::vector<gm_solver*> ss, gm_result* out) {
   }
   const int mode = group ? 4 : s0->xfer ? 3 : 1;
   if (mode == 1 && !s0->comm) return fail(GM_EINVAL, "shard %d/%d has no communicator (gm_solver_comm_init)", s0->rank, W);
-  std::vector<hipEvent_t> ev;
-  auto cleanup = [&]() {
-    for (auto e : ev) (void)hipEventDestroy(e);
-  };
+  // the solve's events, destroyed on EVERY return (the HIPCHK early
+  // returns included: they used to skip cleanup() and leak them)
+  struct Events {
+    std::vector<hipEvent_t> v;
+    void clear() {
+      for (auto e : v) (void)hipEventDestroy(e);
+      v.clear();
+    }
+    ~Events() { clear(); }
+  } ev;
+  auto cleanup = [&]() { ev.clear(); };
   auto new_event = [&](hipEvent_t* e, unsigned fl) -> int {
     HIPCHK(hipEventCreateWithFlags(e, fl));
-    ev.push_back(*e);
+    ev.v.push_back(*e);
     return 0;
   };
   hipEvent_t e0, e1, e2;
@@ -364,6 +371,10 @@ static int run_ranked_shards(std::vector<gm_solver*> ss, gm_result* out) {
       }
     } else if (mode == 1) {
       gm_solver* s = s0;
+      if (s->gabort && s->gabort->load(std::memory_order_acquire)) {
+        cleanup();
+        return fail(GM_EHIP, "RCCL group aborted: a peer shard failed (shard %d/%d)", s->rank, s->world);
+      }
       ncclGroupStart();
       ncclResult_t r = ncclSuccess;
       for (int p = 0; p < W && r == ncclSuccess; p++) {
@@ -413,6 +424,10 @@ static int run_ranked_shards(std::vector<gm_solver*> ss, gm_result* out) {
   }
   HIPCHK(hipGetLastError());
   if (mode == 1) {
+    if (s0->gabort && s0->gabort->load(std::memory_order_acquire)) {
+      cleanup();
+      return fail(GM_EHIP, "RCCL group aborted: a peer shard failed (shard %d/%d)", s0->rank, s0->world);
+    }
     ncclGroupStart();
     ncclResult_t r = ncclAllReduce(s0->st->red, s0->st->red, 4, ncclUint64, ncclSum, s0->comm, st);
     ncclResult_t r2 = ncclAllGather(s0->st->red + 4, s0->errg, 1, ncclUint64, s0->comm, st);

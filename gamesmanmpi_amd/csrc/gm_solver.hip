@@ -52,6 +52,7 @@
 #include <map>
 #include <mutex>
 #include <thread>
+#include <atomic>
 
 #include "../../include/gamesman.h"
 #include "gm_codec.h"
@@ -61,6 +62,23 @@
 
 using namespace gm;
 typedef unsigned long long u64;
+
+// A/B knobs of the measurement labs (tools/*.sh): environment variables read
+// ONLY by a library built with -DGM_LAB=1 (make lab ->
+// libgamesman_hip_lab.so).  In the shipped library every knob reads as unset,
+// so no environment can select a timing-only variant (some of them write
+// wrong words on purpose, e.g. GM_RK_DBG) or change the product's schedule.
+#ifndef GM_LAB
+#define GM_LAB 0
+#endif
+static const char* lab_env(const char* name) {
+#if GM_LAB
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
 
 // ---------------------------------------------------------------------------
 // errors
@@ -79,6 +97,24 @@ static int fail(int code, const char* fmt, ...) {
   do {                                                                              \
     hipError_t e_ = (x);                                                            \
     if (e_ != hipSuccess) return fail(GM_EHIP, "%s: %s", #x, hipGetErrorString(e_)); \
+  } while (0)
+
+// queued one-table PLANES solves (gm_solver_solve_async): a ring slot holds
+// one solve's events (start, forward end, backward end, and its completion,
+// recorded after the counts' copy) and its counts in pinned host memory
+constexpr int kPlaneRing = 8;
+struct PlaneSlot {
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  u64* host = nullptr;
+  double t_enq = 0;  // host clock at enqueue (ms)
+};
+
+// an in-process multi-GPU group aborted (solve_multi's abort_all): no RCCL
+// call may use the aborted communicators
+#define RCCL_LIVE(S)                                                                              \
+  do {                                                                                            \
+    if ((S)->gabort && (S)->gabort->load(std::memory_order_acquire))                              \
+      return fail(GM_EHIP, "RCCL group aborted: a peer shard failed (shard %d/%d)", (S)->rank, (S)->world); \
   } while (0)
 
 enum : uint32_t {
@@ -312,7 +348,8 @@ static bool plane_wanted(const Desc* d, uint32_t flags, int world);
 static int plan_planes(const Desc* d, int rank, int world, uint32_t flags, uint64_t max_table_bytes, gm_plan_t* out,
                        bool* fits);
 static int plane_setup(gm_solver* s, const gm_buffers* buf);
-static int run_planes(std::vector<gm_solver*> ss, gm_result* out);
+static int run_planes(std::vector<gm_solver*> ss, gm_result* out, bool async = false);
+static int plane_collect(gm_solver* s, u64 ticket, gm_result* out);
 static int plane_query(gm_solver* s, const uint64_t* keys_dev, uint64_t n, uint32_t* words_dev);
 static int plane_positions(gm_solver* s, uint64_t* keys_dev, uint64_t cap, uint64_t* n);
 static void plane_checksum_launch(gm_solver* s, u64* acc);
@@ -1003,12 +1040,13 @@ struct gm_solver {
   // whole-solve HIP graphs of a one-table dense solve (run_dense): the
   // forward and the backward launches, captured on the first full solve
   hipGraphExec_t gfwd = nullptr, gbwd = nullptr;
-  // the whole one-table PLANES solve as one HIP graph (run_planes), its counts
-  // copied into pinned host memory at the end of every replay
-  hipGraphExec_t pgexec = nullptr;
+  // one-table PLANES: the counts of a solve in pinned host memory, the
+  // solve's timing events, and the ring of queued solves
+  // (gm_solver_solve_async / gm_solver_collect)
   u64* phost = nullptr;
-  bool pcapture = false;
   hipEvent_t pse[3] = {nullptr, nullptr, nullptr};  // run_planes' timing events
+  PlaneSlot pring[kPlaneRing];
+  u64 pq_next = 0, pq_done = 0;  // tickets issued / collected
   // BUCKETED (gm_bucketed.h): level store, words, in-edges, partition scratch
   u64* bkK = nullptr;
   uint32_t* bkW = nullptr;
@@ -1061,6 +1099,9 @@ struct gm_solver {
   // per key / per row; k = key skew, K keys, rows 0..smax
   uint32_t pstage_k = 0, pkeys = 0, prows = 0;
   ncclComm_t comm2 = nullptr;        // second communicator (ncclCommSplit): the other halo direction
+  // the group's abort flag (solve_multi): once set, its communicators are
+  // being aborted and this shard issues no further RCCL call
+  std::atomic<int>* gabort = nullptr;
   int defer_rc = 0;                  // a deferred failure of this shard's last solve (0: none)
   std::string defer_msg;
   hipStream_t cstream2 = nullptr;    // receive stream of the staged exchange
@@ -2259,9 +2300,13 @@ void gm_solver_destroy(gm_solver* s) {
   for (hipEvent_t e : s->pev) (void)hipEventDestroy(e);
   if (s->gfwd) (void)hipGraphExecDestroy(s->gfwd);
   if (s->gbwd) (void)hipGraphExecDestroy(s->gbwd);
-  if (s->pgexec) (void)hipGraphExecDestroy(s->pgexec);
   for (hipEvent_t e : s->pse)
     if (e) (void)hipEventDestroy(e);
+  for (PlaneSlot& q : s->pring) {
+    for (hipEvent_t e : q.ev)
+      if (e) (void)hipEventDestroy(e);
+    if (q.host) (void)hipHostFree(q.host);
+  }
   if (s->phost) (void)hipHostFree(s->phost);
   if (s->cstream) (void)hipStreamDestroy(s->cstream);
   if (s->cstream2) (void)hipStreamDestroy(s->cstream2);
@@ -2277,6 +2322,30 @@ void gm_solver_destroy(gm_solver* s) {
 static int solve_dense(gm_solver* s, gm_result* out);
 static int solve_bucketed(gm_solver* s, gm_result* out);
 static int run_bucketed_shards(std::vector<gm_solver*> ss, gm_result* out);
+
+// Queued one-table PLANES solves: enqueue without waiting, collect later
+// (in order).  Solves queued back to back run back to back on the solver's
+// stream with no host round trip between them.
+int gm_solver_solve_async(gm_solver* s, uint64_t* ticket) {
+  if (!s || !ticket) return fail(GM_EINVAL, "bad argument");
+  if (s->mode != GM_MODE_PLANES || s->world > 1) return fail(GM_EINVAL, "queued solves: one-table PLANES solvers only");
+  if (s->pq_next - s->pq_done >= (u64)kPlaneRing)
+    return fail(GM_EINVAL, "%d solves queued: collect one first", kPlaneRing);
+  const u64 t = s->pq_next;
+  gm_result scratch;
+  memset(&scratch, 0, sizeof scratch);
+  const int rc = run_planes({s}, &scratch, true);
+  if (rc) return rc;
+  *ticket = t;
+  return 0;
+}
+
+int gm_solver_collect(gm_solver* s, uint64_t ticket, gm_result* out) {
+  if (!s || !out) return fail(GM_EINVAL, "bad argument");
+  memset(out, 0, sizeof *out);
+  if (s->mode != GM_MODE_PLANES || s->world > 1) return fail(GM_EINVAL, "queued solves: one-table PLANES solvers only");
+  return plane_collect(s, ticket, out);
+}
 
 int gm_solver_solve(gm_solver* s, gm_result* out) {
   if (!s || !out) return fail(GM_EINVAL, "bad argument");
@@ -2617,6 +2686,7 @@ static int exchange_bits(std::vector<gm_solver*>& ss, u64 L, int mode, hipStream
     gm_solver* s = ss[0];
     const int down = (s->rank + s->world - 1) % s->world, up = (s->rank + 1) % s->world;
     const u64 nb = blk_count(s), B = s->view.B;
+    RCCL_LIVE(s);
     ncclGroupStart();
     for (u64 j = 0; j < nb; j++) {
       u64 lo, hi;
@@ -2824,7 +2894,8 @@ static int check_halo_plan(std::vector<gm_solver*>& ss, int mode, hipStream_t st
       u64* dmine = dall + all.size();
       hipError_t e = hipMemcpyAsync(dmine, mine.data(), mine.size() * 8, hipMemcpyHostToDevice, st);
       ncclResult_t r = ncclSuccess;
-      if (e == hipSuccess) r = ncclAllGather(dmine, dall, mine.size(), ncclUint64, s0->comm, st);
+      if (s0->gabort && s0->gabort->load(std::memory_order_acquire)) r = ncclInvalidUsage;
+      if (e == hipSuccess && r == ncclSuccess) r = ncclAllGather(dmine, dall, mine.size(), ncclUint64, s0->comm, st);
       if (e == hipSuccess && r == ncclSuccess) e = hipMemcpyAsync(all.data(), dall, all.size() * 8, hipMemcpyDeviceToHost, st);
       if (e == hipSuccess) e = hipStreamSynchronize(st);
       (void)hipFree(dev);
@@ -2879,6 +2950,7 @@ static int exchange_words(std::vector<gm_solver*>& ss, u64 L, int mode, hipStrea
     gm_solver* s = ss[0];
     const int down = (s->rank + s->world - 1) % s->world, up = (s->rank + 1) % s->world;
     const u64 nb = blk_count(s), B = s->view.B;
+    RCCL_LIVE(s);
     if (packed) {
       const u64 nsend = halo_move_all(s, L, 1, s->halo_send, cs);
       const u64 nrecv = halo_recv_count(s, L);
@@ -3248,6 +3320,7 @@ static int run_dense(std::vector<gm_solver*> ss, gm_result* out) {
     hipLaunchKernelGGL(k_fill_red, dim3(1), dim3(1024), 0, st, s->st, s->bcount);
   }
   if (mode == 1) {  // counts and root word summed; every rank's error mask gathered, OR-ed on the host
+    RCCL_LIVE(s0);
     ncclGroupStart();
     ncclResult_t r = ncclAllReduce(s0->st->red, s0->st->red, 4, ncclUint64, ncclSum, s0->comm, st);
     ncclResult_t r2 = ncclAllGather(s0->st->red + 4, s0->errg, 1, ncclUint64, s0->comm, st);
@@ -3870,18 +3943,42 @@ static int solve_multi(int game, int ngpus, const gm_buffers* buf, gm_result* ou
     if (!sh->errg && hipMalloc((void**)&sh->errg, (size_t)ngpus * sizeof(u64)) != hipSuccess)
       return bail(fail(GM_EHIP, "error-mask gather buffer"));
   }
+  // The staged PLANES deal sends its odd-direction halos on a second
+  // communicator per shard (gm_plane_run.h): split here, before any shard
+  // thread runs, one group call over every rank -- so abort_all below knows
+  // every communicator a thread can wait in (a shard that split its own on
+  // first use could be blocked in comm2 while the abort missed it).
+  bool staged_deal = false;
+  for (gm_solver* sh : m.ss) staged_deal = staged_deal || (sh->mode == GM_MODE_PLANES && sh->pstage_k);
+  if (staged_deal) {
+    ncclResult_t r1 = ncclGroupStart();
+    for (int i = 0; i < ngpus && r1 == ncclSuccess; i++) {
+      gm_solver* sh = m.ss[(size_t)i];
+      if (!sh->comm2) r1 = ncclCommSplit(sh->comm, 0, sh->rank, &sh->comm2, nullptr);
+    }
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r1 != ncclSuccess || r2 != ncclSuccess)
+      return bail(fail(GM_EHIP, "ncclCommSplit (staged deal): %s", ncclGetErrorString(r1 != ncclSuccess ? r1 : r2)));
+  }
   std::vector<gm_result> res((size_t)ngpus);
   std::vector<int> rcs((size_t)ngpus, 0);
   std::vector<std::string> msg((size_t)ngpus);
   std::mutex abort_mu;  // one abort of the whole group, by the first thread that fails
+  std::atomic<int> gabort{0};
+  for (gm_solver* sh : m.ss) sh->gabort = &gabort;
   auto abort_all = [&]() {
     std::lock_guard<std::mutex> lk(abort_mu);
     if (aborted) return;
     aborted = true;
+    // published first: a shard that checks it (RCCL_LIVE, before every RCCL
+    // call) issues nothing more on these communicators; then every one of
+    // them -- the primary ones and the staged deal's second ones -- is
+    // aborted, so a peer waiting in any RCCL call on any of them returns
+    gabort.store(1, std::memory_order_release);
     for (size_t i = 0; i < comms.size(); i++)
       if (comms[i]) (void)ncclCommAbort(comms[i]);
-    // (the second communicators of the staged deal are split from these and
-    // are aborted with the shards' own below, after the join)
+    for (gm_solver* sh : m.ss)
+      if (sh && sh->comm2) (void)ncclCommAbort(sh->comm2);
   };
   std::vector<std::thread> th;
   for (int i = 0; i < ngpus; i++)
@@ -3902,12 +3999,10 @@ static int solve_multi(int game, int ngpus, const gm_buffers* buf, gm_result* ou
     });
   for (auto& t : th) t.join();
   (void)hipSetDevice(cur);
+  for (gm_solver* sh : m.ss) sh->gabort = nullptr;
   if (aborted)  // the aborted communicators are not destroyed again with the shards
     for (gm_solver* sh : m.ss)
-      if (sh) {
-        if (sh->comm2) (void)ncclCommAbort(sh->comm2);
-        sh->comm = sh->comm2 = nullptr;
-      }
+      if (sh) sh->comm = sh->comm2 = nullptr;
   for (int i = 0; i < ngpus; i++)
     if (rcs[(size_t)i]) return bail(fail(rcs[(size_t)i], "shard %d: %s", i, msg[(size_t)i].c_str()));
   *out = res[0];

@@ -212,6 +212,27 @@ class Solver:
                 self._alloc(self.positions_hint)
         return self._result(r)
 
+    # -- queued solves (one-table PLANES) ------------------------------------
+    def solve_async(self):
+        """Enqueue a full solve on the solver's stream and return its ticket
+        without waiting (gm_solver_solve_async; one-table PLANES solvers).
+        Solves queued back to back run back to back on the GPU; collect()
+        each one, in ticket order (at most 8 outstanding)."""
+        L = _lib.load()
+        t = ctypes.c_uint64()
+        with self.torch.cuda.device(self.device):
+            _lib.check(L.gm_solver_solve_async(self._h, ctypes.byref(t)))
+        return int(t.value)
+
+    def collect(self, ticket):
+        """Wait for queued solve `ticket`; its SolveResult (ms_total is the
+        solve's device span)."""
+        L = _lib.load()
+        r = _lib.gm_result()
+        with self.torch.cuda.device(self.device):
+            _lib.check(L.gm_solver_collect(self._h, int(ticket), ctypes.byref(r)))
+        return self._result(r)
+
     # -- stop / resume (checkpoints: gamesmanmpi_amd.checkpoint) ------------
     @property
     def steps(self):

@@ -85,9 +85,14 @@ def build_parser():
     p.add_argument("--no-verify", action="store_true",
                    help="skip replaying the module against its descriptor")
     p.add_argument("--verify-samples", type=int, default=200)
+    p.add_argument("--ranked-shards", action="store_true",
+                   help="under torchrun, toot-and-otto: md5-owned RANKED shards (every position "
+                        "resolved by its md5 owner, level words exchanged over RCCL) instead of "
+                        "the default, every rank solving the whole RANKED table; the shards' "
+                        "trace model predicts 22.4 ms at 8 GPUs against 8.5 ms on one "
+                        "(DESIGN.md section 6c), and their RCCL path has not run on hardware")
     p.add_argument("--ranked-replicated", action="store_true",
-                   help="under torchrun, toot-and-otto: every rank solves the whole RANKED table "
-                        "instead of the md5-owned RANKED shards")
+                   help="(the default under torchrun; kept for old command lines)")
     p.add_argument("--json", action="store_true",
                    help="also print a JSON line with counts and timings")
     p.add_argument("--symmetries", action="store_true",
@@ -264,16 +269,16 @@ def main(argv=None):
             from gamesmanmpi_amd.dist import ShardedSolver
             solver = ShardedSolver(spec, rank, world, device="cuda:%d" % local)
             result = solver.solve()
-        elif args.ranked_replicated and agreed_ranked(spec, args.layout, local, world, True):
-            # (--ranked-replicated) every rank solves the whole RANKED table
+        elif not args.ranked_shards and agreed_ranked(spec, args.layout, local, world, True):
+            # (the default) every rank solves the whole RANKED table
             # and writes the md5 share the reference's partition gives it
             from gamesmanmpi_amd.solver import Solver
             solver = Solver(spec, positions=args.positions, device="cuda:%d" % local, layout="ranked")
             solver.replicated = True
             result = solver.solve()
             result.extra.update({"partition": "replicated", "world": world})
-        elif not args.ranked_replicated and agreed_ranked(spec, args.layout, local, world):
-            # toot-and-otto: md5 shards of the RANKED index space -- every
+        elif args.ranked_shards and agreed_ranked(spec, args.layout, local, world):
+            # (--ranked-shards) md5 shards of the RANKED index space -- every
             # position resolved by its md5 owner (src/game_state.py:22-30),
             # each level's words exchanged over RCCL (gm_ranked_shard.h);
             # every rank ends with the whole table and writes its md5 share

@@ -254,6 +254,16 @@ int gm_plan(int game, uint64_t positions, uint32_t flags,
 typedef struct gm_solver gm_solver;
 int gm_solver_create(int game, const gm_buffers *buf, gm_solver **out);
 int gm_solver_solve(gm_solver *s, gm_result *out);
+/* Queued full solves (one-table PLANES solvers): gm_solver_solve_async
+ * enqueues a whole solve on the solver's stream and returns at once with a
+ * ticket; gm_solver_collect waits for that solve and fills *out as
+ * gm_solver_solve would (ms_total = the solve's device span).  Up to 8 may
+ * be queued; collect them in ticket order.  Solves queued back to back run
+ * back to back on the device with no host round trip between them -- the
+ * throughput form of the reference's one-job-at-a-time run()
+ * (src/process.py:37-60). */
+int gm_solver_solve_async(gm_solver *s, uint64_t *ticket);
+int gm_solver_collect(gm_solver *s, uint64_t ticket, gm_result *out);
 /* words_dev[i] = word of keys_dev[i] (GM_NO_WORD if not reachable) */
 int gm_solver_query(gm_solver *s, const uint64_t *keys_dev, uint64_t n,
                     uint32_t *words_dev);

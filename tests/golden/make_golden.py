@@ -17,6 +17,9 @@ What it writes (see tests/golden/README.md):
   movegen/<game>.json    sampled positions: primitive + ORDERED children bytes
                          (src/game_state.py:32-40 expand order)
   md5_owner.json         GameState.get_hash(P) (src/game_state.py:22-30)
+  movegen/toot_6x4.json, deep/toot_6x4.json
+                         BASELINE config 3 at its own size, by samples
+                         (--only toot_6x4; toot_6x4_fixtures)
   reference_runs.json    root lines printed by Process.run
                          (src/process.py:47-52) under the fake MPI
   summary.json           positions/edges/levels/histograms/root line per game
@@ -349,6 +352,96 @@ GAMES = {
 SHA_ONLY = {"toot_4x4"}
 
 
+def toot_6x4_fixtures(outdir, n_movegen=400, n_deep=220, seed=6):
+    """BASELINE config 3 at its own size (toot_and_otto_bitstring.py:8 as
+    shipped, 6x4: 1,187,212,827 positions -- too many to enumerate here), pinned
+    by the reference module itself on SAMPLES:
+      movegen/toot_6x4.json  positions from random playouts of the module's
+                             own gen_moves/do_move, each with primitive() and
+                             the ordered children (src/game_state.py:32-40)
+      md5 rows               GameState.get_hash for P = 1..8 (game_state.py:22-30)
+      deep/toot_6x4.json     positions with >= 16 pieces placed, each solved
+                             EXHAUSTIVELY through the module (every position
+                             reachable from it) with the reference-canonical
+                             retrograde: value and remoteness of the position
+    Returns the md5 samples."""
+    mod = load_ref_game("toot_and_otto_bitstring.py", "gm_toot_6x4", length=6, height=4)
+    rng = random.Random(seed)
+    root = mod.initial_position()
+    pool, depth = {root: 0}, {}
+    while len(pool) < 6 * n_movegen:  # playout positions, every depth
+        pos, d = root, 0
+        while mod.primitive(pos) == UNDECIDED:
+            pos = mod.do_move(pos, rng.choice(mod.gen_moves(pos)))
+            d += 1
+            pool.setdefault(pos, d)
+    keys = sorted(pool, key=canon_bytes)
+    sample = [root] + rng.sample([k for k in keys if k != root], n_movegen - 1)
+    rows = []
+    for pos in sample:
+        p = mod.primitive(pos)
+        ch = [canon_bytes(mod.do_move(pos, m)).hex() for m in mod.gen_moves(pos)] if p == UNDECIDED else []
+        rows.append({"pos": canon_bytes(pos).hex(), "primitive": int(p), "children": ch,
+                     "str_utf8": str(pos).encode("utf-8").hex(), "pieces": pool[pos]})
+    os.makedirs(os.path.join(outdir, "movegen"), exist_ok=True)
+    with open(os.path.join(outdir, "movegen", "toot_6x4.json"), "w") as f:
+        json.dump(rows, f, indent=0)
+
+    def subdag(pos, cap=20000):
+        seen, order, prim, children = {pos: True}, [pos], {}, {}
+        i = 0
+        while i < len(order):
+            k = order[i]
+            i += 1
+            p = mod.primitive(k)
+            prim[k] = p
+            if p != UNDECIDED:
+                children[k] = []
+                continue
+            ch = []
+            for m in mod.gen_moves(k):
+                c = mod.do_move(k, m)
+                ch.append(c)
+                if c not in seen:
+                    seen[c] = True
+                    order.append(c)
+                    if len(order) > cap:
+                        return None
+            children[k] = ch
+        return order, prim, children
+
+    deep, tried = [], set()
+    while len(deep) < n_deep:
+        pos, d = root, 0
+        target = rng.randint(16, 23)
+        while d < target and mod.primitive(pos) == UNDECIDED:
+            pos = mod.do_move(pos, rng.choice(mod.gen_moves(pos)))
+            d += 1
+        if d < 16 or pos in tried:
+            continue
+        tried.add(pos)
+        sub = subdag(pos)
+        if sub is None:
+            continue
+        order, prim, children = sub
+        val, rem = retrograde(prim, children, order)
+        deep.append({"pos": canon_bytes(pos).hex(), "pieces": d, "value": int(val[pos]),
+                     "remoteness": int(rem[pos]), "primitive": int(prim[pos]),
+                     "subgraph_positions": len(order)})
+    os.makedirs(os.path.join(outdir, "deep"), exist_ok=True)
+    with open(os.path.join(outdir, "deep", "toot_6x4.json"), "w") as f:
+        json.dump({"game": "toot_and_otto_bitstring", "params": "length=6,height=4",
+                   "source": "reference test_games/toot_and_otto_bitstring.py (length=6, height=4) through "
+                             "tests/golden/make_golden.py toot_6x4_fixtures, seed %d" % seed,
+                   "semantics": "value / remoteness by the reference-canonical retrograde (SURVEY.md 8a A8/A9) "
+                                "over every position reachable from the listed one",
+                   "rows": deep}, f, indent=0)
+    hist = [sum(1 for r in deep if r["value"] == v) for v in range(4)]
+    print("toot_6x4 fixtures: %d movegen rows, %d deep positions (W/L/T/D %s)" % (len(rows), len(deep), hist),
+          flush=True)
+    return [("toot_6x4", p) for p in [root] + rng.sample(sample, 59)]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-mpi", action="store_true")
@@ -373,6 +466,8 @@ def main():
     for heaps in ((3, 3, 3), (4, 4, 4), (2, 5, 7), (6, 6, 6, 6)):
         todo["sum_fto_" + "_".join(map(str, heaps))] = ("OWN", heaps)
 
+    if args.only and "toot_6x4" in args.only:
+        md5_samples += toot_6x4_fixtures(outdir)
     for name, (fname, kw) in todo.items():
         if args.only and name not in args.only:
             continue

@@ -89,6 +89,7 @@ def test_md5_owner_vectors():
     with open(os.path.join(GOLDEN, "md5_owner.json")) as f:
         rows = json.load(f)
     specs = {n: GameSpec(*CASES[n]) for n in CASES}
+    specs["toot_6x4"] = GameSpec("toot_and_otto_bitstring", "length=6,height=4")  # sampled rows (config 3)
     n = 0
     for row in rows:
         spec = specs[row["game"]]
@@ -222,3 +223,23 @@ def test_planes_bench_shards_plan_8bit_words(world, heaps):
         # planes each way, 8-bit): 16-bit words alone would be 2 GiB
         halo = (1 << 25) * ((r > 0) + (r + 1 < world))
         assert p.table_bytes == (1 << 30) + (1 << 27) + 2 * halo
+
+
+def test_product_library_reads_no_lab_knob():
+    """The measurement labs' A/B environment knobs (some of them write wrong
+    words on purpose, e.g. GM_RK_DBG) and the failure tests' fault injector
+    are compiled into the LAB build only (-DGM_LAB=1,
+    libgamesman_hip_lab.so): the shipped library does not even hold their
+    names, so no environment can select them."""
+    knobs = [b"GM_RK_DBG", b"GM_RK_ORDER", b"GM_RK_SLICED", b"GM_FAULT_STAGED", b"GM_PLANE_STAGE_K",
+             b"GM_PLANE_GRAPH", b"GM_PLANE_SPIN", b"GM_PLANE_FWD_FIRST"]
+    with open(os.path.join(ROOT, "gamesmanmpi_amd", "libgamesman_hip.so"), "rb") as f:
+        prod = f.read()
+    for k in knobs:
+        assert k not in prod, k
+    lab = os.path.join(ROOT, "gamesmanmpi_amd", "libgamesman_hip_lab.so")
+    if os.path.exists(lab):
+        with open(lab, "rb") as f:
+            data = f.read()
+        for k in (b"GM_RK_DBG", b"GM_FAULT_STAGED"):
+            assert k in data, k

@@ -367,27 +367,32 @@ def test_planes_row_deal_group_matches_oracle(world, params, streams):
     np.testing.assert_array_equal(got, want)
 
 
-def test_planes_graph_replay_equals_plain_launches():
-    """GM_PLANE_GRAPH=1 (A/B knob): the whole one-table solve captured once
-    and replayed as one HIP graph gives the plain launches' counts, root and
-    fingerprint on every replay (a child process: the knob is read once)."""
-    import subprocess
-    import sys
-    params = "heaps=31:31:9:6:3"
-    code = ("import json\n"
-            "from gamesmanmpi_amd.games import GameSpec\n"
-            "from gamesmanmpi_amd.solver import Solver\n"
-            "s = Solver(GameSpec('sum_four_to_one', %r))\n"
-            "out = []\n"
-            "for _ in range(3):\n"
-            "    r = s.solve()\n"
-            "    out.append([r.positions, r.edges, r.primitives, r.root_line, s.checksum()['checksum']])\n"
-            "print(json.dumps(out))\n" % params)
-    got = {}
-    for g in ("0", "1"):
-        env = dict(os.environ, GM_PLANE_GRAPH=g)
-        p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=180,
-                           cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-        assert p.returncode == 0, p.stderr[-2000:]
-        got[g] = json.loads(p.stdout.strip().splitlines()[-1])
-    assert got["1"] == got["0"] and got["0"][0] == got["0"][2]
+def test_planes_queued_solves_equal_blocking_ones():
+    """gm_solver_solve_async / gm_solver_collect (the bench's timed loop):
+    queued one-table solves run back to back and each one's counts, root
+    and fingerprint equal a blocking solve's; tickets are collected in
+    order, at most 8 outstanding, and a misuse is an error, not a hang."""
+    from gamesmanmpi_amd import _lib
+    from gamesmanmpi_amd.games import GameSpec
+    from gamesmanmpi_amd.solver import Solver
+    s = Solver(GameSpec("sum_four_to_one", "heaps=31:31:9:6:3"))
+    r0 = s.solve()
+    assert r0.extra["layout"] == "planes"
+    ck0 = s.checksum()["checksum"]
+    want = (r0.positions, r0.edges, r0.primitives, r0.root_line)
+    tickets = [s.solve_async() for _ in range(8)]
+    assert tickets == list(range(tickets[0], tickets[0] + 8))
+    with pytest.raises(_lib.GmError):  # the ring is full
+        s.solve_async()
+    with pytest.raises(_lib.GmError):  # out of order
+        s.collect(tickets[1])
+    for t in tickets:
+        r = s.collect(t)
+        assert (r.positions, r.edges, r.primitives, r.root_line) == want
+        assert r.ms_total > 0 and r.ms_backward > 0
+    assert s.checksum()["checksum"] == ck0
+    t = s.solve_async()  # interleaved with a blocking solve
+    r1 = s.solve()
+    r2 = s.collect(t)
+    assert (r1.positions, r1.root_line) == (r2.positions, r2.root_line) == (want[0], want[3])
+    assert s.checksum()["checksum"] == ck0
