@@ -886,6 +886,189 @@ __global__ __launch_bounds__(kPlaneRunThreads) void k_plane_run(typename PlaneWo
 }
 
 
+// Two plane levels in ONE launch (round 6; the narrow levels of a one-table
+// solve, 8-bit absolute words, at most four outer digits).  A narrow plane
+// level costs about one dependent launch -- boundary, list entry, neighbour
+// rows, the 64-step wavefront, row stores, ~4.5 us -- however few planes it
+// holds, and the solve has ~60 of them.  k_plane_pair resolves levels s and
+// s + 1 together: a wave takes one plane P of level s + 1, FIRST resolves
+// P's k = 1 neighbours Q_j = P - e_j (level s) in its four channels (lane
+// half x 16-bit half: one visit, channel j = outer digit j), THEN P itself,
+// its k = 1 rows straight from the first visit's registers (the upper lane
+// half's through LDS) and its k = 2 rows (level s - 1) from memory.  Every
+// level-s plane is resolved by each of its level-(s + 1) parents (up to four:
+// redundant work, nothing at a narrow level) and STORED by exactly one: the
+// parent P = Q + e_j with j the lowest digit that Q can be raised in (P's
+// digits below j all at their top value).  The dependent chain of the pair is
+// one launch and two wavefronts instead of two launches.  Measured in
+// tools/pair_lab.hip: pairs over levels 4-17 and 107-120 (14 launches fewer)
+// 1.282-1.286 -> 1.225-1.231 ms per 2^30 backward, byte-exact
+// (profiles/r06/pair_lab.txt).
+template <class Fold>
+__device__ __forceinline__ void plane_pair_wavefront(uint32_t L, uint32_t primv, Fold fold, uint32_t* ox,
+                                                     uint32_t* oy) {
+  uint32_t Xh[8], Xl[8], Yh[8], Yl[8];
+#pragma unroll
+  for (int d = 0; d < 8; d++) Xh[d] = Xl[d] = Yh[d] = Yl[d] = 0;
+  fold(Xh, Xl, Yh, Yl);  // E rows: odd bytes raw in Xh / Yh, even bytes low-masked in Xl / Yl
+  uint32_t cur = 0, prev = 0, u1p = 0;
+  uint32_t op[32];
+  const uint32_t A0 = ~0u << L;
+  auto phase = [&](auto PHc) {  // the step chain of plane_x2_visit (8-bit absolute forms)
+    constexpr int PH = decltype(PHc)::value;
+    const uint32_t A = PH ? ~A0 : A0;
+#pragma unroll
+    for (int q = 0; q < 32; q++) {
+      const int d = q >> 2, b = q & 3;
+      const uint32_t sel = 0x0C000C00u | ((4u + (uint32_t)b) << 16) | (uint32_t)b;
+      const uint32_t a = (b & 1) ? perm(Yh[d], Xh[d], sel) : perm(Yl[d], Xl[d], sel);
+      const uint32_t u2r = from_lane_below(u1p);
+      const uint32_t pre = pk_max3w<true>(a, prev, u2r);
+      const uint32_t u1r = from_lane_below(cur);
+      const uint32_t pre_ = PH == 0 ? ((__builtin_amdgcn_sbfe((int)A, q, 1) != 0) ? pre : 0x00FF00FFu) : pre;
+      const uint32_t m = pk_max3w<true>(pre_, cur, u1r);
+      uint32_t f = parent_x2<1>(m);
+      if (PH == 0) {
+        if (q == 0) f = pk_max16(f, primv);
+        op[q] = f;
+      } else {
+        op[q] = __builtin_amdgcn_sbfe((int)A, q, 1) ? f : op[q];
+      }
+      prev = cur;
+      cur = f;
+      u1p = u1r;
+    }
+  };
+  phase(std::integral_constant<int, 0>());
+  phase(std::integral_constant<int, 1>());
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const uint32_t t1 = perm(op[4 * k + 1], op[4 * k], 0x06020400u);
+    const uint32_t t2 = perm(op[4 * k + 3], op[4 * k + 2], 0x06020400u);
+    ox[k] = perm(t2, t1, 0x05040100u);
+    oy[k] = perm(t2, t1, 0x07060302u);
+  }
+}
+__device__ __forceinline__ void plane_pair_fold(uint32_t* Xh, uint32_t* Xl, uint32_t* Yh, uint32_t* Yl,
+                                                const uint32_t* a, const uint32_t* b) {
+#pragma unroll
+  for (int d = 0; d < 8; d++) {
+    Xh[d] = pk_max16(Xh[d], a[d]);
+    Yh[d] = pk_max16(Yh[d], b[d]);
+    Xl[d] = pk_max16(Xl[d], a[d] & 0x00FF00FFu);
+    Yl[d] = pk_max16(Yl[d], b[d] & 0x00FF00FFu);
+  }
+}
+// row L of plane P (both 16-B pieces), or zeros
+__device__ __forceinline__ void plane_pair_row(const uint8_t* tab, bool has, uint32_t P, uint32_t L,
+                                               const uint4* zero, uint32_t* r) {
+  const uint4* src = has ? (const uint4*)(tab + (size_t)P * 1024u + L * 16u) : zero;
+  const uint4 v0 = src[0], v1 = src[kPieceU4];
+  r[0] = v0.x, r[1] = v0.y, r[2] = v0.z, r[3] = v0.w;
+  r[4] = v1.x, r[5] = v1.y, r[6] = v1.z, r[7] = v1.w;
+}
+__device__ __forceinline__ void plane_pair_store(uint8_t* tab, uint32_t P, uint32_t L, const uint32_t* o) {
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  uint4* p = (uint4*)(tab + (size_t)P * 1024u + L * 16u);
+#pragma unroll
+  for (int q = 0; q < 2; q++) {  // write-through, as the grid launches' rows (plane_x2_visit)
+    const v4u v = {o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p + q * kPieceU4), "v"(v) : "memory");
+  }
+}
+// list: level s + 1's planes (uint32 plane indices), n of them; one wave per
+// plane, four waves per workgroup (the grid loop is uniform per workgroup:
+// the LDS exchange's barriers)
+template <int NO>
+__global__ __launch_bounds__(256) void k_plane_pair(uint8_t* __restrict__ tab, const uint32_t* __restrict__ list,
+                                                    uint32_t n, PlaneGeom g, const uint4* __restrict__ zero) {
+  static_assert(NO >= 1 && NO <= 4, "one channel per outer digit");
+  __shared__ uint32_t xch[4][32][16];  // per wave: the upper lane half's two rows, for the lower half
+  const uint32_t lane = threadIdx.x & 63, L = lane & 31, hi = lane >> 5, w = threadIdx.x >> 6;
+  for (uint32_t i0 = blockIdx.x * 4u; i0 < n; i0 += gridDim.x * 4u) {
+    const uint32_t i = i0 + w;
+    const bool valid = i < n;
+    const uint32_t P = list[valid ? i : i0];
+    uint32_t dP[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) dP[j] = j < NO ? (P >> g.shift[j]) & (g.base[j] - 1u) : 0u;
+    // visit 1: channel (hi, half) = outer digit j = 2 hi + half, plane Q_j = P - e_j
+    const uint32_t jx = 2 * hi, jy = 2 * hi + 1;
+    const bool hx = (int)jx < NO && dP[jx] >= 1, hy = (int)jy < NO && dP[jy] >= 1;
+    const uint32_t qx = hx ? P - g.stride[jx] : 0u, qy = hy ? P - g.stride[jy] : 0u;
+    uint32_t dx[4], dy[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      dx[j] = j < NO ? (qx >> g.shift[j]) & (g.base[j] - 1u) : 0u;
+      dy[j] = j < NO ? (qy >> g.shift[j]) & (g.base[j] - 1u) : 0u;
+    }
+    const uint32_t primv1 = L == 0 ? (((hx && qx == 0) ? 0xFFu : 0u) | ((hy && qy == 0) ? 0xFFu << 16 : 0u)) : 0u;
+    uint32_t rx[8], ry[8];
+    plane_pair_wavefront(
+        L, primv1,
+        [&](uint32_t* Xh, uint32_t* Xl, uint32_t* Yh, uint32_t* Yl) {
+#pragma unroll
+          for (int j = 0; j < NO; j++)
+#pragma unroll
+            for (uint32_t k = 1; k <= 2; k++) {
+              uint32_t a[8], b[8];
+              plane_pair_row(tab, hx && dx[j] >= k, qx - k * g.stride[j], L, zero, a);
+              plane_pair_row(tab, hy && dy[j] >= k, qy - k * g.stride[j], L, zero, b);
+              plane_pair_fold(Xh, Xl, Yh, Yl, a, b);
+            }
+        },
+        rx, ry);
+    // Q_j's one writer: every digit of P below j at its top value
+    auto writer = [&](uint32_t j) {
+      bool ok = true;
+#pragma unroll
+      for (uint32_t t = 0; t < 4; t++) ok = ok && (t >= j || dP[t] == g.base[t] - 1u);
+      return ok;
+    };
+    if (valid && hx && writer(jx)) plane_pair_store(tab, qx, L, rx);
+    if (valid && hy && writer(jy)) plane_pair_store(tab, qy, L, ry);
+    if (hi) {
+#pragma unroll
+      for (int d = 0; d < 8; d++) {
+        xch[w][L][d] = hx ? rx[d] : 0u;
+        xch[w][L][8 + d] = hy ? ry[d] : 0u;
+      }
+    }
+    __syncthreads();
+    uint32_t q2[8], q3[8];
+#pragma unroll
+    for (int d = 0; d < 8; d++) {
+      q2[d] = xch[w][L][d];
+      q3[d] = xch[w][L][8 + d];
+    }
+    __syncthreads();  // (the next item's writes)
+    // visit 2: P in the lower lane half's low channel; the other channels idle
+    const uint32_t primv2 = (L == 0 && P == 0) ? 0xFFu : 0u;
+    uint32_t rp[8], rz[8];
+    plane_pair_wavefront(
+        L, primv2,
+        [&](uint32_t* Xh, uint32_t* Xl, uint32_t* Yh, uint32_t* Yl) {
+          uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0}, a[8], r0[8], r1[8];
+#pragma unroll
+          for (int d = 0; d < 8; d++) {
+            r0[d] = hx ? rx[d] : 0u;  // (lower half: Q_0, Q_1)
+            r1[d] = hy ? ry[d] : 0u;
+          }
+          plane_pair_fold(Xh, Xl, Yh, Yl, r0, z);
+          plane_pair_fold(Xh, Xl, Yh, Yl, r1, z);
+          plane_pair_fold(Xh, Xl, Yh, Yl, q2, z);
+          plane_pair_fold(Xh, Xl, Yh, Yl, q3, z);
+#pragma unroll
+          for (int j = 0; j < NO; j++) {
+            plane_pair_row(tab, dP[j] >= 2, P - 2 * g.stride[j], L, zero, a);
+            plane_pair_fold(Xh, Xl, Yh, Yl, a, z);
+          }
+        },
+        rp, rz);
+    if (valid && !hi) plane_pair_store(tab, P, L, rp);
+  }
+}
+
 // Forward pass: the reach bitmap (one bit per position, plane P's row h1 is
 // the 32-bit word bits[P * 32 + h1], bit h0) and the counts.  Moves act on
 // one heap at a time and the only primitive (every heap 0) has no moves, so

@@ -829,6 +829,37 @@ static void plane_reach_launch(gm_solver* s, hipStream_t stream = nullptr) {
   });
 }
 
+// Pairs of narrow plane levels in one launch (k_plane_pair, gm_plane.h):
+// one-table solves of the 8-bit absolute forms with 1-4 outer digits of
+// power-of-two bases, levels (l, l + 1) both wider than a one-workgroup run
+// and both at most kPlanePairMax planes (the pair's redundant first visits
+// grow with the width: 14 pairs over levels 4-17 and 107-120 of the 2^30
+// bench table at the default).  (lab knob GM_PLANE_PAIR_MAX; 0: no pairs)
+constexpr u64 kPlanePairMax = 1200;
+// (A/B, GM_PLANE_FWD=3) the forward's side-stream start: the first level
+// past the widest with at most this many planes (run_planes)
+constexpr u64 kPlaneFwdTail = 2048;
+static u64 plane_pair_max(const gm_solver* s) {
+  static const long long v = [] {
+    const char* e = lab_env("GM_PLANE_PAIR_MAX");
+    return e ? atoll(e) : -1ll;
+  }();
+  const bool ok = s->world <= 1 && s->pform == 1 && !plane_x1(s) && s->pg.no >= 1 && s->pg.no <= 4 && s->pg.pow2;
+  return !ok ? 0 : v >= 0 ? (u64)v : kPlanePairMax;
+}
+// levels l and l + 1 of a one-table solve in one launch
+static void plane_pair_launch(gm_solver* s, uint32_t l) {
+  const u64 a = s->ploff[(size_t)l + 1], n = s->ploff[(size_t)l + 2] - a;  // level l + 1's planes
+  const u64 blocks = std::min<u64>((n + 3) / 4, (u64)s->grid * 4);
+  const uint32_t* list = (const uint32_t*)s->plist + a;
+  plane_no_dispatch(s->pg.no, [&](auto NO) {
+    constexpr int no = decltype(NO)::value;
+    if constexpr (no >= 1 && no <= 4)
+      hipLaunchKernelGGL((k_plane_pair<no>), dim3((uint32_t)blocks), dim3(256), 0, s->stream, (uint8_t*)s->ptab, list,
+                         (uint32_t)n, s->pg, s->pzero);
+  });
+}
+
 // halo segment (level l, peer p) of a shard's send / receive plan: first
 // plane and plane count
 static u64 plane_seg(const std::vector<u64>& off, uint32_t l, int W, int p, u64* n) {
@@ -1377,12 +1408,13 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out, bool async) {
   // the solve's three timing events live with the solver (created once: a
   // create + destroy per event per solve was host time between solves); a
   // queued solve (gm_solver_solve_async) uses its ring slot's own
-  hipEvent_t e0, e1, e2;
+  hipEvent_t e0, e1, e2, etail;
   {
     hipEvent_t* se = async ? s0->pring[s0->pq_next % kPlaneRing].ev : s0->pse;
     for (int i = 0; i < 3; i++)
       if (!se[i]) HIPCHK(hipEventCreate(&se[i]));
-    e0 = se[0], e1 = se[1], e2 = se[2];
+    if (!se[4]) HIPCHK(hipEventCreate(&se[4]));
+    e0 = se[0], e1 = se[1], e2 = se[2], etail = se[4];
   }
   std::vector<hipEvent_t> kr;  // per-level start/stop (shard 0's launches)
   hipEvent_t kx[2];
@@ -1424,15 +1456,42 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out, bool async) {
   // never reads any of it (a plane's words follow from its neighbours'
   // words alone); the finish kernel waits for both.  The reach launch then
   // overlaps the first, narrow plane levels instead of preceding them.
-  const bool overlap = mode == 0 && first == 0 && stop == 2 * T && !timing;
+  // A QUEUED solve (gm_solver_solve_async) runs its forward on the solve
+  // stream before the backward instead: with the next solves already in the
+  // queues, a side-stream forward made every queued solve 0.10-0.14 ms
+  // longer on the device, whether it started with the backward (1.37-1.46
+  // vs 1.27-1.31 ms per 2^30 solve) or at its narrow tail (1.40 ms);
+  // profiles/r06/forward_placement_probe.txt.  (lab knob GM_PLANE_FWD:
+  // 1 = always on the solve stream, 2 = always on the side stream from the
+  // start, 3 = always on the side stream from the narrow tail -- the first
+  // level past the widest with <= kPlaneFwdTail planes; A/B)
+  static const int fwd_mode = [] {
+    const char* e = lab_env("GM_PLANE_FWD");
+    return e ? atoi(e) : 0;
+  }();
+  const bool overlap = mode == 0 && first == 0 && stop == 2 * T && !timing && fwd_mode != 1 &&
+                       (!async || fwd_mode >= 2);
+  uint32_t fwd_at = 0;  // the level whose launch the side-stream forward is enqueued after
+  if (overlap && fwd_mode == 3) {
+    uint32_t pk = 0;
+    for (uint32_t l = 0; l <= S; l++)
+      if (s0->ploff[(size_t)l + 1] - s0->ploff[l] > s0->ploff[(size_t)pk + 1] - s0->ploff[pk]) pk = l;
+    fwd_at = S;
+    for (uint32_t l = pk + 1; l <= S; l++)
+      if (s0->ploff[(size_t)l + 1] - s0->ploff[l] <= kPlaneFwdTail) {
+        fwd_at = l;
+        break;
+      }
+  }
   hipStream_t fs = st;  // the forward's stream
   if (overlap) {
-    if (!s0->cstream) HIPCHK(hipStreamCreateWithFlags(&s0->cstream, hipStreamNonBlocking));
+    if (!s0->cstream) {
+      HIPCHK(hipStreamCreateWithFlags(&s0->cstream, hipStreamNonBlocking));
+    }
     fs = s0->cstream;
   }
   auto t0 = std::chrono::steady_clock::now();
   HIPCHK(hipEventRecord(e0, st));
-  if (overlap) HIPCHK(hipStreamWaitEvent(fs, e0, 0));
   if (fork()) return GM_EHIP;
   auto issue_forward = [&]() -> int {
     if (first == 0) {
@@ -1457,10 +1516,12 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out, bool async) {
     return 0;
   };
   // overlap: the forward (resets, reach map, counts) is enqueued on its side
-  // stream right after the backward's first launch, so the host's first
-  // enqueue is a resolve launch (the forward is read by the finish only)
+  // stream right after the backward's first launch (GM_PLANE_FWD=3: at its
+  // narrow tail, fwd_at), so the host's first enqueue is a resolve launch
+  // (the forward is read by the finish only)
   bool fwd_pending = overlap;
   if (!fwd_pending) {
+    HIPCHK(hipEventRecord(etail, st));  // (the forward's start: ms_forward)
     const int rc = issue_forward();
     if (rc) return rc;
   }
@@ -1493,6 +1554,11 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out, bool async) {
   }
   int last_x = -1;  // last level exchanged on the comm stream
   PlaneBatcher bat0(s0);  // one table: narrow levels in one-workgroup runs
+  const u64 pair_max = mode == 0 ? plane_pair_max(s0) : 0;  // and pairs of narrow levels in one launch
+  static const bool pair_runs = [] {  // (lab knob GM_PLANE_PAIR_RUNS=1: pairs replace the runs; A/B)
+    const char* e = lab_env("GM_PLANE_PAIR_RUNS");
+    return e && atoi(e) == 1;
+  }();
   u64 nlaunch = 0;        // resolve launches of this solve (shard 0's)
   if (staged && stop == 2 * T) {
     if (timing) HIPCHK(hipEventRecord(kr[0], st));
@@ -1510,10 +1576,23 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out, bool async) {
     if (k >= stop) break;
     if (per_level || (timing && l == 0)) HIPCHK(hipEventRecord(kr[2 * l], st));
     if (mode == 0 && !per_level) {
-      bat0.add(s0->ploff[l], s0->ploff[(size_t)l + 1], l, l < S ? s0->ploff[(size_t)l + 2] - s0->ploff[(size_t)l + 1] : 0);
+      const u64 n0 = s0->ploff[(size_t)l + 1] - s0->ploff[l];
+      const u64 n1 = l < S ? s0->ploff[(size_t)l + 2] - s0->ploff[(size_t)l + 1] : 0;
+      const u64 pmin = pair_runs ? 1 : bat0.narrow + 1;  // (pairs of run-narrow levels too: A/B)
+      if (l < S && k + 1 < stop && n0 >= pmin && n1 >= pmin && n0 <= pair_max && n1 <= pair_max) {
+        bat0.flush();  // levels l and l + 1 in one launch (k_plane_pair)
+        plane_pair_launch(s0, l);
+        bat0.launches++;
+        l++;
+      } else {
+        bat0.add(s0->ploff[l], s0->ploff[(size_t)l + 1], l, n1);
+      }
       if (l == S) bat0.flush();
-      if (fwd_pending && bat0.launches > 0) {
+      if (fwd_pending && bat0.launches > 0 && l >= fwd_at) {
         fwd_pending = false;
+        bat0.flush();  // the side stream starts behind this level's launch
+        HIPCHK(hipEventRecord(etail, st));
+        HIPCHK(hipStreamWaitEvent(fs, etail, 0));
         const int rc = issue_forward();
         if (rc) return rc;
       }
@@ -1541,8 +1620,10 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out, bool async) {
     if (per_level || (timing && l == S)) HIPCHK(hipEventRecord(kr[2 * l + 1], st));
   }
   bat0.flush();  // a stop inside a run
-  if (fwd_pending) {  // (nothing launched in the loop)
+  if (fwd_pending) {  // (not reached in the loop)
     fwd_pending = false;
+    HIPCHK(hipEventRecord(etail, st));
+    HIPCHK(hipStreamWaitEvent(fs, etail, 0));
     const int rc = issue_forward();
     if (rc) return rc;
   }
@@ -1618,8 +1699,8 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out, bool async) {
   }
   auto t1 = std::chrono::steady_clock::now();
   float f = 0, b = 0;
-  HIPCHK(hipEventElapsedTime(&f, e0, e1));
-  HIPCHK(hipEventElapsedTime(&b, overlap ? e0 : e1, e2));  // overlap: both phases start at e0
+  HIPCHK(hipEventElapsedTime(&f, etail, e1));  // the forward's own span (it starts at etail)
+  HIPCHK(hipEventElapsedTime(&b, overlap ? e0 : e1, e2));  // overlap: the backward starts at e0
   out->ms_forward = f;
   out->ms_backward = b;
   out->ms_total = std::chrono::duration<double, std::milli>(t1 - t0).count();
@@ -1667,7 +1748,7 @@ static int plane_collect(gm_solver* s, u64 ticket, gm_result* out) {
   u64 red[5];
   memcpy(red, q.host, sizeof red);
   float f = 0, b = 0, t = 0;
-  HIPCHK(hipEventElapsedTime(&f, q.ev[0], q.ev[1]));
+  HIPCHK(hipEventElapsedTime(&f, q.ev[4], q.ev[1]));
   HIPCHK(hipEventElapsedTime(&b, q.ev[0], q.ev[2]));
   HIPCHK(hipEventElapsedTime(&t, q.ev[0], q.ev[3]));
   out->ms_forward = f;

@@ -100,11 +100,12 @@ static int fail(int code, const char* fmt, ...) {
   } while (0)
 
 // queued one-table PLANES solves (gm_solver_solve_async): a ring slot holds
-// one solve's events (start, forward end, backward end, and its completion,
-// recorded after the counts' copy) and its counts in pinned host memory
+// one solve's events (start, forward end, backward end, its completion --
+// recorded after the counts' copy -- and the forward's start) and its counts
+// in pinned host memory
 constexpr int kPlaneRing = 8;
 struct PlaneSlot {
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // (4: the forward's start, no timing)
   u64* host = nullptr;
   double t_enq = 0;  // host clock at enqueue (ms)
 };
@@ -1044,7 +1045,7 @@ struct gm_solver {
   // solve's timing events, and the ring of queued solves
   // (gm_solver_solve_async / gm_solver_collect)
   u64* phost = nullptr;
-  hipEvent_t pse[3] = {nullptr, nullptr, nullptr};  // run_planes' timing events
+  hipEvent_t pse[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // run_planes' events (as PlaneSlot::ev)
   PlaneSlot pring[kPlaneRing];
   u64 pq_next = 0, pq_done = 0;  // tickets issued / collected
   // BUCKETED (gm_bucketed.h): level store, words, in-edges, partition scratch

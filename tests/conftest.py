@@ -45,6 +45,13 @@ CASES = {
     "sum_fto_6_6_6_6": ("sum_four_to_one", "heaps=6:6:6:6"),
 }
 
+# fixtures pinned by SAMPLES only (no full table): md5_owner.json rows and
+# movegen vectors of BASELINE config 3 at its own size (test_toot_6x4_fixtures)
+SAMPLED_CASES = {
+    "toot_6x4": ("toot_and_otto_bitstring", "length=6,height=4"),
+}
+ALL_CASES = dict(CASES, **SAMPLED_CASES)
+
 
 def load_table(name):
     import numpy as np

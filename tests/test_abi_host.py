@@ -10,7 +10,7 @@ import re
 import numpy as np
 import pytest
 
-from conftest import CASES, GOLDEN, ROOT, load_table
+from conftest import ALL_CASES, CASES, GOLDEN, ROOT, load_table
 
 
 def header_symbols():
@@ -88,8 +88,7 @@ def test_md5_owner_vectors():
     from gamesmanmpi_amd.games import GameSpec
     with open(os.path.join(GOLDEN, "md5_owner.json")) as f:
         rows = json.load(f)
-    specs = {n: GameSpec(*CASES[n]) for n in CASES}
-    specs["toot_6x4"] = GameSpec("toot_and_otto_bitstring", "length=6,height=4")  # sampled rows (config 3)
+    specs = {n: GameSpec(*ALL_CASES[n]) for n in ALL_CASES}
     n = 0
     for row in rows:
         spec = specs[row["game"]]

@@ -6,7 +6,7 @@ import hashlib
 import numpy as np
 import pytest
 
-from conftest import CASES, load_table
+from conftest import ALL_CASES, CASES, load_table
 
 pytestmark = pytest.mark.gpu
 
@@ -115,7 +115,7 @@ def test_gpu_md5_owner_kernel():
     for row in rows:
         by_game.setdefault(row["game"], []).append(row)
     for game, rs in by_game.items():
-        spec = GameSpec(*CASES[game])
+        spec = GameSpec(*ALL_CASES[game])
         keys = np.array([spec.encode(bytes.fromhex(r["canon"])) for r in rs],
                         np.uint64)
         kd = torch.from_numpy(keys.view(np.int64)).cuda()

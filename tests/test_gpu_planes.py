@@ -62,6 +62,28 @@ def test_planes_match_oracle(params):
                                                        sol.stats["loss"])
 
 
+@pytest.mark.parametrize("params", ["heaps=31:31:7:7:7:7", "heaps=31:31:15:15:15"])
+def test_planes_level_pairs_match_oracle(params):
+    """Shapes whose narrow plane levels go through k_plane_pair (two levels
+    per launch, the level-s planes resolved redundantly by their level-(s+1)
+    parents and stored by one): four and three outer digits of power-of-two
+    bases, levels of 33..1200 planes paired -- counts, root, whole-table
+    fingerprint and 20,000 sampled words equal the oracle's."""
+    s, r = _planes(params)
+    sol = _oracle(params)
+    assert r.extra["layout"] == "planes"
+    assert (r.positions, r.edges, r.primitives, r.root_line) == (sol.count, sol.edges, sol.stats["primitives"],
+                                                                  sol.root_line)
+    ck = s.checksum()
+    assert (ck["checksum"], ck["win"], ck["loss"]) == ("%016x" % sol.stats["checksum"], sol.stats["win"],
+                                                       sol.stats["loss"])
+    rng = np.random.default_rng(6)
+    keys = rng.integers(0, sol.count, 20000, dtype=np.uint64)
+    w = s.query(keys)
+    want = np.array([sol.word(int(k)) for k in keys], np.uint32)
+    np.testing.assert_array_equal(w, want)
+
+
 def test_planes_kernel_families_agree():
     """16-bit order forms (GM_F_WORDS16, k_plane_resolve) and the one-plane
     kernel on 8-bit words (GM_F_PLANE_X1) give the same words as the

@@ -47,6 +47,9 @@ def kernel_sources_sha16(root_dir):
     return h.hexdigest()[:16]
 
 
+KEYED_WORKLOAD = "toot_and_otto_bitstring length=6,height=4 (bench.py keyed record)"
+
+
 def traffic(workload, out_path, root):
     per, launches = load(root)
     res = {}
@@ -62,7 +65,13 @@ def traffic(workload, out_path, root):
         n = len(launches[name]) / max(1, len({p for p, _ in launches[name]}))
         f = ctr["FETCH_SIZE"] * 1024 * 2 / n
         w = ctr["WRITE_SIZE"] * 1024 / n
-        row = {"workload": workload, "bytes_per_launch": f + w,
+        # one bench.py run holds several records: the synthetic's kernels, the
+        # keyed toot 6x4 record's (RANKED k_rk_*, BUCKETED k_bk_*), the runtime's
+        # copies and fills -- label each kernel by the record it served
+        wl = (KEYED_WORKLOAD if short.startswith(("k_rk_", "k_bk_", "k_rko_"))
+              else workload if short.startswith(("k_plane", "k_dense", "k_fill", "k_checksum"))
+              else "bench.py run (every record: runtime copies / fills)")
+        row = {"workload": wl, "bytes_per_launch": f + w,
                "fetch_bytes_per_launch": f, "write_bytes_per_launch": w,
                "launches": n, "source": root, "kernel_sources_sha16": src_sha,
                # the key bench.py checks: the measured kernel's own gfx950 code
