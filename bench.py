@@ -115,7 +115,8 @@ def plane_bytes(heaps, word_bytes):
       resolve(l): the level's own planes written + the planes of levels l-1
                   and l-2 (its children's planes) read once
                   = w KiB x (n(l) + n(l-1) + n(l-2));
-      reach:      one bit per position written.
+      reach:      one bit per 32-position row written (a reached row holds
+                  every h0 up to the start: gm_plane.h plane_reach_body).
     requested -- what the kernel asks of the memory system: own plane
       written + every neighbour plane row read (one per outer heap and move
       that exists), L2 / Infinity-Cache hits included."""
@@ -136,7 +137,7 @@ def plane_bytes(heaps, word_bytes):
     nbr = sum(planes * sum(min(v, 2) for v in range(h + 1)) // (h + 1) for h in outer)
     P = planes * 1024
     return {"resolve_compulsory": comp, "resolve_requested": pb * (planes + nbr),
-            "pull_compulsory": P / 8.0, "pull_requested": P / 8.0, "launches": len(n)}
+            "pull_compulsory": P / 256.0, "pull_requested": P / 256.0, "launches": len(n)}
 
 
 def keyed_bytes(positions, edges):

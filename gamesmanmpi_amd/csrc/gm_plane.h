@@ -1069,25 +1069,46 @@ __global__ __launch_bounds__(256) void k_plane_pair(uint8_t* __restrict__ tab, c
   }
 }
 
-// Forward pass: the reach bitmap (one bit per position, plane P's row h1 is
-// the 32-bit word bits[P * 32 + h1], bit h0) and the counts.  Moves act on
-// one heap at a time and the only primitive (every heap 0) has no moves, so
-// the positions reachable from the root are the product of each heap's
-// values reachable by its own moves (x -> x-1 for x >= 1, x -> x-2 for
-// x >= 2: every value up to the start, rlim[i]).  One thread per four row
-// words of a plane (one 16-B store, the plane's digits decoded once for
-// them: 48 -> ~25 us on the 2^30 bitmap); counts per block into its
-// BlockCount slot (block_count), summed once per solve (k_fill_red).
+// Forward pass: the reach map and the counts.  Moves act on one heap at a
+// time and the only primitive (every heap 0) has no moves, so the positions
+// reachable from the root are the product of each heap's values reachable by
+// its own moves (x -> x-1 for x >= 1, x -> x-2 for x >= 2: every value up to
+// the start, rlim[i]).  A reached row (plane P, heap-1 value h1) therefore
+// holds exactly the positions h0 = 0..rlim[0], and the map keeps ONE bit per
+// row: bit h1 of the 32-bit word bits[P] (4 MiB -> 128 KiB on the 2^30
+// table; k_plane_reach 26 -> a few us).  plane_row_bits expands it back to
+// the row's 32 position bits for the readers.  One thread per plane (its
+// digits decoded once for 32 rows); counts per block into its BlockCount
+// slot (block_count), summed once per solve (k_fill_red).
+__host__ __device__ __forceinline__ uint32_t plane_row_full(const PlaneGeom& g) {
+  return g.rlim[0] >= 31 ? 0xFFFFFFFFu : ((2u << g.rlim[0]) - 1u);
+}
+
+// the position bits (bit h0) of local row (P, h1): the full row or none
+__device__ __forceinline__ uint32_t plane_row_bits(const uint32_t* __restrict__ bits, const PlaneGeom& g, uint64_t P,
+                                                   uint32_t h1) {
+  return ((bits[P] >> h1) & 1u) ? plane_row_full(g) : 0u;
+}
+
 template <int NO, class CountFn>
 __device__ __forceinline__ void plane_reach_body(uint32_t* __restrict__ bits, const PlaneGeom& g, CountFn count) {
-  const uint64_t nq = (uint64_t)g.nplanes * 8u;  // quads of row words
-  const uint32_t full = g.rlim[0] >= 31 ? 0xFFFFFFFFu : ((2u << g.rlim[0]) - 1u);
+  const uint32_t full = plane_row_full(g);
   const uint32_t c = __builtin_popcount(full), c12 = __builtin_popcount(full >> 1) + __builtin_popcount(full >> 2);
+  // rows this shard reaches in a reached plane: heap-1 values h1off + h1 <= rlim[1]
+  const uint32_t nrow = g.rlim[1] >= g.h1off ? (g.rlim[1] - g.h1off + 1u < 32u ? g.rlim[1] - g.h1off + 1u : 32u) : 0u;
+  const uint32_t rows = nrow >= 32u ? 0xFFFFFFFFu : ((1u << nrow) - 1u);
+  // edges of a reached plane's rows without the outer heaps: sum over its rows
+  // of c * min(h1 + h1off, 2) + c12
+  uint64_t e01 = 0;
+  for (uint32_t h1 = 0; h1 < nrow; h1++) {
+    const uint32_t v = h1 + g.h1off;
+    e01 += (uint64_t)c * (v < 2 ? v : 2u) + c12;
+  }
   uint64_t npos = 0, edges = 0;
-  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t P = (uint32_t)(q >> 3), h1b = ((uint32_t)q & 7u) * 4u;
+  for (uint64_t P = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; P < g.nplanes;
+       P += (uint64_t)gridDim.x * blockDim.x) {
     uint32_t dig[NO > 0 ? NO : 1];
-    plane_global_digits<NO>(g, P, dig);
+    plane_global_digits<NO>(g, (uint32_t)P, dig);
     bool in = true;
     uint32_t ext = 0;  // moves of the heaps other than heaps 0 and 1
 #pragma unroll
@@ -1095,18 +1116,11 @@ __device__ __forceinline__ void plane_reach_body(uint32_t* __restrict__ bits, co
       in = in && dig[j] <= g.rlim[2 + j];
       ext += dig[j] < 2 ? dig[j] : 2u;
     }
-    uint32_t w[4];
-#pragma unroll
-    for (uint32_t k = 0; k < 4; k++) {
-      const uint32_t h1 = h1b + k + g.h1off;  // heap 1's value (the row deal: this shard's rows)
-      const bool ink = in && h1 <= g.rlim[1];
-      w[k] = ink ? full : 0u;
-      if (ink) {
-        npos += c;
-        edges += (uint64_t)c * (ext + (h1 < 2 ? h1 : 2u)) + c12;
-      }
+    bits[P] = in ? rows : 0u;
+    if (in) {
+      npos += (uint64_t)c * nrow;
+      edges += (uint64_t)c * nrow * ext + e01;
     }
-    reinterpret_cast<uint4*>(bits)[q] = make_uint4(w[0], w[1], w[2], w[3]);
   }
   count(npos, edges);
 }

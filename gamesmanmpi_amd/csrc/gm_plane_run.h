@@ -77,7 +77,7 @@ __global__ void k_plane_query(Desc d, PlaneGeom g, const void* tab, const uint32
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
     u64 P;
     uint32_t h0, h1, e, w = NO_WORD;
-    if (plane_locate(d, g, keys[i], &P, &h0, &h1, &e) && ((bits[P * 32u + h1] >> h0) & 1u))
+    if (plane_locate(d, g, keys[i], &P, &h0, &h1, &e) && ((plane_row_bits(bits, g, P, h1) >> h0) & 1u))
       w = plane_vr<WB>(tab, P, h0, h1, e);
     out[i] = w;
   }
@@ -92,7 +92,7 @@ __global__ __launch_bounds__(1024) void k_plane_finish(Desc d, PlaneGeom g, cons
   if (threadIdx.x == 0) {
     u64 P;
     uint32_t h0, h1, e, w = NO_WORD;
-    if (plane_locate(d, g, d.root, &P, &h0, &h1, &e) && ((bits[P * 32u + h1] >> h0) & 1u))
+    if (plane_locate(d, g, d.root, &P, &h0, &h1, &e) && ((plane_row_bits(bits, g, P, h1) >> h0) & 1u))
       w = plane_vr<WB>(tab, P, h0, h1, e);
     st->root_word = w;
   }
@@ -121,7 +121,7 @@ template <int NO>
 __global__ void k_plane_positions(Desc d, PlaneGeom g, const uint32_t* bits, u64* out, u64 cap, u64* count) {
   const u64 nw = (u64)g.nplanes * 32u;
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += (u64)gridDim.x * blockDim.x) {
-    uint32_t w = bits[i];
+    uint32_t w = plane_row_bits(bits, g, i >> 5, (uint32_t)i & 31u);
     if (!w) continue;
     u64 k = atomicAdd(count, (u64)__builtin_popcount(w));
     const u64 base = plane_key<NO>(d, g, (uint32_t)(i >> 5), 0, (uint32_t)i & 31u);
@@ -137,7 +137,7 @@ __global__ __launch_bounds__(256) void k_plane_checksum(Desc d, PlaneGeom g, con
   const u64 nw = (u64)g.nplanes * 32u;
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += (u64)gridDim.x * blockDim.x) {
     const uint32_t P = (uint32_t)(i >> 5), h1 = (uint32_t)i & 31u;
-    uint32_t w = bits[i];
+    uint32_t w = plane_row_bits(bits, g, P, h1);
     if (!w) continue;
     uint32_t os;
     const u64 base = plane_key<NO>(d, g, P, 0, h1, &os);
@@ -333,7 +333,7 @@ static int plane_shape(const Desc* d, int rank, int world, uint32_t flags, Plane
   const u64 pb = 1024ull * ps->wb, hb = g.rowdeal ? 64ull * ps->wb : pb;  // halo entry: plane / two rows
   ps->words_off = 0;
   ps->bits_off = rup256(ps->nlocal * pb);
-  ps->recv_off = ps->bits_off + rup256(ps->nlocal * 128);
+  ps->recv_off = ps->bits_off + rup256(ps->nlocal * 4);  // one reach bit per row
   ps->send_off = ps->recv_off + rup256(ps->nrecv * hb);
   ps->table_bytes = ps->send_off + rup256(ps->nsend * hb);
   ps->zero_off = rup256(scratch_bytes_for(d->max_levels));
@@ -821,7 +821,7 @@ static void plane_no_dispatch(uint32_t no, F&& f) {
   }
 }
 static void plane_reach_launch(gm_solver* s, hipStream_t stream = nullptr) {
-  const u64 nq = (u64)s->pg.nplanes * 8u;  // one thread per four row words
+  const u64 nq = (u64)s->pg.nplanes;  // one thread per plane (its 32 row bits)
   const int grid = (int)std::max<u64>(1, std::min<u64>((nq + 255) / 256, (u64)std::min(s->grid, kCountSlots)));
   plane_no_dispatch(s->pg.no, [&](auto NO) {
     hipLaunchKernelGGL((k_plane_reach<decltype(NO)::value>), dim3(grid), dim3(256), 0, stream ? stream : s->stream,

@@ -130,13 +130,13 @@ def test_plan_sizes():
     assert p.table_slots == 1 << 31 and p.level_capacity >= 1 << 30
     assert p.table_bytes == 16 << 31
     # default: PLANES, one 8-bit word per position (natural rank order, no
-    # holes) + a 1-bit reach map
+    # holes) + a reach map of one bit per 32-position row
     _lib.check(_lib.load().gm_plan(s.id, 0, 0, 0, ctypes.byref(p)))
     assert p.mode == _lib.GM_MODE_PLANES
     assert p.table_slots == 1 << 30
-    assert p.table_bytes == (1 << 30) + (1 << 30) // 8
+    assert p.table_bytes == (1 << 30) + (1 << 30) // 256
     _lib.check(_lib.load().gm_plan(s.id, 0, _lib.GM_F_WORDS16, 0, ctypes.byref(p)))
-    assert p.mode == _lib.GM_MODE_PLANES and p.table_bytes == (2 << 30) + (1 << 30) // 8
+    assert p.mode == _lib.GM_MODE_PLANES and p.table_bytes == (2 << 30) + (1 << 30) // 256
     # the level-major DENSE table on request
     _lib.check(_lib.load().gm_plan(s.id, 0, _lib.GM_F_LEVEL_MAJOR, 0, ctypes.byref(p)))
     assert p.mode == _lib.GM_MODE_DENSE
@@ -202,9 +202,9 @@ def test_planes_word_width_by_root_sum(outer, bytes_per_word):
     n = 1024 * (outer + 1)
     assert p.mode == _lib.GM_MODE_PLANES and p.table_slots == n
     rup = lambda x: (x + 255) // 256 * 256  # noqa: E731
-    assert p.table_bytes == rup(bytes_per_word * n) + rup(n // 8)
+    assert p.table_bytes == rup(bytes_per_word * n) + rup(n // 256)
     _lib.check(_lib.load().gm_plan(s.id, 0, _lib.GM_F_WORDS16, 0, ctypes.byref(p)))
-    assert p.table_bytes == rup(2 * n) + rup(n // 8)
+    assert p.table_bytes == rup(2 * n) + rup(n // 256)
 
 
 @pytest.mark.parametrize("world,heaps", [(4, "31:31:31:31:31:127"), (8, "31:31:31:31:31:255")])
@@ -218,10 +218,11 @@ def test_planes_bench_shards_plan_8bit_words(world, heaps):
         p = _lib.gm_plan_t()
         _lib.check(_lib.load().gm_plan_shard(s.id, r, world, 0, 0, ctypes.byref(p)))
         assert p.mode == _lib.GM_MODE_PLANES and p.table_slots == 1 << 30
-        # 1 GiB of words + 128 MiB of reach bits + the halo slices (2 x 2^15
-        # planes each way, 8-bit): 16-bit words alone would be 2 GiB
+        # 1 GiB of words + 4 MiB of reach bits (one per row) + the halo
+        # slices (2 x 2^15 planes each way, 8-bit): 16-bit words alone would
+        # be 2 GiB
         halo = (1 << 25) * ((r > 0) + (r + 1 < world))
-        assert p.table_bytes == (1 << 30) + (1 << 27) + 2 * halo
+        assert p.table_bytes == (1 << 30) + (1 << 22) + 2 * halo
 
 
 def test_product_library_reads_no_lab_knob():
