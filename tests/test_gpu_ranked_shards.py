@@ -121,3 +121,40 @@ def test_ranked_shards_host_transport_two_processes():
         assert c == ck
         tot += owned
     assert tot == r1.positions
+
+
+def test_ranked_shards_toot_6x4_eight_shards():
+    """BASELINE config 3 at its own size on the reference's production
+    partition (run_savio.sh: md5 ranks; src/game_state.py:22-30): toot 6x4 on
+    eight md5 shards as an in-process group (all on one stream).  Every
+    shard's fingerprint equals the oracle_mt golden, the shards own and
+    resolve exactly their md5 shares, and the 220 reference-solved deep
+    positions (tests/golden/deep/toot_6x4.json) read their exact value and
+    remoteness on the shards."""
+    import json
+    from conftest import GOLDEN
+    from gamesmanmpi_amd.games import GameSpec
+    from gamesmanmpi_amd.keyed import group_keyed_solve
+    with open(os.path.join(GOLDEN, "checksums.json")) as fh:
+        e = json.load(fh)["toot_6x4"]
+    spec = GameSpec(e["game"], e["params"])
+    r, shards = group_keyed_solve(spec, 8, layout="ranked", streams="one")
+    assert r.extra["layout"] == "ranked" and r.extra["partition"] == "md5"
+    assert (r.positions, r.edges, r.primitives, r.root_line) == (e["positions"], e["edges"], e["primitives"],
+                                                                  e["root_line"])
+    for sh in (shards[0], shards[5]):
+        assert sh.checksum()["checksum"] == e["checksum"]
+    stats = [sh.shard_stats() for sh in shards]
+    assert all(res == own for res, own in stats)
+    assert sum(own for _, own in stats) == e["positions"]
+    with open(os.path.join(GOLDEN, "deep", "toot_6x4.json")) as fh:
+        deep = json.load(fh)["rows"]
+    keys = np.array([spec.encode(bytes.fromhex(row["pos"])) for row in deep], np.uint64)
+    own = _owners(spec, keys, 8)
+    for g in (0, 3, 7):
+        w = shards[g].query(keys)
+        for i, row in enumerate(deep):
+            assert (int(w[i]) & 3, int(w[i]) >> 2) == (row["value"], row["remoteness"]), (g, row)
+    # the deep positions spread over the shards' md5 shares
+    assert len(set(own.tolist())) == 8
+    del shards
