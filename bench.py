@@ -564,7 +564,10 @@ def main():
                           layout, "SURVEY 8d keyed: expand 24 B/position + 8 B/edge, resolve 12 B/position + "
                                   "12 B/edge")),
             "timing": ("HIP events on the solve stream in an extra solve of the same launch schedule: "
-                       + ("one event pair around the whole backward (nothing but its %d resolve launches: "
+                       + ("one event pair around the whole backward, ONE launch of k_plane_flow (every plane "
+                          "level; planes wait for their neighbours by ready flags, gm_plane.h)"
+                          if layout == "planes" and world == 1 and kname == "k_plane_flow" else
+                          "one event pair around the whole backward (nothing but its %d resolve launches: "
                           "grid-wide k_plane_resolve* for wide plane levels, one-workgroup k_plane_run for runs "
                           "of narrow ones), average = span / launches" % kn if layout == "planes" and world == 1
                           else "one event pair around this rank's whole staged backward (%d launches over its "

@@ -33,15 +33,16 @@ GM_F_PLANE_LEVEL_SYNC = 4096  # PLANES shards A/B: level-synchronous deal instea
 GM_F_PLANE_NO_RUNS = 8192  # PLANES A/B: no one-workgroup runs of narrow levels / keys
 GM_F_BKS_LOCAL = 16384  # md5-sharded bucketed: local dedup before hashing / sending
 GM_F_RANKED_SHARD = 32768  # gm_plan_keyed_shard: md5 shards of the RANKED layout (toot-and-otto)
+GM_F_PLANE_LEVELS = 65536  # PLANES A/B: per-level launches instead of the one-launch backward (k_plane_flow)
 KERNEL_FLAGS = (GM_F_WORDS32 | GM_F_RESOLVE_SCALAR | GM_F_SHARD_INORDER | GM_F_WORDS16 | GM_F_BK_EXACT
                 | GM_F_GRAPH | GM_F_LEVEL_MAJOR | GM_F_PLANE_X1 | GM_F_PLANE_ROUND_ROBIN
-                | GM_F_PLANE_LEVEL_SYNC | GM_F_PLANE_NO_RUNS
+                | GM_F_PLANE_LEVEL_SYNC | GM_F_PLANE_NO_RUNS | GM_F_PLANE_LEVELS
                 | GM_F_BKS_LOCAL)
 # gm_result.kernels codes (gm_solver.hip DenseResolveKind / DensePullKind)
 RESOLVE_KERNELS = {1: "k_dense_resolve8p", 2: "k_dense_resolve8c", 3: "k_dense_resolve4p",
                    4: "k_dense_resolve4c", 5: "k_dense_resolve4", 6: "k_dense_resolve",
                    7: "k_dense_resolve16p", 8: "k_plane_resolve", 9: "k_plane_resolve_x2",
-                   10: "k_rk_backward"}
+                   10: "k_rk_backward", 11: "k_plane_flow"}
 PULL_KERNELS = {1: "k_dense_pull_words", 2: "k_dense_pull", 3: "k_plane_reach"}
 GM_MODE_HASHED, GM_MODE_DENSE, GM_MODE_BUCKETED, GM_MODE_PLANES, GM_MODE_RANKED = 0, 1, 2, 3, 4
 # host-staged transport (include/gamesman.h gm_xfer_fn)

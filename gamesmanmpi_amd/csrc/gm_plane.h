@@ -835,6 +835,129 @@ __global__ __launch_bounds__(256) void k_plane_resolve_x2(typename PlaneWord<WB>
   plane_keep(v);
 }
 
+// The one-table backward as ONE launch (round 6, the default for one-table
+// 8-bit absolute solves): every plane level in it, a plane resolved as soon
+// as its neighbours are final instead of at a kernel boundary per level.
+//   Items: a wave visit of four planes.  Every level's visits are cut into 8
+// contiguous chunks (XCD x's waves, blockIdx % 8 == x, take chunk x: the
+// per-level launches' plane_share locality) and each chunk is dealt round
+// robin over the XCD's kPlaneFlowSeq sequences; a sequence holds its visits
+// level after level, and its waves take them by ticket (one device counter
+// per sequence, each on a line of its own).  Deadlock-free for any grid: a
+// wave waits only for planes of lower levels, every taken visit is held by a
+// wave that runs, and the lowest unfinished visit's neighbours are final.
+//   Hand-off: a visit stores its rows write-through (sc1, the per-level
+// launches' stores), drains them (s_waitcnt vmcnt(0)), then sets its planes'
+// flags to the solve's epoch (relaxed device-scope stores).  A plane waits
+// for the flags of its four k = 1 neighbours only: its k = 2 neighbour along
+// digit j is the k = 1 neighbour of its k = 1 neighbour along j, final
+// before that one started.  The neighbour rows then come through PLAIN
+// loads: a plane's lines (1 KiB, 8 lines of its own) are first read only
+// after its flag is set, so no L1 or L2 holds an older copy of them within
+// the launch (the launch's acquire cleared what the previous solve left).
+//   Exit: a wave that finds its sequence empty leaves; a wave that waits past
+// kPlaneFlowSpin polls sets the give-up word and ERR bit `stall` and leaves
+// (every other wave sees the word and leaves: the launch always drains).
+// The last wave out resets the counters and the give-up word for the next
+// solve.  tools/flow2_lab.hip: 1.06-1.09 vs 1.34 ms per 2^30 backward for
+// the same visits launched per level, byte-exact on a poisoned table
+// (profiles/r06/flow2_lab.txt).
+constexpr uint32_t kPlaneFlowSeq = 8;      // ticket sequences per XCD
+constexpr uint32_t kPlaneFlowQ = 8 * kPlaneFlowSeq;
+constexpr uint32_t kPlaneFlowLine = 64;    // u32 per counter line
+constexpr uint32_t kPlaneFlowSpin = 1u << 20;
+constexpr uint32_t kPlaneFlowBlocksPerCU = 3;
+struct PlaneFlow {
+  const uint32_t* items;  // visits: 4 planes each (kPlaneAbsent pads), sequence after sequence
+  const uint32_t* qoff;   // [kPlaneFlowQ + 1]: first visit of each sequence
+  uint32_t* ctr;          // [kPlaneFlowQ + 2] lines: tickets, then the exit count and the give-up word
+  uint32_t* flags;        // per plane: the epoch of the solve that finished it
+  uint32_t* err;          // DevState::err
+  uint32_t epoch, stall;
+  uint32_t skip;  // (the lab build's fault injector, GM_FAULT_FLOW: this plane's flag is never set; else kPlaneAbsent)
+  uint32_t mode;  // (lab A/B, GM_PLANE_FLOW_MODE: 1 agent release fence before the flags, 4 agent acquire after the polls)
+};
+typedef __attribute__((address_space(1))) uint32_t plane_gu32;
+__device__ __forceinline__ uint32_t plane_flow_ld(uint32_t* p) {
+  return __hip_atomic_load((plane_gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void plane_flow_st(uint32_t* p, uint32_t v) {
+  __hip_atomic_store((plane_gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <int NO>
+__global__ __launch_bounds__(256) void k_plane_flow(uint8_t* __restrict__ tab, PlaneGeom g,
+                                                    const uint4* __restrict__ zero, PlaneFlow f) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t q = (blockIdx.x & 7u) + 8u * ((blockIdx.x >> 3) % kPlaneFlowSeq);
+  const uint32_t base = f.qoff[q], n = f.qoff[q + 1] - base;
+  uint32_t* const c = f.ctr + kPlaneFlowLine * q;
+  uint32_t* const nout = f.ctr + kPlaneFlowLine * kPlaneFlowQ;
+  uint32_t* const gave = nout + kPlaneFlowLine;
+  uint32_t t = 0;
+  if (lane == 0) t = atomicAdd(c, 1u);
+  t = __builtin_amdgcn_readfirstlane(__shfl(t, 0));
+  while (t < n) {
+    uint32_t tn = 0;  // the next ticket, in flight during this visit
+    if (lane == 0) tn = atomicAdd(c, 1u);
+    const uint32_t* ip = f.items + (size_t)(base + t) * 4u;
+    // lane l < 4 NO waits for the k = 1 neighbour along digit l % NO of plane l / NO
+    uint32_t nbp = kPlaneAbsent;
+    if (NO > 0 && lane < 4u * NO) {
+      const uint32_t pq = ip[lane / (NO > 0 ? NO : 1)], j = lane % (NO > 0 ? NO : 1);
+      uint32_t dg[NO > 0 ? NO : 1];
+      if (pq != kPlaneAbsent) {
+        plane_digits<NO>(g, pq, dg);
+#pragma unroll
+        for (int i = 0; i < NO; i++)
+          if ((uint32_t)i == j && dg[i] >= 1u) nbp = pq - g.stride[i];
+      }
+    }
+    bool ok = nbp == kPlaneAbsent;
+    for (uint32_t spins = 0;; spins++) {
+      if (!ok) ok = plane_flow_ld(f.flags + nbp) == f.epoch;
+      if (__all(ok)) break;
+      if (spins >= kPlaneFlowSpin || plane_flow_ld(gave)) {
+        if (lane == 0) {
+          plane_flow_st(gave, 1u);
+          atomicOr(f.err, f.stall);
+        }
+        t = n;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(4);
+    }
+    if (t >= n) break;
+    if (f.mode & 4u) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    // the polls complete before anything below issues, and no load below
+    // may be moved above them (a compiler barrier, not only a hardware wait)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t p0 = ip[0];
+    PlaneEntry ex, ey;
+    ex.p = ip[2 * (lane >> 5)];
+    ey.p = ip[2 * (lane >> 5) + 1];
+    const bool livex = ex.p != kPlaneAbsent, livey = ey.p != kPlaneAbsent;
+    if (!livex) ex.p = p0;
+    if (!livey) ey.p = p0;
+    plane_x2_visit<1, NO, false, 0, true, true>(tab, g, zero, nullptr, nullptr, ex, ey, livex, livey);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every lane's rows written through before any flag
+    if (f.mode & 1u) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if ((lane & 31) < 2) {
+      const bool live = (lane & 1) ? livey : livex;
+      const uint32_t p = (lane & 1) ? ey.p : ex.p;
+      if (live && p != f.skip) plane_flow_st(f.flags + p, f.epoch);
+    }
+    t = __builtin_amdgcn_readfirstlane(__shfl(tn, 0));
+  }
+  if (lane == 0) {  // the last wave out resets the counters for the next solve
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    if (atomicAdd(nout, 1u) == waves - 1u) {
+      for (uint32_t i = 0; i < kPlaneFlowQ; i++) plane_flow_st(f.ctr + kPlaneFlowLine * i, 0u);
+      plane_flow_st(gave, 0u);
+      plane_flow_st(nout, 0u);
+    }
+  }
+}
+
 // A run of narrow plane levels (or staged keys) in ONE workgroup: the
 // groups [off[i], off[i + 1]) one after another, a workgroup barrier
 // between them.  One CU suffices for a group of a few dozen planes, and the

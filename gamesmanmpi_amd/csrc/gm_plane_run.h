@@ -193,6 +193,10 @@ struct PlaneShape {
   u64 nrecv, nsend;      // halo planes of this shard (all levels)
   u64 words_off, bits_off, recv_off, send_off, table_bytes;  // table buffer layout
   u64 zero_off, list_off, scratch_bytes;                      // scratch layout
+  // the one-launch backward (k_plane_flow): one-table 8-bit absolute forms;
+  // scratch: visits, sequence offsets, counter lines, per-plane flags
+  bool flow;
+  u64 flow_off, flow_qoff_off, flow_ctr_off, flow_flags_off;
   // the staged deal (shards; 0: level-synchronous): key skew k, keys, rows
   uint32_t stage_k, nkeys, nrows;
 };
@@ -340,6 +344,14 @@ static int plane_shape(const Desc* d, int rank, int world, uint32_t flags, Plane
   ps->list_off = ps->zero_off + 4096;
   ps->scratch_bytes =
       ps->list_off + rup256((ps->nlocal + plane_stage_pad(ps)) * (world > 1 && !g.rowdeal ? sizeof(PlaneEntry) : 4));
+  ps->flow = world <= 1 && ps->form == 1 && g.no >= 1;
+  if (ps->flow) {  // visits: every level padded to whole visits of 4 planes
+    ps->flow_off = ps->scratch_bytes;
+    ps->flow_qoff_off = ps->flow_off + rup256((ps->nlocal + 3ull * (ps->S + 1)) * 4);
+    ps->flow_ctr_off = ps->flow_qoff_off + rup256((kPlaneFlowQ + 1) * 4);
+    ps->flow_flags_off = ps->flow_ctr_off + rup256((u64)kPlaneFlowLine * (kPlaneFlowQ + 2) * 4);
+    ps->scratch_bytes = ps->flow_flags_off + rup256(ps->nlocal * 4);
+  }
   return 0;
 }
 
@@ -590,6 +602,9 @@ static int plane_lists(gm_solver* s, const PlaneShape& ps, std::vector<uint8_t>&
   return 0;
 }
 
+template <class F>
+static void plane_no_dispatch(uint32_t no, F&& f);
+
 // solver set-up for PLANES buffers (gm_solver_create_shard)
 static int plane_setup(gm_solver* s, const gm_buffers* buf) {
   PlaneShape ps;
@@ -621,6 +636,56 @@ static int plane_setup(gm_solver* s, const gm_buffers* buf) {
   if (rc) return rc;
   HIPCHK(hipMemset((void*)s->pzero, 0, 4096));
   HIPCHK(hipMemcpy((void*)s->plist, lb.data(), lb.size(), hipMemcpyHostToDevice));
+  s->pflow_ok = false;
+  if (ps.flow) {
+    // k_plane_flow's visits (gm_plane.h): each level's planes in list order,
+    // padded to whole visits; the level's visits cut into 8 contiguous XCD
+    // chunks, a chunk dealt round robin over its XCD's sequences
+    const uint32_t* L = (const uint32_t*)lb.data();
+    std::vector<std::vector<uint32_t>> qv(kPlaneFlowQ);
+    for (uint32_t l = 0; l <= ps.S; l++) {
+      std::vector<uint32_t> v(L + s->ploff[l], L + s->ploff[(size_t)l + 1]);
+      while (v.size() % 4) v.push_back(kPlaneAbsent);
+      const u64 nv = v.size() / 4, chunk = (nv + 7) / 8;
+      for (u64 x = 0; x < 8; x++)
+        for (u64 i = x * chunk; i < std::min(nv, (x + 1) * chunk); i++) {
+          auto& q = qv[x + 8 * ((i - x * chunk) % kPlaneFlowSeq)];
+          q.insert(q.end(), v.begin() + 4 * i, v.begin() + 4 * i + 4);
+        }
+    }
+    std::vector<uint32_t> items, qoff(kPlaneFlowQ + 1, 0);
+    for (uint32_t q = 0; q < kPlaneFlowQ; q++) {
+      qoff[q + 1] = qoff[q] + (uint32_t)(qv[q].size() / 4);
+      items.insert(items.end(), qv[q].begin(), qv[q].end());
+    }
+    if (items.size() > ps.nlocal + 3ull * (ps.S + 1)) return fail(GM_ECORRUPT, "plane flow: %zu visit entries", items.size());
+    PlaneFlow& f = s->pflow;
+    f.items = (const uint32_t*)(sc + ps.flow_off);
+    f.qoff = (const uint32_t*)(sc + ps.flow_qoff_off);
+    f.ctr = (uint32_t*)(sc + ps.flow_ctr_off);
+    f.flags = (uint32_t*)(sc + ps.flow_flags_off);
+    f.err = &s->st->err;
+    f.epoch = 0;
+    f.stall = ERR_PLANE_STALL;
+    f.skip = kPlaneAbsent;
+    f.mode = 0;
+    HIPCHK(hipMemcpy((void*)f.items, items.data(), items.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy((void*)f.qoff, qoff.data(), qoff.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(f.ctr, 0, (size_t)kPlaneFlowLine * (kPlaneFlowQ + 2) * 4));
+    HIPCHK(hipMemset(f.flags, 0, ps.nlocal * 4));
+    // the grid: kPlaneFlowBlocksPerCU workgroups per CU (at most what the
+    // CU holds at once -- every workgroup resident), whole rounds of the 64
+    // sequences
+    int occ = 0;
+    plane_no_dispatch(ps.g.no, [&](auto NO) {
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_plane_flow<decltype(NO)::value>, 256, 0) != hipSuccess)
+        occ = 0;
+    });
+    const u64 cus = (u64)launch_grid() / 8;
+    const u64 blocks = cus * std::min<u64>(kPlaneFlowBlocksPerCU, (u64)std::max(occ, 0)) / kPlaneFlowQ * kPlaneFlowQ;
+    s->pflow_grid = (uint32_t)blocks;
+    s->pflow_ok = blocks >= kPlaneFlowQ;
+  }
   s->w8 = ps.wb == 1;  // (the dense flags; the planes paths read pform)
   s->w16 = ps.wb == 2;
   return 0;
@@ -1337,7 +1402,7 @@ static int plane_result(const std::vector<gm_solver*>& ss, const u64* red, gm_re
   out->levels = (uint32_t)s0->d.max_levels;
   out->max_level_width = 0;
   out->word_bits = 8 * s0->pwb;
-  out->kernels = (plane_x1(s0) ? RK_PLANE : RK_PLANE_X2) | (PK_PLANE << 16);
+  out->kernels = (plane_x1(s0) ? RK_PLANE : s0->pflow_last ? RK_PLANE_FLOW : RK_PLANE_X2) | (PK_PLANE << 16);
   const uint32_t word = red[3] ? (uint32_t)(red[3] - 1) : NO_WORD;
   out->root_word = word;
   if (red[4]) {
@@ -1469,8 +1534,19 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out, bool async) {
     const char* e = lab_env("GM_PLANE_FWD");
     return e ? atoi(e) : 0;
   }();
+  // one table, whole solve: the backward as ONE launch (k_plane_flow,
+  // gm_plane.h) -- GM_F_PLANE_LEVELS keeps the per-level launches (A/B; lab
+  // knob GM_PLANE_FLOW=0 too), and partial / resumed solves take them
+  static const bool flow_knob = [] {
+    const char* e = lab_env("GM_PLANE_FLOW");
+    return !(e && atoi(e) == 0);
+  }();
+  const bool flow = mode == 0 && s0->pflow_ok && first == 0 && stop == 2 * T && flow_knob &&
+                    !(s0->flags & (GM_F_PLANE_LEVELS | GM_F_PLANE_X1));
+  // (the one-launch backward runs after the forward on the solve stream:
+  // the forward's state reset must not race its error bit)
   const bool overlap = mode == 0 && first == 0 && stop == 2 * T && !timing && fwd_mode != 1 &&
-                       (!async || fwd_mode >= 2);
+                       (!async || fwd_mode >= 2) && !flow;
   uint32_t fwd_at = 0;  // the level whose launch the side-stream forward is enqueued after
   if (overlap && fwd_mode == 3) {
     uint32_t pk = 0;
@@ -1560,6 +1636,26 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out, bool async) {
     return e && atoi(e) == 1;
   }();
   u64 nlaunch = 0;        // resolve launches of this solve (shard 0's)
+  s0->pflow_last = flow;
+  if (flow) {
+    if (timing) HIPCHK(hipEventRecord(kr[0], st));
+    PlaneFlow f = s0->pflow;
+    f.skip = kPlaneAbsent;
+    if (const char* e = lab_env("GM_FAULT_FLOW")) f.skip = (uint32_t)atoi(e);  // (read per solve)
+    f.mode = 0;
+    if (const char* e = lab_env("GM_PLANE_FLOW_MODE")) f.mode = (uint32_t)atoi(e);
+    f.epoch = ++s0->pflow.epoch;
+    if (f.epoch == 0) {  // (2^32 solves: the flags start over)
+      HIPCHK(hipMemsetAsync(f.flags, 0, (size_t)s0->pg.nplanes * 4, st));
+      f.epoch = s0->pflow.epoch = 1;
+    }
+    plane_no_dispatch(s0->pg.no, [&](auto NO) {
+      hipLaunchKernelGGL((k_plane_flow<decltype(NO)::value>), dim3(s0->pflow_grid), dim3(256), 0, st,
+                         (uint8_t*)s0->ptab, s0->pg, s0->pzero, f);
+    });
+    nlaunch = 1;
+    if (timing) HIPCHK(hipEventRecord(kr[2 * (size_t)S + 1], st));
+  }
   if (staged && stop == 2 * T) {
     if (timing) HIPCHK(hipEventRecord(kr[0], st));
     int rc = plane_backward_staged(ss, mode, st, &nlaunch);
@@ -1570,7 +1666,7 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out, bool async) {
     if (timing && join()) return GM_EHIP;
     if (timing) HIPCHK(hipEventRecord(kr[2 * (size_t)S + 1], st));
   }
-  for (uint32_t l = 0; l <= S && !staged; l++) {
+  for (uint32_t l = 0; l <= S && !staged && !flow; l++) {
     const int k = T + (int)l;
     if (k < first) continue;
     if (k >= stop) break;
@@ -1627,7 +1723,7 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out, bool async) {
     const int rc = issue_forward();
     if (rc) return rc;
   }
-  if (!staged) nlaunch = mode == 0 && !per_level ? bat0.launches : (u64)(S + 1) * (pipe ? 2 : 1);
+  if (!staged && !flow) nlaunch = mode == 0 && !per_level ? bat0.launches : (u64)(S + 1) * (pipe ? 2 : 1);
   if (last_x >= 0) HIPCHK(hipStreamWaitEvent(st, PE[S + 1 + last_x], 0));  // join the comm stream
   {
     const hipError_t e = hipGetLastError();  // (a failed launch of the backward)

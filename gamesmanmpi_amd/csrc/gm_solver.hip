@@ -130,6 +130,9 @@ enum : uint32_t {
   // halo transfers so that its peers finished, then reported through the
   // end-of-solve reduction; gm_plane_run.h plane_backward_staged)
   ERR_SHARD_FAILED = 512u,
+  // the one-launch PLANES backward (k_plane_flow) gave up waiting for a
+  // neighbour plane: the launch drained, the words are incomplete
+  ERR_PLANE_STALL = 1024u,
 };
 
 // ---------------------------------------------------------------------------
@@ -981,6 +984,7 @@ enum DenseResolveKind : uint32_t {
   RK_PLANE = 8,      // k_plane_resolve: PLANES layout (gm_plane.h), one plane per half-wave
   RK_PLANE_X2 = 9,   // k_plane_resolve_x2: two planes per half-wave, packed 16-bit lanes
   RK_RANKED = 10,    // k_rk_backward: RANKED layout (gm_ranked.h)
+  RK_PLANE_FLOW = 11,  // k_plane_flow: the one-launch PLANES backward (gm_plane.h)
 };
 enum DensePullKind : uint32_t { PK_NONE = 0, PK_WORDS = 1, PK_LANE = 2, PK_PLANE = 3 };
 
@@ -1096,6 +1100,12 @@ struct gm_solver {
   std::vector<u64> ploff;        // per level: first list entry
   std::vector<u64> pbnd;         // shards, per level: first entry that reads a halo plane (they come last)
   std::vector<u64> prcv_off, psnd_off;  // shards, per level: first halo plane received / sent
+  // the one-launch backward (k_plane_flow; one-table 8-bit absolute solves):
+  // visit lists, counters and per-plane flags in the scratch buffer
+  PlaneFlow pflow{};
+  bool pflow_ok = false;
+  bool pflow_last = false;  // the last solve's backward was k_plane_flow
+  uint32_t pflow_grid = 0;
   // staged PLANES shards (run_planes_staged): ploff / prcv_off / psnd_off are
   // per key / per row; k = key skew, K keys, rows 0..smax
   uint32_t pstage_k = 0, pkeys = 0, prows = 0;
@@ -1418,6 +1428,7 @@ static std::string err_text(uint32_t e) {
   if (e & ERR_BUCKET_FULL) s += " hash-bucket-over-capacity";
   if (e & ERR_EDGE_COUNT) s += " edge-count-mismatch";
   if (e & ERR_SHARD_FAILED) s += " shard-failed";
+  if (e & ERR_PLANE_STALL) s += " plane-flow-stalled";
   return s;
 }
 

@@ -160,6 +160,11 @@ typedef struct gm_buffers {
                                   slot resolved by its md5 owner, level words
                                   exchanged; gm_ranked_shard.h) instead of
                                   BUCKETED levels */
+#define GM_F_PLANE_LEVELS 65536u /* PLANES one-table solves: one launch per
+                                  plane level (narrow levels in runs and
+                                  pairs) instead of the one-launch backward
+                                  (k_plane_flow; A/B, and the schedule of
+                                  partial / resumed solves) */
 #define GM_F_GRAPH 256u      /* dense one-table full solves: capture the
                                   forward and backward launches as HIP graphs
                                   on the first solve, replay them after

@@ -232,7 +232,8 @@ def test_product_library_reads_no_lab_knob():
     libgamesman_hip_lab.so): the shipped library does not even hold their
     names, so no environment can select them."""
     knobs = [b"GM_RK_DBG", b"GM_RK_ORDER", b"GM_RK_SLICED", b"GM_FAULT_STAGED", b"GM_PLANE_STAGE_K",
-             b"GM_PLANE_GRAPH", b"GM_PLANE_SPIN", b"GM_PLANE_FWD_FIRST"]
+             b"GM_PLANE_GRAPH", b"GM_PLANE_SPIN", b"GM_PLANE_FWD_FIRST", b"GM_PLANE_FWD", b"GM_PLANE_FLOW",
+             b"GM_FAULT_FLOW", b"GM_PLANE_PAIR_RUNS", b"GM_PLANE_PAIR_MAX"]
     with open(os.path.join(ROOT, "gamesmanmpi_amd", "libgamesman_hip.so"), "rb") as f:
         prod = f.read()
     for k in knobs:

@@ -40,15 +40,23 @@ def _oracle_words(sol, n):
     return np.array([sol.word(k) for k in range(n)], np.uint32)
 
 
+LEVELS = 65536  # GM_F_PLANE_LEVELS: one launch per plane level instead of the one-launch backward
+
+
+@pytest.mark.parametrize("flags", [0, LEVELS])
 @pytest.mark.parametrize("params", ["heaps=31:31", "heaps=31:31:1", "heaps=31:31:3", "heaps=31:31:2:5",
                                     "heaps=31:31:4:0:2", "heaps=31:31:7:7"])
-def test_planes_match_oracle(params):
+def test_planes_match_oracle(params, flags):
     """Every position's value and remoteness (and the counts / root line)
     equal the oracle's, including non-power-of-two and zero-height outer
-    heaps and the plane-less K = 2 shape."""
-    s, r = _planes(params)
+    heaps and the plane-less K = 2 shape -- on the one-launch backward
+    (k_plane_flow, the default with outer heaps) and on one launch per plane
+    level (GM_F_PLANE_LEVELS)."""
+    s, r = _planes(params, flags=flags)
     sol = _oracle(params)
-    assert r.extra["layout"] == "planes" and r.extra["resolve_kernel"] == "k_plane_resolve_x2"  # 8-bit words
+    flow = params != "heaps=31:31" and not flags
+    assert r.extra["layout"] == "planes" and r.extra["resolve_kernel"] == (
+        "k_plane_flow" if flow else "k_plane_resolve_x2")  # 8-bit words
     assert (r.positions, r.edges, r.primitives, r.root_line) == (sol.count, sol.edges, sol.stats["primitives"],
                                                                   sol.root_line)
     keys, val, rem = s.dump()
@@ -62,14 +70,18 @@ def test_planes_match_oracle(params):
                                                        sol.stats["loss"])
 
 
+@pytest.mark.parametrize("flags", [LEVELS, 0])
 @pytest.mark.parametrize("params", ["heaps=31:31:7:7:7:7", "heaps=31:31:15:15:15"])
-def test_planes_level_pairs_match_oracle(params):
-    """Shapes whose narrow plane levels go through k_plane_pair (two levels
-    per launch, the level-s planes resolved redundantly by their level-(s+1)
-    parents and stored by one): four and three outer digits of power-of-two
-    bases, levels of 33..1200 planes paired -- counts, root, whole-table
-    fingerprint and 20,000 sampled words equal the oracle's."""
-    s, r = _planes(params)
+def test_planes_level_pairs_match_oracle(params, flags):
+    """Shapes whose narrow plane levels go through k_plane_pair in the
+    per-level schedule (GM_F_PLANE_LEVELS: two levels per launch, the level-s
+    planes resolved redundantly by their level-(s+1) parents and stored by
+    one): four and three outer digits of power-of-two bases, levels of
+    33..1200 planes paired; and the same shapes on the one-launch backward --
+    counts, root, whole-table fingerprint and 20,000 sampled words equal the
+    oracle's."""
+    s, r = _planes(params, flags=flags)
+    assert r.extra["resolve_kernel"] == ("k_plane_resolve_x2" if flags else "k_plane_flow")
     sol = _oracle(params)
     assert r.extra["layout"] == "planes"
     assert (r.positions, r.edges, r.primitives, r.root_line) == (sol.count, sol.edges, sol.stats["primitives"],
@@ -95,7 +107,7 @@ def test_planes_kernel_families_agree():
     s1, r1 = _planes(params, flags=_lib.GM_F_PLANE_X1)
     assert (r8.extra["word_bits"], r16.extra["word_bits"], r1.extra["word_bits"]) == (8, 16, 8)
     assert (r8.extra["resolve_kernel"], r16.extra["resolve_kernel"], r1.extra["resolve_kernel"]) == (
-        "k_plane_resolve_x2", "k_plane_resolve", "k_plane_resolve")
+        "k_plane_flow", "k_plane_resolve", "k_plane_resolve")
     assert r8.root_line == r16.root_line == r1.root_line
     keys = np.arange(32 * 32 * 16 * 16, dtype=np.uint64)
     w = s8.query(keys)
@@ -144,13 +156,18 @@ def _check_gold(e, r, cks):
     assert (sum(c["win"] for c in cks), sum(c["loss"] for c in cks)) == (e["win"], e["loss"])
 
 
-def test_planes_sum_31x6_checksum():
+@pytest.mark.parametrize("flags", [0, LEVELS])
+def test_planes_sum_31x6_checksum(flags):
     """BASELINE config 4, the bench shape (2^30 positions): every position's
-    value and remoteness by fingerprint against the CPU restatement."""
+    value and remoteness by fingerprint against the CPU restatement -- the
+    one-launch backward (the bench's) and the per-level launches."""
     e = _gold("sum_31x6")
-    s, r = _planes(e["params"])
+    s, r = _planes(e["params"], flags=flags)
     assert r.extra["word_bits"] == 8
+    assert r.extra["resolve_kernel"] == ("k_plane_resolve_x2" if flags else "k_plane_flow")
     _check_gold(e, r, [s.checksum()])
+    r2 = s.solve()  # again on the same table: the flags' epochs and the ticket counters start over
+    _check_gold(e, r2, [s.checksum()])
 
 
 LS, RR = 4096, 2048  # GM_F_PLANE_LEVEL_SYNC, GM_F_PLANE_ROUND_ROBIN
@@ -248,7 +265,7 @@ def test_planes_group_pipelined_equals_in_order(world):
         np.testing.assert_array_equal(a.query(keys), b.query(keys))
 
 
-@pytest.mark.parametrize("flags", [0, 64, 1024])  # 8-bit packed, 16-bit, one plane per half-wave
+@pytest.mark.parametrize("flags", [LEVELS, 64, 1024])  # 8-bit packed, 16-bit, one plane per half-wave
 def test_planes_runs_equal_single_launches(flags):
     """Narrow plane levels run as one-workgroup runs (k_plane_run, a
     barrier between levels) give the words of one grid launch per level

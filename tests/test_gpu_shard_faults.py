@@ -141,3 +141,55 @@ def test_host_transport_fault_every_rank_returns():
         assert secs < LIMIT_S
     assert "injected fault: shard 1" in out[1][2]
     assert "shard-failed" in out[0][2]
+
+
+_FLOW_CHILD = """
+import json, os, sys, time
+sys.path.insert(0, %(root)r)
+from gamesmanmpi_amd import _lib
+from gamesmanmpi_amd.games import GameSpec
+from gamesmanmpi_amd.solver import Solver
+s = Solver(GameSpec("sum_four_to_one", %(params)r), layout="planes")
+t0 = time.time()
+try:
+    s.solve()
+    out = {"rc": 0, "msg": ""}
+except _lib.GmError as e:
+    out = {"rc": e.code, "msg": str(e)}
+out["secs"] = time.time() - t0
+os.environ.pop("GM_FAULT_FLOW", None)  # (read per solve) the same solver again, no fault
+r = s.solve()
+out["again"] = r.root_line
+out["kernel"] = r.extra["resolve_kernel"]
+out["checksum"] = s.checksum()["checksum"]
+print(json.dumps(out))
+"""
+
+
+def test_flow_backward_stall_returns():
+    """The one-launch PLANES backward (k_plane_flow) when a plane never
+    becomes final (GM_FAULT_FLOW: the lab build skips that plane's ready
+    flag): every wave waiting on it gives up after a bounded wait, the launch
+    drains, and the solve fails with "plane-flow-stalled" instead of hanging
+    the GPU; the same solver then solves again to the right fingerprint (the
+    last wave out reset the ticket counters, the next solve's epoch ignores
+    the stale flags)."""
+    import subprocess
+    import sys
+    params = "heaps=31:31:7:7:7:7"
+    from gamesmanmpi_amd.games import GameSpec
+    from gamesmanmpi_amd.solver import Solver
+    s = Solver(GameSpec("sum_four_to_one", params), layout="planes")
+    r = s.solve()
+    want = (r.root_line, s.checksum()["checksum"])
+    del s
+    code = _FLOW_CHILD % {"root": ROOT, "params": params}
+    env = dict(os.environ, GM_LIBPATH=LAB, GM_FAULT_FLOW=str(3 + 8 * 5 + 64 * 2))  # a plane of level 10
+    p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=LIMIT_S + 120, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert out["rc"] != 0 and "plane-flow-stalled" in out["msg"], out
+    assert out["secs"] < LIMIT_S, out
+    assert out["kernel"] == "k_plane_flow"
+    assert (out["again"], out["checksum"]) == want, out

@@ -29,7 +29,10 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/flow_lab.hip -o tools/flow_lab
 //   ./tools/flow_lab K variant [reps] [blocks_per_cu]
 // variants: 0 product launches (k_plane_resolve_x2, per level); 1 flow, sc1
-// loads; 2 flow, sc0|sc1 loads; 3 flow, plain loads behind an agent acquire
+// loads; 2 flow, sc0|sc1 loads; 3 flow, plain loads behind an agent acquire;
+// 9 flow, plain buffer loads and NO acquire (round 6: a line is first read
+// only after its plane's flag is set, so no L1/L2 can hold a stale copy of it
+// -- checked empirically on the poisoned table, every rep)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -349,6 +352,7 @@ int main(int argc, char** argv) {
       if (v == 1) hipLaunchKernelGGL((k_flow<NO, 1>), dim3(blocks), dim3(256), 0, st, tab, ditems, nitems, W, flags, tmo, g, (const uint4*)zero, (uint32_t)tbytes, (uint64_t*)nullptr);
       else if (v == 4) hipLaunchKernelGGL((k_flow<NO, 1, 0>), dim3(blocks), dim3(256), 0, st, tab, ditems, nitems, W, flags, tmo, g, (const uint4*)zero, (uint32_t)tbytes, (uint64_t*)nullptr);
       else if (v == 5) hipLaunchKernelGGL((k_flow<NO, 1, 1, true>), dim3(blocks), dim3(256), 0, st, tab, ditems, nitems, W, flags, tmo, g, (const uint4*)zero, (uint32_t)tbytes, dstamps);
+      else if (v == 9) hipLaunchKernelGGL((k_flow<NO, 0>), dim3(blocks), dim3(256), 0, st, tab, ditems, nitems, W, flags, tmo, g, (const uint4*)zero, (uint32_t)tbytes, (uint64_t*)nullptr);
       else if (v == 2) hipLaunchKernelGGL((k_flow<NO, 2>), dim3(blocks), dim3(256), 0, st, tab, ditems, nitems, W, flags, tmo, g, (const uint4*)zero, (uint32_t)tbytes, (uint64_t*)nullptr);
       else hipLaunchKernelGGL((k_flow<NO, 3>), dim3(blocks), dim3(256), 0, st, tab, ditems, nitems, W, flags, tmo, g, (const uint4*)zero, (uint32_t)tbytes, (uint64_t*)nullptr);
     };
@@ -362,7 +366,11 @@ int main(int argc, char** argv) {
   printf("flow_lab K=%d var %d: %llu planes, %d levels, %u items, grid %u blocks (%d per CU, occupancy API %d), %u waves\n", K,
          var, (unsigned long long)np, S + 1, nitems, blocks, per_cu, occ, W);
   fflush(stdout);
-  run_levels();
+  // the byte reference: the product's launches for var 0, the lab body's own
+  // per-level launches (var 7) otherwise -- the lab body keeps the round-4
+  // contiguous-row layout, the product the round-5 16-B pieces
+  if (var == 0) run_levels();
+  else run_level_lab(7);
   CK(hipStreamSynchronize(st));
   std::vector<uint8_t> ref(tbytes), got(tbytes);
   CK(hipMemcpy(ref.data(), tab, tbytes, hipMemcpyDeviceToHost));
@@ -372,7 +380,7 @@ int main(int argc, char** argv) {
     if (var == 0) {
       CK(hipEventRecord(e0, st));
       run_levels();
-    } else if (var >= 6) {
+    } else if (var >= 6 && var != 9) {
       CK(hipEventRecord(e0, st));
       run_level_lab(var);
     } else {
@@ -386,7 +394,7 @@ int main(int argc, char** argv) {
     float ms;
     CK(hipEventElapsedTime(&ms, e0, e1));
     if (r) ts.push_back(ms);
-    if (var != 0 && var < 6) {
+    if (var != 0 && (var < 6 || var == 9)) {
       uint32_t t = 0;
       CK(hipMemcpy(&t, tmo, 4, hipMemcpyDeviceToHost));
       if (t) {
