@@ -415,8 +415,8 @@ def keyed_record(device):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--heaps", default=None,
                     help="override the synthetic heaps, e.g. 31:31:31:31")
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -47,7 +47,7 @@ def kernel_sources_sha16(root_dir):
     return h.hexdigest()[:16]
 
 
-KEYED_WORKLOAD = "toot_and_otto_bitstring length=6,height=4 (bench.py keyed record)"
+KEYED_WORKLOAD = "toot_and_otto_bitstring length=6,height=4"  # the bench keyed record and tools/pmc_ranked.sh
 
 
 def traffic(workload, out_path, root):
