@@ -884,9 +884,11 @@ __device__ __forceinline__ uint32_t plane_flow_ld(uint32_t* p) {
 __device__ __forceinline__ void plane_flow_st(uint32_t* p, uint32_t v) {
   __hip_atomic_store((plane_gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// (the kernel, k_plane_flow in gm_plane_run.h, runs this body and then the
+// forward's reach map and counts in the same launch)
 template <int NO>
-__global__ __launch_bounds__(256) void k_plane_flow(uint8_t* __restrict__ tab, PlaneGeom g,
-                                                    const uint4* __restrict__ zero, PlaneFlow f) {
+__device__ __forceinline__ void plane_flow_body(uint8_t* __restrict__ tab, const PlaneGeom& g,
+                                                const uint4* __restrict__ zero, const PlaneFlow& f) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t q = (blockIdx.x & 7u) + 8u * ((blockIdx.x >> 3) % kPlaneFlowSeq);
   const uint32_t base = f.qoff[q], n = f.qoff[q + 1] - base;

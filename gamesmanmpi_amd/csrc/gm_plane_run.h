@@ -29,6 +29,23 @@ __global__ __launch_bounds__(256) void k_plane_reach(uint32_t* bits, PlaneGeom g
   }
 }
 
+// The one-launch backward (gm_plane.h plane_flow_body) and, in the same
+// launch, the forward: once a wave's ticket sequence is empty it writes its
+// grid-stride share of the reach map and the counts (k_plane_reach's body).
+// The words never read the reach map, and the forward's ~10 us of work
+// fills waves that the narrow tail levels leave idle instead of a launch of
+// its own before the backward.
+template <int NO>
+__global__ __launch_bounds__(256) void k_plane_flow(uint8_t* tab, PlaneGeom g, const uint4* zero, PlaneFlow f,
+                                                    uint32_t* bits, BlockCount* bc, DevState* st, uint32_t word_bits) {
+  plane_flow_body<NO>(tab, g, zero, f);
+  plane_reach_body<NO>(bits, g, [&](u64 npos, u64 edges) { block_count(bc, npos, edges); });
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st->word_bits = word_bits;
+    if (g.rank == 0) atomicAdd(&st->prims, 1ull);
+  }
+}
+
 // word of local position (h0, h1, P) in value | remoteness << 2 form; e:
 // the position's digit sum (all heaps; read by the relative forms only)
 template <int WB>
@@ -1580,7 +1597,9 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out, bool async) {
       }
       if (stop > 0) {
         if (timing) HIPCHK(hipEventRecord(kx[0], st));
-        for (gm_solver* s : ss) plane_reach_launch(s, overlap ? fs : nullptr);
+        // (the one-launch backward writes the reach map and counts itself)
+        if (!flow)
+          for (gm_solver* s : ss) plane_reach_launch(s, overlap ? fs : nullptr);
         if (timing && join()) return GM_EHIP;
         if (timing) HIPCHK(hipEventRecord(kx[1], st));
       }
@@ -1651,7 +1670,7 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out, bool async) {
     }
     plane_no_dispatch(s0->pg.no, [&](auto NO) {
       hipLaunchKernelGGL((k_plane_flow<decltype(NO)::value>), dim3(s0->pflow_grid), dim3(256), 0, st,
-                         (uint8_t*)s0->ptab, s0->pg, s0->pzero, f);
+                         (uint8_t*)s0->ptab, s0->pg, s0->pzero, f, s0->pbits, s0->bcount, s0->st, s0->pmark());
     });
     nlaunch = 1;
     if (timing) HIPCHK(hipEventRecord(kr[2 * (size_t)S + 1], st));
