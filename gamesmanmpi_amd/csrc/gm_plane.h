@@ -479,12 +479,18 @@ __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
 #ifndef GM_PLANE_RSV_UNR
 #define GM_PLANE_RSV_UNR false
 #endif
-template <int WB, int NO, bool SH, int RS_, bool UNR = true, bool WT = false, bool HR = false>
+// (mid: called once the neighbour rows are folded, before the wavefront --
+// the one-launch backward issues its next visit's polls there)
+struct PlaneNoMid {
+  __device__ void operator()() const {}
+};
+template <int WB, int NO, bool SH, int RS_, bool UNR = true, bool WT = false, bool HR = false, class Mid = PlaneNoMid>
 __device__ __forceinline__ void plane_x2_visit(typename PlaneWord<WB>::T* __restrict__ tab, const PlaneGeom& g,
                                                const uint4* __restrict__ zero,
                                                const typename PlaneWord<WB>::T* __restrict__ recv,
                                                typename PlaneWord<WB>::T* __restrict__ send, const PlaneEntry ex,
-                                               const PlaneEntry ey, const bool livex, const bool livey) {
+                                               const PlaneEntry ey, const bool livex, const bool livey,
+                                               Mid mid = Mid()) {
   typedef PlaneWord<WB> W;
   typedef typename W::T T;
   constexpr int DW = W::DW, NQ = DW / 4;
@@ -633,6 +639,7 @@ __device__ __forceinline__ void plane_x2_visit(typename PlaneWord<WB>::T* __rest
     for (int j = 0; j < NO; j++) fold2(j, 1, j, 2);
     if constexpr (HR) hfold(1, 2);
   }
+  mid();
   const uint32_t primv =
       (g.rank == 0 && L == 0) ? ((ex.p == 0 ? W::kPrim : 0u) | (ey.p == 0 ? W::kPrim << 16 : 0u)) : 0u;
   // step q's results of both planes stay packed [X | Y] in op[q] (OR of
@@ -886,7 +893,7 @@ __device__ __forceinline__ void plane_flow_st(uint32_t* p, uint32_t v) {
 }
 // (the kernel, k_plane_flow in gm_plane_run.h, runs this body and then the
 // forward's reach map and counts in the same launch)
-template <int NO>
+template <int NO, bool PIPE>
 __device__ __forceinline__ void plane_flow_body(uint8_t* __restrict__ tab, const PlaneGeom& g,
                                                 const uint4* __restrict__ zero, const PlaneFlow& f) {
   const uint32_t lane = threadIdx.x & 63;
@@ -895,52 +902,89 @@ __device__ __forceinline__ void plane_flow_body(uint8_t* __restrict__ tab, const
   uint32_t* const c = f.ctr + kPlaneFlowLine * q;
   uint32_t* const nout = f.ctr + kPlaneFlowLine * kPlaneFlowQ;
   uint32_t* const gave = nout + kPlaneFlowLine;
+  constexpr uint32_t NW = NO > 0 ? NO : 1;
+  // lane l < 4 NO watches the k = 1 neighbour along digit l % NO of the
+  // visit's plane l / NO (kPlaneAbsent: nothing to wait for)
+  auto nbr = [&](uint32_t pq) -> uint32_t {
+    uint32_t nbp = kPlaneAbsent;
+    if (NO > 0 && lane < 4u * NO && pq != kPlaneAbsent) {
+      const uint32_t j = lane % NW;
+      uint32_t dg[NW];
+      plane_digits<NO>(g, pq, dg);
+#pragma unroll
+      for (int i = 0; i < NO; i++)
+        if ((uint32_t)i == j && dg[i] >= 1u) nbp = pq - g.stride[i];
+    }
+    return nbp;
+  };
+  // a visit's planes: this lane's X and Y, the first (padding lanes compute
+  // it again, storing nothing) and the plane this lane watches
+  struct Visit {
+    uint32_t x, y, p0, pq;
+  };
+  auto visit_of = [&](uint32_t tk) -> Visit {
+    const uint32_t* ip = f.items + (size_t)(base + tk) * 4u;
+    Visit v;
+    v.x = ip[2 * (lane >> 5)];
+    v.y = ip[2 * (lane >> 5) + 1];
+    v.p0 = ip[0];
+    v.pq = (NO > 0 && lane < 4u * NO) ? ip[lane / NW] : kPlaneAbsent;
+    return v;
+  };
   uint32_t t = 0;
   if (lane == 0) t = atomicAdd(c, 1u);
   t = __builtin_amdgcn_readfirstlane(__shfl(t, 0));
+  Visit cv{kPlaneAbsent, kPlaneAbsent, kPlaneAbsent, kPlaneAbsent};
+  if (t < n) cv = visit_of(t);
+  uint32_t tn = 0;  // the next ticket, in flight during this visit
+  if (lane == 0) tn = atomicAdd(c, 1u);
+  bool ready = false;  // (PIPE) this visit's neighbours seen final during the previous one
   while (t < n) {
-    uint32_t tn = 0;  // the next ticket, in flight during this visit
-    if (lane == 0) tn = atomicAdd(c, 1u);
-    const uint32_t* ip = f.items + (size_t)(base + t) * 4u;
-    // lane l < 4 NO waits for the k = 1 neighbour along digit l % NO of plane l / NO
-    uint32_t nbp = kPlaneAbsent;
-    if (NO > 0 && lane < 4u * NO) {
-      const uint32_t pq = ip[lane / (NO > 0 ? NO : 1)], j = lane % (NO > 0 ? NO : 1);
-      uint32_t dg[NO > 0 ? NO : 1];
-      if (pq != kPlaneAbsent) {
-        plane_digits<NO>(g, pq, dg);
-#pragma unroll
-        for (int i = 0; i < NO; i++)
-          if ((uint32_t)i == j && dg[i] >= 1u) nbp = pq - g.stride[i];
-      }
-    }
-    bool ok = nbp == kPlaneAbsent;
-    for (uint32_t spins = 0;; spins++) {
-      if (!ok) ok = plane_flow_ld(f.flags + nbp) == f.epoch;
-      if (__all(ok)) break;
-      if (spins >= kPlaneFlowSpin || plane_flow_ld(gave)) {
-        if (lane == 0) {
-          plane_flow_st(gave, 1u);
-          atomicOr(f.err, f.stall);
+    if (!ready) {
+      const uint32_t nbp = nbr(cv.pq);
+      bool ok = nbp == kPlaneAbsent;
+      for (uint32_t spins = 0;; spins++) {
+        if (!ok) ok = plane_flow_ld(f.flags + nbp) == f.epoch;
+        if (__all(ok)) break;
+        if (spins >= kPlaneFlowSpin || plane_flow_ld(gave)) {
+          if (lane == 0) {
+            plane_flow_st(gave, 1u);
+            atomicOr(f.err, f.stall);
+          }
+          t = n;
+          break;
         }
-        t = n;
-        break;
+        __builtin_amdgcn_s_sleep(4);
       }
-      __builtin_amdgcn_s_sleep(4);
+      if (t >= n) break;
     }
-    if (t >= n) break;
     if (f.mode & 4u) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    // the polls complete before anything below issues, and no load below
-    // may be moved above them (a compiler barrier, not only a hardware wait)
+    // the polls complete before anything below issues, and no load below may
+    // be moved above them (a compiler barrier, not only a hardware wait)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t p0 = ip[0];
+    const uint32_t tv = __builtin_amdgcn_readfirstlane(__shfl(tn, 0));
+    // PIPE: the next visit's planes and the ticket after it load during this
+    // visit, and its polls go out once this visit's rows are folded (mid):
+    // at the end of the visit their answers are in, usually "final"
+    Visit nv{kPlaneAbsent, kPlaneAbsent, kPlaneAbsent, kPlaneAbsent};
+    uint32_t tnn = 0, nflag = 0, nbn = kPlaneAbsent;
+    if (PIPE && tv < n) {
+      nv = visit_of(tv);
+      if (lane == 0) tnn = atomicAdd(c, 1u);
+    }
     PlaneEntry ex, ey;
-    ex.p = ip[2 * (lane >> 5)];
-    ey.p = ip[2 * (lane >> 5) + 1];
+    ex.p = cv.x;
+    ey.p = cv.y;
     const bool livex = ex.p != kPlaneAbsent, livey = ey.p != kPlaneAbsent;
-    if (!livex) ex.p = p0;
-    if (!livey) ey.p = p0;
-    plane_x2_visit<1, NO, false, 0, true, true>(tab, g, zero, nullptr, nullptr, ex, ey, livex, livey);
+    if (!livex) ex.p = cv.p0;
+    if (!livey) ey.p = cv.p0;
+    auto mid = [&]() {
+      if (PIPE) {
+        nbn = nbr(nv.pq);
+        if (nbn != kPlaneAbsent) nflag = plane_flow_ld(f.flags + nbn);
+      }
+    };
+    plane_x2_visit<1, NO, false, 0, true, true, false>(tab, g, zero, nullptr, nullptr, ex, ey, livex, livey, mid);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every lane's rows written through before any flag
     if (f.mode & 1u) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     if ((lane & 31) < 2) {
@@ -948,7 +992,19 @@ __device__ __forceinline__ void plane_flow_body(uint8_t* __restrict__ tab, const
       const uint32_t p = (lane & 1) ? ey.p : ex.p;
       if (live && p != f.skip) plane_flow_st(f.flags + p, f.epoch);
     }
-    t = __builtin_amdgcn_readfirstlane(__shfl(tn, 0));
+    // (not PIPE: the next ticket is requested here, after the drain, and the
+    // next visit's planes load here -- issued before this visit's row loads,
+    // a device-scope atomic held up their first wait: 1.062-1.066 -> 1.022
+    // ms per step)
+    t = tv;
+    if (PIPE) {
+      ready = __all(nbn == kPlaneAbsent || nflag == f.epoch);
+      cv = nv;
+      tn = tnn;
+    } else if (t < n) {
+      cv = visit_of(t);
+      if (lane == 0) tn = atomicAdd(c, 1u);
+    }
   }
   if (lane == 0) {  // the last wave out resets the counters for the next solve
     const uint32_t waves = gridDim.x * (blockDim.x >> 6);

@@ -35,10 +35,10 @@ __global__ __launch_bounds__(256) void k_plane_reach(uint32_t* bits, PlaneGeom g
 // The words never read the reach map, and the forward's ~10 us of work
 // fills waves that the narrow tail levels leave idle instead of a launch of
 // its own before the backward.
-template <int NO>
+template <int NO, bool PIPE = false>
 __global__ __launch_bounds__(256) void k_plane_flow(uint8_t* tab, PlaneGeom g, const uint4* zero, PlaneFlow f,
                                                     uint32_t* bits, BlockCount* bc, DevState* st, uint32_t word_bits) {
-  plane_flow_body<NO>(tab, g, zero, f);
+  plane_flow_body<NO, PIPE>(tab, g, zero, f);
   plane_reach_body<NO>(bits, g, [&](u64 npos, u64 edges) { block_count(bc, npos, edges); });
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     st->word_bits = word_bits;
@@ -695,7 +695,7 @@ static int plane_setup(gm_solver* s, const gm_buffers* buf) {
     // sequences
     int occ = 0;
     plane_no_dispatch(ps.g.no, [&](auto NO) {
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_plane_flow<decltype(NO)::value>, 256, 0) != hipSuccess)
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_plane_flow<decltype(NO)::value, false>, 256, 0) != hipSuccess)
         occ = 0;
     });
     const u64 cus = (u64)launch_grid() / 8;
@@ -1669,8 +1669,15 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out, bool async) {
       f.epoch = s0->pflow.epoch = 1;
     }
     plane_no_dispatch(s0->pg.no, [&](auto NO) {
-      hipLaunchKernelGGL((k_plane_flow<decltype(NO)::value>), dim3(s0->pflow_grid), dim3(256), 0, st,
-                         (uint8_t*)s0->ptab, s0->pg, s0->pzero, f, s0->pbits, s0->bcount, s0->st, s0->pmark());
+      // (lab knob GM_PLANE_FLOW_PIPE=1: the next visit's polls issued mid-visit
+      // -- measured slower, 1.069 vs 1.022-1.025 ms per step,
+      // profiles/r06/flow_pipe_ab.txt; A/B)
+      if (const char* e = lab_env("GM_PLANE_FLOW_PIPE"); e && atoi(e) == 1)
+        hipLaunchKernelGGL((k_plane_flow<decltype(NO)::value, true>), dim3(s0->pflow_grid), dim3(256), 0, st,
+                           (uint8_t*)s0->ptab, s0->pg, s0->pzero, f, s0->pbits, s0->bcount, s0->st, s0->pmark());
+      else
+        hipLaunchKernelGGL((k_plane_flow<decltype(NO)::value, false>), dim3(s0->pflow_grid), dim3(256), 0, st,
+                           (uint8_t*)s0->ptab, s0->pg, s0->pzero, f, s0->pbits, s0->bcount, s0->st, s0->pmark());
     });
     nlaunch = 1;
     if (timing) HIPCHK(hipEventRecord(kr[2 * (size_t)S + 1], st));
