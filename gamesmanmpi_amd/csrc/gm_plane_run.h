@@ -29,23 +29,6 @@ __global__ __launch_bounds__(256) void k_plane_reach(uint32_t* bits, PlaneGeom g
   }
 }
 
-// The one-launch backward (gm_plane.h plane_flow_body) and, in the same
-// launch, the forward: once a wave's ticket sequence is empty it writes its
-// grid-stride share of the reach map and the counts (k_plane_reach's body).
-// The words never read the reach map, and the forward's ~10 us of work
-// fills waves that the narrow tail levels leave idle instead of a launch of
-// its own before the backward.
-template <int NO, bool PIPE = false>
-__global__ __launch_bounds__(256) void k_plane_flow(uint8_t* tab, PlaneGeom g, const uint4* zero, PlaneFlow f,
-                                                    uint32_t* bits, BlockCount* bc, DevState* st, uint32_t word_bits) {
-  plane_flow_body<NO, PIPE>(tab, g, zero, f);
-  plane_reach_body<NO>(bits, g, [&](u64 npos, u64 edges) { block_count(bc, npos, edges); });
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    st->word_bits = word_bits;
-    if (g.rank == 0) atomicAdd(&st->prims, 1ull);
-  }
-}
-
 // word of local position (h0, h1, P) in value | remoteness << 2 form; e:
 // the position's digit sum (all heaps; read by the relative forms only)
 template <int WB>
@@ -102,10 +85,18 @@ __global__ void k_plane_query(Desc d, PlaneGeom g, const void* tab, const uint32
 
 // the end of a solve, one launch: the root's word (only the shard that owns
 // it; DevState::root_word), then the counts and reduction words (k_fill_red's
-// body) -- one block of 1024 threads
-template <int WB>
+// body) -- one block of 1024 threads.  After the one-launch backward
+// (FLOW, k_plane_flow): the count slots [0, nslots) were STORED by that
+// launch's workgroups, the totals are assigned, not added, the reduction
+// words also go straight into the caller's pinned host buffer (no copy),
+// and the error word is cleared once reported -- so the next one-launch
+// solve needs neither the state fills nor the copy.  (Doing this in the
+// flow launch's last workgroup instead was slower: 1.077-1.082 vs
+// 1.041-1.043 ms per step, profiles/r06/flow_selffin_ab.txt.)
+template <int WB, bool FLOW = false>
 __global__ __launch_bounds__(1024) void k_plane_finish(Desc d, PlaneGeom g, const void* tab, const uint32_t* bits,
-                                                       DevState* st, const BlockCount* bc) {
+                                                       DevState* st, const BlockCount* bc, uint32_t nslots = 0,
+                                                       u64* host = nullptr) {
   if (threadIdx.x == 0) {
     u64 P;
     uint32_t h0, h1, e, w = NO_WORD;
@@ -114,7 +105,70 @@ __global__ __launch_bounds__(1024) void k_plane_finish(Desc d, PlaneGeom g, cons
     st->root_word = w;
   }
   __syncthreads();
-  fill_red_body(st, bc);
+  if (!FLOW) {
+    fill_red_body(st, bc);
+    return;
+  }
+  __shared__ u64 rn[16], re[16];
+  u64 sn = 0, se = 0;
+  for (uint32_t i = threadIdx.x; i < nslots; i += blockDim.x) {
+    sn += bc[i].npos;
+    se += bc[i].edges;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    sn += __shfl_xor(sn, o);
+    se += __shfl_xor(se, o);
+  }
+  if (__lane_id() == 0) {
+    rn[threadIdx.x >> 6] = sn;
+    re[threadIdx.x >> 6] = se;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    sn = se = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); w++) sn += rn[w], se += re[w];
+    const u64 red[5] = {sn, se, st->prims, st->root_word == NO_WORD ? 0ull : (u64)st->root_word + 1ull, (u64)st->err};
+    st->cursor_front = sn;
+    st->edges = se;
+    for (int k = 0; k < 5; k++) st->red[k] = red[k];
+    if (host)
+      for (int k = 0; k < 5; k++) __hip_atomic_store(host + k, red[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    st->err = 0;  // (reported above: the next one-launch solve starts clean)
+  }
+}
+
+// The one-launch backward (gm_plane.h plane_flow_body) and, in the same
+// launch, the forward: once a wave's ticket sequence is empty it writes its
+// grid-stride share of the reach map and the counts (k_plane_reach's body);
+// the narrow tail levels leave most waves idle, so the forward costs no
+// launch of its own.  Each workgroup STORES its count slot (no reset before
+// the solve; k_plane_finish<., true> sums the grid's slots).
+template <int NO, bool PIPE = false>
+__global__ __launch_bounds__(256) void k_plane_flow(uint8_t* tab, PlaneGeom g, const uint4* zero, PlaneFlow f,
+                                                    uint32_t* bits, BlockCount* bc, DevState* st, uint32_t word_bits) {
+  plane_flow_body<NO, PIPE>(tab, g, zero, f);
+  __shared__ u64 rn[4], re[4];
+  plane_reach_body<NO>(bits, g, [&](u64 npos, u64 edges) {
+    for (int o = 32; o > 0; o >>= 1) {
+      npos += __shfl_xor(npos, o);
+      edges += __shfl_xor(edges, o);
+    }
+    if (__lane_id() == 0) {
+      rn[threadIdx.x >> 6] = npos;
+      re[threadIdx.x >> 6] = edges;
+    }
+  });
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u64 sn = 0, se = 0;
+    for (int w = 0; w < 4; w++) sn += rn[w], se += re[w];
+    bc[blockIdx.x].npos = sn;
+    bc[blockIdx.x].edges = se;
+    if (blockIdx.x == 0) {
+      st->word_bits = word_bits;
+      st->prims = g.rank == 0 ? 1ull : 0ull;  // every heap 0: global plane 0 of rank 0
+    }
+  }
 }
 
 // global rank of local position (h0, h1, P); *osum: its outer digit sum
@@ -1590,6 +1644,9 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out, bool async) {
     if (first == 0) {
       for (gm_solver* s : ss) {
         hipStream_t ws = overlap ? fs : s->stream;
+        // (a one-launch solve after another one: that launch left the state
+        // it needs clean -- error word 0, its count slots stored, not added)
+        if (flow && s->pflow_last) continue;
         HIPCHK(hipMemsetAsync(s->st, 0, devstate_bytes(T), ws));
         HIPCHK(hipMemsetAsync(s->bcount, 0, kCountSlots * sizeof(BlockCount), ws));
         // the word width: written by k_plane_reach below (no reach: here)
@@ -1656,6 +1713,14 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out, bool async) {
   }();
   u64 nlaunch = 0;        // resolve launches of this solve (shard 0's)
   s0->pflow_last = flow;
+  // the one-launch solve writes its reduction words straight into pinned host
+  // memory: the queued slot's, or the solver's own for a blocking solve
+  u64* flow_host = nullptr;
+  if (flow) {
+    u64** hp = async ? &s0->pring[s0->pq_next % kPlaneRing].host : &s0->phost;
+    if (!*hp) HIPCHK(hipHostMalloc((void**)hp, 8 * sizeof(u64), hipHostMallocDefault));
+    flow_host = *hp;
+  }
   if (flow) {
     if (timing) HIPCHK(hipEventRecord(kr[0], st));
     PlaneFlow f = s0->pflow;
@@ -1771,15 +1836,20 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out, bool async) {
   }
   for (gm_solver* s : ss)
     plane_form_dispatch(s, [&](auto WB, auto) {
-      hipLaunchKernelGGL(k_plane_finish<decltype(WB)::value>, dim3(1), dim3(1024), 0, st, s->d, s->pg,
-                         (const void*)s->ptab, s->pbits, s->st, (const BlockCount*)s->bcount);
+      if (flow)  // (the one-launch solve: its own count slots, the result straight to pinned memory)
+        hipLaunchKernelGGL((k_plane_finish<decltype(WB)::value, true>), dim3(1), dim3(1024), 0, st, s->d, s->pg,
+                           (const void*)s->ptab, s->pbits, s->st, (const BlockCount*)s->bcount, s->pflow_grid,
+                           flow_host);
+      else
+        hipLaunchKernelGGL((k_plane_finish<decltype(WB)::value, false>), dim3(1), dim3(1024), 0, st, s->d, s->pg,
+                           (const void*)s->ptab, s->pbits, s->st, (const BlockCount*)s->bcount, 0u, (u64*)nullptr);
     });
   HIPCHK(hipGetLastError());
   if (async) {  // queued: the counts into the slot's pinned memory, then its completion event
     PlaneSlot& q = s0->pring[s0->pq_next % kPlaneRing];
     if (!q.host) HIPCHK(hipHostMalloc((void**)&q.host, 8 * sizeof(u64), hipHostMallocDefault));
     if (!q.ev[3]) HIPCHK(hipEventCreate(&q.ev[3]));
-    HIPCHK(hipMemcpyAsync(q.host, s0->st->red, 5 * sizeof(u64), hipMemcpyDeviceToHost, st));
+    if (!flow) HIPCHK(hipMemcpyAsync(q.host, s0->st->red, 5 * sizeof(u64), hipMemcpyDeviceToHost, st));
     HIPCHK(hipEventRecord(q.ev[3], st));
     s0->pq_next++;
     cleanup();
@@ -1800,7 +1870,7 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out, bool async) {
     // (into pinned host memory: a pageable destination is staged and waited
     // for inside the copy call)
     if (!s->phost) HIPCHK(hipHostMalloc((void**)&s->phost, 8 * sizeof(u64), hipHostMallocDefault));
-    HIPCHK(hipMemcpyAsync(s->phost, s->st->red, sizeof r, hipMemcpyDeviceToHost, st));
+    if (!flow) HIPCHK(hipMemcpyAsync(s->phost, s->st->red, sizeof r, hipMemcpyDeviceToHost, st));
     HIPCHK(mode == 0 ? plane_wait(st) : hipStreamSynchronize(st));
     memcpy(r, s->phost, sizeof r);
     if (mode == 3) {
