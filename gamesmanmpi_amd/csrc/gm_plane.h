@@ -931,13 +931,30 @@ __device__ __forceinline__ void plane_flow_body(uint8_t* __restrict__ tab, const
     v.pq = (NO > 0 && lane < 4u * NO) ? ip[lane / NW] : kPlaneAbsent;
     return v;
   };
-  uint32_t t = 0;
-  if (lane == 0) t = atomicAdd(c, 1u);
-  t = __builtin_amdgcn_readfirstlane(__shfl(t, 0));
-  Visit cv{kPlaneAbsent, kPlaneAbsent, kPlaneAbsent, kPlaneAbsent};
-  if (t < n) cv = visit_of(t);
-  uint32_t tn = 0;  // the next ticket, in flight during this visit
-  if (lane == 0) tn = atomicAdd(c, 1u);
+  const Visit none{kPlaneAbsent, kPlaneAbsent, kPlaneAbsent, kPlaneAbsent};
+  auto ticket = [&]() -> uint32_t {  // (lane 0's device atomic; read with readfirstlane(__shfl(., 0)))
+    uint32_t v = 0;
+    if (lane == 0) v = atomicAdd(c, 1u);
+    return v;
+  };
+  auto uni = [](uint32_t v) { return __builtin_amdgcn_readfirstlane(__shfl(v, 0)); };
+  uint32_t t = uni(ticket());
+  Visit cv = t < n ? visit_of(t) : none;
+  // PIPE: the ticket after next is in flight during a visit (requested after
+  // the previous drain, read after this one); the next visit's planes load
+  // after the previous drain, and its polls go out once this visit's rows are
+  // folded (mid) -- at the drain their answers are in, usually "final", so
+  // the next visit loads its rows at once.  Not PIPE: the next ticket and the
+  // next visit's planes are requested after the drain (issued before the row
+  // loads, a device-scope atomic held up their first wait: 1.062-1.066 ->
+  // 1.022 ms per step) and each visit polls before its rows.
+  uint32_t tn = ticket(), tn2 = 0;
+  Visit nv = none;
+  if (PIPE) {
+    tn = uni(tn);
+    nv = tn < n ? visit_of(tn) : none;
+    tn2 = ticket();
+  }
   bool ready = false;  // (PIPE) this visit's neighbours seen final during the previous one
   while (t < n) {
     if (!ready) {
@@ -962,22 +979,13 @@ __device__ __forceinline__ void plane_flow_body(uint8_t* __restrict__ tab, const
     // the polls complete before anything below issues, and no load below may
     // be moved above them (a compiler barrier, not only a hardware wait)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t tv = __builtin_amdgcn_readfirstlane(__shfl(tn, 0));
-    // PIPE: the next visit's planes and the ticket after it load during this
-    // visit, and its polls go out once this visit's rows are folded (mid):
-    // at the end of the visit their answers are in, usually "final"
-    Visit nv{kPlaneAbsent, kPlaneAbsent, kPlaneAbsent, kPlaneAbsent};
-    uint32_t tnn = 0, nflag = 0, nbn = kPlaneAbsent;
-    if (PIPE && tv < n) {
-      nv = visit_of(tv);
-      if (lane == 0) tnn = atomicAdd(c, 1u);
-    }
     PlaneEntry ex, ey;
     ex.p = cv.x;
     ey.p = cv.y;
     const bool livex = ex.p != kPlaneAbsent, livey = ey.p != kPlaneAbsent;
     if (!livex) ex.p = cv.p0;
     if (!livey) ey.p = cv.p0;
+    uint32_t nflag = 0, nbn = kPlaneAbsent;
     auto mid = [&]() {
       if (PIPE) {
         nbn = nbr(nv.pq);
@@ -992,18 +1000,21 @@ __device__ __forceinline__ void plane_flow_body(uint8_t* __restrict__ tab, const
       const uint32_t p = (lane & 1) ? ey.p : ex.p;
       if (live && p != f.skip) plane_flow_st(f.flags + p, f.epoch);
     }
-    // (not PIPE: the next ticket is requested here, after the drain, and the
-    // next visit's planes load here -- issued before this visit's row loads,
-    // a device-scope atomic held up their first wait: 1.062-1.066 -> 1.022
-    // ms per step)
-    t = tv;
     if (PIPE) {
       ready = __all(nbn == kPlaneAbsent || nflag == f.epoch);
+      t = tn;
       cv = nv;
-      tn = tnn;
-    } else if (t < n) {
-      cv = visit_of(t);
-      if (lane == 0) tn = atomicAdd(c, 1u);
+      tn = uni(tn2);
+      if (t < n) {
+        nv = tn < n ? visit_of(tn) : none;
+        tn2 = ticket();
+      }
+    } else {
+      t = uni(tn);
+      if (t < n) {
+        cv = visit_of(t);
+        tn = ticket();
+      }
     }
   }
   if (lane == 0) {  // the last wave out resets the counters for the next solve

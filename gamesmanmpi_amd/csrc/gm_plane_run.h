@@ -143,7 +143,7 @@ __global__ __launch_bounds__(1024) void k_plane_finish(Desc d, PlaneGeom g, cons
 // the narrow tail levels leave most waves idle, so the forward costs no
 // launch of its own.  Each workgroup STORES its count slot (no reset before
 // the solve; k_plane_finish<., true> sums the grid's slots).
-template <int NO, bool PIPE = false>
+template <int NO, bool PIPE = true>
 __global__ __launch_bounds__(256) void k_plane_flow(uint8_t* tab, PlaneGeom g, const uint4* zero, PlaneFlow f,
                                                     uint32_t* bits, BlockCount* bc, DevState* st, uint32_t word_bits) {
   plane_flow_body<NO, PIPE>(tab, g, zero, f);
@@ -749,7 +749,7 @@ static int plane_setup(gm_solver* s, const gm_buffers* buf) {
     // sequences
     int occ = 0;
     plane_no_dispatch(ps.g.no, [&](auto NO) {
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_plane_flow<decltype(NO)::value, false>, 256, 0) != hipSuccess)
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_plane_flow<decltype(NO)::value, true>, 256, 0) != hipSuccess)
         occ = 0;
     });
     const u64 cus = (u64)launch_grid() / 8;
@@ -1734,10 +1734,11 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out, bool async) {
       f.epoch = s0->pflow.epoch = 1;
     }
     plane_no_dispatch(s0->pg.no, [&](auto NO) {
-      // (lab knob GM_PLANE_FLOW_PIPE=1: the next visit's polls issued mid-visit
-      // -- measured slower, 1.069 vs 1.022-1.025 ms per step,
+      // (lab knob GM_PLANE_FLOW_PIPE=0: each visit polls before its rows;
+      // the pipelined form -- the next visit's polls mid-visit, tickets two
+      // ahead -- 1.017-1.021 vs 1.029-1.034 ms per step on one box,
       // profiles/r06/flow_pipe_ab.txt; A/B)
-      if (const char* e = lab_env("GM_PLANE_FLOW_PIPE"); e && atoi(e) == 1)
+      if (const char* e = lab_env("GM_PLANE_FLOW_PIPE"); !(e && atoi(e) == 0))
         hipLaunchKernelGGL((k_plane_flow<decltype(NO)::value, true>), dim3(s0->pflow_grid), dim3(256), 0, st,
                            (uint8_t*)s0->ptab, s0->pg, s0->pzero, f, s0->pbits, s0->bcount, s0->st, s0->pmark());
       else
