@@ -52,7 +52,8 @@ template <int NO, uint32_t NSUB, int SLP>
 __global__ __launch_bounds__(256) void k_flow2(uint8_t* __restrict__ tab, const uint32_t* __restrict__ items,
                                                const uint32_t* __restrict__ xoff, uint32_t* __restrict__ ctr,
                                                uint32_t* __restrict__ flags, uint32_t epoch, uint32_t* __restrict__ tmo,
-                                               PlaneGeom g, const uint4* __restrict__ zero) {
+                                               PlaneGeom g, const uint4* __restrict__ zero,
+                                               uint64_t* __restrict__ stamp) {
   // sequence q: XCD x = blockIdx % 8, sub-sequence (blockIdx / 8) % NSUB;
   // its counter on a line (and channel) of its own
   const uint32_t lane = threadIdx.x & 63, q = (blockIdx.x & 7u) + 8u * ((blockIdx.x >> 3) % NSUB);
@@ -95,6 +96,7 @@ __global__ __launch_bounds__(256) void k_flow2(uint8_t* __restrict__ tab, const 
       const uint32_t p = (lane & 1) ? ey.p : ex.p;
       const bool live = (lane & 1) ? livey : livex;
       if (live) __hip_atomic_store((gu32*)(flags + p), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (live && stamp) stamp[p] = __builtin_amdgcn_s_memrealtime();  // (var 2: when each plane became final)
     }
     t = __builtin_amdgcn_readfirstlane(__shfl(tn, 0));
   }
@@ -184,6 +186,8 @@ int main(int argc, char** argv) {
   tmo = ctr + 64 * NQ;
   hipStream_t st;
   CK(hipStreamCreate(&st));
+  uint64_t* dstamp = nullptr;
+  CK(hipMalloc(&dstamp, np * 8));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -205,7 +209,7 @@ int main(int argc, char** argv) {
     auto go = [&](auto ns, auto sl) {
       hipLaunchKernelGGL((k_flow2<NO, decltype(ns)::value, decltype(sl)::value>), dim3(blocks), dim3(256), 0, st, tab,
                          (const uint32_t*)ditems, (const uint32_t*)dxoff, ctr, flags, epoch, tmo, g,
-                         (const uint4*)zero);
+                         (const uint4*)zero, var == 2 ? dstamp : (uint64_t*)nullptr);
     };
     auto sel = [&](auto ns) {
       switch (SLP) {
@@ -261,6 +265,18 @@ int main(int argc, char** argv) {
       printf("rep %d: %zu differing bytes, first at %zu (plane %zu): got %02x want %02x MISMATCH\n", r, bad, first,
              first / 1024, got[first], ref[first]);
       return 2;
+    }
+  }
+  if (var == 2) {  // per plane level: when its first / last plane became final (100 MHz ticks from the first)
+    std::vector<uint64_t> h(np);
+    CK(hipMemcpy(h.data(), dstamp, np * 8, hipMemcpyDeviceToHost));
+    uint64_t t0 = ~0ull;
+    for (uint64_t P = 0; P < np; P++) t0 = std::min(t0, h[P]);
+    printf("level first_us last_us planes\n");
+    for (int s = 0; s <= S; s++) {
+      uint64_t a = ~0ull, b = 0;
+      for (uint32_t P : lev[s]) a = std::min(a, h[P]), b = std::max(b, h[P]);
+      printf("%d %.2f %.2f %zu\n", s, (a - t0) / 100.0, (b - t0) / 100.0, lev[s].size());
     }
   }
   float best = 1e9, sum = 0;
