@@ -45,7 +45,9 @@ LEVELS = 65536  # GM_F_PLANE_LEVELS: one launch per plane level instead of the o
 
 @pytest.mark.parametrize("flags", [0, LEVELS])
 @pytest.mark.parametrize("params", ["heaps=31:31", "heaps=31:31:1", "heaps=31:31:3", "heaps=31:31:2:5",
-                                    "heaps=31:31:4:0:2", "heaps=31:31:7:7"])
+                                    "heaps=31:31:4:0:2", "heaps=31:31:7:7",
+                                    "heaps=31:31:1:2:1:2:1",      # five outer digits, mixed bases
+                                    "heaps=31:31:1:1:1:1:1:1"])   # six (kPlaneMaxOuter)
 def test_planes_match_oracle(params, flags):
     """Every position's value and remoteness (and the counts / root line)
     equal the oracle's, including non-power-of-two and zero-height outer
