@@ -869,8 +869,9 @@ __global__ __launch_bounds__(256) void k_plane_resolve_x2(typename PlaneWord<WB>
 // solve.  tools/flow2_lab.hip: 1.06-1.09 vs 1.34 ms per 2^30 backward for
 // the same visits launched per level, byte-exact on a poisoned table
 // (profiles/r06/flow2_lab.txt).
-constexpr uint32_t kPlaneFlowSeq = 8;      // ticket sequences per XCD
-constexpr uint32_t kPlaneFlowQ = 8 * kPlaneFlowSeq;
+constexpr uint32_t kPlaneFlowSeq = 8;      // ticket sequences per XCD (PlaneFlow::nseq; lab A/B up to kPlaneFlowSeqMax)
+constexpr uint32_t kPlaneFlowSeqMax = 16;
+constexpr uint32_t kPlaneFlowQ = 8 * kPlaneFlowSeqMax;  // counter lines / sequence offsets provisioned
 constexpr uint32_t kPlaneFlowLine = 64;    // u32 per counter line
 constexpr uint32_t kPlaneFlowSpin = 1u << 20;
 constexpr uint32_t kPlaneFlowBlocksPerCU = 3;
@@ -882,6 +883,7 @@ struct PlaneFlow {
   uint32_t* err;          // DevState::err
   uint32_t epoch, stall;
   uint32_t skip;  // (the lab build's fault injector, GM_FAULT_FLOW: this plane's flag is never set; else kPlaneAbsent)
+  uint32_t nseq;  // ticket sequences per XCD (kPlaneFlowSeq)
   uint32_t mode;  // (lab A/B, GM_PLANE_FLOW_MODE: 1 agent release fence before the flags, 4 agent acquire after the polls)
 };
 typedef __attribute__((address_space(1))) uint32_t plane_gu32;
@@ -897,7 +899,7 @@ template <int NO, bool PIPE>
 __device__ __forceinline__ void plane_flow_body(uint8_t* __restrict__ tab, const PlaneGeom& g,
                                                 const uint4* __restrict__ zero, const PlaneFlow& f) {
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t q = (blockIdx.x & 7u) + 8u * ((blockIdx.x >> 3) % kPlaneFlowSeq);
+  const uint32_t q = (blockIdx.x & 7u) + 8u * ((blockIdx.x >> 3) % f.nseq);
   const uint32_t base = f.qoff[q], n = f.qoff[q + 1] - base;
   uint32_t* const c = f.ctr + kPlaneFlowLine * q;
   uint32_t* const nout = f.ctr + kPlaneFlowLine * kPlaneFlowQ;
@@ -971,7 +973,8 @@ __device__ __forceinline__ void plane_flow_body(uint8_t* __restrict__ tab, const
           t = n;
           break;
         }
-        __builtin_amdgcn_s_sleep(4);
+        if (f.mode & 16u) __builtin_amdgcn_s_sleep(1);  // (lab A/B: GM_PLANE_FLOW_MODE bit 16)
+        else __builtin_amdgcn_s_sleep(4);
       }
       if (t >= n) break;
     }

@@ -713,19 +713,23 @@ static int plane_setup(gm_solver* s, const gm_buffers* buf) {
     // padded to whole visits; the level's visits cut into 8 contiguous XCD
     // chunks, a chunk dealt round robin over its XCD's sequences
     const uint32_t* L = (const uint32_t*)lb.data();
-    std::vector<std::vector<uint32_t>> qv(kPlaneFlowQ);
+    // (lab knob GM_PLANE_FLOW_SEQ: sequences per XCD, 1..kPlaneFlowSeqMax; A/B)
+    uint32_t nseq = kPlaneFlowSeq;
+    if (const char* e = lab_env("GM_PLANE_FLOW_SEQ")) nseq = std::max(1u, std::min(kPlaneFlowSeqMax, (uint32_t)atoi(e)));
+    const uint32_t nq = 8 * nseq;
+    std::vector<std::vector<uint32_t>> qv(nq);
     for (uint32_t l = 0; l <= ps.S; l++) {
       std::vector<uint32_t> v(L + s->ploff[l], L + s->ploff[(size_t)l + 1]);
       while (v.size() % 4) v.push_back(kPlaneAbsent);
       const u64 nv = v.size() / 4, chunk = (nv + 7) / 8;
       for (u64 x = 0; x < 8; x++)
         for (u64 i = x * chunk; i < std::min(nv, (x + 1) * chunk); i++) {
-          auto& q = qv[x + 8 * ((i - x * chunk) % kPlaneFlowSeq)];
+          auto& q = qv[x + 8 * ((i - x * chunk) % nseq)];
           q.insert(q.end(), v.begin() + 4 * i, v.begin() + 4 * i + 4);
         }
     }
     std::vector<uint32_t> items, qoff(kPlaneFlowQ + 1, 0);
-    for (uint32_t q = 0; q < kPlaneFlowQ; q++) {
+    for (uint32_t q = 0; q < nq; q++) {
       qoff[q + 1] = qoff[q] + (uint32_t)(qv[q].size() / 4);
       items.insert(items.end(), qv[q].begin(), qv[q].end());
     }
@@ -738,6 +742,7 @@ static int plane_setup(gm_solver* s, const gm_buffers* buf) {
     f.err = &s->st->err;
     f.epoch = 0;
     f.stall = ERR_PLANE_STALL;
+    f.nseq = nseq;
     f.skip = kPlaneAbsent;
     f.mode = 0;
     HIPCHK(hipMemcpy((void*)f.items, items.data(), items.size() * 4, hipMemcpyHostToDevice));
@@ -753,9 +758,11 @@ static int plane_setup(gm_solver* s, const gm_buffers* buf) {
         occ = 0;
     });
     const u64 cus = (u64)launch_grid() / 8;
-    const u64 blocks = cus * std::min<u64>(kPlaneFlowBlocksPerCU, (u64)std::max(occ, 0)) / kPlaneFlowQ * kPlaneFlowQ;
+    u64 bpc = std::min<u64>(kPlaneFlowBlocksPerCU, (u64)std::max(occ, 0));
+    if (const char* e = lab_env("GM_PLANE_FLOW_BPC")) bpc = std::min<u64>(bpc, (u64)std::max(1, atoi(e)));  // (lab A/B)
+    const u64 blocks = cus * bpc / nq * nq;
     s->pflow_grid = (uint32_t)blocks;
-    s->pflow_ok = blocks >= kPlaneFlowQ;
+    s->pflow_ok = blocks >= nq;
   }
   s->w8 = ps.wb == 1;  // (the dense flags; the planes paths read pform)
   s->w16 = ps.wb == 2;
