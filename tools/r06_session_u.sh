@@ -1,7 +1,7 @@
 #!/bin/bash
 # final-kernel profiles: driver-line bench, rocprofv3 kernel stats, PMC passes (bench + RANKED toot 6x4)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
-out=gpurun_out/r06final2
+out=gpurun_out/r06final3
 mkdir -p $out
 export TMPDIR=/tmp
 timeout -k 10 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $out/bench.json 2> $out/bench.err || { tail $out/bench.err; exit 1; }
