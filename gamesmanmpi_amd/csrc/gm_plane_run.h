@@ -1644,6 +1644,17 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out, bool async) {
     }
     fs = s0->cstream;
   }
+  // a queued one-launch solve records only its start and its completion:
+  // the forward has no launch of its own and every timing marker between
+  // solves is a gap on the device (the trace: ~20 us between one solve's
+  // finish and the next launch); ms_forward 0, ms_backward = the whole span
+  // (lab knob GM_PLANE_FLOW_LITE=0: all five events; A/B)
+  static const bool lite_knob = [] {
+    const char* e = lab_env("GM_PLANE_FLOW_LITE");
+    return !(e && atoi(e) == 0);
+  }();
+  const bool lite = async && flow && lite_knob;
+  if (async) s0->pring[s0->pq_next % kPlaneRing].lite = lite;
   auto t0 = std::chrono::steady_clock::now();
   HIPCHK(hipEventRecord(e0, st));
   if (fork()) return GM_EHIP;
@@ -1670,7 +1681,7 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out, bool async) {
     }
     HIPCHK(hipGetLastError());
     if (join()) return GM_EHIP;
-    HIPCHK(hipEventRecord(e1, fs));  // overlap: the forward's end on its own stream
+    if (!lite) HIPCHK(hipEventRecord(e1, fs));  // overlap: the forward's end on its own stream
     if (fork()) return GM_EHIP;
     return 0;
   };
@@ -1680,7 +1691,7 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out, bool async) {
   // (the forward is read by the finish only)
   bool fwd_pending = overlap;
   if (!fwd_pending) {
-    HIPCHK(hipEventRecord(etail, st));  // (the forward's start: ms_forward)
+    if (!lite) HIPCHK(hipEventRecord(etail, st));  // (the forward's start: ms_forward)
     const int rc = issue_forward();
     if (rc) return rc;
   }
@@ -1833,7 +1844,7 @@ static int run_planes(std::vector<gm_solver*> ss, gm_result* out, bool async) {
     }
   }
   if (join()) return GM_EHIP;
-  HIPCHK(hipEventRecord(e2, st));
+  if (!lite) HIPCHK(hipEventRecord(e2, st));
   if (overlap) HIPCHK(hipStreamWaitEvent(st, e1, 0));  // the counts and state resets before the finish
   if (stop < 2 * T) {
     HIPCHK(hipStreamSynchronize(st));
@@ -1948,9 +1959,13 @@ static int plane_collect(gm_solver* s, u64 ticket, gm_result* out) {
   u64 red[5];
   memcpy(red, q.host, sizeof red);
   float f = 0, b = 0, t = 0;
-  HIPCHK(hipEventElapsedTime(&f, q.ev[4], q.ev[1]));
-  HIPCHK(hipEventElapsedTime(&b, q.ev[0], q.ev[2]));
   HIPCHK(hipEventElapsedTime(&t, q.ev[0], q.ev[3]));
+  if (q.lite) {  // (a one-launch solve: start and completion only)
+    b = t;
+  } else {
+    HIPCHK(hipEventElapsedTime(&f, q.ev[4], q.ev[1]));
+    HIPCHK(hipEventElapsedTime(&b, q.ev[0], q.ev[2]));
+  }
   out->ms_forward = f;
   out->ms_backward = b;
   out->ms_total = t;  // device span of the queued solve (its host wall overlaps other solves)

@@ -108,6 +108,7 @@ struct PlaneSlot {
   hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // (4: the forward's start, no timing)
   u64* host = nullptr;
   double t_enq = 0;  // host clock at enqueue (ms)
+  bool lite = false;  // only ev[0] and ev[3] recorded (a queued one-launch solve)
 };
 
 // an in-process multi-GPU group aborted (solve_multi's abort_all): no RCCL
