@@ -418,7 +418,7 @@ static int plane_shape(const Desc* d, int rank, int world, uint32_t flags, Plane
   ps->flow = world <= 1 && ps->form == 1 && g.no >= 1;
   if (ps->flow) {  // visits: every level padded to whole visits of 4 planes
     ps->flow_off = ps->scratch_bytes;
-    ps->flow_qoff_off = ps->flow_off + rup256((ps->nlocal + 3ull * (ps->S + 1)) * 4);
+    ps->flow_qoff_off = ps->flow_off + rup256((ps->nlocal + 24ull * (ps->S + 1)) * 4);  // (<= 3 pads per level and XCD)
     ps->flow_ctr_off = ps->flow_qoff_off + rup256((kPlaneFlowQ + 1) * 4);
     ps->flow_flags_off = ps->flow_ctr_off + rup256((u64)kPlaneFlowLine * (kPlaneFlowQ + 2) * 4);
     ps->scratch_bytes = ps->flow_flags_off + rup256(ps->nlocal * 4);
@@ -718,8 +718,30 @@ static int plane_setup(gm_solver* s, const gm_buffers* buf) {
     if (const char* e = lab_env("GM_PLANE_FLOW_SEQ")) nseq = std::max(1u, std::min(kPlaneFlowSeqMax, (uint32_t)atoi(e)));
     const uint32_t nq = 8 * nseq;
     std::vector<std::vector<uint32_t>> qv(nq);
+    // (lab knob GM_PLANE_FLOW_DEAL=1: XCD x takes the planes whose top outer
+    // digit lies in slab x of 8 -- the same XCD for a plane at every level,
+    // so neighbours along the other digits share its L2 -- instead of an
+    // even chunk of every level; A/B)
+    const char* deal_e = lab_env("GM_PLANE_FLOW_DEAL");
+    const bool slabs = deal_e && atoi(deal_e) == 1 && ps.g.no >= 2;
+    const uint32_t tb = ps.g.base[ps.g.no > 0 ? ps.g.no - 1 : 0];
     for (uint32_t l = 0; l <= ps.S; l++) {
       std::vector<uint32_t> v(L + s->ploff[l], L + s->ploff[(size_t)l + 1]);
+      if (slabs) {
+        std::vector<std::vector<uint32_t>> xv(8);
+        for (uint32_t P : v) {
+          const uint32_t top = (uint32_t)((P / ps.g.stride[ps.g.no - 1]) % tb);
+          xv[std::min(7u, top * 8u / tb)].push_back(P);
+        }
+        for (uint32_t x = 0; x < 8; x++) {
+          while (xv[x].size() % 4) xv[x].push_back(kPlaneAbsent);
+          for (u64 i = 0; i < xv[x].size() / 4; i++) {
+            auto& q = qv[x + 8 * (i % nseq)];
+            q.insert(q.end(), xv[x].begin() + 4 * i, xv[x].begin() + 4 * i + 4);
+          }
+        }
+        continue;
+      }
       while (v.size() % 4) v.push_back(kPlaneAbsent);
       const u64 nv = v.size() / 4, chunk = (nv + 7) / 8;
       for (u64 x = 0; x < 8; x++)
@@ -733,7 +755,7 @@ static int plane_setup(gm_solver* s, const gm_buffers* buf) {
       qoff[q + 1] = qoff[q] + (uint32_t)(qv[q].size() / 4);
       items.insert(items.end(), qv[q].begin(), qv[q].end());
     }
-    if (items.size() > ps.nlocal + 3ull * (ps.S + 1)) return fail(GM_ECORRUPT, "plane flow: %zu visit entries", items.size());
+    if (items.size() > ps.nlocal + 24ull * (ps.S + 1)) return fail(GM_ECORRUPT, "plane flow: %zu visit entries", items.size());
     PlaneFlow& f = s->pflow;
     f.items = (const uint32_t*)(sc + ps.flow_off);
     f.qoff = (const uint32_t*)(sc + ps.flow_qoff_off);
