@@ -1,7 +1,7 @@
 #!/bin/bash
 # full -m gpu suite + smoke on the k_plane_flow tree
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
-out=gpurun_out/r06ai
+out=gpurun_out/r06al
 mkdir -p $out
 export TMPDIR=/tmp
 timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $out/gpu_tests.txt 2>&1 || { tail -40 $out/gpu_tests.txt; exit 1; }
